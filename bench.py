@@ -1,0 +1,202 @@
+"""Headline benchmark: row-update apply GB/s (device-resident), dense f32 rows.
+
+Workload (BASELINE.json configs[1]): one DenseRow<float> table of
+2^20 rows x 256 cols per GPU (initialised N(0, 0.1)); one step = applying B = 8 worker
+batches, each a full Appendix-A stream (ClientSendOpLogMsg payload) holding one dense
+record per row in a per-batch random row order, updates N(0, 0.01).  Streams and table
+are resident in HBM before the timed region.  Synthetic data, generated on the GPU.
+
+Algorithmic bytes per step: sum_b (20 + N*(4 + 4R)) + 2 * N * 4R.
+value = bytes of all ranks / max-over-ranks wall time.  Multi-GPU: each rank owns a
+2^20-row shard (row range) and receives its own already-split batches, as the reference
+client splits oplogs by owning server (abstract_bg_worker.cpp:590-649): no collective,
+weak scaling.
+
+cpu_baseline: the CPU oracle (restated Server::ApplyOpLogUpdateVersion loop, one
+thread = one reference server thread) on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU shard")
+    p.add_argument("--cols", type=int, default=256)
+    p.add_argument("--batches", type=int, default=8)
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="target CPU time of the cpu_baseline sample (0 disables)")
+    p.add_argument("--cpu-rows", type=int, default=1 << 16)
+    p.add_argument("--pmc-json", default=None,
+                   help="per-launch HBM bytes of dense_apply from a rocprofv3 --pmc pass")
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (CPU restatement of the reference apply loop) on a bounded sample."""
+    import numpy as np
+    from oracle.oracle import OracleServer, DENSE, F32
+    from parameter_server_amd import wire
+    rows, cap, B = args.cpu_rows, args.cols, args.batches
+    rng = np.random.RandomState(1234)
+    init = rng.normal(0, 0.1, size=(rows, cap)).astype(np.float32)
+    streams = []
+    for b in range(B):
+        r = np.random.RandomState(1234 + b)
+        streams.append(wire.dense_stream_np(1, r.permutation(rows).astype(np.int32),
+                                            r.normal(0, 0.01, size=(rows, cap)).astype(np.float32)))
+    bgs = list(range(100, 100 + B))
+    orc = OracleServer(bgs)
+    orc.create_table(1, DENSE, F32, cap)
+    orc.load_dense_rows(1, 0, init)
+    step_bytes = sum(s.size for s in streams) + 2 * rows * cap * 4
+    steps, elapsed, ver = 0, 0.0, 0
+    while elapsed < args.cpu_seconds or steps == 0:
+        t0 = time.perf_counter()
+        for b in range(B):
+            assert orc.apply_stream(streams[b], bgs[b], ver) == 0
+        elapsed += time.perf_counter() - t0
+        steps += 1
+        ver += 1
+    orc.close()
+    return {"value": step_bytes * steps / elapsed / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} rows x {cap} f32, {B} batches/step, {steps} steps in {elapsed:.1f} s "
+                      f"(oracle/psx_oracle.c restatement of server.cpp:120-179, 1 thread)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import parameter_server_amd as psa
+    from parameter_server_amd import wire
+
+    rows, cap, B = args.rows, args.cols, args.batches
+    base = rank * rows                       # this shard's first row id
+    g = torch.Generator(device="cuda").manual_seed(1234 + 7919 * rank)
+    table0 = torch.randn(rows, cap, device="cuda", generator=g) * 0.1
+    streams = []
+    for b in range(B):
+        perm = torch.randperm(rows, device="cuda", generator=g).to(torch.int32) + base
+        upd = torch.randn(rows, cap, device="cuda", generator=g) * 0.01
+        streams.append(wire.dense_stream_torch(1, perm, upd))
+        del upd, perm
+    torch.cuda.synchronize()
+
+    bgs = [100 + b for b in range(B)]
+    srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
+    srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
+                                     row_offset=base, max_rows=rows))
+    srv.load_rows(1, base, None, on_device_ptr=table0.data_ptr(), num_rows=rows)
+    del table0
+    torch.cuda.empty_cache()
+
+    ver = [0]
+
+    def step():
+        srv.apply_device([(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)])
+        ver[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    srv.sync()
+    torch.cuda.synchronize()
+
+    srv.timing(True)
+    srv.timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    srv.sync()
+    kernels = {k: srv.timing_read(k) for k in ("decode_streams", "dense_index", "dense_verify",
+                                               "dense_apply", "finish_call")}
+    srv.timing(False)
+
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    stream_bytes = sum(s.numel() for s in streams)
+    step_bytes = stream_bytes + 2 * rows * cap * 4            # per GPU
+    total_bytes = step_bytes * args.steps * world
+    value = total_bytes / elapsed / 1e9
+
+    apply_ms, apply_n = kernels["dense_apply"]
+    apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
+    achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
+    traffic = None
+    if args.pmc_json and os.path.exists(args.pmc_json):
+        traffic = json.load(open(args.pmc_json)).get("dense_apply_hbm_bytes_per_launch")
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(args)
+        line = {
+            "metric": "row-update apply GB/s (device-resident), dense float rows",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (GPU-generated N(0,0.1) table, N(0,0.01) updates, random row order per batch)",
+            "config": {
+                "workload": f"C2: DenseRow<float> table {rows} rows x {cap} cols per GPU, "
+                            f"{B} worker batches (Appendix-A streams) applied per step",
+                "rows_per_gpu": rows, "cols": cap, "batches_per_step": B,
+                "algorithmic_bytes_per_step_per_gpu": step_bytes,
+                "parallelism": f"row-range shards x{world}, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "dense_apply",
+                "achieved": round(achieved, 2) if achieved else None,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic,
+                "avg_launch_ms": round(apply_avg_s * 1e3, 4),
+            },
+            "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    srv.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

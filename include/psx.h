@@ -1,0 +1,172 @@
+/*
+ * psx.h — C ABI of the MI355X row-update apply path (Bosen / petuum_ps server apply).
+ *
+ * This is the drop-in boundary for ONE hot path of the reference: the server-side
+ * apply of serialized worker increments (ClientSendOpLogMsg payloads) into dense and
+ * sparse parameter-table rows, plus serve-back of row bytes.  Every entry point is a
+ * plain C function over plain pointers and sizes; no torch or HIP C++ types appear in
+ * the signatures (a `void*` HIP stream handle is the only device-runtime object).
+ *
+ * Reference seams each entry point replaces (paths relative to the reference repo):
+ *   psx_ctx_create          Server::Init                 src/petuum_ps/server/server.cpp:18-31
+ *   psx_register_sender     bg_version_map_[bg] = -1     src/petuum_ps/server/server.cpp:21-24
+ *   psx_table_create        Server::CreateTable /        src/petuum_ps/server/server.cpp:33-44
+ *                           ServerTable::ServerTable     src/petuum_ps/server/server_table.cpp:19-93
+ *   psx_apply_stream        Server::ApplyOpLogUpdateVersion
+ *                                                        src/petuum_ps/server/server.hpp:46-48,
+ *                                                        src/petuum_ps/server/server.cpp:120-179
+ *   psx_apply_streams_device  the same, for K device-resident messages applied in order
+ *   psx_table_load_rows     AbstractRow::ResetRowData    src/petuum_ps_common/storage/numeric_store_row.hpp:142-145
+ *   psx_table_read_rows     VectorStore::CopyToMem       src/petuum_ps_common/storage/vector_store.hpp:115-118
+ *   psx_serialize_rows      ServerRow::Serialize         src/petuum_ps/server/server_row.hpp:65-71
+ *   psx_row_flags           ServerRow::IsDirty / FindRow src/petuum_ps/server/server_row.hpp:90-96,
+ *                                                        src/petuum_ps/server/server_table.cpp:136-141
+ *
+ * Error behaviour: the reference aborts via glog CHECK on a version gap
+ * (server.cpp:124-126) or an unknown table id (serialized_oplog_reader.hpp:112-120).
+ * Here every call returns a psx_status instead; a failed call applies nothing.
+ * Errors discovered by device kernels (malformed records, out-of-range rows) are
+ * reported by the next psx_sync() on the same context.
+ *
+ * Threading: one host thread per context (one context = one server shard = one
+ * reference ServerThread, server_thread.hpp:90).  Buffers are borrowed for the call
+ * (host buffers) or until the next psx_sync() (device buffers).
+ */
+#ifndef PSX_H_
+#define PSX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSX_ABI_VERSION 1
+
+/* Maximum number of messages fused into one psx_apply_streams_device call. */
+#define PSX_MAX_FUSED_STREAMS 16
+/* Maximum number of tables per context. */
+#define PSX_MAX_TABLES 64
+
+typedef enum psx_status {
+  PSX_OK = 0,
+  PSX_ERR_INVALID_ARG = 1,    /* null pointer, bad config, misaligned device stream */
+  PSX_ERR_VERSION = 2,        /* CHECK_EQ(bg_version+1, version) server.cpp:124 */
+  PSX_ERR_UNKNOWN_TABLE = 3,  /* CHECK(table_iter != end) serialized_oplog_reader.hpp:112 */
+  PSX_ERR_MALFORMED = 4,      /* stream shorter than its headers say, negative counts */
+  PSX_ERR_ROW_RANGE = 5,      /* row id not owned by this shard's row range */
+  PSX_ERR_CAPACITY = 6,       /* sparse row exceeded max_entries / column >= capacity */
+  PSX_ERR_DEVICE = 7,         /* HIP runtime error */
+  PSX_ERR_OOM = 8,            /* device allocation failed */
+  PSX_ERR_BUFFER_TOO_SMALL = 9,
+  PSX_ERR_UNSUPPORTED = 10,   /* e.g. the same table twice inside one message */
+  PSX_ERR_SENDER = 11,        /* bg id never registered (Server::Init bg_ids) */
+  PSX_ERR_NO_DEVICE = 12      /* no HIP device visible */
+} psx_status;
+
+/* Row storage kinds (TableInfo.row_type -> registered AbstractRow). */
+typedef enum psx_row_kind {
+  PSX_ROW_DENSE = 0,      /* DenseRow<V>          = NumericStoreRow<VectorStore,V>   dense_row.hpp:9-41 */
+  PSX_ROW_SORTED_MAP = 1, /* SortedVectorMapRow<V>= NumericStoreRow<SortedVectorMapStore,V> */
+  PSX_ROW_MAP = 2         /* SparseRow<V>         = NumericStoreRow<MapStore,V>      sparse_row.hpp */
+} psx_row_kind;
+
+typedef enum psx_dtype {
+  PSX_F32 = 0,
+  PSX_F64 = 1,
+  PSX_I32 = 2,
+  PSX_I64 = 3
+} psx_dtype;
+
+/* Mirrors the fields of TableInfo (configs.hpp:170-210) the apply path reads, plus
+ * the shard geometry that replaces ServerTable's boost::unordered_map<row_id,row>:
+ * row r is owned iff (r - row_offset) % row_stride == 0 and its slot
+ * (r - row_offset) / row_stride < max_rows.  row_stride = 1 gives a row-range shard;
+ * row_stride = num_comm_channels * num_clients reproduces the reference's modulo
+ * placement (context.hpp:291-304). */
+typedef struct psx_table_config {
+  int32_t table_id;
+  int32_t row_kind;                 /* psx_row_kind */
+  int32_t dtype;                    /* psx_dtype */
+  int32_t oplog_dense_serialized;   /* TableInfo.oplog_dense_serialized */
+  int64_t row_capacity;             /* TableInfo.row_capacity (dense width) */
+  int64_t dense_row_oplog_capacity; /* TableInfo.dense_row_oplog_capacity (dense record width) */
+  int64_t row_offset;
+  int64_t row_stride;
+  int64_t max_rows;
+  int64_t max_entries;              /* sorted/map rows: device slots per row */
+} psx_table_config;
+
+/* One device-resident ClientSendOpLogMsg payload (ps_msgs.hpp:1003-1055 after its
+ * 41-byte header): `data` points at the serialized stream, 4-byte aligned. */
+typedef struct psx_stream {
+  const void *data;
+  size_t size;        /* get_avai_size() */
+  int32_t bg_id;      /* sender bg thread id */
+  uint32_t version;   /* ClientSendOpLogMsg::get_version() */
+} psx_stream;
+
+typedef struct psx_ctx psx_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int32_t psx_abi_version(void);
+psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out);
+psx_status psx_ctx_destroy(psx_ctx *ctx);
+/* Use an external hipStream_t (e.g. the caller's compute stream); NULL restores the
+ * context's own stream. */
+psx_status psx_ctx_set_stream(psx_ctx *ctx, void *hip_stream);
+void *psx_ctx_get_stream(psx_ctx *ctx);
+psx_status psx_register_sender(psx_ctx *ctx, int32_t bg_id);
+/* Version last applied for a sender (-1 before its first message). */
+psx_status psx_sender_version(psx_ctx *ctx, int32_t bg_id, int64_t *version);
+
+/* ---- tables -------------------------------------------------------------- */
+psx_status psx_table_create(psx_ctx *ctx, const psx_table_config *cfg);
+/* Overwrite num_rows dense rows starting at row id first_row (row ids step by
+ * row_stride) with src (num_rows * row_capacity values); marks the rows present.
+ * src_on_device != 0 means src is device memory. */
+psx_status psx_table_load_rows(psx_ctx *ctx, int32_t table_id, int64_t first_row,
+                               int64_t num_rows, const void *src, int32_t src_on_device);
+/* Copy num_rows dense rows (same addressing) into dst; absent rows read as zero. */
+psx_status psx_table_read_rows(psx_ctx *ctx, int32_t table_id, int64_t first_row,
+                               int64_t num_rows, void *dst, int32_t dst_on_device);
+/* Per-row flags for num_rows rows: bit0 = row exists (created on first touch,
+ * server.cpp:163-166), bit1 = dirty since last psx_clear_dirty. */
+psx_status psx_row_flags(psx_ctx *ctx, int32_t table_id, int64_t first_row,
+                         int64_t num_rows, uint8_t *dst);
+psx_status psx_clear_dirty(psx_ctx *ctx, int32_t table_id);
+
+/* ---- apply (the hot path) -------------------------------------------------- */
+/* Server::ApplyOpLogUpdateVersion: host bytes, borrowed only for the call. */
+psx_status psx_apply_stream(psx_ctx *ctx, const void *oplog, size_t oplog_size,
+                            int32_t bg_id, uint32_t version);
+/* n device-resident messages, applied as if by n ApplyOpLogUpdateVersion calls in
+ * array order (per-row update order preserved => bit-exact float sums).  Asynchronous
+ * on the context stream; device buffers must stay valid until psx_sync(). */
+psx_status psx_apply_streams_device(psx_ctx *ctx, const psx_stream *streams, int32_t n);
+/* Wait for all queued work and report any device-detected error. */
+psx_status psx_sync(psx_ctx *ctx);
+
+/* ---- serve-back -------------------------------------------------------------- */
+/* Serialize rows exactly as ServerRow::Serialize (dense: V[capacity]; sorted map:
+ * Entry{int32,V}[n] in store order; map: {int32,V}[n]) framed as RecordBuff records
+ * {int32 row_id; size_t size; bytes} (record_buff.hpp:41-53).  Absent rows are
+ * skipped.  *used receives the bytes written. */
+psx_status psx_serialize_rows(psx_ctx *ctx, int32_t table_id, const int32_t *row_ids,
+                              int32_t n, void *out, size_t cap, size_t *used);
+
+/* ---- diagnostics ---------------------------------------------------------------- */
+const char *psx_last_error(psx_ctx *ctx);
+const char *psx_status_string(psx_status s);
+/* Per-kernel HIP-event timing on the context stream (off by default). */
+psx_status psx_timing_enable(psx_ctx *ctx, int32_t on);
+psx_status psx_timing_read(psx_ctx *ctx, const char *kernel, double *total_ms,
+                           int64_t *launches);
+psx_status psx_timing_reset(psx_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PSX_H_ */

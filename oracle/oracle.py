@@ -1,0 +1,199 @@
+"""ctypes wrapper over oracle/psx_oracle.c — TEST INFRASTRUCTURE ONLY.
+
+This is the parity checker.  It restates Server::ApplyOpLogUpdateVersion
+(src/petuum_ps/server/server.cpp:120-179) and the row stores on the CPU.  Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libpsx_oracle.so")
+_lib = None
+
+DENSE, SORTED_MAP, MAP = 0, 1, 2
+F32, F64, I32, I64 = 0, 1, 2, 3
+NP_DTYPE = {F32: np.float32, F64: np.float64, I32: np.int32, I64: np.int64}
+
+ST_OK = 0
+
+
+def build():
+    """Compile the oracle with gcc (make)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(_HERE, "psx_oracle.c")
+        if (not os.path.exists(_LIB_PATH)
+                or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+        L.orc_server_create.restype = vp
+        L.orc_server_destroy.argtypes = [vp]
+        L.orc_register_sender.argtypes = [vp, i32]
+        L.orc_table_create.argtypes = [vp, i32, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64, i64]
+        L.orc_apply_stream.argtypes = [vp, vp, sz, i32, ctypes.c_uint32]
+        L.orc_sender_version.argtypes = [vp, i32]
+        L.orc_sender_version.restype = i64
+        L.orc_row_exists.argtypes = [vp, i32, i32]
+        L.orc_row_dirty.argtypes = [vp, i32, i32]
+        L.orc_num_rows.argtypes = [vp, i32]
+        L.orc_num_rows.restype = i64
+        L.orc_load_dense_rows.argtypes = [vp, i32, i64, i64, i64, vp]
+        L.orc_read_dense_rows.argtypes = [vp, i32, i64, i64, i64, vp]
+        L.orc_serialize_row.argtypes = [vp, i32, i32, vp, sz]
+        L.orc_serialize_row.restype = i64
+        L.orc_serialize_records.argtypes = [vp, i32, vp, i32, vp, sz]
+        L.orc_serialize_records.restype = i64
+        L.orc_get.argtypes = [vp, i32, i32, i32, vp]
+        L.orc_row_inc.argtypes = [vp, i32, i32, i32, vp]
+        L.orc_pack_stream.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, sz]
+        L.orc_pack_stream.restype = sz
+        L.orc_partition_server.argtypes = [i32, i32, i32, i32]
+        L.orc_partition_server.restype = i32
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class OracleServer:
+    """Mirror of petuum::Server (server.hpp) restricted to the apply path."""
+
+    def __init__(self, bg_ids=()):
+        self._L = lib()
+        self._s = self._L.orc_server_create()
+        self.tables = {}
+        for bg in bg_ids:
+            self.register_sender(bg)
+
+    def close(self):
+        if self._s:
+            self._L.orc_server_destroy(self._s)
+            self._s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def register_sender(self, bg):
+        assert self._L.orc_register_sender(self._s, bg) == ST_OK
+
+    def create_table(self, table_id, kind, dtype, row_capacity, oplog_dense_serialized=True,
+                     dense_row_oplog_capacity=None):
+        cap = row_capacity if dense_row_oplog_capacity is None else dense_row_oplog_capacity
+        st = self._L.orc_table_create(self._s, table_id, kind, dtype,
+                                      1 if oplog_dense_serialized else 0, row_capacity, cap)
+        assert st == ST_OK, st
+        self.tables[table_id] = (kind, dtype, row_capacity)
+
+    def apply_stream(self, data, bg, version):
+        """Server::ApplyOpLogUpdateVersion; returns the status code."""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        buf = np.ascontiguousarray(buf)
+        return self._L.orc_apply_stream(self._s, _ptr(buf) if buf.size else None,
+                                        buf.size, bg, version)
+
+    def sender_version(self, bg):
+        return self._L.orc_sender_version(self._s, bg)
+
+    def row_exists(self, table_id, row_id):
+        return bool(self._L.orc_row_exists(self._s, table_id, row_id))
+
+    def row_dirty(self, table_id, row_id):
+        return bool(self._L.orc_row_dirty(self._s, table_id, row_id))
+
+    def num_rows(self, table_id):
+        return self._L.orc_num_rows(self._s, table_id)
+
+    def load_dense_rows(self, table_id, first_row, rows, stride=1):
+        kind, dt, cap = self.tables[table_id]
+        a = np.ascontiguousarray(rows, dtype=NP_DTYPE[dt]).reshape(-1, cap)
+        assert self._L.orc_load_dense_rows(self._s, table_id, first_row, stride, a.shape[0], _ptr(a)) == 0
+
+    def read_dense_rows(self, table_id, first_row, n, stride=1):
+        kind, dt, cap = self.tables[table_id]
+        out = np.zeros((n, cap), dtype=NP_DTYPE[dt])
+        assert self._L.orc_read_dense_rows(self._s, table_id, first_row, stride, n, _ptr(out)) == 0
+        return out
+
+    def serialize_row(self, table_id, row_id):
+        kind, dt, cap = self.tables[table_id]
+        nb = max(64, cap * 16)
+        while True:
+            out = np.zeros(nb, dtype=np.uint8)
+            r = self._L.orc_serialize_row(self._s, table_id, row_id, _ptr(out), nb)
+            if r == -2:
+                nb *= 4
+                continue
+            return None if r == -1 else out[:r].tobytes()
+
+    def serialize_records(self, table_id, row_ids):
+        ids = np.ascontiguousarray(row_ids, dtype=np.int32)
+        nb = 1 << 16
+        while True:
+            out = np.zeros(nb, dtype=np.uint8)
+            r = self._L.orc_serialize_records(self._s, table_id, _ptr(ids), ids.size, _ptr(out), nb)
+            if r == -2:
+                nb *= 4
+                continue
+            assert r >= 0, r
+            return out[:r].tobytes()
+
+    def get(self, table_id, row_id, col):
+        kind, dt, cap = self.tables[table_id]
+        out = np.zeros(1, dtype=NP_DTYPE[dt])
+        assert self._L.orc_get(self._s, table_id, row_id, col, _ptr(out)) == 0
+        return out[0]
+
+    def row_inc(self, table_id, row_id, col, delta):
+        kind, dt, cap = self.tables[table_id]
+        d = np.array([delta], dtype=NP_DTYPE[dt])
+        assert self._L.orc_row_inc(self._s, table_id, row_id, col, _ptr(d)) == 0
+
+
+def pack_stream(tables):
+    """Build one ClientSendOpLogMsg payload with the reference packer's layout.
+
+    tables: list of dicts {table_id, dtype, dense_serialized, row_ids (int32[n]),
+    oplogs (V[n, capacity])} — restates RowOpLogSerializer/OpLogSerializer
+    (row_oplog_serializer.hpp:139-166, oplog_serializer.hpp:12-37).
+    """
+    L = lib()
+    n = len(tables)
+    tid = np.array([t["table_id"] for t in tables], dtype=np.int32)
+    dts = np.array([t["dtype"] for t in tables], dtype=np.int32)
+    ds = np.array([1 if t["dense_serialized"] else 0 for t in tables], dtype=np.int32)
+    ops = [np.ascontiguousarray(t["oplogs"], dtype=NP_DTYPE[t["dtype"]]) for t in tables]
+    caps = np.array([o.shape[1] if o.ndim == 2 else 0 for o in ops], dtype=np.int64)
+    rids = [np.ascontiguousarray(t["row_ids"], dtype=np.int32) for t in tables]
+    nrows = np.array([r.size for r in rids], dtype=np.int64)
+    rid_ptrs = (ctypes.c_void_p * max(n, 1))(*[r.ctypes.data for r in rids])
+    op_ptrs = (ctypes.c_void_p * max(n, 1))(*[o.ctypes.data for o in ops])
+    total = L.orc_pack_stream(n, _ptr(tid), _ptr(dts), _ptr(ds), _ptr(caps), _ptr(nrows),
+                              ctypes.cast(rid_ptrs, ctypes.c_void_p),
+                              ctypes.cast(op_ptrs, ctypes.c_void_p), None, 0)
+    assert total != ctypes.c_size_t(-1).value
+    if total == 0:
+        return b""
+    out = np.zeros(total, dtype=np.uint8)
+    w = L.orc_pack_stream(n, _ptr(tid), _ptr(dts), _ptr(ds), _ptr(caps), _ptr(nrows),
+                          ctypes.cast(rid_ptrs, ctypes.c_void_p),
+                          ctypes.cast(op_ptrs, ctypes.c_void_p), _ptr(out), total)
+    assert w == total
+    return out.tobytes()
+
+
+def partition_server(row_id, num_channels, num_clients, channel):
+    return lib().orc_partition_server(row_id, num_channels, num_clients, channel)

@@ -1,0 +1,701 @@
+/*
+ * psx_oracle.c — CPU restatement of the Bosen (petuum_ps) row-update apply path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP path in
+ * parameter_server_amd/.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product path never links or calls it.
+ *
+ * Pinning: the reference cannot be compiled in this image (its row/store headers
+ * include glog/logging.h and boost headers, neither installed, and stand-in headers are
+ * not allowed), so this restatement is pinned by the reference's own known-answer
+ * tests, transcribed as fixtures in tests/golden/reference_kats.json:
+ *   tests/petuum_ps/storage/store_test.cpp:42-49   (VectorInc)
+ *   tests/petuum_ps/storage/store_test.cpp:80-92   (SIncGet)
+ *   tests/petuum_ps/storage/store_test.cpp:94-116  (SShrink)
+ *   apps/lda/src/row_test.cpp:11-46                (SortedVectorMapRow inc + serialize)
+ * The wire-format walk (SerializedOpLogReader) is restated from the code and has no
+ * reference test of its own: "parity unpinned" for the stream framing itself.
+ *
+ * Every function cites the reference file:line it restates (paths relative to the
+ * reference repo root).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_OK 0
+#define ORC_ERR_INVALID_ARG 1
+#define ORC_ERR_VERSION 2
+#define ORC_ERR_UNKNOWN_TABLE 3
+#define ORC_ERR_MALFORMED 4
+#define ORC_ERR_CAPACITY 6
+#define ORC_ERR_UNSUPPORTED 10
+#define ORC_ERR_SENDER 11
+
+enum { KIND_DENSE = 0, KIND_SORTED_MAP = 1, KIND_MAP = 2 };
+enum { DT_F32 = 0, DT_F64 = 1, DT_I32 = 2, DT_I64 = 3 };
+
+static size_t dt_size(int dt) { return (dt == DT_F32 || dt == DT_I32) ? 4 : 8; }
+
+/* ------------------------------------------------------------------------ */
+/* Scalar helpers: V += d and V == 0 for the four value types.  Integer adds wrap
+ * (two's complement), which is what the reference's int32/int64 += does on every
+ * platform it builds for. */
+typedef union { float f; double d; int32_t i; int64_t l; uint64_t raw; } val_t;
+
+static val_t v_load(const void *p, int dt) {
+  val_t v; v.raw = 0;
+  memcpy(&v, p, dt_size(dt));
+  return v;
+}
+static void v_store(void *p, val_t v, int dt) { memcpy(p, &v, dt_size(dt)); }
+static val_t v_add(val_t a, val_t b, int dt) {
+  val_t r; r.raw = 0;
+  switch (dt) {
+    case DT_F32: r.f = a.f + b.f; break;
+    case DT_F64: r.d = a.d + b.d; break;
+    case DT_I32: r.i = (int32_t)((uint32_t)a.i + (uint32_t)b.i); break;
+    default: r.l = (int64_t)((uint64_t)a.l + (uint64_t)b.l); break;
+  }
+  return r;
+}
+static int v_is_zero(val_t a, int dt) {
+  switch (dt) {
+    case DT_F32: return a.f == 0.0f;
+    case DT_F64: return a.d == 0.0;
+    case DT_I32: return a.i == 0;
+    default: return a.l == 0;
+  }
+}
+/* a < b and a > b as in SortedVectorMapStore::LinearSearchAndMove
+ * (sorted_vector_map_store.hpp:241-286). */
+static int v_lt(val_t a, val_t b, int dt) {
+  switch (dt) {
+    case DT_F32: return a.f < b.f;
+    case DT_F64: return a.d < b.d;
+    case DT_I32: return a.i < b.i;
+    default: return a.l < b.l;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Open-addressing int32 -> int64 map; stands in for boost::unordered_map<int32,
+ * ServerRow*> (server_table.hpp:158) and std::unordered_map<int32,V> (map_store.hpp:45). */
+typedef struct {
+  int32_t *keys;
+  int64_t *vals;
+  uint8_t *used;   /* 0 empty, 1 used, 2 tombstone */
+  int64_t cap;
+  int64_t count;
+  int64_t tombs;
+} imap_t;
+
+static uint64_t hash32(int32_t k) {
+  uint64_t x = (uint32_t)k;
+  x ^= x >> 16; x *= 0x7feb352dULL; x ^= x >> 15; x *= 0x846ca68bULL; x ^= x >> 16;
+  return x;
+}
+static int imap_init(imap_t *m, int64_t cap) {
+  int64_t c = 16;
+  while (c < cap * 2) c <<= 1;
+  m->keys = (int32_t *)calloc((size_t)c, sizeof(int32_t));
+  m->vals = (int64_t *)calloc((size_t)c, sizeof(int64_t));
+  m->used = (uint8_t *)calloc((size_t)c, 1);
+  m->cap = c; m->count = 0; m->tombs = 0;
+  return (m->keys && m->vals && m->used) ? 0 : -1;
+}
+static void imap_free(imap_t *m) { free(m->keys); free(m->vals); free(m->used); memset(m, 0, sizeof(*m)); }
+static int64_t imap_find(const imap_t *m, int32_t k) {
+  if (m->cap == 0) return -1;
+  uint64_t i = hash32(k) & (uint64_t)(m->cap - 1);
+  for (;;) {
+    if (m->used[i] == 0) return -1;
+    if (m->used[i] == 1 && m->keys[i] == k) return (int64_t)i;
+    i = (i + 1) & (uint64_t)(m->cap - 1);
+  }
+}
+static int imap_grow(imap_t *m);
+static int64_t imap_insert(imap_t *m, int32_t k, int64_t v) {
+  int64_t f = imap_find(m, k);
+  if (f >= 0) { m->vals[f] = v; return f; }
+  if ((m->count + m->tombs + 1) * 2 > m->cap) { if (imap_grow(m)) return -1; }
+  uint64_t i = hash32(k) & (uint64_t)(m->cap - 1);
+  while (m->used[i] == 1) i = (i + 1) & (uint64_t)(m->cap - 1);
+  if (m->used[i] == 2) m->tombs--;
+  m->used[i] = 1; m->keys[i] = k; m->vals[i] = v; m->count++;
+  return (int64_t)i;
+}
+static int imap_grow(imap_t *m) {
+  imap_t n;
+  if (imap_init(&n, (m->count + 1) * 2)) return -1;
+  for (int64_t i = 0; i < m->cap; ++i)
+    if (m->used[i] == 1) imap_insert(&n, m->keys[i], m->vals[i]);
+  imap_free(m);
+  *m = n;
+  return 0;
+}
+static void imap_erase_at(imap_t *m, int64_t slot) { m->used[slot] = 2; m->count--; m->tombs++; }
+
+/* ------------------------------------------------------------------------ */
+/* Rows. */
+typedef struct {
+  /* dense: VectorStore<V> (vector_store.hpp:64-102), zeroed at Init */
+  uint8_t *dense;
+  /* sorted map: SortedVectorMapStore<V> (sorted_vector_map_store.hpp) */
+  uint8_t *entries;      /* Entry<V>{int32 first; V second} packed per the C++ layout */
+  int64_t num_entries;
+  int64_t capacity;
+  /* map: MapStore<V> (map_store.hpp:45) col -> index into vals */
+  imap_t map;
+  int dirty;             /* ServerRow::dirty_ (server_row.hpp:133) */
+} orc_row;
+
+typedef struct {
+  int32_t table_id;
+  int kind, dt;
+  int dense_serialized;
+  int64_t row_capacity;
+  int64_t oplog_capacity;
+  imap_t index;          /* row_id -> row number */
+  orc_row **rows;
+  int64_t nrows, rows_cap;
+} orc_table;
+
+typedef struct {
+  orc_table *tables[64];
+  int ntables;
+  int32_t bg_ids[1024];
+  int64_t bg_versions[1024];
+  int nbg;
+} orc_server;
+
+/* sizeof(Entry<V>) with natural alignment: {int32, int32} = 8, {int32, 8B} = 16. */
+static size_t entry_size(int dt) { return dt_size(dt) == 4 ? 8 : 16; }
+static size_t entry_val_off(int dt) { return dt_size(dt) == 4 ? 4 : 8; }
+
+orc_server *orc_server_create(void) { return (orc_server *)calloc(1, sizeof(orc_server)); }
+
+static void row_free(orc_table *t, orc_row *r) {
+  free(r->dense); free(r->entries);
+  if (t->kind == KIND_MAP) imap_free(&r->map);
+  free(r);
+}
+
+void orc_server_destroy(orc_server *s) {
+  if (!s) return;
+  for (int i = 0; i < s->ntables; ++i) {
+    orc_table *t = s->tables[i];
+    for (int64_t r = 0; r < t->nrows; ++r) row_free(t, t->rows[r]);
+    free(t->rows); imap_free(&t->index); free(t);
+  }
+  free(s);
+}
+
+/* Server::Init: bg_version_map_[bg] = -1 (server.cpp:21-24). */
+int orc_register_sender(orc_server *s, int32_t bg) {
+  for (int i = 0; i < s->nbg; ++i) if (s->bg_ids[i] == bg) return ORC_OK;
+  if (s->nbg >= 1024) return ORC_ERR_INVALID_ARG;
+  s->bg_ids[s->nbg] = bg; s->bg_versions[s->nbg] = -1; s->nbg++;
+  return ORC_OK;
+}
+
+static orc_table *find_table(orc_server *s, int32_t table_id) {
+  for (int i = 0; i < s->ntables; ++i) if (s->tables[i]->table_id == table_id) return s->tables[i];
+  return NULL;
+}
+
+/* Server::CreateTable / ServerTable::ServerTable (server.cpp:33-44,
+ * server_table.cpp:19-93). */
+int orc_table_create(orc_server *s, int32_t table_id, int kind, int dt, int dense_serialized,
+                     int64_t row_capacity, int64_t oplog_capacity) {
+  if (s->ntables >= 64 || find_table(s, table_id)) return ORC_ERR_INVALID_ARG;
+  if (kind < 0 || kind > 2 || dt < 0 || dt > 3) return ORC_ERR_INVALID_ARG;
+  if (dense_serialized && (oplog_capacity <= 0)) return ORC_ERR_INVALID_ARG;
+  if (kind == KIND_DENSE && dense_serialized && oplog_capacity > row_capacity) return ORC_ERR_INVALID_ARG;
+  orc_table *t = (orc_table *)calloc(1, sizeof(orc_table));
+  t->table_id = table_id; t->kind = kind; t->dt = dt; t->dense_serialized = dense_serialized;
+  t->row_capacity = row_capacity; t->oplog_capacity = oplog_capacity;
+  imap_init(&t->index, 1024);
+  s->tables[s->ntables++] = t;
+  return ORC_OK;
+}
+
+/* ServerTable::CreateRow -> AbstractRow::Init(row_capacity) (server_table.cpp:143-162). */
+static orc_row *create_row(orc_table *t, int32_t row_id) {
+  orc_row *r = (orc_row *)calloc(1, sizeof(orc_row));
+  if (t->kind == KIND_DENSE) {
+    r->dense = (uint8_t *)calloc((size_t)(t->row_capacity ? t->row_capacity : 1), dt_size(t->dt));
+  } else if (t->kind == KIND_SORTED_MAP) {
+    /* SortedVectorMapStore::Init(capacity) (sorted_vector_map_store.hpp:131-135) */
+    r->capacity = t->row_capacity;
+    r->entries = (uint8_t *)malloc((size_t)(r->capacity ? r->capacity : 1) * entry_size(t->dt));
+  } else {
+    imap_init(&r->map, 16);
+  }
+  if (t->nrows == t->rows_cap) {
+    t->rows_cap = t->rows_cap ? t->rows_cap * 2 : 1024;
+    t->rows = (orc_row **)realloc(t->rows, (size_t)t->rows_cap * sizeof(orc_row *));
+  }
+  t->rows[t->nrows] = r;
+  imap_insert(&t->index, row_id, t->nrows);
+  t->nrows++;
+  return r;
+}
+
+static orc_row *find_row(orc_table *t, int32_t row_id) {
+  int64_t slot = imap_find(&t->index, row_id);
+  return slot < 0 ? NULL : t->rows[t->index.vals[slot]];
+}
+
+/* ---- SortedVectorMapStore<V> (sorted_vector_map_store.hpp) --------------- */
+#define ENT_KEY(r, i, es) (*(int32_t *)((r)->entries + (size_t)(i) * (es)))
+#define ENT_VALP(r, i, es, vo) ((r)->entries + (size_t)(i) * (es) + (vo))
+
+/* FindIndex (:230-238) */
+static int64_t svm_find(const orc_row *r, int32_t key, size_t es) {
+  for (int64_t i = 0; i < r->num_entries; ++i) if (ENT_KEY(r, i, es) == key) return i;
+  return -1;
+}
+
+/* LinearSearchAndMove(vector_idx, forward=false) (:264-285): bubble backward while
+ * the new value is strictly greater than its predecessor. */
+static void svm_move_backward(orc_row *r, int64_t idx, int dt) {
+  size_t es = entry_size(dt), vo = entry_val_off(dt);
+  val_t val = v_load(ENT_VALP(r, idx, es, vo), dt);
+  int64_t new_idx = idx;
+  for (int64_t i = idx - 1; i >= 0; --i) {
+    if (v_lt(v_load(ENT_VALP(r, i, es, vo), dt), val, dt)) new_idx = i;
+    else break;
+  }
+  if (new_idx < idx) {
+    uint8_t tmp[16];
+    memcpy(tmp, r->entries + (size_t)idx * es, es);
+    memmove(r->entries + (size_t)(new_idx + 1) * es, r->entries + (size_t)new_idx * es,
+            (size_t)(idx - new_idx) * es);
+    memcpy(r->entries + (size_t)new_idx * es, tmp, es);
+  }
+}
+
+/* Inc(key, delta) (:175-197) over the private Inc (:305-337).  Capacity growth
+ * (+kBlockSize=64) and compaction (:288-301) only change allocation, never the
+ * observable entry order, so they are restated as plain reallocation. */
+static void svm_inc(orc_row *r, int32_t key, val_t delta, int dt) {
+  size_t es = entry_size(dt), vo = entry_val_off(dt);
+  if (v_is_zero(delta, dt)) return;                      /* :306 */
+  int64_t idx = svm_find(r, key, es);
+  if (idx == -1) {                                       /* :309-322 insert */
+    if (r->num_entries == r->capacity) {
+      r->capacity += 64;
+      r->entries = (uint8_t *)realloc(r->entries, (size_t)r->capacity * es);
+    }
+    idx = r->num_entries++;
+    memset(r->entries + (size_t)idx * es, 0, es);
+    ENT_KEY(r, idx, es) = key;
+    v_store(ENT_VALP(r, idx, es, vo), delta, dt);
+    svm_move_backward(r, idx, dt);
+    return;
+  }
+  /* :325-334 found: add in place (NO re-sort), remove on reaching zero */
+  val_t nv = v_add(v_load(ENT_VALP(r, idx, es, vo), dt), delta, dt);
+  v_store(ENT_VALP(r, idx, es, vo), nv, dt);
+  if (v_is_zero(nv, dt)) {
+    memmove(r->entries + (size_t)idx * es, r->entries + (size_t)(idx + 1) * es,
+            (size_t)(r->num_entries - idx - 1) * es);      /* RemoveOneEntryAndCompact :288-291 */
+    r->num_entries--;
+  }
+}
+
+/* ---- MapStore<V>::Inc (map_store.hpp:60-65) -------------------------------- */
+static void map_inc(orc_row *r, int32_t col, val_t delta, int dt) {
+  int64_t slot = imap_find(&r->map, col);
+  if (slot < 0) slot = imap_insert(&r->map, col, 0);   /* data_[col_id] default-inserts 0 */
+  val_t cur; cur.raw = (uint64_t)r->map.vals[slot];    /* value bits live in the map slot */
+  val_t nv = v_add(cur, delta, dt);
+  if (dt_size(dt) == 4) nv.raw &= 0xffffffffULL;
+  r->map.vals[slot] = (int64_t)nv.raw;
+  if (v_is_zero(nv, dt)) imap_erase_at(&r->map, slot);
+}
+
+/* NumericStoreRow::ApplyBatchIncUnsafe (numeric_store_row.hpp:166-175) for one sparse
+ * record, dispatched on the store type. */
+static void apply_sparse_record(orc_table *t, orc_row *r, const int32_t *cols,
+                                const uint8_t *vals, int32_t n) {
+  size_t vs = dt_size(t->dt);
+  for (int32_t i = 0; i < n; ++i) {
+    val_t d = v_load(vals + (size_t)i * vs, t->dt);
+    if (t->kind == KIND_DENSE) {
+      /* VectorStore::Inc (vector_store.hpp:100-102) */
+      uint8_t *p = r->dense + (size_t)cols[i] * vs;
+      v_store(p, v_add(v_load(p, t->dt), d, t->dt), t->dt);
+    } else if (t->kind == KIND_SORTED_MAP) {
+      svm_inc(r, cols[i], d, t->dt);
+    } else {
+      map_inc(r, cols[i], d, t->dt);
+    }
+  }
+}
+
+/* NumericStoreRow::ApplyDenseBatchIncUnsafe (numeric_store_row.hpp:177-185):
+ * val[i] += upd[i] for i < num_updates (= dense_row_oplog_capacity). For non-dense
+ * stores the reference's GetPtr does not exist; a dense record is applied element
+ * by element through Inc (the per-column meaning of a dense oplog). */
+static void apply_dense_record(orc_table *t, orc_row *r, const uint8_t *upd, int64_t n) {
+  size_t vs = dt_size(t->dt);
+  if (t->kind == KIND_DENSE) {
+    for (int64_t i = 0; i < n; ++i) {
+      uint8_t *p = r->dense + (size_t)i * vs;
+      v_store(p, v_add(v_load(p, t->dt), v_load(upd + (size_t)i * vs, t->dt), t->dt), t->dt);
+    }
+  } else {
+    for (int64_t i = 0; i < n; ++i) {
+      val_t d = v_load(upd + (size_t)i * vs, t->dt);
+      if (t->kind == KIND_SORTED_MAP) svm_inc(r, (int32_t)i, d, t->dt);
+      else map_inc(r, (int32_t)i, d, t->dt);
+    }
+  }
+}
+
+static int32_t rd32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
+static uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+
+/* Walk the stream exactly as SerializedOpLogReader::Restart/Next/StartNewTable
+ * (serialized_oplog_reader.hpp:30-133) with AbstractRowOpLog::ParseSparseSerializedOpLog
+ * (abstract_row_oplog.hpp:64-78) / DenseRowOpLog::ParseDenseSerializedOpLog
+ * (dense_row_oplog.hpp:138-144).  apply=0 only validates; apply=1 applies each record
+ * through ServerTable::ApplyRowOpLog (server_table.cpp:164-189), creating missing rows
+ * first (server.cpp:163-166). */
+static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) {
+  if (size < 4) return ORC_ERR_MALFORMED;
+  int32_t num_tables = rd32(b);
+  size_t off = 4;
+  if (num_tables < 0) return ORC_ERR_MALFORMED;
+  int32_t seen[64]; int nseen = 0;
+  for (int32_t tt = 0; tt < num_tables; ++tt) {
+    if (off + 16 > size) return ORC_ERR_MALFORMED;
+    int32_t table_id = rd32(b + off);
+    uint64_t update_size = rd64(b + off + 4);
+    int32_t num_rows = rd32(b + off + 12);
+    off += 16;
+    orc_table *t = find_table(s, table_id);
+    if (!t) return ORC_ERR_UNKNOWN_TABLE;
+    if (update_size != dt_size(t->dt) || num_rows < 0) return ORC_ERR_MALFORMED;
+    for (int i = 0; i < nseen; ++i) if (seen[i] == table_id) return ORC_ERR_UNSUPPORTED;
+    if (nseen < 64) seen[nseen++] = table_id;
+    size_t vs = dt_size(t->dt);
+    for (int32_t k = 0; k < num_rows; ++k) {
+      if (off + 4 > size) return ORC_ERR_MALFORMED;
+      int32_t row_id = rd32(b + off);
+      off += 4;
+      if (t->dense_serialized) {
+        size_t rs = (size_t)t->oplog_capacity * vs;
+        if (off + rs > size) return ORC_ERR_MALFORMED;
+        if (apply) {
+          orc_row *r = find_row(t, row_id);
+          if (!r) r = create_row(t, row_id);
+          apply_dense_record(t, r, b + off, t->oplog_capacity);
+          r->dirty = 1;
+        }
+        off += rs;
+      } else {
+        if (off + 4 > size) return ORC_ERR_MALFORMED;
+        int32_t n = rd32(b + off);
+        if (n < 0) return ORC_ERR_MALFORMED;
+        size_t rs = 4 + (size_t)n * (4 + vs);
+        if (off + rs > size) return ORC_ERR_MALFORMED;
+        const int32_t *cols = (const int32_t *)(b + off + 4);
+        if (!apply && t->kind == KIND_DENSE) {
+          for (int32_t i = 0; i < n; ++i) {
+            int32_t c; memcpy(&c, b + off + 4 + (size_t)i * 4, 4);
+            if (c < 0 || c >= t->row_capacity) return ORC_ERR_CAPACITY;
+          }
+        }
+        if (apply) {
+          orc_row *r = find_row(t, row_id);
+          if (!r) r = create_row(t, row_id);
+          /* cols may be unaligned in a host buffer: copy out */
+          int32_t *cc = (int32_t *)malloc((size_t)(n ? n : 1) * 4);
+          memcpy(cc, cols, (size_t)n * 4);
+          apply_sparse_record(t, r, cc, b + off + 4 + (size_t)n * 4, n);
+          free(cc);
+          r->dirty = 1;
+        }
+        off += rs;
+      }
+    }
+  }
+  return ORC_OK;
+}
+
+/* Server::ApplyOpLogUpdateVersion (server.cpp:120-179). */
+int orc_apply_stream(orc_server *s, const void *oplog, size_t size, int32_t bg, uint32_t version) {
+  int bi = -1;
+  for (int i = 0; i < s->nbg; ++i) if (s->bg_ids[i] == bg) bi = i;
+  if (bi < 0) return ORC_ERR_SENDER;
+  if (s->bg_versions[bi] + 1 != (int64_t)version) return ORC_ERR_VERSION;   /* :124-126 */
+  if (size == 0) { s->bg_versions[bi] = version; return ORC_OK; }          /* :128 */
+  const uint8_t *b = (const uint8_t *)oplog;
+  if (size >= 4 && rd32(b) == 0) { s->bg_versions[bi] = version; return ORC_OK; } /* Restart() false */
+  int st = walk_stream(s, b, size, 0);
+  if (st != ORC_OK) return st;
+  s->bg_versions[bi] = version;
+  return walk_stream(s, b, size, 1);
+}
+
+int64_t orc_sender_version(orc_server *s, int32_t bg) {
+  for (int i = 0; i < s->nbg; ++i) if (s->bg_ids[i] == bg) return s->bg_versions[i];
+  return -2;
+}
+
+/* ---- row access ------------------------------------------------------------ */
+int orc_row_exists(orc_server *s, int32_t table_id, int32_t row_id) {
+  orc_table *t = find_table(s, table_id);
+  return (t && find_row(t, row_id)) ? 1 : 0;
+}
+int orc_row_dirty(orc_server *s, int32_t table_id, int32_t row_id) {
+  orc_table *t = find_table(s, table_id);
+  orc_row *r = t ? find_row(t, row_id) : NULL;
+  return r ? r->dirty : 0;
+}
+int64_t orc_num_rows(orc_server *s, int32_t table_id) {
+  orc_table *t = find_table(s, table_id);
+  return t ? t->nrows : -1;
+}
+
+/* AbstractRow::ResetRowData (numeric_store_row.hpp:142-145 -> VectorStore::ResetData
+ * vector_store.hpp:89-92) for a dense row, creating it if absent. */
+int orc_load_dense_row(orc_server *s, int32_t table_id, int32_t row_id, const void *src) {
+  orc_table *t = find_table(s, table_id);
+  if (!t || t->kind != KIND_DENSE) return ORC_ERR_INVALID_ARG;
+  orc_row *r = find_row(t, row_id);
+  if (!r) r = create_row(t, row_id);
+  memcpy(r->dense, src, (size_t)t->row_capacity * dt_size(t->dt));
+  return ORC_OK;
+}
+
+/* Bulk variant: rows first_row, first_row+stride, ... */
+int orc_load_dense_rows(orc_server *s, int32_t table_id, int64_t first_row, int64_t stride,
+                        int64_t n, const void *src) {
+  orc_table *t = find_table(s, table_id);
+  if (!t || t->kind != KIND_DENSE) return ORC_ERR_INVALID_ARG;
+  size_t rb = (size_t)t->row_capacity * dt_size(t->dt);
+  for (int64_t i = 0; i < n; ++i) {
+    int st = orc_load_dense_row(s, table_id, (int32_t)(first_row + i * stride),
+                                (const uint8_t *)src + (size_t)i * rb);
+    if (st) return st;
+  }
+  return ORC_OK;
+}
+
+/* VectorStore::CopyToMem (vector_store.hpp:115-118); absent rows read as zero. */
+int orc_read_dense_rows(orc_server *s, int32_t table_id, int64_t first_row, int64_t stride,
+                        int64_t n, void *dst) {
+  orc_table *t = find_table(s, table_id);
+  if (!t || t->kind != KIND_DENSE) return ORC_ERR_INVALID_ARG;
+  size_t rb = (size_t)t->row_capacity * dt_size(t->dt);
+  for (int64_t i = 0; i < n; ++i) {
+    orc_row *r = find_row(t, (int32_t)(first_row + i * stride));
+    uint8_t *d = (uint8_t *)dst + (size_t)i * rb;
+    if (r) memcpy(d, r->dense, rb); else memset(d, 0, rb);
+  }
+  return ORC_OK;
+}
+
+/* ServerRow::Serialize -> store Serialize: VectorStore (vector_store.hpp:75-80),
+ * SortedVectorMapStore (:148-152, entries in store order), MapStore (map_store.hpp:89-100;
+ * the reference emits unordered_map order, this oracle emits ascending column order —
+ * parity for MapStore rows is defined on the {col -> value} map).
+ * Returns the byte count, or -1 if the row is absent, or -2 if cap is too small. */
+int64_t orc_serialize_row(orc_server *s, int32_t table_id, int32_t row_id, void *out, size_t cap) {
+  orc_table *t = find_table(s, table_id);
+  orc_row *r = t ? find_row(t, row_id) : NULL;
+  if (!r) return -1;
+  size_t vs = dt_size(t->dt);
+  if (t->kind == KIND_DENSE) {
+    size_t nb = (size_t)t->row_capacity * vs;
+    if (nb > cap) return -2;
+    memcpy(out, r->dense, nb);
+    return (int64_t)nb;
+  }
+  if (t->kind == KIND_SORTED_MAP) {
+    size_t es = entry_size(t->dt);
+    size_t nb = (size_t)r->num_entries * es;
+    if (nb > cap) return -2;
+    memcpy(out, r->entries, nb);
+    return (int64_t)nb;
+  }
+  size_t rec = 4 + vs;
+  size_t nb = (size_t)r->map.count * rec;
+  if (nb > cap) return -2;
+  /* collect and sort by column */
+  int64_t n = 0;
+  int32_t *cols = (int32_t *)malloc((size_t)(r->map.count + 1) * 4);
+  uint64_t *vals = (uint64_t *)malloc((size_t)(r->map.count + 1) * 8);
+  for (int64_t i = 0; i < r->map.cap; ++i)
+    if (r->map.used[i] == 1) { cols[n] = r->map.keys[i]; vals[n] = (uint64_t)r->map.vals[i]; n++; }
+  for (int64_t i = 1; i < n; ++i) {          /* insertion sort: rows are small */
+    int32_t c = cols[i]; uint64_t v = vals[i]; int64_t j = i - 1;
+    while (j >= 0 && cols[j] > c) { cols[j + 1] = cols[j]; vals[j + 1] = vals[j]; --j; }
+    cols[j + 1] = c; vals[j + 1] = v;
+  }
+  uint8_t *o = (uint8_t *)out;
+  for (int64_t i = 0; i < n; ++i) {
+    memcpy(o, &cols[i], 4);
+    memcpy(o + 4, &vals[i], vs);
+    o += rec;
+  }
+  free(cols); free(vals);
+  return (int64_t)nb;
+}
+
+/* Value lookup for any row type: Get(col) (vector_store.hpp:94-98,
+ * sorted_vector_map_store.hpp:160-165, map_store.hpp:51-58). Writes raw bytes. */
+int orc_get(orc_server *s, int32_t table_id, int32_t row_id, int32_t col, void *out) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  size_t vs = dt_size(t->dt);
+  memset(out, 0, vs);
+  orc_row *r = find_row(t, row_id);
+  if (!r) return ORC_OK;
+  if (t->kind == KIND_DENSE) {
+    if (col >= 0 && col < t->row_capacity) memcpy(out, r->dense + (size_t)col * vs, vs);
+  } else if (t->kind == KIND_SORTED_MAP) {
+    size_t es = entry_size(t->dt);
+    int64_t i = svm_find(r, col, es);
+    if (i >= 0) memcpy(out, ENT_VALP(r, i, es, entry_val_off(t->dt)), vs);
+  } else {
+    int64_t slot = imap_find(&r->map, col);
+    if (slot >= 0) { uint64_t v = (uint64_t)r->map.vals[slot]; memcpy(out, &v, vs); }
+  }
+  return ORC_OK;
+}
+
+/* Direct store-level entry point used by the known-answer tests: apply one
+ * Inc(col, delta) to a row (creating it), i.e. AbstractRow::ApplyIncUnsafe
+ * (numeric_store_row.hpp:160-164). */
+int orc_row_inc(orc_server *s, int32_t table_id, int32_t row_id, int32_t col, const void *delta) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  orc_row *r = find_row(t, row_id);
+  if (!r) r = create_row(t, row_id);
+  apply_sparse_record(t, r, &col, (const uint8_t *)delta, 1);
+  return ORC_OK;
+}
+
+/* ---- pack (client side) ------------------------------------------------------ */
+/* Size of one row record for a DenseRowOpLog holding `vals` (capacity values):
+ * SerializedOpLogBuffer::AppendRowOpLog (row_oplog_serializer.hpp:41-56) with
+ * GetDenseSerializedSize (dense_row_oplog.hpp:107-109) or, after
+ * ClearZerosAndGetNoneZeroSize (:91-101), GetSparseSerializedSize (:103-106). */
+static size_t count_nonzero(const uint8_t *vals, int64_t cap, int dt) {
+  size_t nz = 0, vs = dt_size(dt);
+  for (int64_t c = 0; c < cap; ++c) if (!v_is_zero(v_load(vals + (size_t)c * vs, dt), dt)) nz++;
+  return nz;
+}
+
+/* Build one Appendix-A stream (the payload of one ClientSendOpLogMsg) from per-table
+ * dense oplog matrices, as CreateOpLogMsgs + OpLogSerializer + RowOpLogSerializer do
+ * (abstract_bg_worker.cpp:590-649, oplog_serializer.hpp:12-37,
+ * row_oplog_serializer.hpp:139-166):
+ *   int32 num_tables; per table (ascending table_id, std::map order):
+ *   int32 table_id; size_t update_size; int32 num_rows; records...
+ * Dense records: SerializeDense (dense_row_oplog.hpp:133-136) = V[capacity];
+ * sparse: SerializeSparse (:112-131) = int32 n; int32 cols[n] ascending non-zero; V vals[n].
+ * Tables with no rows are omitted (FinalizeOpLogMsgStats erases them,
+ * abstract_bg_worker.cpp:568-588).  Returns bytes written, or 0 if cap too small,
+ * or (size_t)-1 on bad input.  Pass out=NULL to size. */
+size_t orc_pack_stream(int ntables, const int32_t *table_ids, const int32_t *dtypes,
+                       const int32_t *dense_serialized, const int64_t *capacities,
+                       const int64_t *nrows, const int32_t *const *row_ids,
+                       const void *const *oplogs, void *out, size_t cap) {
+  int order[64];
+  if (ntables < 0 || ntables > 64) return (size_t)-1;
+  int n_nonempty = 0;
+  for (int i = 0; i < ntables; ++i) if (nrows[i] > 0) order[n_nonempty++] = i;
+  for (int i = 1; i < n_nonempty; ++i) {            /* ascending table id */
+    int x = order[i], j = i - 1;
+    while (j >= 0 && table_ids[order[j]] > table_ids[x]) { order[j + 1] = order[j]; --j; }
+    order[j + 1] = x;
+  }
+  size_t total = 4;
+  for (int k = 0; k < n_nonempty; ++k) {
+    int i = order[k];
+    size_t vs = dt_size(dtypes[i]);
+    total += 16;
+    for (int64_t r = 0; r < nrows[i]; ++r) {
+      const uint8_t *v = (const uint8_t *)oplogs[i] + (size_t)r * (size_t)capacities[i] * vs;
+      if (dense_serialized[i]) total += 4 + (size_t)capacities[i] * vs;
+      else total += 8 + count_nonzero(v, capacities[i], dtypes[i]) * (4 + vs);
+    }
+  }
+  if (n_nonempty == 0) total = 0;   /* empty message: avai_size 0 (abstract_bg_worker.cpp:670-682) */
+  if (!out) return total;
+  if (total > cap) return 0;
+  if (total == 0) return 0;
+  uint8_t *o = (uint8_t *)out;
+  int32_t nt = n_nonempty;
+  memcpy(o, &nt, 4); o += 4;
+  for (int k = 0; k < n_nonempty; ++k) {
+    int i = order[k];
+    int dt = dtypes[i];
+    uint64_t us = dt_size(dt);
+    int32_t nr = (int32_t)nrows[i];
+    memcpy(o, &table_ids[i], 4); memcpy(o + 4, &us, 8); memcpy(o + 12, &nr, 4); o += 16;
+    for (int64_t r = 0; r < nrows[i]; ++r) {
+      const uint8_t *v = (const uint8_t *)oplogs[i] + (size_t)r * (size_t)capacities[i] * us;
+      memcpy(o, &row_ids[i][r], 4); o += 4;
+      if (dense_serialized[i]) {
+        memcpy(o, v, (size_t)capacities[i] * us); o += (size_t)capacities[i] * us;
+      } else {
+        int32_t nz = (int32_t)count_nonzero(v, capacities[i], dt);
+        memcpy(o, &nz, 4);
+        uint8_t *ci = o + 4, *vi = o + 4 + (size_t)nz * 4;
+        for (int64_t c = 0; c < capacities[i]; ++c) {
+          const uint8_t *p = v + (size_t)c * us;
+          if (v_is_zero(v_load(p, dt), dt)) continue;
+          int32_t cc = (int32_t)c;
+          memcpy(ci, &cc, 4); ci += 4;
+          memcpy(vi, p, us); vi += us;
+        }
+        o = vi;
+      }
+    }
+  }
+  return total;
+}
+
+/* GlobalContext::GetPartitionServerID (context.hpp:291-304):
+ * client = (row / C) % num_clients; channel = row % C;
+ * server thread id = client*1000 + 1 + channel (context.hpp:100-104,410-414). */
+int32_t orc_partition_server(int32_t row_id, int32_t num_channels, int32_t num_clients,
+                             int32_t channel) {
+  int32_t client = (row_id / num_channels) % num_clients;
+  return client * 1000 + 1 + channel;
+}
+
+/* ---- serve-back framing ------------------------------------------------------- */
+/* RecordBuff::Append (record_buff.hpp:41-53): {int32 id; size_t size; bytes}.
+ * Serialize a list of rows of one table into consecutive records, skipping absent
+ * rows.  Returns bytes written, or -2 when cap is too small. */
+int64_t orc_serialize_records(orc_server *s, int32_t table_id, const int32_t *row_ids, int32_t n,
+                              void *out, size_t cap) {
+  uint8_t *o = (uint8_t *)out;
+  size_t used = 0;
+  uint8_t *tmp = NULL; size_t tmp_cap = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    orc_table *t = find_table(s, table_id);
+    orc_row *r = t ? find_row(t, row_ids[i]) : NULL;
+    if (!r) continue;
+    size_t need = (size_t)t->row_capacity * 16 + (size_t)r->num_entries * 16 +
+                  (size_t)(t->kind == KIND_MAP ? r->map.count : 0) * 16 + 16;
+    if (need > tmp_cap) { free(tmp); tmp_cap = need; tmp = (uint8_t *)malloc(tmp_cap); }
+    int64_t nb = orc_serialize_row(s, table_id, row_ids[i], tmp, tmp_cap);
+    if (nb < 0) { free(tmp); return -3; }
+    if (used + 12 + (size_t)nb > cap) { free(tmp); return -2; }
+    uint64_t sz = (uint64_t)nb;
+    memcpy(o + used, &row_ids[i], 4); memcpy(o + used + 4, &sz, 8);
+    memcpy(o + used + 12, tmp, (size_t)nb);
+    used += 12 + (size_t)nb;
+  }
+  free(tmp);
+  return (int64_t)used;
+}

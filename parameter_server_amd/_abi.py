@@ -1,0 +1,105 @@
+"""ctypes binding of include/psx.h (libpsx.so, built in-tree for gfx950).
+
+There is no fallback: if libpsx.so is missing or cannot be loaded, importing the
+binding raises.  The product path never touches oracle/.
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpsx.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psx.h")
+
+PSX_OK = 0
+STATUS_NAMES = {
+    0: "PSX_OK", 1: "PSX_ERR_INVALID_ARG", 2: "PSX_ERR_VERSION", 3: "PSX_ERR_UNKNOWN_TABLE",
+    4: "PSX_ERR_MALFORMED", 5: "PSX_ERR_ROW_RANGE", 6: "PSX_ERR_CAPACITY", 7: "PSX_ERR_DEVICE",
+    8: "PSX_ERR_OOM", 9: "PSX_ERR_BUFFER_TOO_SMALL", 10: "PSX_ERR_UNSUPPORTED",
+    11: "PSX_ERR_SENDER", 12: "PSX_ERR_NO_DEVICE",
+}
+ROW_DENSE, ROW_SORTED_MAP, ROW_MAP = 0, 1, 2
+F32, F64, I32, I64 = 0, 1, 2, 3
+MAX_FUSED_STREAMS = 16
+
+
+class psx_table_config(ctypes.Structure):
+    _fields_ = [
+        ("table_id", ctypes.c_int32),
+        ("row_kind", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("oplog_dense_serialized", ctypes.c_int32),
+        ("row_capacity", ctypes.c_int64),
+        ("dense_row_oplog_capacity", ctypes.c_int64),
+        ("row_offset", ctypes.c_int64),
+        ("row_stride", ctypes.c_int64),
+        ("max_rows", ctypes.c_int64),
+        ("max_entries", ctypes.c_int64),
+    ]
+
+
+class psx_stream(ctypes.Structure):
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("size", ctypes.c_size_t),
+        ("bg_id", ctypes.c_int32),
+        ("version", ctypes.c_uint32),
+    ]
+
+
+class PsxError(RuntimeError):
+    def __init__(self, status, msg):
+        self.status = status
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+
+
+_lib = None
+
+
+def header_functions():
+    """Names of every function declared in include/psx.h."""
+    src = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(psx_[a-z_0-9]+)\s*\(", src)))
+
+
+def load():
+    """Load libpsx.so; raises OSError if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} not built: run `make -C parameter_server_amd/csrc` "
+                      "or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u32, sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                             ctypes.c_uint32, ctypes.c_size_t)
+    P = ctypes.POINTER
+    sigs = {
+        "psx_abi_version": ([], i32),
+        "psx_ctx_create": ([i32, i32, P(vp)], ctypes.c_int),
+        "psx_ctx_destroy": ([vp], ctypes.c_int),
+        "psx_ctx_set_stream": ([vp, vp], ctypes.c_int),
+        "psx_ctx_get_stream": ([vp], vp),
+        "psx_register_sender": ([vp, i32], ctypes.c_int),
+        "psx_sender_version": ([vp, i32, P(i64)], ctypes.c_int),
+        "psx_table_create": ([vp, P(psx_table_config)], ctypes.c_int),
+        "psx_table_load_rows": ([vp, i32, i64, i64, vp, i32], ctypes.c_int),
+        "psx_table_read_rows": ([vp, i32, i64, i64, vp, i32], ctypes.c_int),
+        "psx_row_flags": ([vp, i32, i64, i64, vp], ctypes.c_int),
+        "psx_clear_dirty": ([vp, i32], ctypes.c_int),
+        "psx_apply_stream": ([vp, vp, sz, i32, u32], ctypes.c_int),
+        "psx_apply_streams_device": ([vp, P(psx_stream), i32], ctypes.c_int),
+        "psx_sync": ([vp], ctypes.c_int),
+        "psx_serialize_rows": ([vp, i32, vp, i32, vp, sz, P(sz)], ctypes.c_int),
+        "psx_last_error": ([vp], ctypes.c_char_p),
+        "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),
+        "psx_timing_enable": ([vp, i32], ctypes.c_int),
+        "psx_timing_read": ([vp, ctypes.c_char_p, P(ctypes.c_double), P(i64)], ctypes.c_int),
+        "psx_timing_reset": ([vp], ctypes.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L

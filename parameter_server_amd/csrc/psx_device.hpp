@@ -1,0 +1,74 @@
+// psx_device.hpp — definitions shared by the host runtime and the CDNA4 kernels.
+//
+// Device layout (one context = one server shard, see DESIGN.md "Data layout in HBM"):
+//   dense table   : V rows[max_rows][row_capacity]            (slot-major, row_capacity*sizeof(V) B/row)
+//   row flags     : uint8 flags[max_rows]  bit0 exists, bit1 dirty  (ServerRow::dirty_, server_row.hpp:133)
+//   inverse index : int32 inv[max_rows][B]  record number of slot s in message b, -1 = absent.
+//                   All -1 between calls: the apply kernel restores every entry it reads.
+//   segments      : Seg segs[kMaxFused][kMaxTables]  (stream b, table t) decoded by decode_streams
+#pragma once
+#include <cstdint>
+
+namespace psx {
+
+constexpr int kMaxFused = 16;   // == PSX_MAX_FUSED_STREAMS
+constexpr int kMaxTables = 64;  // == PSX_MAX_TABLES
+constexpr int kWave = 64;
+
+// Status bits (device-written).  Per-call word = status[0] (reset by decode at the
+// start of each call), sticky word = status[1] (OR of all calls since psx_sync).
+enum : uint32_t {
+  kStMalformed = 1u << 0,
+  kStUnknownTable = 1u << 1,
+  kStRowRange = 1u << 2,
+  kStCapacity = 1u << 3,
+  kStUnsupported = 1u << 4,
+  kStDuplicateRow = 1u << 5,   // a row appears twice in one message: replay on the ordered path
+};
+constexpr uint32_t kStFatal = kStMalformed | kStUnknownTable | kStRowRange | kStCapacity |
+                              kStUnsupported;
+
+// Table directory passed by value to the decoder.
+struct TableDir {
+  int32_t n;
+  int32_t table_id[kMaxTables];
+  int32_t vsize[kMaxTables];
+  int32_t dense_serialized[kMaxTables];
+  int64_t oplog_cap[kMaxTables];
+};
+
+// Device-resident messages of one fused call, passed by value.
+struct StreamSet {
+  const uint8_t *data[kMaxFused];
+  uint64_t size[kMaxFused];
+  uint64_t recoff_base[kMaxFused];   // sparse record-offset workspace start per stream
+  int32_t n;
+};
+
+// One (stream, table) segment.
+struct Seg {
+  int64_t rec0;       // byte offset of the first record's row_id, -1 = table absent
+  int32_t num_rows;
+  int32_t sparse;     // 1: record offsets live in recoff[recoff_base[b] + k]
+};
+
+// Arguments of dense_apply (passed by value).
+struct DenseArgs {
+  StreamSet ss;
+  const Seg *segs;
+  int t;
+  int B;
+  int64_t stride;     // record stride in bytes = 4 + cap*sizeof(V)
+  int64_t cap;        // dense_row_oplog_capacity (elements applied per record)
+  int64_t row_cap;    // row_capacity (elements per table row)
+  int64_t max_rows;
+  void *table;
+  uint8_t *flags;
+  int32_t *inv;
+  const uint32_t *counters;
+  uint32_t *sticky;
+  uint32_t *call_status;
+  const uint8_t *zero_chunk;   // >= 2 KiB of zeros, stands in for absent messages
+};
+
+}  // namespace psx

@@ -1,0 +1,673 @@
+// psx_runtime.cpp — host runtime behind include/psx.h.
+//
+// One psx_ctx == one reference ServerThread's Server (server_thread.hpp:90): it owns
+// the shard's tables in HBM, the per-sender version map (server.cpp:21-24,124-126) and
+// a HIP stream.  Every apply call enqueues the kernel pipeline of psx_kernels.hip and
+// returns; device-detected errors surface at psx_sync().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/psx.h"
+#include "psx_device.hpp"
+
+namespace psx {
+hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
+                         uint32_t *call_status, uint32_t *counters, hipStream_t st);
+hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
+                              int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
+                              uint32_t *call_status, hipStream_t st);
+hipError_t launch_dense_verify(const int32_t *inv, int t, int B, int64_t max_rows, uint32_t *counters,
+                               hipStream_t st);
+hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, hipStream_t st);
+hipError_t launch_flags_or(uint8_t *flags, int64_t first, int64_t num, uint8_t bits, hipStream_t st);
+hipError_t launch_flags_and(uint8_t *flags, int64_t num, uint8_t bits, hipStream_t st);
+hipError_t launch_gather_rows(int dtype, const void *table, const int64_t *slots, int32_t n,
+                              int64_t row_cap, void *out, hipStream_t st);
+
+hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st);
+}  // namespace psx
+
+namespace {
+
+constexpr int kRing = 64;   // per-call status slots
+
+int vsize_of(int32_t dt) { return (dt == PSX_F32 || dt == PSX_I32) ? 4 : 8; }
+
+struct TableState {
+  psx_table_config cfg{};
+  int vsize = 4;
+  void *d_data = nullptr;
+  uint8_t *d_flags = nullptr;
+  int32_t *d_inv = nullptr;
+};
+
+struct EventPair {
+  std::string name;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct psx_ctx {
+  int device = 0;
+  int32_t server_id = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  std::map<int32_t, int64_t> versions;   // bg_version_map_
+  std::vector<TableState> tables;
+  psx::Seg *d_segs = nullptr;
+  uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring
+  uint32_t *d_counters = nullptr;
+  uint8_t *d_zero = nullptr;
+  uint64_t *d_recoff = nullptr;
+  size_t recoff_cap = 0;                 // entries
+  uint8_t *d_staging = nullptr;
+  size_t staging_cap = 0;
+  int64_t call_seq = 0;
+  int64_t pending_calls = 0;
+  psx_status deferred = PSX_OK;
+  std::string err;
+  bool timing = false;
+  std::vector<EventPair> pending_ev;
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, std::pair<double, int64_t>> times;
+};
+
+namespace {
+
+psx_status fail(psx_ctx *c, psx_status s, const std::string &msg) {
+  if (c) c->err = msg;
+  return s;
+}
+
+psx_status hip_fail(psx_ctx *c, hipError_t e, const char *what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(c, e == hipErrorOutOfMemory ? PSX_ERR_OOM : PSX_ERR_DEVICE, m);
+}
+
+#define HIP_TRY(c, expr)                                   \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
+    if (_e != hipSuccess) return hip_fail((c), _e, #expr); \
+  } while (0)
+
+hipEvent_t get_event(psx_ctx *c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Run `launch` on the context stream, bracketed by HIP events when timing is on.
+template <typename F>
+psx_status timed(psx_ctx *c, const char *name, F launch) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->timing) {
+    a = get_event(c);
+    b = get_event(c);
+    if (a) hipEventRecord(a, c->stream);
+  }
+  hipError_t e = launch();
+  if (e != hipSuccess) return hip_fail(c, e, name);
+  if (c->timing && a && b) {
+    hipEventRecord(b, c->stream);
+    c->pending_ev.push_back({name, a, b});
+  }
+  return PSX_OK;
+}
+
+void collect_timing(psx_ctx *c) {
+  for (auto &p : c->pending_ev) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      auto &acc = c->times[p.name];
+      acc.first += ms;
+      acc.second += 1;
+    }
+    c->ev_pool.push_back(p.a);
+    c->ev_pool.push_back(p.b);
+  }
+  c->pending_ev.clear();
+}
+
+TableState *find_table(psx_ctx *c, int32_t table_id, int *index = nullptr) {
+  for (size_t i = 0; i < c->tables.size(); ++i)
+    if (c->tables[i].cfg.table_id == table_id) {
+      if (index) *index = (int)i;
+      return &c->tables[i];
+    }
+  return nullptr;
+}
+
+// Slot of row r in table t, or -1 (context.hpp:291-304 geometry, see psx.h).
+int64_t slot_of(const TableState &t, int64_t r) {
+  int64_t d = r - t.cfg.row_offset;
+  if (d < 0 || d % t.cfg.row_stride) return -1;
+  d /= t.cfg.row_stride;
+  return d < t.cfg.max_rows ? d : -1;
+}
+
+uint32_t rd32h(const uint8_t *p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+uint64_t rd64h(const uint8_t *p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+
+// Host walk of one message (host bytes): SerializedOpLogReader semantics
+// (serialized_oplog_reader.hpp:30-133) — validates everything the device pipeline
+// would flag, so psx_apply_stream can fail synchronously and apply nothing.
+psx_status host_validate(psx_ctx *c, const uint8_t *p, size_t size) {
+  if (size == 0) return PSX_OK;
+  if (size < 4) return fail(c, PSX_ERR_MALFORMED, "stream shorter than num_tables");
+  int32_t ntab = (int32_t)rd32h(p);
+  if (ntab < 0) return fail(c, PSX_ERR_MALFORMED, "negative num_tables");
+  size_t off = 4;
+  std::vector<int32_t> seen;
+  for (int32_t k = 0; k < ntab; ++k) {
+    if (off + 16 > size) return fail(c, PSX_ERR_MALFORMED, "truncated table header");
+    int32_t tid = (int32_t)rd32h(p + off);
+    uint64_t usz = rd64h(p + off + 4);
+    int32_t nrows = (int32_t)rd32h(p + off + 12);
+    off += 16;
+    TableState *t = find_table(c, tid);
+    if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "table_id = " + std::to_string(tid) + " not found!");
+    if (usz != (uint64_t)t->vsize || nrows < 0) return fail(c, PSX_ERR_MALFORMED, "bad update_size/num_rows");
+    if (std::find(seen.begin(), seen.end(), tid) != seen.end())
+      return fail(c, PSX_ERR_UNSUPPORTED, "table appears twice in one message");
+    seen.push_back(tid);
+    for (int32_t r = 0; r < nrows; ++r) {
+      if (off + 4 > size) return fail(c, PSX_ERR_MALFORMED, "truncated record");
+      int32_t rid = (int32_t)rd32h(p + off);
+      if (slot_of(*t, rid) < 0)
+        return fail(c, PSX_ERR_ROW_RANGE, "row " + std::to_string(rid) + " not owned by this shard");
+      off += 4;
+      if (t->cfg.oplog_dense_serialized) {
+        size_t rs = (size_t)t->cfg.dense_row_oplog_capacity * t->vsize;
+        if (off + rs > size) return fail(c, PSX_ERR_MALFORMED, "truncated dense record");
+        off += rs;
+      } else {
+        if (off + 4 > size) return fail(c, PSX_ERR_MALFORMED, "truncated sparse record");
+        int32_t n = (int32_t)rd32h(p + off);
+        if (n < 0) return fail(c, PSX_ERR_MALFORMED, "negative record length");
+        size_t rs = 4 + (size_t)n * (4 + t->vsize);
+        if (off + rs > size) return fail(c, PSX_ERR_MALFORMED, "truncated sparse record");
+        off += rs;
+      }
+    }
+  }
+  return PSX_OK;
+}
+
+bool has_sparse_serialized(const psx_ctx *c) {
+  for (auto &t : c->tables)
+    if (!t.cfg.oplog_dense_serialized) return true;
+  return false;
+}
+
+// Enqueue the device pipeline for n messages already resident in HBM (versions checked).
+psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
+  psx::StreamSet ss{};
+  ss.n = n;
+  size_t rec_need = 0;
+  const bool sparse = has_sparse_serialized(c);
+  for (int i = 0; i < n; ++i) {
+    ss.data[i] = (const uint8_t *)s[i].data;
+    ss.size[i] = s[i].size;
+    ss.recoff_base[i] = rec_need;
+    if (sparse) rec_need += s[i].size / 8 + 1;
+  }
+  if (rec_need > c->recoff_cap) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->d_recoff) hipFree(c->d_recoff);
+    c->d_recoff = nullptr;
+    HIP_TRY(c, hipMalloc(&c->d_recoff, rec_need * sizeof(uint64_t)));
+    c->recoff_cap = rec_need;
+  }
+  psx::TableDir dir{};
+  dir.n = (int32_t)c->tables.size();
+  for (size_t i = 0; i < c->tables.size(); ++i) {
+    dir.table_id[i] = c->tables[i].cfg.table_id;
+    dir.vsize[i] = c->tables[i].vsize;
+    dir.dense_serialized[i] = c->tables[i].cfg.oplog_dense_serialized;
+    dir.oplog_cap[i] = c->tables[i].cfg.dense_row_oplog_capacity;
+  }
+  const int ring = (int)(c->call_seq % kRing);
+  uint32_t *sticky = c->d_status;
+  uint32_t *call_st = c->d_status + 1 + ring;
+  psx_status st = timed(c, "decode_streams", [&] {
+    return psx::launch_decode(ss, dir, c->d_segs, c->d_recoff, call_st, c->d_counters, c->stream);
+  });
+  if (st) return st;
+  for (size_t ti = 0; ti < c->tables.size(); ++ti) {
+    TableState &t = c->tables[ti];
+    if (t.cfg.row_kind != PSX_ROW_DENSE || !t.cfg.oplog_dense_serialized) continue;
+    const int64_t stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
+    st = timed(c, "dense_index", [&] {
+      return psx::launch_dense_index(ss, c->d_segs, (int)ti, n, stride, t.cfg.row_offset,
+                                     t.cfg.row_stride, t.cfg.max_rows, t.d_inv, call_st, c->stream);
+    });
+    if (st) return st;
+    st = timed(c, "dense_verify", [&] {
+      return psx::launch_dense_verify(t.d_inv, (int)ti, n, t.cfg.max_rows, c->d_counters, c->stream);
+    });
+    if (st) return st;
+    psx::DenseArgs a{};
+    a.ss = ss;
+    a.segs = c->d_segs;
+    a.t = (int)ti;
+    a.B = n;
+    a.stride = stride;
+    a.cap = t.cfg.dense_row_oplog_capacity;
+    a.row_cap = t.cfg.row_capacity;
+    a.max_rows = t.cfg.max_rows;
+    a.table = t.d_data;
+    a.flags = t.d_flags;
+    a.inv = t.d_inv;
+    a.counters = c->d_counters;
+    a.sticky = sticky;
+    a.call_status = call_st;
+    a.zero_chunk = c->d_zero;
+    st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream); });
+    if (st) return st;
+  }
+  st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, c->stream); });
+  if (st) return st;
+  c->call_seq++;
+  c->pending_calls++;
+  return PSX_OK;
+}
+
+psx_status sync_impl(psx_ctx *c) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  collect_timing(c);
+  uint32_t sticky = 0;
+  HIP_TRY(c, hipMemcpy(&sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (sticky) {
+    uint32_t zero = 0;
+    HIP_TRY(c, hipMemcpy(c->d_status, &zero, sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  c->pending_calls = 0;
+  psx_status d = c->deferred;
+  c->deferred = PSX_OK;
+  if (d != PSX_OK) return d;
+  if (sticky & psx::kStUnknownTable) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table id in a device stream");
+  if (sticky & psx::kStMalformed) return fail(c, PSX_ERR_MALFORMED, "malformed device stream");
+  if (sticky & psx::kStRowRange) return fail(c, PSX_ERR_ROW_RANGE, "row id outside this shard's range");
+  if (sticky & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "row capacity exceeded");
+  if (sticky & psx::kStUnsupported) return fail(c, PSX_ERR_UNSUPPORTED, "table repeated within one message");
+  if (sticky & psx::kStDuplicateRow)
+    return fail(c, PSX_ERR_UNSUPPORTED,
+                "a row occurs twice in one message; the ordered replay path is not built yet "
+                "(messages from that call on were not applied)");
+  return PSX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t psx_abi_version(void) { return PSX_ABI_VERSION; }
+
+const char *psx_status_string(psx_status s) {
+  switch (s) {
+    case PSX_OK: return "ok";
+    case PSX_ERR_INVALID_ARG: return "invalid argument";
+    case PSX_ERR_VERSION: return "version gap";
+    case PSX_ERR_UNKNOWN_TABLE: return "unknown table";
+    case PSX_ERR_MALFORMED: return "malformed stream";
+    case PSX_ERR_ROW_RANGE: return "row outside shard";
+    case PSX_ERR_CAPACITY: return "capacity exceeded";
+    case PSX_ERR_DEVICE: return "device error";
+    case PSX_ERR_OOM: return "out of device memory";
+    case PSX_ERR_BUFFER_TOO_SMALL: return "buffer too small";
+    case PSX_ERR_UNSUPPORTED: return "unsupported";
+    case PSX_ERR_SENDER: return "unknown sender";
+    case PSX_ERR_NO_DEVICE: return "no HIP device";
+  }
+  return "?";
+}
+
+psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
+  if (!out) return PSX_ERR_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PSX_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return PSX_ERR_INVALID_ARG;
+  psx_ctx *c = new psx_ctx();
+  c->device = device;
+  c->server_id = server_id;
+  auto cleanup = [&](psx_status s) {
+    psx_ctx_destroy(c);
+    return s;
+  };
+  if (hipSetDevice(device) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
+  c->stream = c->own;
+  if (hipMalloc(&c->d_segs, sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
+      hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + kRing)) != hipSuccess ||
+      hipMalloc(&c->d_counters, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
+      hipMalloc(&c->d_zero, 4096) != hipSuccess)
+    return cleanup(PSX_ERR_OOM);
+  if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (1 + kRing)) != hipSuccess ||
+      hipMemset(c->d_zero, 0, 4096) != hipSuccess ||
+      hipMemset(c->d_counters, 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
+    return cleanup(PSX_ERR_DEVICE);
+  *out = c;
+  return PSX_OK;
+}
+
+psx_status psx_ctx_destroy(psx_ctx *c) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (auto &t : c->tables) {
+    if (t.d_data) hipFree(t.d_data);
+    if (t.d_flags) hipFree(t.d_flags);
+    if (t.d_inv) hipFree(t.d_inv);
+  }
+  for (auto &p : c->pending_ev) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  if (c->d_segs) hipFree(c->d_segs);
+  if (c->d_status) hipFree(c->d_status);
+  if (c->d_counters) hipFree(c->d_counters);
+  if (c->d_zero) hipFree(c->d_zero);
+  if (c->d_recoff) hipFree(c->d_recoff);
+  if (c->d_staging) hipFree(c->d_staging);
+  if (c->own) hipStreamDestroy(c->own);
+  delete c;
+  return PSX_OK;
+}
+
+psx_status psx_ctx_set_stream(psx_ctx *c, void *hip_stream) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
+  return PSX_OK;
+}
+
+void *psx_ctx_get_stream(psx_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+psx_status psx_register_sender(psx_ctx *c, int32_t bg_id) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  if (!c->versions.count(bg_id)) c->versions[bg_id] = -1;
+  return PSX_OK;
+}
+
+psx_status psx_sender_version(psx_ctx *c, int32_t bg_id, int64_t *version) {
+  if (!c || !version) return PSX_ERR_INVALID_ARG;
+  auto it = c->versions.find(bg_id);
+  if (it == c->versions.end()) return fail(c, PSX_ERR_SENDER, "unknown sender");
+  *version = it->second;
+  return PSX_OK;
+}
+
+psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
+  if (!c || !cfg) return PSX_ERR_INVALID_ARG;
+  if (c->tables.size() >= (size_t)psx::kMaxTables) return fail(c, PSX_ERR_INVALID_ARG, "too many tables");
+  if (find_table(c, cfg->table_id)) return fail(c, PSX_ERR_INVALID_ARG, "table exists");
+  if (cfg->dtype < PSX_F32 || cfg->dtype > PSX_I64) return fail(c, PSX_ERR_INVALID_ARG, "bad dtype");
+  if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
+  if (cfg->max_rows <= 0 || cfg->row_stride <= 0) return fail(c, PSX_ERR_INVALID_ARG, "bad shard geometry");
+  if (cfg->max_rows > (int64_t)1 << 31) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
+  if (cfg->row_kind != PSX_ROW_DENSE || !cfg->oplog_dense_serialized)
+    return fail(c, PSX_ERR_UNSUPPORTED, "only dense rows with dense-serialized oplogs are built so far");
+  if (cfg->row_capacity <= 0) return fail(c, PSX_ERR_INVALID_ARG, "row_capacity must be > 0");
+  if (cfg->dense_row_oplog_capacity <= 0 || cfg->dense_row_oplog_capacity > cfg->row_capacity)
+    return fail(c, PSX_ERR_INVALID_ARG, "dense_row_oplog_capacity must be in [1, row_capacity]");
+  HIP_TRY(c, hipSetDevice(c->device));
+  TableState t;
+  t.cfg = *cfg;
+  t.vsize = vsize_of(cfg->dtype);
+  const size_t data_bytes = (size_t)cfg->max_rows * (size_t)cfg->row_capacity * t.vsize;
+  const size_t inv_bytes = (size_t)cfg->max_rows * psx::kMaxFused * sizeof(int32_t);
+  hipError_t e = hipMalloc(&t.d_data, data_bytes);
+  if (e == hipSuccess) e = hipMalloc(&t.d_flags, (size_t)cfg->max_rows);
+  if (e == hipSuccess) e = hipMalloc(&t.d_inv, inv_bytes);
+  if (e == hipSuccess) e = hipMemsetAsync(t.d_data, 0, data_bytes, c->stream);   // VectorStore::Init zeroes
+  if (e == hipSuccess) e = hipMemsetAsync(t.d_flags, 0, (size_t)cfg->max_rows, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(t.d_inv, 0xff, inv_bytes, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    if (t.d_data) hipFree(t.d_data);
+    if (t.d_flags) hipFree(t.d_flags);
+    if (t.d_inv) hipFree(t.d_inv);
+    return hip_fail(c, e, "table allocation");
+  }
+  c->tables.push_back(t);
+  return PSX_OK;
+}
+
+static psx_status row_range(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows,
+                            TableState **out, int64_t *first_slot) {
+  TableState *t = find_table(c, table_id);
+  if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
+  if (num_rows < 0) return fail(c, PSX_ERR_INVALID_ARG, "num_rows < 0");
+  int64_t s = slot_of(*t, first_row);
+  if (s < 0 || s + num_rows > t->cfg.max_rows) return fail(c, PSX_ERR_ROW_RANGE, "row range outside shard");
+  *out = t;
+  *first_slot = s;
+  return PSX_OK;
+}
+
+psx_status psx_table_load_rows(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows,
+                               const void *src, int32_t src_on_device) {
+  if (!c || (!src && num_rows)) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t rb = (size_t)t->cfg.row_capacity * t->vsize;
+  HIP_TRY(c, hipMemcpyAsync((uint8_t *)t->d_data + (size_t)s * rb, src, (size_t)num_rows * rb,
+                            src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, psx::launch_flags_or(t->d_flags, s, num_rows, 1, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_table_read_rows(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows,
+                               void *dst, int32_t dst_on_device) {
+  if (!c || (!dst && num_rows)) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t rb = (size_t)t->cfg.row_capacity * t->vsize;
+  HIP_TRY(c, hipMemcpyAsync(dst, (const uint8_t *)t->d_data + (size_t)s * rb, (size_t)num_rows * rb,
+                            dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_row_flags(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows, uint8_t *dst) {
+  if (!c || (!dst && num_rows)) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipMemcpyAsync(dst, t->d_flags + s, (size_t)num_rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_clear_dirty(psx_ctx *c, int32_t table_id) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  TableState *t = find_table(c, table_id);
+  if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, psx::launch_flags_and(t->d_flags, t->cfg.max_rows, (uint8_t)~2u, c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) {
+  if (!c || !s || n <= 0 || n > PSX_MAX_FUSED_STREAMS) return PSX_ERR_INVALID_ARG;
+  // Version rule of Server::ApplyOpLogUpdateVersion (server.cpp:124-126), checked for
+  // the whole batch before anything is enqueued.
+  std::map<int32_t, int64_t> v = c->versions;
+  for (int i = 0; i < n; ++i) {
+    if (s[i].size && (!s[i].data || ((uintptr_t)s[i].data & 3)))
+      return fail(c, PSX_ERR_INVALID_ARG, "device stream must be non-null and 4-byte aligned");
+    auto it = v.find(s[i].bg_id);
+    if (it == v.end()) return fail(c, PSX_ERR_SENDER, "bg_id " + std::to_string(s[i].bg_id) + " not registered");
+    if (it->second + 1 != (int64_t)s[i].version)
+      return fail(c, PSX_ERR_VERSION, "bg_thread_id = " + std::to_string(s[i].bg_id) + ": expected version " +
+                                          std::to_string(it->second + 1) + ", got " + std::to_string(s[i].version));
+    it->second = s[i].version;
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->pending_calls >= kRing - 1) {
+    psx_status d = sync_impl(c);
+    if (d != PSX_OK) c->deferred = d;
+  }
+  psx_status st = enqueue_apply(c, s, n);
+  if (st) return st;
+  c->versions = v;
+  return PSX_OK;
+}
+
+psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, int32_t bg_id,
+                            uint32_t version) {
+  if (!c || (oplog_size && !oplog)) return PSX_ERR_INVALID_ARG;
+  auto it = c->versions.find(bg_id);
+  if (it == c->versions.end()) return fail(c, PSX_ERR_SENDER, "bg_id " + std::to_string(bg_id) + " not registered");
+  if (it->second + 1 != (int64_t)version)
+    return fail(c, PSX_ERR_VERSION, "bg_thread_id = " + std::to_string(bg_id) + ": expected version " +
+                                        std::to_string(it->second + 1) + ", got " + std::to_string(version));
+  const uint8_t *p = (const uint8_t *)oplog;
+  if (oplog_size == 0 || (oplog_size >= 4 && rd32h(p) == 0)) {   // server.cpp:128, Restart() false
+    it->second = version;
+    return PSX_OK;
+  }
+  psx_status st = host_validate(c, p, oplog_size);
+  if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  // The staging buffer may still feed an earlier call's kernels.
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (oplog_size > c->staging_cap) {
+    if (c->d_staging) hipFree(c->d_staging);
+    c->d_staging = nullptr;
+    c->staging_cap = 0;
+    HIP_TRY(c, hipMalloc(&c->d_staging, oplog_size));
+    c->staging_cap = oplog_size;
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->d_staging, oplog, oplog_size, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));   // the caller frees `oplog` after we return
+  psx_stream one{c->d_staging, oplog_size, bg_id, version};
+  if (c->pending_calls >= kRing - 1) {
+    psx_status d = sync_impl(c);
+    if (d != PSX_OK) c->deferred = d;
+  }
+  st = enqueue_apply(c, &one, 1);
+  if (st) return st;
+  it->second = version;
+  return PSX_OK;
+}
+
+psx_status psx_sync(psx_ctx *c) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  return sync_impl(c);
+}
+
+psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_ids, int32_t n, void *out,
+                              size_t cap, size_t *used) {
+  if (!c || !used || n < 0 || (n && !row_ids)) return PSX_ERR_INVALID_ARG;
+  *used = 0;
+  TableState *t = find_table(c, table_id);
+  if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
+  if (n == 0) return PSX_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::vector<int64_t> slots(n);
+  for (int32_t i = 0; i < n; ++i) slots[i] = slot_of(*t, row_ids[i]);
+  const size_t rb = (size_t)t->cfg.row_capacity * t->vsize;
+  int64_t *d_slots = nullptr;
+  uint8_t *d_out = nullptr;
+  HIP_TRY(c, hipMalloc(&d_slots, sizeof(int64_t) * n));
+  hipError_t e = hipMalloc(&d_out, rb * n);
+  if (e != hipSuccess) {
+    hipFree(d_slots);
+    return hip_fail(c, e, "serialize buffer");
+  }
+  std::vector<uint8_t> rows(rb * n);
+  e = hipMemcpyAsync(d_slots, slots.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = psx::launch_gather_rows(t->cfg.dtype, t->d_data, d_slots, n, t->cfg.row_capacity, d_out, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(rows.data(), d_out, rb * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d_slots);
+  hipFree(d_out);
+  if (e != hipSuccess) return hip_fail(c, e, "serialize gather");
+  // presence from the flags (absent rows are skipped, as ServerTable only serializes
+  // rows that exist in storage_)
+  std::vector<uint8_t> present(n, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    if (slots[i] < 0) continue;
+    uint8_t f = 0;
+    HIP_TRY(c, hipMemcpy(&f, t->d_flags + slots[i], 1, hipMemcpyDeviceToHost));
+    present[i] = f & 1;
+  }
+  size_t off = 0;
+  uint8_t *o = (uint8_t *)out;
+  for (int32_t i = 0; i < n; ++i) {
+    if (!present[i]) continue;
+    if (off + 12 + rb > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize: output buffer too small");
+    uint64_t sz = rb;
+    memcpy(o + off, &row_ids[i], 4);
+    memcpy(o + off + 4, &sz, 8);
+    memcpy(o + off + 12, rows.data() + (size_t)i * rb, rb);
+    off += 12 + rb;
+  }
+  *used = off;
+  return PSX_OK;
+}
+
+const char *psx_last_error(psx_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+psx_status psx_timing_enable(psx_ctx *c, int32_t on) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  c->timing = on != 0;
+  return PSX_OK;
+}
+
+psx_status psx_timing_read(psx_ctx *c, const char *kernel, double *total_ms, int64_t *launches) {
+  if (!c || !kernel || !total_ms || !launches) return PSX_ERR_INVALID_ARG;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  collect_timing(c);
+  auto it = c->times.find(kernel);
+  *total_ms = it == c->times.end() ? 0.0 : it->second.first;
+  *launches = it == c->times.end() ? 0 : it->second.second;
+  return PSX_OK;
+}
+
+psx_status psx_timing_reset(psx_ctx *c) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  collect_timing(c);
+  c->times.clear();
+  return PSX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+"""Host-side mirror of the reference's server apply interface, over the C ABI.
+
+Names follow src/petuum_ps/server/server.hpp (Server::Init, CreateTable,
+ApplyOpLogUpdateVersion, GetBgVersion) and configs.hpp (TableInfo), so the parity
+tests read like the reference's own call sites (server_thread.cpp:224-299).  Errors
+that the reference turns into glog CHECK aborts raise PsxError here.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import PsxError, psx_stream, psx_table_config
+
+NP_DTYPE = {_abi.F32: np.float32, _abi.F64: np.float64, _abi.I32: np.int32, _abi.I64: np.int64}
+
+
+@dataclass
+class TableInfo:
+    """The TableInfo fields the apply path reads (configs.hpp:170-210) plus shard geometry."""
+    row_kind: int = _abi.ROW_DENSE
+    dtype: int = _abi.F32
+    row_capacity: int = 0
+    oplog_dense_serialized: bool = True
+    dense_row_oplog_capacity: int = 0   # 0 -> row_capacity
+    row_offset: int = 0
+    row_stride: int = 1
+    max_rows: int = 0
+    max_entries: int = 0
+
+
+def _check(L, ctx, st):
+    if st != _abi.PSX_OK:
+        msg = L.psx_last_error(ctx).decode() if ctx else ""
+        raise PsxError(st, msg)
+
+
+class Server:
+    """One shard (one reference ServerThread's Server) on one GPU."""
+
+    def __init__(self, device=0, server_id=1, bg_ids=()):
+        self._L = _abi.load()
+        self._ctx = ctypes.c_void_p()
+        _check(self._L, None, self._L.psx_ctx_create(device, server_id, ctypes.byref(self._ctx)))
+        self.device = device
+        self.tables = {}
+        for bg in bg_ids:
+            self.register_sender(bg)
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if self._ctx:
+            self._L.psx_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def register_sender(self, bg_id):
+        _check(self._L, self._ctx, self._L.psx_register_sender(self._ctx, bg_id))
+
+    def set_stream(self, hip_stream_handle):
+        _check(self._L, self._ctx, self._L.psx_ctx_set_stream(self._ctx, hip_stream_handle))
+
+    # -- Server API (server.hpp) ----------------------------------------------
+    def CreateTable(self, table_id, info: TableInfo):
+        cfg = psx_table_config(
+            table_id=table_id, row_kind=info.row_kind, dtype=info.dtype,
+            oplog_dense_serialized=1 if info.oplog_dense_serialized else 0,
+            row_capacity=info.row_capacity,
+            dense_row_oplog_capacity=info.dense_row_oplog_capacity or info.row_capacity,
+            row_offset=info.row_offset, row_stride=info.row_stride, max_rows=info.max_rows,
+            max_entries=info.max_entries)
+        _check(self._L, self._ctx, self._L.psx_table_create(self._ctx, ctypes.byref(cfg)))
+        self.tables[table_id] = info
+
+    def ApplyOpLogUpdateVersion(self, oplog, oplog_size, bg_thread_id, version):
+        """Host-bytes apply, as Server::ApplyOpLogUpdateVersion (server.cpp:120-179)."""
+        buf = np.frombuffer(oplog, dtype=np.uint8) if isinstance(oplog, (bytes, bytearray)) else oplog
+        buf = np.ascontiguousarray(buf)
+        ptr = ctypes.c_void_p(buf.ctypes.data) if oplog_size else None
+        _check(self._L, self._ctx,
+               self._L.psx_apply_stream(self._ctx, ptr, oplog_size, bg_thread_id, version))
+
+    def GetBgVersion(self, bg_thread_id):
+        v = ctypes.c_int64()
+        _check(self._L, self._ctx, self._L.psx_sender_version(self._ctx, bg_thread_id, ctypes.byref(v)))
+        return v.value
+
+    # -- device-resident path -----------------------------------------------------
+    def apply_device(self, streams):
+        """streams: sequence of (device_ptr, nbytes, bg_id, version); applied in order."""
+        n = len(streams)
+        arr = (psx_stream * n)()
+        for i, (ptr, nbytes, bg, ver) in enumerate(streams):
+            arr[i].data = ptr
+            arr[i].size = nbytes
+            arr[i].bg_id = bg
+            arr[i].version = ver
+        _check(self._L, self._ctx, self._L.psx_apply_streams_device(self._ctx, arr, n))
+
+    def sync(self):
+        _check(self._L, self._ctx, self._L.psx_sync(self._ctx))
+
+    # -- rows --------------------------------------------------------------------------
+    def _np(self, table_id):
+        return NP_DTYPE[self.tables[table_id].dtype]
+
+    def load_rows(self, table_id, first_row, rows, on_device_ptr=None, num_rows=None):
+        if on_device_ptr is not None:
+            _check(self._L, self._ctx, self._L.psx_table_load_rows(
+                self._ctx, table_id, first_row, num_rows, on_device_ptr, 1))
+            return
+        info = self.tables[table_id]
+        a = np.ascontiguousarray(rows, dtype=self._np(table_id)).reshape(-1, info.row_capacity)
+        _check(self._L, self._ctx, self._L.psx_table_load_rows(
+            self._ctx, table_id, first_row, a.shape[0], ctypes.c_void_p(a.ctypes.data), 0))
+
+    def read_rows(self, table_id, first_row, num_rows):
+        info = self.tables[table_id]
+        out = np.zeros((num_rows, info.row_capacity), dtype=self._np(table_id))
+        _check(self._L, self._ctx, self._L.psx_table_read_rows(
+            self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data), 0))
+        return out
+
+    def row_flags(self, table_id, first_row, num_rows):
+        out = np.zeros(num_rows, dtype=np.uint8)
+        _check(self._L, self._ctx, self._L.psx_row_flags(
+            self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+    def clear_dirty(self, table_id):
+        _check(self._L, self._ctx, self._L.psx_clear_dirty(self._ctx, table_id))
+
+    def serialize_rows(self, table_id, row_ids):
+        ids = np.ascontiguousarray(row_ids, dtype=np.int32)
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, dtype=np.uint8)
+            used = ctypes.c_size_t()
+            st = self._L.psx_serialize_rows(self._ctx, table_id, ctypes.c_void_p(ids.ctypes.data),
+                                            ids.size, ctypes.c_void_p(out.ctypes.data), cap,
+                                            ctypes.byref(used))
+            if st == 9:   # PSX_ERR_BUFFER_TOO_SMALL
+                cap *= 4
+                continue
+            _check(self._L, self._ctx, st)
+            return out[:used.value].tobytes()
+
+    # -- timing ------------------------------------------------------------------------
+    def timing(self, on=True):
+        _check(self._L, self._ctx, self._L.psx_timing_enable(self._ctx, 1 if on else 0))
+
+    def timing_read(self, kernel):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        _check(self._L, self._ctx, self._L.psx_timing_read(self._ctx, kernel.encode(),
+                                                           ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def timing_reset(self):
+        _check(self._L, self._ctx, self._L.psx_timing_reset(self._ctx))

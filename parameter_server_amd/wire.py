@@ -1,0 +1,69 @@
+"""Vectorised builders for the reference's oplog stream format (Appendix A of SURVEY.md).
+
+One ClientSendOpLogMsg payload (ps_msgs.hpp:1003-1055, after the 41-byte header):
+    int32 num_tables
+    per table: int32 table_id; size_t update_size; int32 num_rows; records...
+    dense record : int32 row_id; V[dense_row_oplog_capacity]     (dense_row_oplog.hpp:133-136)
+    sparse record: int32 row_id; int32 n; int32 cols[n]; V vals[n] (dense_row_oplog.hpp:112-131)
+Layout as written by OpLogSerializer + RowOpLogSerializer (oplog_serializer.hpp:12-37,
+row_oplog_serializer.hpp:139-166).  These builders are how bench.py and the tests
+produce synthetic worker batches; tests cross-check them against the oracle's packer.
+"""
+import numpy as np
+
+TABLE_HEADER_BYTES = 16   # int32 table_id + size_t update_size + int32 num_rows
+
+
+def dense_record_bytes(cap, vsize):
+    return 4 + cap * vsize
+
+
+def dense_stream_bytes(num_rows, cap, vsize):
+    return 4 + TABLE_HEADER_BYTES + num_rows * dense_record_bytes(cap, vsize)
+
+
+def dense_stream_np(table_id, row_ids, payload):
+    """One single-table dense stream as a numpy uint8 array."""
+    payload = np.ascontiguousarray(payload)
+    n, cap = payload.shape
+    vsize = payload.dtype.itemsize
+    words_per_rec = 1 + cap * vsize // 4
+    out = np.zeros(dense_stream_bytes(n, cap, vsize), dtype=np.uint8)
+    hdr = out[:20].view(np.int32)
+    hdr[0] = 1
+    hdr[1] = table_id
+    out[8:16].view(np.uint64)[0] = vsize
+    hdr[4] = n
+    recs = out[20:].view(np.int32).reshape(n, words_per_rec)
+    recs[:, 0] = np.asarray(row_ids, dtype=np.int32)
+    recs[:, 1:] = payload.view(np.int32).reshape(n, words_per_rec - 1)
+    return out
+
+
+def sparse_stream_np(table_id, vsize, rows):
+    """rows: list of (row_id, cols int32[n], vals V[n]); one single-table sparse stream."""
+    parts = [np.array([1, table_id], dtype=np.int32).view(np.uint8),
+             np.array([vsize], dtype=np.uint64).view(np.uint8),
+             np.array([len(rows)], dtype=np.int32).view(np.uint8)]
+    for rid, cols, vals in rows:
+        parts.append(np.array([rid, len(cols)], dtype=np.int32).view(np.uint8))
+        parts.append(np.ascontiguousarray(cols, dtype=np.int32).view(np.uint8))
+        parts.append(np.ascontiguousarray(vals).view(np.uint8))
+    return np.concatenate(parts)
+
+
+def dense_stream_torch(table_id, row_ids, payload):
+    """Device-side builder: row_ids int32[n] and payload V[n, cap] are torch tensors on the
+    GPU; returns a uint8 CUDA tensor holding the stream (4-byte aligned)."""
+    import torch
+    n, cap = payload.shape
+    vsize = payload.element_size()
+    words_per_rec = 1 + cap * vsize // 4
+    nbytes = dense_stream_bytes(n, cap, vsize)
+    out = torch.empty(nbytes // 4, dtype=torch.int32, device=payload.device)
+    hdr = torch.tensor([1, table_id, vsize, 0, n], dtype=torch.int32)   # update_size hi word = 0
+    out[:5].copy_(hdr)
+    recs = out[5:].view(n, words_per_rec)
+    recs[:, 0].copy_(row_ids.to(torch.int32))
+    recs[:, 1:].copy_(payload.contiguous().view(torch.int32).view(n, words_per_rec - 1))
+    return out.view(torch.uint8)

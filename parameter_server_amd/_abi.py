@@ -57,8 +57,9 @@ _lib = None
 
 
 def header_functions():
-    """Names of every function declared in include/psx.h."""
-    src = open(HEADER_PATH).read()
+    """Names of every function declared in include/*.h."""
+    inc = os.path.dirname(HEADER_PATH)
+    src = "".join(open(os.path.join(inc, f)).read() for f in sorted(os.listdir(inc)) if f.endswith(".h"))
     return sorted(set(re.findall(r"\b(psx_[a-z_0-9]+)\s*\(", src)))
 
 
@@ -96,6 +97,8 @@ def load():
         "psx_timing_enable": ([vp, i32], ctypes.c_int),
         "psx_timing_read": ([vp, ctypes.c_char_p, P(ctypes.c_double), P(i64)], ctypes.c_int),
         "psx_timing_reset": ([vp], ctypes.c_int),
+        "psx_debug_set_variant": ([i32, i32], i32),
+        "psx_debug_get_variant": ([i32], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -52,6 +52,14 @@ struct Seg {
   int32_t sparse;     // 1: record offsets live in recoff[recoff_base[b] + k]
 };
 
+// Inverse-index addressing: entry (slot s, message b) lives at inv[s*ss + b*sb].
+// Batch-major ([b][s]: ss = 1, sb = max_rows) keeps one message's scattered writes
+// inside a max_rows*4-byte window so the XCD L2s can merge them.
+struct InvLayout {
+  int64_t ss;
+  int64_t sb;
+};
+
 // Arguments of dense_apply (passed by value).
 struct DenseArgs {
   StreamSet ss;
@@ -65,6 +73,8 @@ struct DenseArgs {
   void *table;
   uint8_t *flags;
   int32_t *inv;
+  int64_t inv_ss;
+  int64_t inv_sb;
   const uint32_t *counters;
   uint32_t *sticky;
   uint32_t *call_status;

@@ -117,7 +117,7 @@ __device__ __forceinline__ int64_t slot_of(int32_t rid, const Geo &g) {
 
 // dense_index: grid-stride over every record of every message containing table t.
 __global__ void __launch_bounds__(256) dense_index_kernel(StreamSet ss, const Seg *segs, int t, int B,
-                                                         int64_t stride, Geo g, int32_t *inv,
+                                                         int64_t stride, Geo g, int32_t *inv, InvLayout L,
                                                          uint32_t *call_status) {
   const int64_t gsz = (int64_t)gridDim.x * blockDim.x;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -129,13 +129,13 @@ __global__ void __launch_bounds__(256) dense_index_kernel(StreamSet ss, const Se
       const int32_t rid = ld32(base + i * stride);
       const int64_t s = slot_of(rid, g);
       if (s < 0) { atomicOr(call_status, kStRowRange); continue; }
-      inv[s * B + b] = (int32_t)i;
+      inv[s * L.ss + b * L.sb] = (int32_t)i;
     }
   }
 }
 
 // dense_verify: counters[t][b] = number of slots claimed by message b.
-__global__ void __launch_bounds__(256) dense_verify_kernel(const int32_t *inv, int t, int B,
+__global__ void __launch_bounds__(256) dense_verify_kernel(const int32_t *inv, InvLayout L, int t, int B,
                                                           int64_t max_rows, uint32_t *counters) {
   __shared__ uint32_t part[kMaxFused];
   if (threadIdx.x < kMaxFused) part[threadIdx.x] = 0;
@@ -145,10 +145,10 @@ __global__ void __launch_bounds__(256) dense_verify_kernel(const int32_t *inv, i
   for (int b = 0; b < kMaxFused; ++b) cnt[b] = 0;
   const int64_t gsz = (int64_t)gridDim.x * blockDim.x;
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < max_rows; s += gsz) {
-    const int32_t *row = inv + s * B;
+    const int32_t *row = inv + s * L.ss;
 #pragma unroll
     for (int b = 0; b < kMaxFused; ++b)
-      if (b < B) cnt[b] += row[b] >= 0 ? 1u : 0u;
+      if (b < B) cnt[b] += row[b * L.sb] >= 0 ? 1u : 0u;
   }
 #pragma unroll
   for (int b = 0; b < kMaxFused; ++b) {
@@ -231,10 +231,10 @@ __global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
   for (int b = 0; b < BMAX; ++b) {
     idx[b] = -1;
     if (b < B && in_range) {
-      idx[b] = a.inv[my_slot * B + b];
+      idx[b] = a.inv[my_slot * a.inv_ss + b * a.inv_sb];
       if (idx[b] >= 0) {
         touched = true;
-        a.inv[my_slot * B + b] = -1;
+        a.inv[my_slot * a.inv_ss + b * a.inv_sb] = -1;
       }
     }
   }
@@ -286,6 +286,239 @@ __global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// dense_apply_v2: 16 bytes per lane per load.  Record payloads start 4 bytes after a
+// row id, so they are only 4-byte aligned: the loads are unaligned global_load_dwordx4
+// (gfx950 runs HSA in unaligned-access mode; hipcc emits dwordx4 for align-4 memcpy).
+// Record loads may be non-temporal (read once).  TILE slots per wave-tile; PAIR touched
+// slots in flight per wave; the grid is sized to the resident capacity and strides
+// over tiles, so the tail is one tile, not one wave-lifetime.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const uint8_t *p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(p));
+  } else {
+    u32x4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+  }
+}
+__device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
+
+template <typename V> struct Vec;
+template <> struct Vec<float> {
+  __device__ static u32x4 add(u32x4 a, u32x4 b) {
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(__uint_as_float(a[i]) + __uint_as_float(b[i]));
+    return r;
+  }
+};
+template <> struct Vec<int32_t> {
+  __device__ static u32x4 add(u32x4 a, u32x4 b) { return a + b; }
+};
+template <> struct Vec<double> {
+  __device__ static u32x4 add(u32x4 a, u32x4 b) {
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      double x = __longlong_as_double((long long)(((uint64_t)a[2 * i + 1] << 32) | a[2 * i]));
+      double y = __longlong_as_double((long long)(((uint64_t)b[2 * i + 1] << 32) | b[2 * i]));
+      uint64_t z = (uint64_t)__double_as_longlong(x + y);
+      r[2 * i] = (uint32_t)z;
+      r[2 * i + 1] = (uint32_t)(z >> 32);
+    }
+    return r;
+  }
+};
+template <> struct Vec<int64_t> {
+  __device__ static u32x4 add(u32x4 a, u32x4 b) {
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint64_t z = (((uint64_t)a[2 * i + 1] << 32) | a[2 * i]) + (((uint64_t)b[2 * i + 1] << 32) | b[2 * i]);
+      r[2 * i] = (uint32_t)z;
+      r[2 * i + 1] = (uint32_t)(z >> 32);
+    }
+    return r;
+  }
+};
+
+template <typename V, int BMAX, int TILE, bool NT, int PAIR>
+__global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
+  constexpr int VS = (int)sizeof(V);
+  constexpr int EPV = 16 / VS;        // elements per 16-byte lane vector
+  constexpr int CHUNK = 64 * EPV;     // elements per wave-wide vector pass
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int B = a.B;
+
+  bool skip = (*a.call_status & kStFatal) != 0 || (*a.sticky & kStDuplicateRow) != 0;
+  bool dup = false;
+  const uint8_t *pay0[BMAX];   // payload of record 0 of message b (nullptr: table absent)
+#pragma unroll
+  for (int b = 0; b < BMAX; ++b) {
+    pay0[b] = nullptr;
+    if (b < B) {
+      const Seg sg = a.segs[b * kMaxTables + a.t];
+      if (sg.rec0 >= 0 && !sg.sparse) {
+        pay0[b] = a.ss.data[b] + sg.rec0 + 4;
+        if (a.counters[a.t * kMaxFused + b] != (uint32_t)sg.num_rows) dup = true;
+      }
+    }
+  }
+  if (dup && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.call_status, kStDuplicateRow);
+  skip = skip || dup;
+
+  const int64_t vec_elems = (a.cap / EPV) * EPV;   // elements covered by full lane vectors
+  const int64_t row_bytes = a.row_cap * VS;
+  uint8_t *table = reinterpret_cast<uint8_t *>(a.table);
+  const int64_t ntiles = (a.max_rows + TILE - 1) / TILE;
+
+  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
+    const int64_t s0 = tile * TILE;
+    const int64_t my_slot = s0 + lane;
+    const bool mine = lane < TILE && my_slot < a.max_rows;
+    int32_t idx[BMAX];
+    bool touched = false;
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) {
+      idx[b] = -1;
+      if (b < B && mine) {
+        idx[b] = a.inv[my_slot * a.inv_ss + b * a.inv_sb];
+        if (idx[b] >= 0) {
+          touched = true;
+          a.inv[my_slot * a.inv_ss + b * a.inv_sb] = -1;
+        }
+      }
+    }
+    if (skip) continue;
+    if (touched) a.flags[my_slot] = 3;   // exists | dirty
+    uint64_t live = __ballot(touched);
+
+    while (live) {
+      int ks[PAIR];
+      bool has[PAIR];
+#pragma unroll
+      for (int q = 0; q < PAIR; ++q) {
+        has[q] = live != 0;
+        ks[q] = has[q] ? __builtin_ctzll(live) : 0;
+        if (has[q]) live &= live - 1;
+      }
+      const uint8_t *rp[PAIR][BMAX];
+      bool pres[PAIR][BMAX];
+      uint8_t *trow[PAIR];
+#pragma unroll
+      for (int q = 0; q < PAIR; ++q) {
+        trow[q] = table + (s0 + ks[q]) * row_bytes;
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) {
+          const int32_t i = __builtin_amdgcn_readlane(idx[b], ks[q]);
+          pres[q][b] = has[q] && pay0[b] != nullptr && i >= 0;
+          rp[q][b] = pres[q][b] ? pay0[b] + (int64_t)i * a.stride : a.zero_chunk;
+        }
+      }
+      for (int64_t c0 = 0; c0 < vec_elems; c0 += CHUNK) {
+        const int64_t e0 = c0 + (int64_t)lane * EPV;
+        const bool full = e0 < vec_elems;
+        u32x4 t[PAIR];
+        u32x4 u[PAIR][BMAX];
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          t[q] = (full && has[q]) ? load16<false>(trow[q] + e0 * VS) : u32x4{0, 0, 0, 0};
+#pragma unroll
+          for (int b = 0; b < BMAX; ++b) {
+            const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * VS : a.zero_chunk + lane * 16;
+            u[q][b] = full ? load16<NT>(src) : u32x4{0, 0, 0, 0};
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          u32x4 acc = t[q];
+#pragma unroll
+          for (int b = 0; b < BMAX; ++b)
+            if (pres[q][b]) acc = Vec<V>::add(acc, u[q][b]);
+          if (full && has[q]) store16(trow[q] + e0 * VS, acc);
+        }
+      }
+      // ragged tail (cap % EPV elements): element-wise on the first lanes
+      const int64_t tail = a.cap - vec_elems;
+      if (tail) {
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          if (has[q] && lane < tail) {
+            const int64_t e = vec_elems + lane;
+            V acc = *reinterpret_cast<const V *>(trow[q] + e * VS);
+#pragma unroll
+            for (int b = 0; b < BMAX; ++b)
+              if (pres[q][b]) acc = Elem<V>::add(acc, Elem<V>::load_rec(rp[q][b] + e * VS));
+            *reinterpret_cast<V *>(trow[q] + e * VS) = acc;
+          }
+        }
+      }
+    }
+  }
+}
+
+// dense_index_v2: flattened (message, record) space, UNROLL row-id loads in flight per
+// thread before any store.
+template <int UNROLL, bool NT>
+__global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const Seg *segs, int t, int B,
+                                                            int64_t stride, Geo g, int32_t *inv, InvLayout L,
+                                                            uint32_t *call_status) {
+  __shared__ int64_t pre[kMaxFused + 1];
+  __shared__ const uint8_t *base[kMaxFused];
+  if (threadIdx.x == 0) {
+    int64_t acc = 0;
+    for (int b = 0; b < kMaxFused; ++b) {
+      pre[b] = acc;
+      base[b] = nullptr;
+      if (b < B) {
+        const Seg sg = segs[b * kMaxTables + t];
+        if (sg.rec0 >= 0 && !sg.sparse) {
+          acc += sg.num_rows;
+          base[b] = ss.data[b] + sg.rec0;
+        }
+      }
+    }
+    pre[kMaxFused] = acc;
+  }
+  __syncthreads();
+  const int64_t total = pre[kMaxFused];
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r0 < total; r0 += G * UNROLL) {
+    int32_t rid[UNROLL];
+    int32_t bi[UNROLL];
+    int64_t ii[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t r = r0 + u * G;
+      bi[u] = -1;
+      ii[u] = 0;
+      rid[u] = 0;
+      if (r < total) {
+        int b = 0;
+        while (b + 1 < B && pre[b + 1] <= r) ++b;
+        bi[u] = b;
+        ii[u] = r - pre[b];
+        const int32_t *p = reinterpret_cast<const int32_t *>(base[b] + ii[u] * stride);
+        rid[u] = NT ? __builtin_nontemporal_load(p) : *p;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (bi[u] < 0) continue;
+      const int64_t s = slot_of(rid[u], g);
+      if (s < 0) { atomicOr(call_status, kStRowRange); continue; }
+      inv[s * L.ss + bi[u] * L.sb] = (int32_t)ii[u];
+    }
+  }
+}
+
 // finish_call: fold the per-call status into the sticky word and free the ring slot.
 __global__ void finish_call_kernel(uint32_t *sticky, uint32_t *call_status) {
   if (threadIdx.x == 0) {
@@ -325,33 +558,89 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
   return hipGetLastError();
 }
 
+int g_index_variant = 2;
+int g_apply_variant = 4;
+int g_inv_layout = 1;
+
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows,
-                              int32_t *inv, uint32_t *call_status, hipStream_t st) {
+                              int32_t *inv, InvLayout L, uint32_t *call_status, hipStream_t st) {
   Geo g{row_offset, row_stride, max_rows};
-  hipLaunchKernelGGL(dense_index_kernel, dim3(4096), dim3(256), 0, st, ss, segs, t, B, stride, g,
-                     inv, call_status);
+  switch (g_index_variant) {
+    case 0:
+      hipLaunchKernelGGL(dense_index_kernel, dim3(4096), dim3(256), 0, st, ss, segs, t, B, stride, g,
+                         inv, L, call_status);
+      break;
+    case 1:
+      hipLaunchKernelGGL((dense_index_v2_kernel<8, false>), dim3(2048), dim3(256), 0, st, ss, segs, t, B,
+                         stride, g, inv, L, call_status);
+      break;
+    default:
+      hipLaunchKernelGGL((dense_index_v2_kernel<8, true>), dim3(2048), dim3(256), 0, st, ss, segs, t, B,
+                         stride, g, inv, L, call_status);
+      break;
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_dense_verify(const int32_t *inv, int t, int B, int64_t max_rows, uint32_t *counters,
-                               hipStream_t st) {
+hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, int64_t max_rows,
+                               uint32_t *counters, hipStream_t st) {
   int64_t blocks = (max_rows + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(dense_verify_kernel, dim3((unsigned)blocks), dim3(256), 0, st, inv, t, B, max_rows,
+  hipLaunchKernelGGL(dense_verify_kernel, dim3((unsigned)blocks), dim3(256), 0, st, inv, L, t, B, max_rows,
                      counters);
   return hipGetLastError();
 }
 
+// Resident-capacity grid for a persistent-style kernel (blocks per CU x CUs).
+template <typename K>
+static unsigned resident_blocks(K kernel, int64_t want) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  int64_t cap = (int64_t)per_cu * cus;
+  if (want < cap) cap = want;
+  return (unsigned)(cap < 1 ? 1 : cap);
+}
+
+template <typename V, int BMAX, int TILE, bool NT, int PAIR>
+static void launch_v2(const DenseArgs &a, hipStream_t st) {
+  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR>;
+  const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
+  const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <typename V, int BMAX>
+static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
+  switch (g_apply_variant) {
+    case 0: {
+      const int64_t tiles = (a.max_rows + 63) / 64;
+      hipLaunchKernelGGL((dense_apply_kernel<V, BMAX>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, a);
+      break;
+    }
+    case 1: launch_v2<V, BMAX, 64, false, 1>(a, st); break;
+    case 2: launch_v2<V, BMAX, 64, true, 1>(a, st); break;
+    case 3: launch_v2<V, BMAX, 16, true, 1>(a, st); break;
+    case 4: launch_v2<V, BMAX, 16, true, 2>(a, st); break;
+    default: launch_v2<V, BMAX, 64, true, 2>(a, st); break;
+  }
+}
+
 template <typename V>
 static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
-  const int64_t tiles = (a.max_rows + 63) / 64;
-  const int64_t blocks = (tiles + 3) / 4;
   if (a.B <= 8)
-    hipLaunchKernelGGL((dense_apply_kernel<V, 8>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    launch_apply_bmax<V, 8>(a, st);
   else
-    hipLaunchKernelGGL((dense_apply_kernel<V, 16>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    launch_apply_bmax<V, 16>(a, st);
   return hipGetLastError();
 }
 

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -21,9 +22,10 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
                          uint32_t *call_status, uint32_t *counters, hipStream_t st);
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
-                              uint32_t *call_status, hipStream_t st);
-hipError_t launch_dense_verify(const int32_t *inv, int t, int B, int64_t max_rows, uint32_t *counters,
-                               hipStream_t st);
+                              InvLayout L, uint32_t *call_status, hipStream_t st);
+hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, int64_t max_rows,
+                               uint32_t *counters, hipStream_t st);
+extern int g_inv_layout;
 hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, hipStream_t st);
 hipError_t launch_flags_or(uint8_t *flags, int64_t first, int64_t num, uint8_t bits, hipStream_t st);
 hipError_t launch_flags_and(uint8_t *flags, int64_t num, uint8_t bits, hipStream_t st);
@@ -257,13 +259,15 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
     TableState &t = c->tables[ti];
     if (t.cfg.row_kind != PSX_ROW_DENSE || !t.cfg.oplog_dense_serialized) continue;
     const int64_t stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
+    // 0: slot-major [s][b]; 1: batch-major [b][s] (default)
+    const psx::InvLayout L = psx::g_inv_layout ? psx::InvLayout{1, t.cfg.max_rows} : psx::InvLayout{n, 1};
     st = timed(c, "dense_index", [&] {
       return psx::launch_dense_index(ss, c->d_segs, (int)ti, n, stride, t.cfg.row_offset,
-                                     t.cfg.row_stride, t.cfg.max_rows, t.d_inv, call_st, c->stream);
+                                     t.cfg.row_stride, t.cfg.max_rows, t.d_inv, L, call_st, c->stream);
     });
     if (st) return st;
     st = timed(c, "dense_verify", [&] {
-      return psx::launch_dense_verify(t.d_inv, (int)ti, n, t.cfg.max_rows, c->d_counters, c->stream);
+      return psx::launch_dense_verify(t.d_inv, L, (int)ti, n, t.cfg.max_rows, c->d_counters, c->stream);
     });
     if (st) return st;
     psx::DenseArgs a{};
@@ -278,6 +282,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
     a.table = t.d_data;
     a.flags = t.d_flags;
     a.inv = t.d_inv;
+    a.inv_ss = L.ss;
+    a.inv_sb = L.sb;
     a.counters = c->d_counters;
     a.sticky = sticky;
     a.call_status = call_st;
@@ -671,3 +677,40 @@ psx_status psx_timing_reset(psx_ctx *c) {
 }
 
 }  // extern "C"
+
+// ---- experiment hooks (include/psx_debug.h) ----------------------------------
+#include "../../include/psx_debug.h"
+namespace psx {
+extern int g_index_variant;
+extern int g_apply_variant;
+extern int g_inv_layout;
+}  // namespace psx
+
+extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
+  int *v = which == PSX_VARIANT_DENSE_INDEX ? &psx::g_index_variant
+           : which == PSX_VARIANT_DENSE_APPLY ? &psx::g_apply_variant
+           : which == PSX_VARIANT_INV_LAYOUT ? &psx::g_inv_layout : nullptr;
+  if (!v) return -1;
+  int old = *v;
+  *v = variant;
+  return old;
+}
+
+extern "C" int32_t psx_debug_get_variant(int32_t which) {
+  if (which == PSX_VARIANT_DENSE_INDEX) return psx::g_index_variant;
+  if (which == PSX_VARIANT_DENSE_APPLY) return psx::g_apply_variant;
+  if (which == PSX_VARIANT_INV_LAYOUT) return psx::g_inv_layout;
+  return -1;
+}
+
+namespace {
+// PSX_INDEX_VARIANT / PSX_APPLY_VARIANT override the default kernels at load time
+// (used to run the parity suite against every variant).
+struct VariantEnv {
+  VariantEnv() {
+    if (const char *v = getenv("PSX_INDEX_VARIANT")) psx::g_index_variant = atoi(v);
+    if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
+    if (const char *v = getenv("PSX_INV_LAYOUT")) psx::g_inv_layout = atoi(v);
+  }
+} variant_env;
+}  // namespace

@@ -243,3 +243,36 @@ def test_large_fused_apply_against_torch_reference():
 def test_smoke_entry():
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("index_variant", [0, 1, 2])
+@pytest.mark.parametrize("layout", [0, 1])
+def test_every_kernel_variant_bit_exact(apply_variant, index_variant, layout):
+    """Every selectable index/apply kernel variant (include/psx_debug.h) matches the oracle,
+    including a ragged row tail (cap 301) and 8-byte values."""
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    old_a = L.psx_debug_set_variant(1, apply_variant)
+    old_i = L.psx_debug_set_variant(0, index_variant)
+    old_l = L.psx_debug_set_variant(2, layout)
+    try:
+        for dt, cap, B in [(F32, 301, 9), (F64, 130, 8), (I32, 64, 3)]:
+            rng = np.random.RandomState(apply_variant * 10 + index_variant + cap)
+            rows = 333
+            srv, orc = _pair(dt, rows, cap)
+            init = _vals(rng, (rows, cap), dt)
+            srv.load_rows(1, 0, init)
+            orc.load_dense_rows(1, 0, init)
+            streams = []
+            for b in range(B):
+                n = rng.randint(1, rows + 1)
+                streams.append(wire.dense_stream_np(1, rng.permutation(rows)[:n].astype(np.int32),
+                                                    _vals(rng, (n, cap), dt)))
+            _apply_both(srv, orc, streams, [100 + b for b in range(B)], [0] * B)
+            assert np.array_equal(_bits(srv.read_rows(1, 0, rows)), _bits(orc.read_dense_rows(1, 0, rows)))
+            srv.close()
+    finally:
+        L.psx_debug_set_variant(1, old_a)
+        L.psx_debug_set_variant(0, old_i)
+        L.psx_debug_set_variant(2, old_l)

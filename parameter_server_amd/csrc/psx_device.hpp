@@ -81,4 +81,37 @@ struct DenseArgs {
   const uint8_t *zero_chunk;   // >= 2 KiB of zeros, stands in for absent messages
 };
 
+// Fast-path dense tables of one call (for the duplicate-row gate).
+struct TableMask {
+  int32_t n;
+  int32_t t[kMaxTables];
+};
+
+// Arguments of the ordered path (psx_ordered.hip).
+struct OrdArgs {
+  StreamSet ss;
+  const Seg *segs;
+  int t;
+  int B;
+  int kind;               // psx_row_kind
+  int dense_records;      // 1: records are dense V[cap] (duplicate-row replay)
+  int64_t stride;         // dense record stride
+  int64_t cap;            // dense_row_oplog_capacity
+  int64_t row_cap;        // row_capacity (dense width; bound on sparse columns)
+  int64_t row_offset, row_stride, max_rows;
+  const uint64_t *recoff;
+  int32_t *cnt;
+  int32_t *off;
+  int32_t *tsum;
+  int32_t *list;
+  void *dense;
+  int32_t *nent;
+  uint8_t *entries;
+  int64_t max_entries;
+  uint8_t *flags;
+  uint32_t *call_status;
+  const uint32_t *sticky;
+  int force;              // replay: ignore the sticky duplicate flag
+};
+
 }  // namespace psx

@@ -520,9 +520,10 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
 }
 
 // finish_call: fold the per-call status into the sticky word and free the ring slot.
-__global__ void finish_call_kernel(uint32_t *sticky, uint32_t *call_status) {
+__global__ void finish_call_kernel(uint32_t *sticky, uint32_t *call_status, uint32_t *call_log) {
   if (threadIdx.x == 0) {
     *sticky |= *call_status;
+    *call_log = *call_status;
     *call_status = 0;
   }
 }
@@ -547,6 +548,11 @@ __global__ void gather_rows_kernel(const V *table, const int64_t *slots, int32_t
   const int64_t s = slots[r];
   for (int64_t e = threadIdx.x; e < row_cap; e += blockDim.x)
     out[(int64_t)r * row_cap + e] = s >= 0 ? table[s * row_cap + e] : V(0);
+}
+
+__global__ void gather_flags_kernel(const uint8_t *flags, const int64_t *slots, int32_t n, uint8_t *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = slots[i] >= 0 ? flags[slots[i]] : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -653,8 +659,8 @@ hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st) {
   }
 }
 
-hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, hipStream_t st) {
-  hipLaunchKernelGGL(finish_call_kernel, dim3(1), dim3(64), 0, st, sticky, call_status);
+hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, uint32_t *call_log, hipStream_t st) {
+  hipLaunchKernelGGL(finish_call_kernel, dim3(1), dim3(64), 0, st, sticky, call_status, call_log);
   return hipGetLastError();
 }
 
@@ -685,6 +691,13 @@ hipError_t launch_gather_rows(int dtype, const void *table, const int64_t *slots
     default: hipLaunchKernelGGL(gather_rows_kernel<int64_t>, dim3(n), dim3(256), 0, st,
                                 (const int64_t *)table, slots, n, row_cap, (int64_t *)out); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_flags(const uint8_t *flags, const int64_t *slots, int32_t n, uint8_t *out,
+                               hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, st, flags, slots, n, out);
   return hipGetLastError();
 }
 

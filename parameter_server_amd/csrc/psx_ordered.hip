@@ -1,0 +1,526 @@
+// psx_ordered.hip — the ordered apply path (counting sort by slot, then one wave per row).
+//
+// Used for every table whose records are sparse ({int32 n; int32 cols[n]; V vals[n]},
+// AbstractRowOpLog::ParseSparseSerializedOpLog, abstract_row_oplog.hpp:64-78) and, as a
+// replay, for dense tables when a row occurs twice inside one message.
+//
+//   ordered_count  cnt[slot] += 1 per record (also validates row range / columns)
+//   scan_*         off = exclusive prefix of cnt (max_rows + 1 entries)
+//   ordered_fill   list[off[slot] + --cnt[slot]] = flattened record number r
+//                  (r orders records by (message, position) = reference apply order;
+//                  cnt returns to zero, the invariant between calls)
+//   ordered_apply  one wave per touched slot: sort the slot's r-list, then apply the
+//                  records in order with the reference store semantics:
+//                    DenseRow     VectorStore::Inc          vector_store.hpp:100-102
+//                    SortedMapRow SortedVectorMapStore::Inc sorted_vector_map_store.hpp:175-197,305-337
+//                    SparseRow    MapStore::Inc             map_store.hpp:60-65
+//                  Sorted-map rows are staged in LDS and updated with wave-parallel
+//                  find / bubble / compact, reproducing the reference's entry ORDER
+//                  byte for byte (it is history dependent: found keys are not re-sorted).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "psx_device.hpp"
+
+namespace psx {
+
+
+__device__ __forceinline__ int32_t o_ld32(const uint8_t *p) { return *reinterpret_cast<const int32_t *>(p); }
+
+__device__ __forceinline__ int64_t o_slot(int32_t rid, const OrdArgs &a) {
+  int64_t d = (int64_t)rid - a.row_offset;
+  if (d < 0) return -1;
+  if (a.row_stride != 1) {
+    if (d % a.row_stride) return -1;
+    d /= a.row_stride;
+  }
+  return d < a.max_rows ? d : -1;
+}
+
+__device__ __forceinline__ bool o_gate(const OrdArgs &a) {
+  const uint32_t st = *a.call_status;
+  if (st & (kStFatal | kStDuplicateRow)) return false;
+  if (!a.force && (*a.sticky & kStDuplicateRow)) return false;
+  return true;
+}
+
+// Flattened record space r in [0, pre[B]) in (message, position) order.
+struct RecSpace {
+  int64_t pre[kMaxFused + 1];
+  int64_t first[kMaxFused];   // dense: byte offset of record 0; sparse: index into recoff
+  int32_t sparse[kMaxFused];
+};
+
+__device__ void build_space(const OrdArgs &a, RecSpace &rs) {
+  int64_t acc = 0;
+  for (int b = 0; b < kMaxFused; ++b) {
+    rs.pre[b] = acc;
+    rs.first[b] = 0;
+    rs.sparse[b] = 0;
+    if (b < a.B) {
+      const Seg sg = a.segs[b * kMaxTables + a.t];
+      if (sg.rec0 >= 0) {
+        acc += sg.num_rows;
+        rs.first[b] = sg.rec0;
+        rs.sparse[b] = sg.sparse;
+      }
+    }
+  }
+  rs.pre[kMaxFused] = acc;
+}
+
+// Locate record r: message b and the byte offset of its row id.
+__device__ __forceinline__ void locate(const OrdArgs &a, const RecSpace &rs, int64_t r, int &b, uint64_t &off) {
+  b = 0;
+  while (b + 1 < a.B && rs.pre[b + 1] <= r) ++b;
+  const int64_t k = r - rs.pre[b];
+  off = rs.sparse[b] ? a.recoff[rs.first[b] + k] : (uint64_t)(rs.first[b] + k * a.stride);
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
+  __shared__ RecSpace rs;
+  if (threadIdx.x == 0) build_space(a, rs);
+  __syncthreads();
+  const int64_t total = rs.pre[kMaxFused];
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
+    int b;
+    uint64_t off;
+    locate(a, rs, r, b, off);
+    const uint8_t *p = a.ss.data[b] + off;
+    const int64_t s = o_slot(o_ld32(p), a);
+    if (s < 0) { atomicOr(a.call_status, kStRowRange); continue; }
+    if (!a.dense_records && a.kind == 0) {
+      // sparse record into a dense row: every column must lie inside the row
+      const int32_t n = o_ld32(p + 4);
+      const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
+      for (int32_t i = 0; i < n; ++i)
+        if (cols[i] < 0 || cols[i] >= a.row_cap) { atomicOr(a.call_status, kStCapacity); break; }
+    }
+    atomicAdd(&a.cnt[s], 1);
+  }
+}
+
+// Three-phase exclusive scan of cnt[0, n) into off[0, n]; tiles of 1024.
+__global__ void __launch_bounds__(256) scan_tiles_kernel(const int32_t *cnt, int64_t n, int32_t *off,
+                                                        int32_t *tsum) {
+  __shared__ int32_t wsum[4];
+  const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x * 4;
+  int32_t v[4];
+  int32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = base + j < n ? cnt[base + j] : 0;
+    s += v[j];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t incl = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    int32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int32_t wpre = 0;
+  for (int i = 0; i < w; ++i) wpre += wsum[i];
+  int32_t run = wpre + incl - s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (base + j < n) off[base + j] = run;
+    run += v[j];
+  }
+  if (threadIdx.x == 255) tsum[blockIdx.x] = wpre + incl;
+}
+
+__global__ void __launch_bounds__(1024) scan_sums_kernel(int32_t *tsum, int64_t ntiles, int32_t *off, int64_t n) {
+  __shared__ int32_t carry;
+  __shared__ int32_t wsum[16];
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t c = 0; c < ntiles; c += 1024) {
+    const int64_t i = c + threadIdx.x;
+    const int32_t x = i < ntiles ? tsum[i] : 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int32_t incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      int32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int32_t wpre = 0;
+    for (int k = 0; k < w; ++k) wpre += wsum[k];
+    const int32_t excl = carry + wpre + incl - x;
+    __syncthreads();
+    if (i < ntiles) tsum[i] = excl;
+    if (threadIdx.x == 1023) carry = excl + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) off[n] = carry;
+}
+
+__global__ void __launch_bounds__(256) scan_add_kernel(int32_t *off, int64_t n, const int32_t *tsum) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) off[i] += tsum[i >> 10];
+}
+
+__global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
+  __shared__ RecSpace rs;
+  if (threadIdx.x == 0) build_space(a, rs);
+  __syncthreads();
+  const int64_t total = rs.pre[kMaxFused];
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
+    int b;
+    uint64_t off;
+    locate(a, rs, r, b, off);
+    const int64_t s = o_slot(o_ld32(a.ss.data[b] + off), a);
+    if (s < 0) continue;
+    const int32_t p = atomicSub(&a.cnt[s], 1) - 1;
+    a.list[a.off[s] + p] = (int32_t)r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-level helpers.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename V> struct OV;
+template <> struct OV<float> {
+  __device__ static float add(float x, float y) { return x + y; }
+};
+template <> struct OV<double> {
+  __device__ static double add(double x, double y) { return x + y; }
+};
+template <> struct OV<int32_t> {
+  __device__ static int32_t add(int32_t x, int32_t y) { return (int32_t)((uint32_t)x + (uint32_t)y); }
+};
+template <> struct OV<int64_t> {
+  __device__ static int64_t add(int64_t x, int64_t y) { return (int64_t)((uint64_t)x + (uint64_t)y); }
+};
+
+// Records hold V values at 4-byte alignment: read/write them bytewise-safe.
+template <typename V>
+__device__ __forceinline__ V ldv(const uint8_t *p) {
+  V v;
+  __builtin_memcpy(&v, p, sizeof(V));
+  return v;
+}
+template <typename V>
+__device__ __forceinline__ void stv(uint8_t *p, V v) {
+  __builtin_memcpy(p, &v, sizeof(V));
+}
+
+// Entry<V>{int32 first; V second} with the C++ layout: 8 bytes, or 16 with 4 pad bytes.
+template <typename V> struct Ent {
+  static constexpr int ES = sizeof(V) == 4 ? 8 : 16;
+  static constexpr int VO = sizeof(V) == 4 ? 4 : 8;
+};
+
+// Sort the r-list of one slot (L <= 64) by value, one entry per lane: rank = number of
+// smaller entries (r values are distinct).
+__device__ __forceinline__ int32_t wave_rank_sort(int32_t r, int L, int lane, int32_t *scratch) {
+  int rank = 0;
+  for (int k = 0; k < L; ++k) {
+    const int32_t x = __shfl(r, k, 64);
+    rank += (x < r) ? 1 : 0;
+  }
+  if (lane < L) scratch[rank] = r;
+  wave_sync();
+  const int32_t out = lane < L ? scratch[lane] : 0;
+  wave_sync();
+  return out;
+}
+
+template <typename V, int KIND>
+__global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
+  extern __shared__ __align__(16) uint8_t dyn[];
+  __shared__ int32_t sort_scratch[4][64];
+  __shared__ RecSpace rs;
+  if (threadIdx.x == 0) build_space(a, rs);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  if (wib >= wpb) return;
+  const bool go = o_gate(a);
+  constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
+  uint8_t *E = dyn + (size_t)wib * (size_t)a.max_entries * ES;   // this wave's row image
+  const int64_t wave_g = (int64_t)blockIdx.x * wpb + wib;
+  const int64_t nwaves = (int64_t)gridDim.x * wpb;
+  const int64_t ntiles = (a.max_rows + 63) / 64;
+
+  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
+    const int64_t s0 = tile * 64;
+    const int64_t ms = s0 + lane;
+    int32_t o0 = 0, o1 = 0;
+    if (ms < a.max_rows) {
+      o0 = a.off[ms];
+      o1 = a.off[ms + 1];
+    }
+    const bool touched = o1 > o0;
+    if (!go) continue;
+    if (touched) a.flags[ms] = 3;
+    uint64_t live = __ballot(touched);
+    while (live) {
+      const int k = __builtin_ctzll(live);
+      live &= live - 1;
+      const int64_t slot = s0 + k;
+      const int32_t beg = __shfl(o0, k, 64);
+      const int32_t L = __shfl(o1, k, 64) - beg;
+      int32_t *lst = a.list + beg;
+      // order the slot's records by r = (message, position)
+      int32_t mine = 0;
+      if (L <= 64) {
+        mine = wave_rank_sort(lane < L ? lst[lane] : 0x7fffffff, L, lane, sort_scratch[wib]);
+      } else if (lane == 0) {
+        for (int32_t i = 1; i < L; ++i) {   // rare: > 64 records for one row in one call
+          const int32_t x = lst[i];
+          int32_t j = i - 1;
+          while (j >= 0 && lst[j] > x) { lst[j + 1] = lst[j]; --j; }
+          lst[j + 1] = x;
+        }
+      }
+      if (L > 64) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+      }
+
+      // stage the row
+      int32_t n = 0;
+      if (KIND != 0) {
+        n = a.nent[slot];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.entries + slot * a.max_entries * ES);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(E);
+        for (int32_t w = lane; w < n * (ES / 4); w += 64) dst[w] = src[w];
+        wave_sync();
+      }
+      uint8_t *drow = reinterpret_cast<uint8_t *>(a.dense) + slot * a.row_cap * (int64_t)sizeof(V);
+
+      for (int32_t q = 0; q < L; ++q) {
+        const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
+        int b;
+        uint64_t roff;
+        locate(a, rs, r, b, roff);
+        const uint8_t *rec = a.ss.data[b] + roff;
+        if (a.dense_records) {
+          // duplicate-row replay of a dense record: row[e] += rec[e] (lane owns e)
+          for (int64_t e = lane; e < a.cap; e += 64) {
+            V x = ldv<V>(drow + e * sizeof(V));
+            x = OV<V>::add(x, ldv<V>(rec + 4 + e * sizeof(V)));
+            stv<V>(drow + e * sizeof(V), x);
+          }
+          continue;
+        }
+        const int32_t nn = o_ld32(rec + 4);
+        const uint8_t *cols = rec + 8;
+        const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
+        if (KIND == 0) {
+          // VectorStore::Inc per (col, val), in record order.  Lanes run in parallel
+          // when the record's columns are strictly ascending (what both reference
+          // packers emit); otherwise lane 0 walks it.
+          bool asc = true;
+          for (int32_t c0 = 0; c0 < nn; c0 += 64) {
+            const int32_t i = c0 + lane;
+            const bool bad = i < nn && i > 0 && o_ld32(cols + i * 4) <= o_ld32(cols + (i - 1) * 4);
+            if (__ballot(bad)) asc = false;
+          }
+          if (asc) {
+            for (int32_t c0 = 0; c0 < nn; c0 += 64) {
+              const int32_t i = c0 + lane;
+              if (i < nn) {
+                uint8_t *p = drow + (int64_t)o_ld32(cols + i * 4) * sizeof(V);
+                stv<V>(p, OV<V>::add(ldv<V>(p), ldv<V>(vals + (int64_t)i * sizeof(V))));
+              }
+            }
+          } else if (lane == 0) {
+            for (int32_t i = 0; i < nn; ++i) {
+              uint8_t *p = drow + (int64_t)o_ld32(cols + i * 4) * sizeof(V);
+              stv<V>(p, OV<V>::add(ldv<V>(p), ldv<V>(vals + (int64_t)i * sizeof(V))));
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          continue;
+        }
+        // sorted-map / map rows: each Inc(col, delta) in order, wave-parallel over entries
+        for (int32_t i = 0; i < nn; ++i) {
+          const int32_t key = o_ld32(cols + i * 4);
+          const V delta = ldv<V>(vals + (int64_t)i * sizeof(V));
+          if (delta == V(0)) continue;                         // :306
+          int32_t idx = -1;                                    // FindIndex :230-238
+          for (int32_t c0 = 0; c0 < n && idx < 0; c0 += 64) {
+            const int32_t j = c0 + lane;
+            const bool m = j < n && o_ld32(E + j * ES) == key;
+            const uint64_t bal = __ballot(m);
+            if (bal) idx = c0 + __builtin_ctzll(bal);
+          }
+          if (idx < 0) {
+            if (n >= a.max_entries) {
+              if (lane == 0) atomicOr(a.call_status, kStCapacity);
+              continue;
+            }
+            int32_t p = n;
+            if (KIND == 1) {
+              // LinearSearchAndMove backward (:264-285): the new entry lands after the
+              // last entry whose value is not strictly smaller than delta.
+              int32_t pmax = -1;
+              for (int32_t c0 = 0; c0 < n; c0 += 64) {
+                const int32_t j = c0 + lane;
+                const bool m = j < n && !(delta > ldv<V>(E + j * ES + VO));
+                const uint64_t bal = __ballot(m);
+                if (bal) pmax = c0 + 63 - __builtin_clzll(bal);
+              }
+              p = pmax + 1;
+              for (int32_t c = n - 1; c >= p; c -= 64) {       // shift [p, n) right by one
+                const int32_t j = c - lane;
+                uint32_t w[ES / 4];
+                const bool act = j >= p;
+                if (act)
+                  for (int x = 0; x < ES / 4; ++x) w[x] = reinterpret_cast<const uint32_t *>(E + j * ES)[x];
+                wave_sync();
+                if (act)
+                  for (int x = 0; x < ES / 4; ++x) reinterpret_cast<uint32_t *>(E + (j + 1) * ES)[x] = w[x];
+                wave_sync();
+              }
+            }
+            if (lane == 0) {
+              for (int x = 0; x < ES / 4; ++x) reinterpret_cast<uint32_t *>(E + p * ES)[x] = 0;
+              *reinterpret_cast<int32_t *>(E + p * ES) = key;
+              stv<V>(E + p * ES + VO, delta);
+            }
+            wave_sync();
+            ++n;
+          } else {
+            // found: add in place (no re-sort, :325-327); remove on zero (:329-334)
+            V nv = OV<V>::add(ldv<V>(E + idx * ES + VO), delta);
+            wave_sync();
+            if (lane == 0) stv<V>(E + idx * ES + VO, nv);
+            wave_sync();
+            if (nv == V(0)) {
+              if (KIND == 1) {
+                for (int32_t c = idx + 1; c < n; c += 64) {    // shift (idx, n) left by one
+                  const int32_t j = c + lane;
+                  uint32_t w[ES / 4];
+                  const bool act = j < n;
+                  if (act)
+                    for (int x = 0; x < ES / 4; ++x) w[x] = reinterpret_cast<const uint32_t *>(E + j * ES)[x];
+                  wave_sync();
+                  if (act)
+                    for (int x = 0; x < ES / 4; ++x) reinterpret_cast<uint32_t *>(E + (j - 1) * ES)[x] = w[x];
+                  wave_sync();
+                }
+              } else if (idx != n - 1) {
+                // MapStore::Inc erases (map_store.hpp:63-64); unordered: move last into hole
+                if (lane < ES / 4)
+                  reinterpret_cast<uint32_t *>(E + idx * ES)[lane] =
+                      reinterpret_cast<const uint32_t *>(E + (n - 1) * ES)[lane];
+                wave_sync();
+              }
+              --n;
+            }
+          }
+        }
+      }
+      if (KIND != 0) {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(a.entries + slot * a.max_entries * ES);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(E);
+        for (int32_t w = lane; w < n * (ES / 4); w += 64) dst[w] = src[w];
+        if (lane == 0) a.nent[slot] = n;
+        wave_sync();
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Serve-back of sorted/map rows: gather (count, entries) for a list of slots.
+template <int ES>
+__global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entries, int64_t max_entries,
+                                      const int64_t *slots, int32_t n, int32_t *out_n, uint8_t *out) {
+  const int r = blockIdx.x;
+  if (r >= n) return;
+  const int64_t s = slots[r];
+  const int32_t k = s >= 0 ? nent[s] : 0;
+  if (threadIdx.x == 0) out_n[r] = k;
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(entries + s * max_entries * ES);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(out + (int64_t)r * max_entries * ES);
+  for (int32_t w = threadIdx.x; w < k * (ES / 4); w += blockDim.x) dst[w] = src[w];
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
+  const int64_t n = a.max_rows;
+  const int64_t ntiles = (n + 1023) / 1024;
+  hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(scan_tiles_kernel, dim3((unsigned)ntiles), dim3(256), 0, st, a.cnt, n, a.off, a.tsum);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(1024), 0, st, a.tsum, ntiles, a.off, n);
+  hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a.off, n, a.tsum);
+  hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
+  // waves per block limited by the LDS row images
+  int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
+  int64_t per_wave = a.kind == 0 ? 0 : a.max_entries * esz;
+  int wpb = 4;
+  while (wpb > 1 && per_wave * wpb > 150 * 1024) --wpb;
+  const size_t lds = (size_t)per_wave * wpb;
+  const int64_t tiles = (n + 63) / 64;
+  int64_t blocks = (tiles + wpb - 1) / wpb;
+  if (blocks > 4096) blocks = 4096;
+#define PSX_ORD(V)                                                                                 \
+  do {                                                                                             \
+    if (a.kind == 0)                                                                               \
+      hipLaunchKernelGGL((ordered_apply_kernel<V, 0>), dim3((unsigned)blocks), dim3(256), lds, st, a, wpb); \
+    else if (a.kind == 1)                                                                          \
+      hipLaunchKernelGGL((ordered_apply_kernel<V, 1>), dim3((unsigned)blocks), dim3(256), lds, st, a, wpb); \
+    else                                                                                           \
+      hipLaunchKernelGGL((ordered_apply_kernel<V, 2>), dim3((unsigned)blocks), dim3(256), lds, st, a, wpb); \
+  } while (0)
+  switch (dtype) {
+    case 0: PSX_ORD(float); break;
+    case 1: PSX_ORD(double); break;
+    case 2: PSX_ORD(int32_t); break;
+    default: PSX_ORD(int64_t); break;
+  }
+#undef PSX_ORD
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *entries, int64_t max_entries,
+                                 const int64_t *slots, int32_t n, int32_t *out_n, uint8_t *out,
+                                 hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (dtype == 0 || dtype == 2)
+    hipLaunchKernelGGL(gather_entries_kernel<8>, dim3(n), dim3(256), 0, st, nent, entries, max_entries, slots,
+                       n, out_n, out);
+  else
+    hipLaunchKernelGGL(gather_entries_kernel<16>, dim3(n), dim3(256), 0, st, nent, entries, max_entries, slots,
+                       n, out_n, out);
+  return hipGetLastError();
+}
+
+// Gate: a duplicate row inside any message of a fast-path dense table turns the whole
+// call into a replay (nothing is applied now).
+__global__ void gate_kernel(const Seg *segs, const uint32_t *counters, TableMask m, int B, uint32_t *call_status) {
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < m.n; ++i) {
+    const int t = m.t[i];
+    for (int b = 0; b < B; ++b) {
+      const Seg sg = segs[b * kMaxTables + t];
+      if (sg.rec0 >= 0 && !sg.sparse && counters[t * kMaxFused + b] != (uint32_t)sg.num_rows) {
+        atomicOr(call_status, kStDuplicateRow);
+        return;
+      }
+    }
+  }
+}
+
+hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
+                       uint32_t *call_status, hipStream_t st) {
+  hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, st, segs, counters, m, B, call_status);
+  return hipGetLastError();
+}
+
+}  // namespace psx

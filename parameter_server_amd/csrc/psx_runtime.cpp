@@ -26,13 +26,21 @@ hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64
 hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, int64_t max_rows,
                                uint32_t *counters, hipStream_t st);
 extern int g_inv_layout;
-hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, hipStream_t st);
+hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, uint32_t *log, hipStream_t st);
 hipError_t launch_flags_or(uint8_t *flags, int64_t first, int64_t num, uint8_t bits, hipStream_t st);
 hipError_t launch_flags_and(uint8_t *flags, int64_t num, uint8_t bits, hipStream_t st);
 hipError_t launch_gather_rows(int dtype, const void *table, const int64_t *slots, int32_t n,
                               int64_t row_cap, void *out, hipStream_t st);
+hipError_t launch_gather_flags(const uint8_t *flags, const int64_t *slots, int32_t n, uint8_t *out,
+                               hipStream_t st);
 
 hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st);
+hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st);
+hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
+                       uint32_t *call_status, hipStream_t st);
+hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *entries, int64_t max_entries,
+                                 const int64_t *slots, int32_t n, int32_t *out_n, uint8_t *out,
+                                 hipStream_t st);
 }  // namespace psx
 
 namespace {
@@ -44,9 +52,28 @@ int vsize_of(int32_t dt) { return (dt == PSX_F32 || dt == PSX_I32) ? 4 : 8; }
 struct TableState {
   psx_table_config cfg{};
   int vsize = 4;
-  void *d_data = nullptr;
+  int es = 8;                      // sizeof(Entry<V>) for sorted/map rows
+  int64_t max_entries = 0;
+  void *d_data = nullptr;          // dense rows
+  int32_t *d_nent = nullptr;       // sorted/map: entries per slot
+  uint8_t *d_entries = nullptr;    // sorted/map: [max_rows][max_entries] Entry<V>
   uint8_t *d_flags = nullptr;
-  int32_t *d_inv = nullptr;
+  int32_t *d_inv = nullptr;        // fast dense path inverse index
+  int32_t *d_cnt = nullptr;        // ordered path: per-slot counts (zero between calls)
+  int32_t *d_off = nullptr;        // ordered path: exclusive prefix (max_rows + 1)
+  int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
+  bool fast() const { return cfg.row_kind == PSX_ROW_DENSE && cfg.oplog_dense_serialized; }
+};
+
+void free_table(TableState &t) {
+  void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv, t.d_cnt, t.d_off, t.d_tsum};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
+}
+
+struct PendingCall {
+  std::vector<psx_stream> streams;
+  int ring;
 };
 
 struct EventPair {
@@ -64,13 +91,16 @@ struct psx_ctx {
   std::map<int32_t, int64_t> versions;   // bg_version_map_
   std::vector<TableState> tables;
   psx::Seg *d_segs = nullptr;
-  uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring
+  uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
   uint32_t *d_counters = nullptr;
   uint8_t *d_zero = nullptr;
   uint64_t *d_recoff = nullptr;
   size_t recoff_cap = 0;                 // entries
   uint8_t *d_staging = nullptr;
   size_t staging_cap = 0;
+  int32_t *d_list = nullptr;             // ordered path: record lists
+  size_t list_cap = 0;
+  std::vector<PendingCall> pending;      // calls since the last psx_sync (duplicate-row replay)
   int64_t call_seq = 0;
   int64_t pending_calls = 0;
   psx_status deferred = PSX_OK;
@@ -222,23 +252,36 @@ bool has_sparse_serialized(const psx_ctx *c) {
 }
 
 // Enqueue the device pipeline for n messages already resident in HBM (versions checked).
-psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
+// force_ordered: every table goes through the ordered path (duplicate-row replay).
+psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_ordered) {
   psx::StreamSet ss{};
   ss.n = n;
-  size_t rec_need = 0;
+  size_t rec_need = 0, list_need = 0;
   const bool sparse = has_sparse_serialized(c);
+  bool any_ordered = sparse || force_ordered;
   for (int i = 0; i < n; ++i) {
     ss.data[i] = (const uint8_t *)s[i].data;
     ss.size[i] = s[i].size;
     ss.recoff_base[i] = rec_need;
     if (sparse) rec_need += s[i].size / 8 + 1;
+    list_need += s[i].size / 8 + 1;       // every record is >= 8 bytes
   }
-  if (rec_need > c->recoff_cap) {
+  if (rec_need > c->recoff_cap || (any_ordered && list_need > c->list_cap)) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->d_recoff) hipFree(c->d_recoff);
-    c->d_recoff = nullptr;
-    HIP_TRY(c, hipMalloc(&c->d_recoff, rec_need * sizeof(uint64_t)));
-    c->recoff_cap = rec_need;
+    if (rec_need > c->recoff_cap) {
+      if (c->d_recoff) hipFree(c->d_recoff);
+      c->d_recoff = nullptr;
+      c->recoff_cap = 0;
+      HIP_TRY(c, hipMalloc(&c->d_recoff, rec_need * sizeof(uint64_t)));
+      c->recoff_cap = rec_need;
+    }
+    if (any_ordered && list_need > c->list_cap) {
+      if (c->d_list) hipFree(c->d_list);
+      c->d_list = nullptr;
+      c->list_cap = 0;
+      HIP_TRY(c, hipMalloc(&c->d_list, list_need * sizeof(int32_t)));
+      c->list_cap = list_need;
+    }
   }
   psx::TableDir dir{};
   dir.n = (int32_t)c->tables.size();
@@ -251,16 +294,23 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
   const int ring = (int)(c->call_seq % kRing);
   uint32_t *sticky = c->d_status;
   uint32_t *call_st = c->d_status + 1 + ring;
+  uint32_t *call_log = c->d_status + 1 + kRing + ring;
   psx_status st = timed(c, "decode_streams", [&] {
     return psx::launch_decode(ss, dir, c->d_segs, c->d_recoff, call_st, c->d_counters, c->stream);
   });
   if (st) return st;
+
+  // 1) fast dense tables: inverse index + per-message claim counts
+  psx::TableMask fast{};
+  std::vector<psx::InvLayout> layouts(c->tables.size());
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
-    if (t.cfg.row_kind != PSX_ROW_DENSE || !t.cfg.oplog_dense_serialized) continue;
+    if (!t.fast() || force_ordered) continue;
+    fast.t[fast.n++] = (int32_t)ti;
     const int64_t stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
     // 0: slot-major [s][b]; 1: batch-major [b][s] (default)
     const psx::InvLayout L = psx::g_inv_layout ? psx::InvLayout{1, t.cfg.max_rows} : psx::InvLayout{n, 1};
+    layouts[ti] = L;
     st = timed(c, "dense_index", [&] {
       return psx::launch_dense_index(ss, c->d_segs, (int)ti, n, stride, t.cfg.row_offset,
                                      t.cfg.row_stride, t.cfg.max_rows, t.d_inv, L, call_st, c->stream);
@@ -270,20 +320,65 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
       return psx::launch_dense_verify(t.d_inv, L, (int)ti, n, t.cfg.max_rows, c->d_counters, c->stream);
     });
     if (st) return st;
-    psx::DenseArgs a{};
+  }
+  // 2) a duplicate row in any fast table turns the whole call into a replay
+  if (fast.n && any_ordered) {
+    st = timed(c, "dup_gate", [&] {
+      return psx::launch_gate(c->d_segs, c->d_counters, fast, n, call_st, c->stream);
+    });
+    if (st) return st;
+  }
+  // 3) ordered tables
+  for (size_t ti = 0; ti < c->tables.size(); ++ti) {
+    TableState &t = c->tables[ti];
+    if (t.fast() && !force_ordered) continue;
+    psx::OrdArgs a{};
     a.ss = ss;
     a.segs = c->d_segs;
     a.t = (int)ti;
     a.B = n;
-    a.stride = stride;
+    a.kind = t.cfg.row_kind;
+    a.dense_records = t.cfg.oplog_dense_serialized;
+    a.stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
+    a.cap = t.cfg.dense_row_oplog_capacity;
+    a.row_cap = t.cfg.row_capacity;
+    a.row_offset = t.cfg.row_offset;
+    a.row_stride = t.cfg.row_stride;
+    a.max_rows = t.cfg.max_rows;
+    a.recoff = c->d_recoff;
+    a.cnt = t.d_cnt;
+    a.off = t.d_off;
+    a.tsum = t.d_tsum;
+    a.list = c->d_list;
+    a.dense = t.d_data;
+    a.nent = t.d_nent;
+    a.entries = t.d_entries;
+    a.max_entries = t.max_entries;
+    a.flags = t.d_flags;
+    a.call_status = call_st;
+    a.sticky = sticky;
+    a.force = force_ordered ? 1 : 0;
+    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered(t.cfg.dtype, a, c->stream); });
+    if (st) return st;
+  }
+  // 4) fast dense apply
+  for (int i = 0; i < fast.n; ++i) {
+    const int ti = fast.t[i];
+    TableState &t = c->tables[ti];
+    psx::DenseArgs a{};
+    a.ss = ss;
+    a.segs = c->d_segs;
+    a.t = ti;
+    a.B = n;
+    a.stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
     a.cap = t.cfg.dense_row_oplog_capacity;
     a.row_cap = t.cfg.row_capacity;
     a.max_rows = t.cfg.max_rows;
     a.table = t.d_data;
     a.flags = t.d_flags;
     a.inv = t.d_inv;
-    a.inv_ss = L.ss;
-    a.inv_sb = L.sb;
+    a.inv_ss = layouts[ti].ss;
+    a.inv_sb = layouts[ti].sb;
     a.counters = c->d_counters;
     a.sticky = sticky;
     a.call_status = call_st;
@@ -291,10 +386,23 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n) {
     st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream); });
     if (st) return st;
   }
-  st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, c->stream); });
+  st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
   if (st) return st;
+  PendingCall pc;
+  pc.streams.assign(s, s + n);
+  pc.ring = ring;
+  c->pending.push_back(pc);
   c->call_seq++;
   c->pending_calls++;
+  return PSX_OK;
+}
+
+psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
+  if (sticky & psx::kStUnknownTable) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table id in a device stream");
+  if (sticky & psx::kStMalformed) return fail(c, PSX_ERR_MALFORMED, "malformed device stream");
+  if (sticky & psx::kStRowRange) return fail(c, PSX_ERR_ROW_RANGE, "row id outside this shard's range");
+  if (sticky & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "row capacity exceeded (column >= row_capacity or sorted/map row over max_entries)");
+  if (sticky & psx::kStUnsupported) return fail(c, PSX_ERR_UNSUPPORTED, "table repeated within one message");
   return PSX_OK;
 }
 
@@ -304,24 +412,42 @@ psx_status sync_impl(psx_ctx *c) {
   collect_timing(c);
   uint32_t sticky = 0;
   HIP_TRY(c, hipMemcpy(&sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<PendingCall> pending;
+  pending.swap(c->pending);
+  c->pending_calls = 0;
   if (sticky) {
     uint32_t zero = 0;
     HIP_TRY(c, hipMemcpy(c->d_status, &zero, sizeof(uint32_t), hipMemcpyHostToDevice));
   }
-  c->pending_calls = 0;
   psx_status d = c->deferred;
   c->deferred = PSX_OK;
   if (d != PSX_OK) return d;
-  if (sticky & psx::kStUnknownTable) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table id in a device stream");
-  if (sticky & psx::kStMalformed) return fail(c, PSX_ERR_MALFORMED, "malformed device stream");
-  if (sticky & psx::kStRowRange) return fail(c, PSX_ERR_ROW_RANGE, "row id outside this shard's range");
-  if (sticky & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "row capacity exceeded");
-  if (sticky & psx::kStUnsupported) return fail(c, PSX_ERR_UNSUPPORTED, "table repeated within one message");
-  if (sticky & psx::kStDuplicateRow)
-    return fail(c, PSX_ERR_UNSUPPORTED,
-                "a row occurs twice in one message; the ordered replay path is not built yet "
-                "(messages from that call on were not applied)");
-  return PSX_OK;
+  uint32_t replay_sticky = 0;
+  if (sticky & psx::kStDuplicateRow) {
+    // A message held a row twice: that call and every later one were skipped.  Replay
+    // them, in order, on the ordered path (per-row record order preserved).
+    std::vector<uint32_t> log(kRing);
+    HIP_TRY(c, hipMemcpy(log.data(), c->d_status + 1 + kRing, sizeof(uint32_t) * kRing, hipMemcpyDeviceToHost));
+    size_t first = pending.size();
+    for (size_t i = 0; i < pending.size(); ++i)
+      if (log[pending[i].ring] & psx::kStDuplicateRow) { first = i; break; }
+    for (size_t i = first; i < pending.size(); ++i) {
+      psx_status st = enqueue_apply(c, pending[i].streams.data(), (int32_t)pending[i].streams.size(), true);
+      if (st) return st;
+    }
+    c->pending.clear();
+    c->pending_calls = 0;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    collect_timing(c);
+    HIP_TRY(c, hipMemcpy(&replay_sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (replay_sticky) {
+      uint32_t zero = 0;
+      HIP_TRY(c, hipMemcpy(c->d_status, &zero, sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+  }
+  psx_status e = sticky_error(c, sticky & ~psx::kStDuplicateRow);
+  if (e) return e;
+  return sticky_error(c, replay_sticky);
 }
 
 }  // namespace
@@ -366,11 +492,11 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
   c->stream = c->own;
   if (hipMalloc(&c->d_segs, sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
-      hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + kRing)) != hipSuccess ||
+      hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
       hipMalloc(&c->d_counters, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
       hipMalloc(&c->d_zero, 4096) != hipSuccess)
     return cleanup(PSX_ERR_OOM);
-  if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (1 + kRing)) != hipSuccess ||
+  if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
       hipMemset(c->d_zero, 0, 4096) != hipSuccess ||
       hipMemset(c->d_counters, 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
     return cleanup(PSX_ERR_DEVICE);
@@ -382,11 +508,8 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (!c) return PSX_ERR_INVALID_ARG;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (auto &t : c->tables) {
-    if (t.d_data) hipFree(t.d_data);
-    if (t.d_flags) hipFree(t.d_flags);
-    if (t.d_inv) hipFree(t.d_inv);
-  }
+  for (auto &t : c->tables) free_table(t);
+  if (c->d_list) hipFree(c->d_list);
   for (auto &p : c->pending_ev) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -434,29 +557,53 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (cfg->dtype < PSX_F32 || cfg->dtype > PSX_I64) return fail(c, PSX_ERR_INVALID_ARG, "bad dtype");
   if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
   if (cfg->max_rows <= 0 || cfg->row_stride <= 0) return fail(c, PSX_ERR_INVALID_ARG, "bad shard geometry");
-  if (cfg->max_rows > (int64_t)1 << 31) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
-  if (cfg->row_kind != PSX_ROW_DENSE || !cfg->oplog_dense_serialized)
-    return fail(c, PSX_ERR_UNSUPPORTED, "only dense rows with dense-serialized oplogs are built so far");
-  if (cfg->row_capacity <= 0) return fail(c, PSX_ERR_INVALID_ARG, "row_capacity must be > 0");
-  if (cfg->dense_row_oplog_capacity <= 0 || cfg->dense_row_oplog_capacity > cfg->row_capacity)
-    return fail(c, PSX_ERR_INVALID_ARG, "dense_row_oplog_capacity must be in [1, row_capacity]");
-  HIP_TRY(c, hipSetDevice(c->device));
+  if (cfg->max_rows > ((int64_t)1 << 31) - 2) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
   TableState t;
   t.cfg = *cfg;
   t.vsize = vsize_of(cfg->dtype);
-  const size_t data_bytes = (size_t)cfg->max_rows * (size_t)cfg->row_capacity * t.vsize;
-  const size_t inv_bytes = (size_t)cfg->max_rows * psx::kMaxFused * sizeof(int32_t);
-  hipError_t e = hipMalloc(&t.d_data, data_bytes);
-  if (e == hipSuccess) e = hipMalloc(&t.d_flags, (size_t)cfg->max_rows);
-  if (e == hipSuccess) e = hipMalloc(&t.d_inv, inv_bytes);
-  if (e == hipSuccess) e = hipMemsetAsync(t.d_data, 0, data_bytes, c->stream);   // VectorStore::Init zeroes
-  if (e == hipSuccess) e = hipMemsetAsync(t.d_flags, 0, (size_t)cfg->max_rows, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(t.d_inv, 0xff, inv_bytes, c->stream);
+  t.es = t.vsize == 4 ? 8 : 16;
+  if (cfg->row_kind == PSX_ROW_DENSE) {
+    if (cfg->row_capacity <= 0) return fail(c, PSX_ERR_INVALID_ARG, "row_capacity must be > 0");
+    if (cfg->oplog_dense_serialized &&
+        (cfg->dense_row_oplog_capacity <= 0 || cfg->dense_row_oplog_capacity > cfg->row_capacity))
+      return fail(c, PSX_ERR_INVALID_ARG, "dense_row_oplog_capacity must be in [1, row_capacity]");
+  } else {
+    // A dense record needs NumericStoreRow::ApplyDenseBatchIncUnsafe -> store GetPtr,
+    // which only VectorStore has (vector_store.hpp:104-108).
+    if (cfg->oplog_dense_serialized)
+      return fail(c, PSX_ERR_UNSUPPORTED, "sorted/map rows take sparse-serialized oplogs only");
+    t.max_entries = cfg->max_entries > 0 ? cfg->max_entries : cfg->row_capacity;
+    if (t.max_entries <= 0) return fail(c, PSX_ERR_INVALID_ARG, "sorted/map rows need max_entries (or row_capacity) > 0");
+    if (t.max_entries * t.es > 150 * 1024)
+      return fail(c, PSX_ERR_UNSUPPORTED, "max_entries * sizeof(Entry) must fit one wave's LDS image (150 KiB)");
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t R = (size_t)cfg->max_rows;
+  const size_t ntiles = (R + 1023) / 1024;
+  hipError_t e = hipSuccess;
+  if (cfg->row_kind == PSX_ROW_DENSE) {
+    const size_t data_bytes = R * (size_t)cfg->row_capacity * t.vsize;
+    e = hipMalloc(&t.d_data, data_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_data, 0, data_bytes, c->stream);   // VectorStore::Init zeroes
+  } else {
+    e = hipMalloc(&t.d_nent, R * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_entries, R * (size_t)t.max_entries * t.es);
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_nent, 0, R * sizeof(int32_t), c->stream);
+  }
+  if (e == hipSuccess) e = hipMalloc(&t.d_flags, R);
+  if (e == hipSuccess) e = hipMemsetAsync(t.d_flags, 0, R, c->stream);
+  if (e == hipSuccess && t.fast()) {
+    const size_t inv_bytes = R * psx::kMaxFused * sizeof(int32_t);
+    e = hipMalloc(&t.d_inv, inv_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_inv, 0xff, inv_bytes, c->stream);
+  }
+  if (e == hipSuccess) e = hipMalloc(&t.d_cnt, R * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(t.d_cnt, 0, R * sizeof(int32_t), c->stream);
+  if (e == hipSuccess) e = hipMalloc(&t.d_off, (R + 1) * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&t.d_tsum, ntiles * sizeof(int32_t));
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
-    if (t.d_data) hipFree(t.d_data);
-    if (t.d_flags) hipFree(t.d_flags);
-    if (t.d_inv) hipFree(t.d_inv);
+    free_table(t);
     return hip_fail(c, e, "table allocation");
   }
   c->tables.push_back(t);
@@ -482,6 +629,7 @@ psx_status psx_table_load_rows(psx_ctx *c, int32_t table_id, int64_t first_row, 
   int64_t s;
   psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
   if (st) return st;
+  if (t->cfg.row_kind != PSX_ROW_DENSE) return fail(c, PSX_ERR_UNSUPPORTED, "load_rows: dense tables only");
   HIP_TRY(c, hipSetDevice(c->device));
   const size_t rb = (size_t)t->cfg.row_capacity * t->vsize;
   HIP_TRY(c, hipMemcpyAsync((uint8_t *)t->d_data + (size_t)s * rb, src, (size_t)num_rows * rb,
@@ -498,6 +646,8 @@ psx_status psx_table_read_rows(psx_ctx *c, int32_t table_id, int64_t first_row, 
   int64_t s;
   psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
   if (st) return st;
+  if (t->cfg.row_kind != PSX_ROW_DENSE)
+    return fail(c, PSX_ERR_UNSUPPORTED, "read_rows: dense tables only (use psx_serialize_rows)");
   HIP_TRY(c, hipSetDevice(c->device));
   const size_t rb = (size_t)t->cfg.row_capacity * t->vsize;
   HIP_TRY(c, hipMemcpyAsync(dst, (const uint8_t *)t->d_data + (size_t)s * rb, (size_t)num_rows * rb,
@@ -547,7 +697,7 @@ psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) 
     psx_status d = sync_impl(c);
     if (d != PSX_OK) c->deferred = d;
   }
-  psx_status st = enqueue_apply(c, s, n);
+  psx_status st = enqueue_apply(c, s, n, false);
   if (st) return st;
   c->versions = v;
   return PSX_OK;
@@ -585,10 +735,12 @@ psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, in
     psx_status d = sync_impl(c);
     if (d != PSX_OK) c->deferred = d;
   }
-  st = enqueue_apply(c, &one, 1);
+  st = enqueue_apply(c, &one, 1, false);
   if (st) return st;
   it->second = version;
-  return PSX_OK;
+  // Host messages are applied synchronously, like the reference server thread; this
+  // also lets a duplicate-row replay read the staging buffer before it is reused.
+  return sync_impl(c);
 }
 
 psx_status psx_sync(psx_ctx *c) {
@@ -607,42 +759,64 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   std::vector<int64_t> slots(n);
   for (int32_t i = 0; i < n; ++i) slots[i] = slot_of(*t, row_ids[i]);
-  const size_t rb = (size_t)t->cfg.row_capacity * t->vsize;
+  const bool dense = t->cfg.row_kind == PSX_ROW_DENSE;
+  const size_t rb = dense ? (size_t)t->cfg.row_capacity * t->vsize : (size_t)t->max_entries * t->es;
   int64_t *d_slots = nullptr;
   uint8_t *d_out = nullptr;
-  HIP_TRY(c, hipMalloc(&d_slots, sizeof(int64_t) * n));
-  hipError_t e = hipMalloc(&d_out, rb * n);
-  if (e != hipSuccess) {
-    hipFree(d_slots);
-    return hip_fail(c, e, "serialize buffer");
-  }
+  int32_t *d_cnt = nullptr;
+  uint8_t *d_flags = nullptr;
   std::vector<uint8_t> rows(rb * n);
-  e = hipMemcpyAsync(d_slots, slots.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = psx::launch_gather_rows(t->cfg.dtype, t->d_data, d_slots, n, t->cfg.row_capacity, d_out, c->stream);
+  std::vector<int32_t> counts(n, 0);
+  std::vector<uint8_t> flags(n, 0);
+  hipError_t e = hipMalloc(&d_slots, sizeof(int64_t) * n);
+  if (e == hipSuccess) e = hipMalloc(&d_out, rb * n);
+  if (e == hipSuccess) e = hipMalloc(&d_cnt, sizeof(int32_t) * n);
+  if (e == hipSuccess) e = hipMalloc(&d_flags, n);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_slots, slots.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess)
+    e = dense ? psx::launch_gather_rows(t->cfg.dtype, t->d_data, d_slots, n, t->cfg.row_capacity, d_out, c->stream)
+              : psx::launch_gather_entries(t->cfg.dtype, t->d_nent, t->d_entries, t->max_entries, d_slots, n, d_cnt,
+                                           d_out, c->stream);
+  if (e == hipSuccess) e = psx::launch_gather_flags(t->d_flags, d_slots, n, d_flags, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(rows.data(), d_out, rb * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && !dense) e = hipMemcpyAsync(counts.data(), d_cnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flags, n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  hipFree(d_slots);
-  hipFree(d_out);
+  if (d_slots) hipFree(d_slots);
+  if (d_out) hipFree(d_out);
+  if (d_cnt) hipFree(d_cnt);
+  if (d_flags) hipFree(d_flags);
   if (e != hipSuccess) return hip_fail(c, e, "serialize gather");
-  // presence from the flags (absent rows are skipped, as ServerTable only serializes
-  // rows that exist in storage_)
-  std::vector<uint8_t> present(n, 0);
-  for (int32_t i = 0; i < n; ++i) {
-    if (slots[i] < 0) continue;
-    uint8_t f = 0;
-    HIP_TRY(c, hipMemcpy(&f, t->d_flags + slots[i], 1, hipMemcpyDeviceToHost));
-    present[i] = f & 1;
-  }
+  // RecordBuff::Append framing {int32 row_id; size_t size; bytes} (record_buff.hpp:41-53);
+  // rows absent from the shard's storage are skipped, as ServerTable only holds created rows.
   size_t off = 0;
   uint8_t *o = (uint8_t *)out;
   for (int32_t i = 0; i < n; ++i) {
-    if (!present[i]) continue;
-    if (off + 12 + rb > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize: output buffer too small");
-    uint64_t sz = rb;
+    if (slots[i] < 0 || !(flags[i] & 1)) continue;
+    const uint8_t *src = rows.data() + (size_t)i * rb;
+    size_t body;
+    if (dense) {
+      body = rb;                                          // VectorStore::Serialize
+    } else if (t->cfg.row_kind == PSX_ROW_SORTED_MAP) {
+      body = (size_t)counts[i] * t->es;                   // Entry<V>[n] as stored
+    } else {
+      body = (size_t)counts[i] * (4 + t->vsize);          // MapStore::Serialize packs {int32, V}
+    }
+    if (off + 12 + body > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize: output buffer too small");
+    uint64_t sz = body;
     memcpy(o + off, &row_ids[i], 4);
     memcpy(o + off + 4, &sz, 8);
-    memcpy(o + off + 12, rows.data() + (size_t)i * rb, rb);
-    off += 12 + rb;
+    if (t->cfg.row_kind == PSX_ROW_MAP) {
+      uint8_t *d = o + off + 12;
+      for (int32_t k = 0; k < counts[i]; ++k) {
+        memcpy(d, src + (size_t)k * t->es, 4);
+        memcpy(d + 4, src + (size_t)k * t->es + (t->vsize == 4 ? 4 : 8), t->vsize);
+        d += 4 + t->vsize;
+      }
+    } else {
+      memcpy(o + off + 12, src, body);
+    }
+    off += 12 + body;
   }
   *used = off;
   return PSX_OK;

@@ -186,20 +186,14 @@ def test_device_stream_errors_reported_at_sync():
     srv.sync()                                         # error state cleared
 
 
-def test_duplicate_row_in_one_message_is_not_silently_merged():
-    """A row twice in one message: the fused path must not apply it out of order."""
-    srv, _ = _pair(F32, 10, 8, bgs=[100])
+def test_duplicate_row_in_one_message_applied_in_order():
+    """A row twice in one message is replayed on the ordered path: both records apply."""
+    srv, orc = _pair(F32, 10, 8, bgs=[100])
     s = wire.dense_stream_np(1, np.array([3, 4, 3], np.int32), np.ones((3, 8), np.float32))
-    d = torch.from_numpy(s).cuda()
-    torch.cuda.synchronize()
-    srv.apply_device([(d.data_ptr(), d.numel(), 100, 0)])
-    try:
-        srv.sync()
-        got = srv.read_rows(1, 0, 10)
-        assert np.all(got[3] == 2.0) and np.all(got[4] == 1.0)
-    except PsxError as e:
-        assert e.status == 10
-        assert not srv.read_rows(1, 0, 10).any()
+    _apply_both(srv, orc, [s], [100], [0])
+    got = srv.read_rows(1, 0, 10)
+    assert np.all(got[3] == 2.0) and np.all(got[4] == 1.0)
+    assert np.array_equal(_bits(got), _bits(orc.read_dense_rows(1, 0, 10)))
 
 
 def test_dirty_flags_and_serialize_rows():

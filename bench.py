@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=1 << 16)
     p.add_argument("--pmc-json", default=None,
                    help="per-launch HBM bytes of dense_apply from a rocprofv3 --pmc pass")
+    p.add_argument("--workload", default="c2", choices=["c2", "c3"],
+                   help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows")
     return p.parse_args()
 
 
@@ -75,8 +77,95 @@ def cpu_baseline(args):
                       f"(oracle/psx_oracle.c restatement of server.cpp:120-179, 1 thread)"}
 
 
+def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234):
+    """SortedVectorMapRow<int32> rows, K columns; B batches of per_batch
+    distinct Zipf(s=1) rows, nnz uniform [1, 32], ascending unique columns, values
+    +-{1..3} (first batch positive)."""
+    import numpy as np
+    from parameter_server_amd import wire
+    rng = np.random.RandomState(seed)
+    p = 1.0 / np.arange(1, rows + 1)
+    p /= p.sum()
+    streams, nupd = [], 0
+    for b in range(B):
+        ids = rng.choice(rows, size=per_batch, replace=False, p=p)
+        ks = rng.randint(1, 33, size=per_batch)
+        recs = []
+        for rid, k in zip(ids, ks):
+            cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+            sign = 1 if b == 0 else rng.choice([-1, 1], size=k)
+            recs.append((int(rid), cols, (rng.randint(1, 4, size=k) * sign).astype(np.int32)))
+        nupd += int(ks.sum())
+        streams.append(wire.sparse_stream_np(3, 4, recs))
+    return streams, nupd
+
+
+def run_c3(args):
+    """Sparse int count rows (C3): reports updates/s (and stream GB/s) on 1 GPU."""
+    import numpy as np
+    import torch
+    import parameter_server_amd as psa
+    rows, K, B = 100_000, 1024, args.batches
+    streams, nupd = c3_streams(rows, K, B)
+    dev = [torch.from_numpy(s).cuda() for s in streams]
+    bgs = [100 + b for b in range(B)]
+    srv = psa.Server(0, 1, bgs)
+    srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
+                                     oplog_dense_serialized=False, max_rows=rows, max_entries=K))
+    ver = [0]
+
+    def step():
+        srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
+        ver[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    srv.sync()
+    srv.timing(True)
+    srv.timing_reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    srv.sync()
+    kern = {k: srv.timing_read(k) for k in ("decode_streams", "ordered_apply", "finish_call")}
+    stream_bytes = sum(s.size for s in streams)
+    cpu = None
+    if args.cpu_seconds > 0:
+        from oracle.oracle import OracleServer, SORTED_MAP, I32
+        orc = OracleServer(bgs)
+        orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+        n, ce, v = 0, 0.0, 0
+        while ce < args.cpu_seconds or n == 0:
+            t = time.perf_counter()
+            for b in range(B):
+                assert orc.apply_stream(streams[b], bgs[b], v) == 0
+            ce += time.perf_counter() - t
+            n += 1
+            v += 1
+        cpu = {"value": round(nupd * n / ce / 1e6, 3), "unit": "M updates/s", "cores": 1, "kind": "port",
+               "sample": f"same {B} streams, {n} steps in {ce:.1f} s (oracle, 1 thread)"}
+    print(json.dumps({
+        "metric": "sparse int row-update apply (SortedVectorMapRow<int32>), C3",
+        "value": round(nupd * args.steps / el / 1e6, 3), "unit": "M updates/s",
+        "stream_GBps": round(stream_bytes * args.steps / el / 1e9, 3),
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+        "dtype": "int32", "data": "synthetic (Zipf rows, uniform nnz 1..32, values +-1..3)",
+        "config": {"workload": f"C3: {rows} rows x K={K}, {B} batches x 10000 rows/step",
+                   "updates_per_step": nupd, "stream_bytes_per_step": stream_bytes},
+        "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
+        "cpu_baseline": cpu}), flush=True)
+    srv.close()
+
+
 def main():
     args = parse()
+    if args.workload == "c3":
+        return run_c3(args)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))

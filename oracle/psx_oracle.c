@@ -339,16 +339,31 @@ static void apply_sparse_record(orc_table *t, orc_row *r, const int32_t *cols,
  * val[i] += upd[i] for i < num_updates (= dense_row_oplog_capacity). For non-dense
  * stores the reference's GetPtr does not exist; a dense record is applied element
  * by element through Inc (the per-column meaning of a dense oplog). */
+#define ORC_DENSE_LOOP(T, ADD)                                   \
+  do {                                                           \
+    T *val = (T *)r->dense;                                      \
+    for (int64_t i = 0; i < n; ++i) {                            \
+      T u;                                                       \
+      memcpy(&u, upd + (size_t)i * sizeof(T), sizeof(T));        \
+      val[i] = ADD(val[i], u);                                   \
+    }                                                            \
+  } while (0)
+#define ORC_FADD(a, b) ((a) + (b))
+#define ORC_I32ADD(a, b) ((int32_t)((uint32_t)(a) + (uint32_t)(b)))
+#define ORC_I64ADD(a, b) ((int64_t)((uint64_t)(a) + (uint64_t)(b)))
+
 static void apply_dense_record(orc_table *t, orc_row *r, const uint8_t *upd, int64_t n) {
-  size_t vs = dt_size(t->dt);
   if (t->kind == KIND_DENSE) {
-    for (int64_t i = 0; i < n; ++i) {
-      uint8_t *p = r->dense + (size_t)i * vs;
-      v_store(p, v_add(v_load(p, t->dt), v_load(upd + (size_t)i * vs, t->dt), t->dt), t->dt);
+    /* the typed `val[i] += upd[i]` loop of numeric_store_row.hpp:181-184 */
+    switch (t->dt) {
+      case DT_F32: ORC_DENSE_LOOP(float, ORC_FADD); break;
+      case DT_F64: ORC_DENSE_LOOP(double, ORC_FADD); break;
+      case DT_I32: ORC_DENSE_LOOP(int32_t, ORC_I32ADD); break;
+      default: ORC_DENSE_LOOP(int64_t, ORC_I64ADD); break;
     }
   } else {
     for (int64_t i = 0; i < n; ++i) {
-      val_t d = v_load(upd + (size_t)i * vs, t->dt);
+      val_t d = v_load(upd + (size_t)i * dt_size(t->dt), t->dt);
       if (t->kind == KIND_SORTED_MAP) svm_inc(r, (int32_t)i, d, t->dt);
       else map_inc(r, (int32_t)i, d, t->dt);
     }

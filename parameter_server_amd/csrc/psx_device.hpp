@@ -104,6 +104,8 @@ struct OrdArgs {
   int32_t *off;
   int32_t *tsum;
   int32_t *list;
+  int32_t *touched;       // slots with >= 1 record this call (unordered)
+  uint32_t *ntouched;     // its length (zeroed by decode_streams)
   void *dense;
   int32_t *nent;
   uint8_t *entries;

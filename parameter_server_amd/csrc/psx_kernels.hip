@@ -32,10 +32,26 @@ __device__ __forceinline__ uint64_t ld64_a4(const uint8_t *p) {
 }
 
 // ---------------------------------------------------------------------------
-// decode_streams: grid = B workgroups of 64 threads; lane 0 walks one message.
-__global__ void __launch_bounds__(64) decode_streams_kernel(StreamSet ss, TableDir dir, Seg *segs,
-                                                            uint64_t *recoff, uint32_t *call_status,
-                                                            uint32_t *counters) {
+// decode_streams: grid = B workgroups of 1024 threads; thread 0 walks one message's
+// headers.  Sparse tables' variable-length records form a dependency chain (each size
+// comes from its n), so the walk is sequential: the block stages the stream through
+// LDS in 64 KiB windows and thread 0 hops record to record at LDS latency.
+constexpr int kDecodeThreads = 1024;
+constexpr int kDecodeWindowWords = 8192;    // 32 KiB window
+constexpr uint32_t kUnk = 0xFFFFFFFFu;      // chain position unknown (header outside window / bad)
+
+__global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSet ss, TableDir dir, Seg *segs,
+                                                                        uint64_t *recoff, uint32_t *call_status,
+                                                                        uint32_t *counters, uint32_t *ntouched) {
+  __shared__ uint32_t win[kDecodeWindowWords];
+  __shared__ uint32_t j1[kDecodeWindowWords], j2[kDecodeWindowWords], j4[kDecodeWindowWords];
+  __shared__ uint32_t qlist[kDecodeWindowWords / 8];   // chain positions starting 4-record hops
+  __shared__ uint32_t slist[kDecodeWindowWords / 2];   // single-record positions (window tail)
+  __shared__ uint32_t sh_nq, sh_ns;
+  __shared__ int32_t sh_bad;
+  __shared__ uint64_t sh_off, sh_rk, sh_left;
+  __shared__ int32_t sh_state;   // 0 walking headers, 1 sparse walk needs a window, 2 done
+  __shared__ int32_t sh_t, sh_ntab, sh_k;
   const int b = blockIdx.x;
   for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
     Seg s;
@@ -44,56 +60,160 @@ __global__ void __launch_bounds__(64) decode_streams_kernel(StreamSet ss, TableD
     s.sparse = 0;
     segs[b * kMaxTables + t] = s;
     counters[t * kMaxFused + b] = 0;
+    if (b == 0) ntouched[t] = 0;
   }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
   const uint8_t *p = ss.data[b];
   const uint64_t size = ss.size[b];
-  if (size == 0) return;                       // empty message (server.cpp:128)
-  if (size < 4) { atomicOr(call_status, kStMalformed); return; }
-  const int32_t ntab = ld32(p);
-  if (ntab < 0) { atomicOr(call_status, kStMalformed); return; }
-  uint64_t off = 4;
-  uint64_t rk = ss.recoff_base[b];
-  for (int32_t k = 0; k < ntab; ++k) {
-    if (off + 16 > size) { atomicOr(call_status, kStMalformed); return; }
-    const int32_t tid = ld32(p + off);
-    const uint64_t usz = ld64_a4(p + off + 4);
-    const int32_t nrows = ld32(p + off + 12);
-    off += 16;
-    int t = -1;
-    for (int i = 0; i < dir.n; ++i)
-      if (dir.table_id[i] == tid) t = i;
-    if (t < 0) { atomicOr(call_status, kStUnknownTable); return; }
-    if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { atomicOr(call_status, kStMalformed); return; }
-    Seg &sg = segs[b * kMaxTables + t];
-    if (sg.rec0 >= 0) { atomicOr(call_status, kStUnsupported); return; }
-    if (dir.dense_serialized[t]) {
-      const uint64_t stride = 4 + (uint64_t)dir.oplog_cap[t] * dir.vsize[t];
-      const uint64_t need = (uint64_t)nrows * stride;
-      if (off + need > size) { atomicOr(call_status, kStMalformed); return; }
-      sg.rec0 = (int64_t)off;
-      sg.num_rows = nrows;
-      sg.sparse = 0;
-      off += need;
+  if (threadIdx.x == 0) {
+    sh_state = 2;
+    sh_off = 4;
+    sh_k = 0;
+    sh_rk = ss.recoff_base[b];
+    if (size == 0) {
+      // empty message (server.cpp:128)
+    } else if (size < 4 || ld32(p) < 0) {
+      atomicOr(call_status, kStMalformed);
     } else {
-      // Sparse records {int32 row; int32 n; int32 cols[n]; V vals[n]}
-      // (AbstractRowOpLog::ParseSparseSerializedOpLog, abstract_row_oplog.hpp:64-78):
-      // sizes chain, so the walk is sequential.
-      sg.rec0 = (int64_t)rk;   // index of the first record offset
-      sg.num_rows = nrows;
-      sg.sparse = 1;
-      const uint64_t per = 4 + (uint64_t)dir.vsize[t];
-      for (int32_t r = 0; r < nrows; ++r) {
-        if (off + 8 > size) { atomicOr(call_status, kStMalformed); return; }
-        const int32_t n = ld32(p + off + 4);
-        if (n < 0) { atomicOr(call_status, kStMalformed); return; }
-        const uint64_t rs = 8 + (uint64_t)n * per;
-        if (off + rs > size) { atomicOr(call_status, kStMalformed); return; }
-        recoff[rk++] = off;
-        off += rs;
+      sh_ntab = ld32(p);
+      sh_state = 0;
+    }
+  }
+  for (;;) {
+    // A) thread 0 advances over table headers until a sparse table needs the window
+    //    walk or the message ends.  (Nobody else touches the shared state here.)
+    if (threadIdx.x == 0) {
+      while (sh_state == 0) {
+        // next table header (SerializedOpLogReader::StartNewTable, :87-121)
+        if (sh_k >= sh_ntab) { sh_state = 2; break; }
+        uint64_t off = sh_off;
+        if (off + 16 > size) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
+        const int32_t tid = ld32(p + off);
+        const uint64_t usz = ld64_a4(p + off + 4);
+        const int32_t nrows = ld32(p + off + 12);
+        off += 16;
+        int t = -1;
+        for (int i = 0; i < dir.n; ++i)
+          if (dir.table_id[i] == tid) t = i;
+        if (t < 0) { atomicOr(call_status, kStUnknownTable); sh_state = 2; break; }
+        if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
+        Seg *sg = &segs[b * kMaxTables + t];
+        if (sg->rec0 >= 0) { atomicOr(call_status, kStUnsupported); sh_state = 2; break; }
+        if (dir.dense_serialized[t]) {
+          const uint64_t stride = 4 + (uint64_t)dir.oplog_cap[t] * dir.vsize[t];
+          const uint64_t need = (uint64_t)nrows * stride;
+          if (off + need > size) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
+          sg->rec0 = (int64_t)off;
+          sg->num_rows = nrows;
+          sg->sparse = 0;
+          sh_off = off + need;
+          sh_k = sh_k + 1;
+        } else {
+          sg->rec0 = (int64_t)sh_rk;   // index of the first record offset
+          sg->num_rows = nrows;
+          sg->sparse = 1;
+          sh_t = t;
+          sh_off = off;
+          sh_left = (uint64_t)nrows;
+          if (nrows) sh_state = 1;
+          else sh_k = sh_k + 1;
+        }
       }
     }
+    __syncthreads();
+    if (sh_state == 2) break;
+    // B) stage a window starting at the current record (4-byte aligned by construction)
+    const uint64_t w0 = sh_off;
+    uint64_t wbytes = size - w0;
+    if (wbytes > (uint64_t)kDecodeWindowWords * 4) wbytes = (uint64_t)kDecodeWindowWords * 4;
+    const uint32_t nw = (uint32_t)(wbytes / 4);
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x)
+      win[i] = reinterpret_cast<const uint32_t *>(p + w0)[i];
+    // C) jump tables over the window (all threads): j1[q] = word index of the record
+    //    after a record starting at word q, j2 = j1 o j1, j4 = j2 o j2; kUnk where a
+    //    header lies outside the window or the record is malformed.
+    const uint64_t wpr = 1 + (uint64_t)dir.vsize[sh_t] / 4;   // words per (col, val) pair
+    for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
+      uint32_t v = kUnk;
+      if (q + 1 < nw) {
+        const int32_t n = (int32_t)win[q + 1];
+        if (n >= 0) {
+          const uint64_t nxt = (uint64_t)q + 2 + (uint64_t)n * wpr;
+          if (w0 + nxt * 4 <= size && nxt < kUnk) v = (uint32_t)nxt;
+        }
+      }
+      j1[q] = v;
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
+      const uint32_t a1 = j1[q];
+      j2[q] = a1 < nw ? j1[a1] : kUnk;
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
+      const uint32_t a2 = j2[q];
+      j4[q] = a2 < nw ? j2[a2] : kUnk;
+    }
+    __syncthreads();
+    // D) thread 0 hops the chain 4 records at a time, then singly near the window end
+    if (threadIdx.x == 0) {
+      uint64_t left = sh_left;
+      uint32_t w = (uint32_t)((sh_off - w0) / 4);
+      uint32_t nq = 0, ns = 0;
+      int bad = 0;
+      while (left >= 4 && w < nw && j4[w] != kUnk) {
+        qlist[nq++] = w;
+        w = j4[w];
+        left -= 4;
+      }
+      while (left && w + 1 < nw) {
+        const int32_t n = (int32_t)win[w + 1];
+        if (n < 0) { bad = 1; break; }
+        const uint64_t nxt = (uint64_t)w + 2 + (uint64_t)n * wpr;
+        if (w0 + nxt * 4 > size) { bad = 1; break; }
+        slist[ns++] = w;
+        --left;
+        if (nxt >= nw) { w = kUnk; sh_off = w0 + nxt * 4; break; }
+        w = (uint32_t)nxt;
+      }
+      if (!bad && left && w != kUnk && w + 1 >= nw && w0 + (uint64_t)w * 4 + 8 > size) bad = 1;   // truncated
+      if (w != kUnk) sh_off = w0 + (uint64_t)w * 4;
+      sh_nq = nq;
+      sh_ns = ns;
+      sh_bad = bad;
+      sh_left = left;
+    }
+    __syncthreads();
+    // E) expand hops into record offsets (all threads)
+    {
+      const uint32_t nq = sh_nq, ns = sh_ns;
+      const uint64_t rk = sh_rk;
+      for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) {
+        uint32_t q = qlist[i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          recoff[rk + 4 * (uint64_t)i + k] = w0 + (uint64_t)q * 4;
+          q = j1[q];
+        }
+      }
+      for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) recoff[rk + 4 * (uint64_t)nq + i] = w0 + (uint64_t)slist[i] * 4;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (sh_bad) {
+        atomicOr(call_status, kStMalformed);
+        sh_state = 2;
+      } else {
+        sh_rk = sh_rk + 4 * (uint64_t)sh_nq + sh_ns;
+        if (!sh_left) {
+          sh_state = 0;
+          sh_k = sh_k + 1;
+        } else if (sh_off + 8 > size) {
+          atomicOr(call_status, kStMalformed);
+          sh_state = 2;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -558,9 +678,9 @@ __global__ void gather_flags_kernel(const uint8_t *flags, const int64_t *slots, 
 // ---------------------------------------------------------------------------
 // Host-side launchers (internal to libpsx).
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
-                         uint32_t *call_status, uint32_t *counters, hipStream_t st) {
-  hipLaunchKernelGGL(decode_streams_kernel, dim3(ss.n), dim3(64), 0, st, ss, dir, segs, recoff,
-                     call_status, counters);
+                         uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, hipStream_t st) {
+  hipLaunchKernelGGL(decode_streams_kernel, dim3(ss.n), dim3(kDecodeThreads), 0, st, ss, dir, segs, recoff,
+                     call_status, counters, ntouched);
   return hipGetLastError();
 }
 

@@ -83,21 +83,45 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
-    int b;
-    uint64_t off;
-    locate(a, rs, r, b, off);
-    const uint8_t *p = a.ss.data[b] + off;
-    const int64_t s = o_slot(o_ld32(p), a);
-    if (s < 0) { atomicOr(a.call_status, kStRowRange); continue; }
-    if (!a.dense_records && a.kind == 0) {
-      // sparse record into a dense row: every column must lie inside the row
-      const int32_t n = o_ld32(p + 4);
-      const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
-      for (int32_t i = 0; i < n; ++i)
-        if (cols[i] < 0 || cols[i] >= a.row_cap) { atomicOr(a.call_status, kStCapacity); break; }
+  const int lane = threadIdx.x & 63;
+  // every lane runs the same trip count so the wave-aggregated append below sees the
+  // whole wave
+  const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+  for (int64_t r0 = base0; r0 < total; r0 += G) {
+    const int64_t r = r0 + lane;
+    bool first = false;
+    int64_t s = -1;
+    if (r < total) {
+      int b;
+      uint64_t off;
+      locate(a, rs, r, b, off);
+      const uint8_t *p = a.ss.data[b] + off;
+      s = o_slot(o_ld32(p), a);
+      if (s < 0) {
+        atomicOr(a.call_status, kStRowRange);
+      } else {
+        if (!a.dense_records && a.kind == 0) {
+          // sparse record into a dense row: every column must lie inside the row
+          const int32_t n = o_ld32(p + 4);
+          const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
+          for (int32_t i = 0; i < n; ++i)
+            if (cols[i] < 0 || cols[i] >= a.row_cap) { atomicOr(a.call_status, kStCapacity); break; }
+        }
+        first = atomicAdd(&a.cnt[s], 1) == 0;
+      }
     }
-    atomicAdd(&a.cnt[s], 1);
+    // append first-touched slots to the touched list, one atomic per wave
+    const uint64_t m = __ballot(first);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(a.ntouched, (uint32_t)__builtin_popcountll(m));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if (first) {
+        const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+        a.touched[base + rank] = (int32_t)s;
+      }
+    }
   }
 }
 
@@ -251,26 +275,15 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
   uint8_t *E = dyn + (size_t)wib * (size_t)a.max_entries * ES;   // this wave's row image
   const int64_t wave_g = (int64_t)blockIdx.x * wpb + wib;
   const int64_t nwaves = (int64_t)gridDim.x * wpb;
-  const int64_t ntiles = (a.max_rows + 63) / 64;
 
-  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
-    const int64_t s0 = tile * 64;
-    const int64_t ms = s0 + lane;
-    int32_t o0 = 0, o1 = 0;
-    if (ms < a.max_rows) {
-      o0 = a.off[ms];
-      o1 = a.off[ms + 1];
-    }
-    const bool touched = o1 > o0;
-    if (!go) continue;
-    if (touched) a.flags[ms] = 3;
-    uint64_t live = __ballot(touched);
-    while (live) {
-      const int k = __builtin_ctzll(live);
-      live &= live - 1;
-      const int64_t slot = s0 + k;
-      const int32_t beg = __shfl(o0, k, 64);
-      const int32_t L = __shfl(o1, k, 64) - beg;
+  // one touched row per wave at a time (rows are independent; hot rows spread out)
+  const int64_t nt = go ? (int64_t)*a.ntouched : 0;
+  for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
+    const int64_t slot = a.touched[ti];
+    if (lane == 0) a.flags[slot] = 3;
+    {
+      const int32_t beg = a.off[slot];
+      const int32_t L = a.off[slot + 1] - beg;
       int32_t *lst = a.list + beg;
       // order the slot's records by r = (message, position)
       int32_t mine = 0;
@@ -437,6 +450,236 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
 }
 
 // ---------------------------------------------------------------------------
+// Register-resident row image for sorted/map rows of <= 64*J entries: entry i lives in
+// lane i % 64, register i / 64 ("striped").  FindIndex and the insert position are J
+// compares + ballots; the one-slot shifts of LinearSearchAndMove / RemoveOneEntryAndCompact
+// are wave rotates (DPP wave_ror:1 / wave_rol:1) plus a select — no LDS round trips.
+template <typename T>
+__device__ __forceinline__ T dpp_rot(T x, bool right) {
+  if constexpr (sizeof(T) == 4) {
+    int v = __builtin_bit_cast(int, x);
+    v = right ? __builtin_amdgcn_update_dpp(0, v, 0x13C, 0xf, 0xf, false)    // wave_ror:1: lane l <- l-1
+              : __builtin_amdgcn_update_dpp(0, v, 0x134, 0xf, 0xf, false);   // wave_rol:1: lane l <- l+1
+    return __builtin_bit_cast(T, v);
+  } else {
+    long long v = __builtin_bit_cast(long long, x);
+    int lo = (int)v, hi = (int)(v >> 32);
+    if (right) {
+      lo = __builtin_amdgcn_update_dpp(0, lo, 0x13C, 0xf, 0xf, false);
+      hi = __builtin_amdgcn_update_dpp(0, hi, 0x13C, 0xf, 0xf, false);
+    } else {
+      lo = __builtin_amdgcn_update_dpp(0, lo, 0x134, 0xf, 0xf, false);
+      hi = __builtin_amdgcn_update_dpp(0, hi, 0x134, 0xf, 0xf, false);
+    }
+    return __builtin_bit_cast(T, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T bcast(T x, int src) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), src));
+  } else {
+    long long v = __builtin_bit_cast(long long, x);
+    int lo = __builtin_amdgcn_readlane((int)v, src), hi = __builtin_amdgcn_readlane((int)(v >> 32), src);
+    return __builtin_bit_cast(T, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+
+template <typename V, int KIND, int J>
+__global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
+  __shared__ RecSpace rs;
+  __shared__ int32_t sort_scratch[4][64];
+  if (threadIdx.x == 0) build_space(a, rs);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  const bool go = o_gate(a);
+  constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + wib;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int32_t cap = (int32_t)a.max_entries;
+
+  // one touched row per wave at a time (rows are independent; hot rows spread out)
+  const int64_t nt = go ? (int64_t)*a.ntouched : 0;
+  for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
+    const int64_t slot = a.touched[ti];
+    if (lane == 0) a.flags[slot] = 3;
+    {
+      const int32_t beg = a.off[slot];
+      const int32_t L = a.off[slot + 1] - beg;
+      int32_t *lst = a.list + beg;
+      int32_t mine = 0;
+      if (L <= 64) {
+        mine = wave_rank_sort(lane < L ? lst[lane] : 0x7fffffff, L, lane, sort_scratch[wib]);
+      } else {
+        if (lane == 0) {
+          for (int32_t i = 1; i < L; ++i) {
+            const int32_t x = lst[i];
+            int32_t j = i - 1;
+            while (j >= 0 && lst[j] > x) { lst[j + 1] = lst[j]; --j; }
+            lst[j + 1] = x;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+      }
+      // load the row image
+      int32_t n = a.nent[slot];
+      const uint8_t *row = a.entries + slot * a.max_entries * ES;
+      int32_t key[J];
+      V val[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int32_t i = j * 64 + lane;
+        key[j] = i < n ? o_ld32(row + (int64_t)i * ES) : 0;
+        val[j] = i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
+      }
+      for (int32_t q = 0; q < L; ++q) {
+        const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
+        int b;
+        uint64_t roff;
+        locate(a, rs, r, b, roff);
+        const uint8_t *rec = a.ss.data[b] + roff;
+        const int32_t nn = o_ld32(rec + 4);
+        const uint8_t *cols = rec + 8;
+        const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
+        for (int32_t c0 = 0; c0 < nn; c0 += 64) {
+          const int32_t pi = c0 + lane;
+          const int32_t my_col = pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0;
+          const V my_d = pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0);
+          const int32_t cnt = nn - c0 < 64 ? nn - c0 : 64;
+          for (int32_t t = 0; t < cnt; ++t) {
+            const int32_t c = __builtin_amdgcn_readlane(my_col, t);
+            const V d = bcast(my_d, t);
+            if (d == V(0)) continue;                                  // :306
+            int32_t idx = -1;                                         // FindIndex :230-238
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+              if (j * 64 < n && idx < 0) {
+                const uint64_t bal = __ballot(j * 64 + lane < n && key[j] == c);
+                if (bal) idx = j * 64 + __builtin_ctzll(bal);
+              }
+            }
+            if (idx < 0) {
+              if (n >= cap) {
+                if (lane == 0) atomicOr(a.call_status, kStCapacity);
+                continue;
+              }
+              int32_t p = n;
+              if (KIND == 1) {
+                // LinearSearchAndMove backward (:264-285)
+                int32_t pmax = -1;
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                  if (j * 64 < n) {
+                    const uint64_t bal = __ballot(j * 64 + lane < n && !(d > val[j]));
+                    if (bal) pmax = j * 64 + 63 - __builtin_clzll(bal);
+                  }
+                }
+                p = pmax + 1;
+                // entries [p, n) move to i + 1: descending j, rotate right by one lane
+                const int jhi = n >> 6, jlo = p >> 6;   // chunks holding entries p+1 .. n
+#pragma unroll
+                for (int j = J - 1; j >= 0; --j) {
+                  if (j <= jhi && j >= jlo) {
+                    const int32_t kr = dpp_rot(key[j], true);
+                    const V vr = dpp_rot(val[j], true);
+                    int32_t kp = 0;
+                    V vp = V(0);
+                    if (j > 0) {
+                      kp = dpp_rot(key[j - 1], true);
+                      vp = dpp_rot(val[j - 1], true);
+                    }
+                    const int32_t i = j * 64 + lane;
+                    const int32_t ks = lane == 0 ? kp : kr;
+                    const V vs = lane == 0 ? vp : vr;
+                    if (i > p && i <= n) {
+                      key[j] = ks;
+                      val[j] = vs;
+                    }
+                  }
+                }
+              }
+#pragma unroll
+              for (int j = 0; j < J; ++j)
+                if (j * 64 + lane == p) {
+                  key[j] = c;
+                  val[j] = d;
+                }
+              ++n;
+            } else {
+              // found: add in place (:325-327), remove on zero (:329-334)
+              V nv = V(0);
+#pragma unroll
+              for (int j = 0; j < J; ++j) {
+                if (j * 64 + lane == idx) val[j] = OV<V>::add(val[j], d);
+                if (j == (idx >> 6)) nv = bcast(val[j], idx & 63);
+              }
+              if (nv == V(0)) {
+                if (KIND == 1) {
+                  // entries (idx, n) move to i - 1: ascending j, rotate left by one lane
+                  const int jlo = idx >> 6, jhi = (n - 1) >> 6;   // chunks holding idx .. n-2
+#pragma unroll
+                  for (int j = 0; j < J; ++j) {
+                    if (j >= jlo && j <= jhi) {
+                      const int32_t kl = dpp_rot(key[j], false);
+                      const V vl = dpp_rot(val[j], false);
+                      int32_t kn = 0;
+                      V vn = V(0);
+                      if (j + 1 < J) {
+                        kn = dpp_rot(key[j + 1], false);
+                        vn = dpp_rot(val[j + 1], false);
+                      }
+                      const int32_t i = j * 64 + lane;
+                      const int32_t ks = lane == 63 ? kn : kl;
+                      const V vs = lane == 63 ? vn : vl;
+                      if (i >= idx && i < n - 1) {
+                        key[j] = ks;
+                        val[j] = vs;
+                      }
+                    }
+                  }
+                } else {
+                  // MapStore erase; unordered: the last entry fills the hole
+                  int32_t lk = 0;
+                  V lv = V(0);
+#pragma unroll
+                  for (int j = 0; j < J; ++j)
+                    if (j == ((n - 1) >> 6)) {
+                      lk = __builtin_amdgcn_readlane(key[j], (n - 1) & 63);
+                      lv = bcast(val[j], (n - 1) & 63);
+                    }
+#pragma unroll
+                  for (int j = 0; j < J; ++j)
+                    if (j * 64 + lane == idx) {
+                      key[j] = lk;
+                      val[j] = lv;
+                    }
+                }
+                --n;
+              }
+            }
+          }
+        }
+      }
+      // write the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)
+      uint8_t *wrow = a.entries + slot * a.max_entries * ES;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int32_t i = j * 64 + lane;
+        if (i < n) {
+          *reinterpret_cast<int32_t *>(wrow + (int64_t)i * ES) = key[j];
+          if (ES == 16) *reinterpret_cast<int32_t *>(wrow + (int64_t)i * ES + 4) = 0;
+          stv<V>(wrow + (int64_t)i * ES + VO, val[j]);
+        }
+      }
+      if (lane == 0) a.nent[slot] = n;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Serve-back of sorted/map rows: gather (count, entries) for a list of slots.
 template <int ES>
 __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entries, int64_t max_entries,
@@ -460,13 +703,36 @@ hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(1024), 0, st, a.tsum, ntiles, a.off, n);
   hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a.off, n, a.tsum);
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
-  // waves per block limited by the LDS row images
+  const int64_t tiles = (n + 63) / 64;
+  if (a.kind != 0 && a.max_entries <= 1024) {
+    int64_t blocks = (tiles + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+#define PSX_REG(V, KIND)                                                                           \
+  do {                                                                                             \
+    if (a.max_entries <= 64)                                                                       \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+    else if (a.max_entries <= 256)                                                                 \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+    else                                                                                           \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+  } while (0)
+#define PSX_REGK(V) do { if (a.kind == 1) PSX_REG(V, 1); else PSX_REG(V, 2); } while (0)
+    switch (dtype) {
+      case 0: PSX_REGK(float); break;
+      case 1: PSX_REGK(double); break;
+      case 2: PSX_REGK(int32_t); break;
+      default: PSX_REGK(int64_t); break;
+    }
+#undef PSX_REGK
+#undef PSX_REG
+    return hipGetLastError();
+  }
+  // LDS row images (max_entries > 1024) or dense rows
   int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
   int64_t per_wave = a.kind == 0 ? 0 : a.max_entries * esz;
   int wpb = 4;
   while (wpb > 1 && per_wave * wpb > 150 * 1024) --wpb;
   const size_t lds = (size_t)per_wave * wpb;
-  const int64_t tiles = (n + 63) / 64;
   int64_t blocks = (tiles + wpb - 1) / wpb;
   if (blocks > 4096) blocks = 4096;
 #define PSX_ORD(V)                                                                                 \

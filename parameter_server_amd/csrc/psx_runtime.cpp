@@ -19,7 +19,7 @@
 
 namespace psx {
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
-                         uint32_t *call_status, uint32_t *counters, hipStream_t st);
+                         uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, hipStream_t st);
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
                               InvLayout L, uint32_t *call_status, hipStream_t st);
@@ -62,11 +62,12 @@ struct TableState {
   int32_t *d_cnt = nullptr;        // ordered path: per-slot counts (zero between calls)
   int32_t *d_off = nullptr;        // ordered path: exclusive prefix (max_rows + 1)
   int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
+  int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
   bool fast() const { return cfg.row_kind == PSX_ROW_DENSE && cfg.oplog_dense_serialized; }
 };
 
 void free_table(TableState &t) {
-  void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv, t.d_cnt, t.d_off, t.d_tsum};
+  void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv, t.d_cnt, t.d_off, t.d_tsum, t.d_touched};
   for (void *p : ptrs)
     if (p) hipFree(p);
 }
@@ -93,6 +94,7 @@ struct psx_ctx {
   psx::Seg *d_segs = nullptr;
   uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
   uint32_t *d_counters = nullptr;
+  uint32_t *d_ntouched = nullptr;        // ordered path: touched-row count per table
   uint8_t *d_zero = nullptr;
   uint64_t *d_recoff = nullptr;
   size_t recoff_cap = 0;                 // entries
@@ -296,7 +298,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   uint32_t *call_st = c->d_status + 1 + ring;
   uint32_t *call_log = c->d_status + 1 + kRing + ring;
   psx_status st = timed(c, "decode_streams", [&] {
-    return psx::launch_decode(ss, dir, c->d_segs, c->d_recoff, call_st, c->d_counters, c->stream);
+    return psx::launch_decode(ss, dir, c->d_segs, c->d_recoff, call_st, c->d_counters, c->d_ntouched, c->stream);
   });
   if (st) return st;
 
@@ -350,6 +352,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.off = t.d_off;
     a.tsum = t.d_tsum;
     a.list = c->d_list;
+    a.touched = t.d_touched;
+    a.ntouched = c->d_ntouched + ti;
     a.dense = t.d_data;
     a.nent = t.d_nent;
     a.entries = t.d_entries;
@@ -494,7 +498,8 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   if (hipMalloc(&c->d_segs, sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
       hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
       hipMalloc(&c->d_counters, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
-      hipMalloc(&c->d_zero, 4096) != hipSuccess)
+      hipMalloc(&c->d_zero, 4096) != hipSuccess ||
+      hipMalloc(&c->d_ntouched, sizeof(uint32_t) * psx::kMaxTables) != hipSuccess)
     return cleanup(PSX_ERR_OOM);
   if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
       hipMemset(c->d_zero, 0, 4096) != hipSuccess ||
@@ -519,6 +524,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->d_status) hipFree(c->d_status);
   if (c->d_counters) hipFree(c->d_counters);
   if (c->d_zero) hipFree(c->d_zero);
+  if (c->d_ntouched) hipFree(c->d_ntouched);
   if (c->d_recoff) hipFree(c->d_recoff);
   if (c->d_staging) hipFree(c->d_staging);
   if (c->own) hipStreamDestroy(c->own);
@@ -601,6 +607,7 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (e == hipSuccess) e = hipMemsetAsync(t.d_cnt, 0, R * sizeof(int32_t), c->stream);
   if (e == hipSuccess) e = hipMalloc(&t.d_off, (R + 1) * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&t.d_tsum, ntiles * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&t.d_touched, R * sizeof(int32_t));
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     free_table(t);

@@ -48,7 +48,7 @@ def _pair(kind, dt, rows, ncols, max_entries=None, bgs=range(100, 116)):
 
 def _apply(srv, orc, streams, bgs, vers=None):
     vers = vers or [0] * len(streams)
-    dev = [torch.from_numpy(np.ascontiguousarray(s)).cuda() for s in streams]
+    dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
     torch.cuda.synchronize()
     srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg, v in zip(dev, bgs, vers)])
     srv.sync()
@@ -269,3 +269,15 @@ def test_c3_lda_config_parity():
     _apply(srv, orc, streams, bgs)
     ids = sorted(touched)
     assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids)
+
+
+@pytest.mark.parametrize("dt", [I32, F64])
+def test_sorted_map_wide_rows_lds_path(dt):
+    """max_entries > 1024 takes the LDS row-image kernel instead of the register one."""
+    rng = np.random.RandomState(23)
+    rows, K = 200, 3000
+    srv, orc = _pair(SORTED_MAP, dt, rows, K, max_entries=2048)
+    streams = [wire.sparse_stream_np(3, VS[dt], _sparse_rows(rng, rows, 1500, 120, dt, max_nnz=300))
+               for _ in range(4)]
+    _apply(srv, orc, streams, [100, 101, 102, 103])
+    assert srv.serialize_rows(3, list(range(rows))) == orc.serialize_records(3, list(range(rows)))

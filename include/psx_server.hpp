@@ -1,0 +1,120 @@
+// psx_server.hpp — header-only C++ mirror of the reference server-apply interface over
+// the C ABI (include/psx.h).  Method names and argument meaning follow
+// src/petuum_ps/server/server.hpp (Server::Init, CreateTable, ApplyOpLogUpdateVersion,
+// GetBgVersion) and configs.hpp (TableInfo); errors that the reference turns into glog
+// CHECK aborts (server.cpp:124-126, serialized_oplog_reader.hpp:112) throw psx::Error.
+//
+// A maintainer swaps `petuum::Server` for `psx::Server` inside ServerThread
+// (server_thread.hpp:90); see INTEGRATION.md.
+#pragma once
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "psx.h"
+
+namespace psx {
+
+class Error : public std::runtime_error {
+ public:
+  Error(psx_status s, const std::string &msg)
+      : std::runtime_error(std::string(psx_status_string(s)) + ": " + msg), status(s) {}
+  psx_status status;
+};
+
+// The TableInfo fields the apply path reads (configs.hpp:170-210) plus shard geometry.
+struct TableInfo {
+  int32_t row_kind = PSX_ROW_DENSE;   // DenseRow / SortedVectorMapRow / SparseRow
+  int32_t dtype = PSX_F32;
+  int64_t row_capacity = 0;
+  bool oplog_dense_serialized = true;
+  int64_t dense_row_oplog_capacity = 0;   // 0 -> row_capacity
+  int64_t row_offset = 0;
+  int64_t row_stride = 1;
+  int64_t max_rows = 0;
+  int64_t max_entries = 0;
+};
+
+class Server {
+ public:
+  Server() = default;
+  Server(const Server &) = delete;
+  Server &operator=(const Server &) = delete;
+  ~Server() {
+    if (ctx_) psx_ctx_destroy(ctx_);
+  }
+
+  // Server::Init(server_id, bg_ids) (server.cpp:18-31), plus the GPU this shard lives on.
+  void Init(int32_t server_id, const std::vector<int32_t> &bg_ids, int32_t device = 0) {
+    Check(psx_ctx_create(device, server_id, &ctx_));
+    for (int32_t bg : bg_ids) Check(psx_register_sender(ctx_, bg));
+  }
+
+  // Server::CreateTable(table_id, table_info) (server.cpp:33-44).
+  void CreateTable(int32_t table_id, const TableInfo &ti) {
+    psx_table_config c{};
+    c.table_id = table_id;
+    c.row_kind = ti.row_kind;
+    c.dtype = ti.dtype;
+    c.oplog_dense_serialized = ti.oplog_dense_serialized ? 1 : 0;
+    c.row_capacity = ti.row_capacity;
+    c.dense_row_oplog_capacity = ti.dense_row_oplog_capacity ? ti.dense_row_oplog_capacity : ti.row_capacity;
+    c.row_offset = ti.row_offset;
+    c.row_stride = ti.row_stride;
+    c.max_rows = ti.max_rows;
+    c.max_entries = ti.max_entries;
+    Check(psx_table_create(ctx_, &c));
+  }
+
+  // Server::ApplyOpLogUpdateVersion (server.hpp:46-48, server.cpp:120-179): the oplog
+  // bytes are borrowed for the call only, as in the reference.
+  void ApplyOpLogUpdateVersion(const void *oplog, size_t oplog_size, int32_t bg_thread_id,
+                               uint32_t version) {
+    Check(psx_apply_stream(ctx_, oplog, oplog_size, bg_thread_id, version));
+  }
+
+  // Batched, device-resident form: n messages applied as n sequential calls.
+  void ApplyOpLogsDevice(const std::vector<psx_stream> &msgs) {
+    Check(psx_apply_streams_device(ctx_, msgs.data(), (int32_t)msgs.size()));
+  }
+
+  void Sync() { Check(psx_sync(ctx_)); }
+
+  // Server::GetBgVersion (server.cpp:186-188).
+  int32_t GetBgVersion(int32_t bg_thread_id) {
+    int64_t v = 0;
+    Check(psx_sender_version(ctx_, bg_thread_id, &v));
+    return (int32_t)v;
+  }
+
+  // ServerRow::Serialize framed as RecordBuff records (server_row.hpp:65-71,
+  // record_buff.hpp:41-53), for the rows listed.
+  std::vector<uint8_t> SerializeRows(int32_t table_id, const std::vector<int32_t> &row_ids) {
+    size_t cap = 1 << 16;
+    for (;;) {
+      std::vector<uint8_t> out(cap);
+      size_t used = 0;
+      psx_status s = psx_serialize_rows(ctx_, table_id, row_ids.data(), (int32_t)row_ids.size(), out.data(),
+                                        cap, &used);
+      if (s == PSX_ERR_BUFFER_TOO_SMALL) {
+        cap *= 4;
+        continue;
+      }
+      Check(s);
+      out.resize(used);
+      return out;
+    }
+  }
+
+  psx_ctx *handle() const { return ctx_; }
+
+ private:
+  void Check(psx_status s) {
+    if (s != PSX_OK) throw Error(s, ctx_ ? psx_last_error(ctx_) : "");
+  }
+  psx_ctx *ctx_ = nullptr;
+};
+
+}  // namespace psx

@@ -44,6 +44,9 @@ def parse():
                    help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows; "
                         "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange")
     p.add_argument("--c4-rows", type=int, default=10_000_000, help="C4 total rows (all shards)")
+    p.add_argument("--pcie", action="store_true",
+                   help="also time the host-buffer form: pinned H2D of the 8 messages + apply + D2H of "
+                        "every (dirty) row, i.e. the rate including PCIe (reported, never `value`)")
     return p.parse_args()
 
 
@@ -258,6 +261,40 @@ def run_c4(args):
         dist.destroy_process_group()
 
 
+def run_pcie(args, srv, streams, rows, cap, bgs, ver):
+    """Host-resident form of C2: messages start in pinned host memory (worker socket
+    buffers) and every dirty row is served back to host memory each step."""
+    import torch
+    host = [s.cpu().pin_memory() for s in streams]
+    dev = [torch.empty_like(s) for s in streams]
+    table_host = torch.empty(rows * cap, dtype=torch.float32).pin_memory()
+    table_dev = torch.empty(rows * cap, dtype=torch.float32, device="cuda")
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    first = srv.tables[1].row_offset
+    cur = torch.cuda.current_stream()
+
+    def step():
+        for h, d in zip(host, dev):
+            d.copy_(h, non_blocking=True)
+        srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
+        ver[0] += 1
+        assert L.psx_table_read_rows(srv.handle, 1, first, rows, table_dev.data_ptr(), 1) == 0
+        table_host.copy_(table_dev, non_blocking=True)
+        cur.synchronize()
+
+    step()
+    t0 = time.perf_counter()
+    n = max(3, args.steps // 2)
+    for _ in range(n):
+        step()
+    el = time.perf_counter() - t0
+    moved = sum(s.numel() for s in streams) + rows * cap * 4
+    return {"pcie_inclusive_GBps": round(moved * n / el / 1e9, 2), "ms_per_step": round(el / n * 1e3, 3),
+            "bytes_per_step": moved,
+            "what": "pinned H2D of all messages + fused apply + D2H of every row (served back), per step"}
+
+
 def main():
     args = parse()
     if args.workload == "c3":
@@ -342,6 +379,7 @@ def main():
     if args.pmc_json and os.path.exists(args.pmc_json):
         traffic = json.load(open(args.pmc_json)).get("dense_apply_hbm_bytes_per_launch")
 
+    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie else None
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
@@ -379,6 +417,8 @@ def main():
             "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},
             "cpu_baseline": cpu,
         }
+        if pcie:
+            line["pcie_inclusive"] = pcie
         print(json.dumps(line), flush=True)
     srv.close()
     if world > 1:

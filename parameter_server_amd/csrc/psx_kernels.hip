@@ -685,7 +685,7 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
 }
 
 int g_index_variant = 2;
-int g_apply_variant = 4;
+int g_apply_variant = 6;
 int g_inv_layout = 1;
 
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
@@ -761,9 +761,23 @@ static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
   }
 }
 
+// Variant 6 (default): the message-count template BMAX is the next power of two >= B
+// and the number of rows in flight per wave grows as B shrinks, so every wave keeps
+// ~8-18 16-byte loads in flight whatever the batch width (B = 1 for a single message).
+template <typename V>
+static void launch_adaptive(const DenseArgs &a, hipStream_t st) {
+  if (a.B <= 1) launch_v2<V, 1, 16, true, 8>(a, st);
+  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4>(a, st);
+  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3>(a, st);
+  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2>(a, st);
+  else launch_v2<V, 16, 16, true, 1>(a, st);
+}
+
 template <typename V>
 static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 8)
+  if (g_apply_variant == 6)
+    launch_adaptive<V>(a, st);
+  else if (a.B <= 8)
     launch_apply_bmax<V, 8>(a, st);
   else
     launch_apply_bmax<V, 16>(a, st);

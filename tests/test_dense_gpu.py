@@ -51,7 +51,7 @@ def _apply_both(srv, orc, streams, bgs, versions):
 
 
 @pytest.mark.parametrize("dt", [F32, F64, I32, I64])
-@pytest.mark.parametrize("B", [1, 3, 8, 16])
+@pytest.mark.parametrize("B", [1, 2, 3, 5, 8, 16])
 def test_fused_apply_bit_exact(dt, B):
     rng = np.random.RandomState(100 + B + 7 * dt)
     rows, cap = 700, 64
@@ -239,7 +239,7 @@ def test_smoke_entry():
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("index_variant", [0, 1, 2])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_every_kernel_variant_bit_exact(apply_variant, index_variant, layout):

@@ -16,7 +16,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--rows", type=int, default=1 << 20)
 p.add_argument("--cols", type=int, default=256)
 p.add_argument("--batches", type=int, default=8)
-p.add_argument("--apply", default="0,1,2,3,4,5")
+p.add_argument("--apply", default="0,1,2,3,4,5,6")
 p.add_argument("--index", default="0,1,2")
 p.add_argument("--layouts", default="0,1")
 p.add_argument("--rounds", type=int, default=3)

@@ -58,7 +58,7 @@ struct TableState {
   int32_t *d_nent = nullptr;       // sorted/map: entries per slot
   uint8_t *d_entries = nullptr;    // sorted/map: [max_rows][max_entries] Entry<V>
   uint8_t *d_flags = nullptr;
-  int32_t *d_inv = nullptr;        // fast dense path inverse index
+  int32_t *d_inv[2] = {nullptr, nullptr};   // fast dense path inverse index, one per call slot
   int32_t *d_cnt = nullptr;        // ordered path: per-slot counts (zero between calls)
   int32_t *d_off = nullptr;        // ordered path: exclusive prefix (max_rows + 1)
   int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
@@ -67,7 +67,8 @@ struct TableState {
 };
 
 void free_table(TableState &t) {
-  void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv, t.d_cnt, t.d_off, t.d_tsum, t.d_touched};
+  void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched};
   for (void *p : ptrs)
     if (p) hipFree(p);
 }
@@ -91,13 +92,19 @@ struct psx_ctx {
   hipStream_t stream = nullptr;
   std::map<int32_t, int64_t> versions;   // bg_version_map_
   std::vector<TableState> tables;
-  psx::Seg *d_segs = nullptr;
+  // Per-call state lives in two slots (call k uses slot k & 1) so that the decode/index
+  // stage of call k+1 can run on the side stream while call k applies on the main stream.
+  psx::Seg *d_segs[2] = {nullptr, nullptr};
+  uint32_t *d_counters[2] = {nullptr, nullptr};
+  uint32_t *d_ntouched[2] = {nullptr, nullptr};   // ordered path: touched-row count per table
+  uint64_t *d_recoff[2] = {nullptr, nullptr};
+  size_t recoff_cap[2] = {0, 0};                  // entries
+  hipStream_t side = nullptr;                     // decode/index/verify stage
+  hipEvent_t ev_ready[2] = {nullptr, nullptr};    // slot's index stage done (side -> main)
+  hipEvent_t ev_free[2] = {nullptr, nullptr};     // slot's apply stage done (main -> side)
+  bool pipeline = false;                          // PSX_PIPELINE=1: overlap (no gain measured, DRAM-bound)
   uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
-  uint32_t *d_counters = nullptr;
-  uint32_t *d_ntouched = nullptr;        // ordered path: touched-row count per table
   uint8_t *d_zero = nullptr;
-  uint64_t *d_recoff = nullptr;
-  size_t recoff_cap = 0;                 // entries
   uint8_t *d_staging = nullptr;
   size_t staging_cap = 0;
   int32_t *d_list = nullptr;             // ordered path: record lists
@@ -142,22 +149,26 @@ hipEvent_t get_event(psx_ctx *c) {
   return e;
 }
 
-// Run `launch` on the context stream, bracketed by HIP events when timing is on.
+// Run `launch` (which enqueues on `st`), bracketed by HIP events on `st` when timing is on.
 template <typename F>
-psx_status timed(psx_ctx *c, const char *name, F launch) {
+psx_status timed(psx_ctx *c, const char *name, F launch, hipStream_t st) {
   hipEvent_t a = nullptr, b = nullptr;
   if (c->timing) {
     a = get_event(c);
     b = get_event(c);
-    if (a) hipEventRecord(a, c->stream);
+    if (a) hipEventRecord(a, st);
   }
   hipError_t e = launch();
   if (e != hipSuccess) return hip_fail(c, e, name);
   if (c->timing && a && b) {
-    hipEventRecord(b, c->stream);
+    hipEventRecord(b, st);
     c->pending_ev.push_back({name, a, b});
   }
   return PSX_OK;
+}
+template <typename F>
+psx_status timed(psx_ctx *c, const char *name, F launch) {
+  return timed(c, name, launch, c->stream);
 }
 
 void collect_timing(psx_ctx *c) {
@@ -256,6 +267,10 @@ bool has_sparse_serialized(const psx_ctx *c) {
 // Enqueue the device pipeline for n messages already resident in HBM (versions checked).
 // force_ordered: every table goes through the ordered path (duplicate-row replay).
 psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_ordered) {
+  const int slot = (int)(c->call_seq & 1);
+  // Stage 1 (decode, index, verify) runs on the side stream once the slot's previous
+  // user (call k-2) has finished applying; stage 2 runs on the main stream after it.
+  hipStream_t prep = c->pipeline ? c->side : c->stream;
   psx::StreamSet ss{};
   ss.n = n;
   size_t rec_need = 0, list_need = 0;
@@ -268,14 +283,15 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (sparse) rec_need += s[i].size / 8 + 1;
     list_need += s[i].size / 8 + 1;       // every record is >= 8 bytes
   }
-  if (rec_need > c->recoff_cap || (any_ordered && list_need > c->list_cap)) {
+  if (rec_need > c->recoff_cap[slot] || (any_ordered && list_need > c->list_cap)) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (rec_need > c->recoff_cap) {
-      if (c->d_recoff) hipFree(c->d_recoff);
-      c->d_recoff = nullptr;
-      c->recoff_cap = 0;
-      HIP_TRY(c, hipMalloc(&c->d_recoff, rec_need * sizeof(uint64_t)));
-      c->recoff_cap = rec_need;
+    HIP_TRY(c, hipStreamSynchronize(c->side));
+    if (rec_need > c->recoff_cap[slot]) {
+      if (c->d_recoff[slot]) hipFree(c->d_recoff[slot]);
+      c->d_recoff[slot] = nullptr;
+      c->recoff_cap[slot] = 0;
+      HIP_TRY(c, hipMalloc(&c->d_recoff[slot], rec_need * sizeof(uint64_t)));
+      c->recoff_cap[slot] = rec_need;
     }
     if (any_ordered && list_need > c->list_cap) {
       if (c->d_list) hipFree(c->d_list);
@@ -297,9 +313,15 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   uint32_t *sticky = c->d_status;
   uint32_t *call_st = c->d_status + 1 + ring;
   uint32_t *call_log = c->d_status + 1 + kRing + ring;
-  psx_status st = timed(c, "decode_streams", [&] {
-    return psx::launch_decode(ss, dir, c->d_segs, c->d_recoff, call_st, c->d_counters, c->d_ntouched, c->stream);
-  });
+  psx::Seg *segs = c->d_segs[slot];
+  uint32_t *counters = c->d_counters[slot];
+  if (c->pipeline) HIP_TRY(c, hipStreamWaitEvent(prep, c->ev_free[slot], 0));
+  psx_status st = timed(
+      c, "decode_streams",
+      [&] {
+        return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], prep);
+      },
+      prep);
   if (st) return st;
 
   // 1) fast dense tables: inverse index + per-message claim counts
@@ -313,20 +335,28 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     // 0: slot-major [s][b]; 1: batch-major [b][s] (default)
     const psx::InvLayout L = psx::g_inv_layout ? psx::InvLayout{1, t.cfg.max_rows} : psx::InvLayout{n, 1};
     layouts[ti] = L;
-    st = timed(c, "dense_index", [&] {
-      return psx::launch_dense_index(ss, c->d_segs, (int)ti, n, stride, t.cfg.row_offset,
-                                     t.cfg.row_stride, t.cfg.max_rows, t.d_inv, L, call_st, c->stream);
-    });
+    st = timed(
+        c, "dense_index",
+        [&] {
+          return psx::launch_dense_index(ss, segs, (int)ti, n, stride, t.cfg.row_offset, t.cfg.row_stride,
+                                         t.cfg.max_rows, t.d_inv[slot], L, call_st, prep);
+        },
+        prep);
     if (st) return st;
-    st = timed(c, "dense_verify", [&] {
-      return psx::launch_dense_verify(t.d_inv, L, (int)ti, n, t.cfg.max_rows, c->d_counters, c->stream);
-    });
+    st = timed(
+        c, "dense_verify",
+        [&] { return psx::launch_dense_verify(t.d_inv[slot], L, (int)ti, n, t.cfg.max_rows, counters, prep); },
+        prep);
     if (st) return st;
+  }
+  if (c->pipeline) {
+    HIP_TRY(c, hipEventRecord(c->ev_ready[slot], prep));
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_ready[slot], 0));
   }
   // 2) a duplicate row in any fast table turns the whole call into a replay
   if (fast.n && any_ordered) {
     st = timed(c, "dup_gate", [&] {
-      return psx::launch_gate(c->d_segs, c->d_counters, fast, n, call_st, c->stream);
+      return psx::launch_gate(segs, counters, fast, n, call_st, c->stream);
     });
     if (st) return st;
   }
@@ -336,7 +366,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (t.fast() && !force_ordered) continue;
     psx::OrdArgs a{};
     a.ss = ss;
-    a.segs = c->d_segs;
+    a.segs = segs;
     a.t = (int)ti;
     a.B = n;
     a.kind = t.cfg.row_kind;
@@ -347,13 +377,13 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.row_offset = t.cfg.row_offset;
     a.row_stride = t.cfg.row_stride;
     a.max_rows = t.cfg.max_rows;
-    a.recoff = c->d_recoff;
+    a.recoff = c->d_recoff[slot];
     a.cnt = t.d_cnt;
     a.off = t.d_off;
     a.tsum = t.d_tsum;
     a.list = c->d_list;
     a.touched = t.d_touched;
-    a.ntouched = c->d_ntouched + ti;
+    a.ntouched = c->d_ntouched[slot] + ti;
     a.dense = t.d_data;
     a.nent = t.d_nent;
     a.entries = t.d_entries;
@@ -371,7 +401,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     TableState &t = c->tables[ti];
     psx::DenseArgs a{};
     a.ss = ss;
-    a.segs = c->d_segs;
+    a.segs = segs;
     a.t = ti;
     a.B = n;
     a.stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
@@ -380,10 +410,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.max_rows = t.cfg.max_rows;
     a.table = t.d_data;
     a.flags = t.d_flags;
-    a.inv = t.d_inv;
+    a.inv = t.d_inv[slot];
     a.inv_ss = layouts[ti].ss;
     a.inv_sb = layouts[ti].sb;
-    a.counters = c->d_counters;
+    a.counters = counters;
     a.sticky = sticky;
     a.call_status = call_st;
     a.zero_chunk = c->d_zero;
@@ -392,6 +422,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   }
   st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
   if (st) return st;
+  if (c->pipeline) HIP_TRY(c, hipEventRecord(c->ev_free[slot], c->stream));
   PendingCall pc;
   pc.streams.assign(s, s + n);
   pc.ring = ring;
@@ -412,6 +443,7 @@ psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
 
 psx_status sync_impl(psx_ctx *c) {
   HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   collect_timing(c);
   uint32_t sticky = 0;
@@ -495,15 +527,24 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
   c->stream = c->own;
-  if (hipMalloc(&c->d_segs, sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
-      hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
-      hipMalloc(&c->d_counters, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
-      hipMalloc(&c->d_zero, 4096) != hipSuccess ||
-      hipMalloc(&c->d_ntouched, sizeof(uint32_t) * psx::kMaxTables) != hipSuccess)
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
+  for (int k = 0; k < 2; ++k) {
+    if (hipEventCreateWithFlags(&c->ev_ready[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming) != hipSuccess)
+      return cleanup(PSX_ERR_DEVICE);
+    if (hipMalloc(&c->d_segs[k], sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
+        hipMalloc(&c->d_counters[k], sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
+        hipMalloc(&c->d_ntouched[k], sizeof(uint32_t) * psx::kMaxTables) != hipSuccess)
+      return cleanup(PSX_ERR_OOM);
+    if (hipMemset(c->d_counters[k], 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
+      return cleanup(PSX_ERR_DEVICE);
+  }
+  if (const char *pv = getenv("PSX_PIPELINE")) c->pipeline = atoi(pv) != 0;
+  if (hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
+      hipMalloc(&c->d_zero, 4096) != hipSuccess)
     return cleanup(PSX_ERR_OOM);
   if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
-      hipMemset(c->d_zero, 0, 4096) != hipSuccess ||
-      hipMemset(c->d_counters, 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
+      hipMemset(c->d_zero, 0, 4096) != hipSuccess)
     return cleanup(PSX_ERR_DEVICE);
   *out = c;
   return PSX_OK;
@@ -512,6 +553,7 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
 psx_status psx_ctx_destroy(psx_ctx *c) {
   if (!c) return PSX_ERR_INVALID_ARG;
   hipSetDevice(c->device);
+  if (c->side) hipStreamSynchronize(c->side);
   if (c->stream) hipStreamSynchronize(c->stream);
   for (auto &t : c->tables) free_table(t);
   if (c->d_list) hipFree(c->d_list);
@@ -520,12 +562,17 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
     hipEventDestroy(p.b);
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
-  if (c->d_segs) hipFree(c->d_segs);
+  for (int k = 0; k < 2; ++k) {
+    if (c->d_segs[k]) hipFree(c->d_segs[k]);
+    if (c->d_counters[k]) hipFree(c->d_counters[k]);
+    if (c->d_ntouched[k]) hipFree(c->d_ntouched[k]);
+    if (c->d_recoff[k]) hipFree(c->d_recoff[k]);
+    if (c->ev_ready[k]) hipEventDestroy(c->ev_ready[k]);
+    if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
+  }
+  if (c->side) hipStreamDestroy(c->side);
   if (c->d_status) hipFree(c->d_status);
-  if (c->d_counters) hipFree(c->d_counters);
   if (c->d_zero) hipFree(c->d_zero);
-  if (c->d_ntouched) hipFree(c->d_ntouched);
-  if (c->d_recoff) hipFree(c->d_recoff);
   if (c->d_staging) hipFree(c->d_staging);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
@@ -535,6 +582,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
 psx_status psx_ctx_set_stream(psx_ctx *c, void *hip_stream) {
   if (!c) return PSX_ERR_INVALID_ARG;
   HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
   return PSX_OK;
@@ -600,8 +648,10 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (e == hipSuccess) e = hipMemsetAsync(t.d_flags, 0, R, c->stream);
   if (e == hipSuccess && t.fast()) {
     const size_t inv_bytes = R * psx::kMaxFused * sizeof(int32_t);
-    e = hipMalloc(&t.d_inv, inv_bytes);
-    if (e == hipSuccess) e = hipMemsetAsync(t.d_inv, 0xff, inv_bytes, c->stream);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+      e = hipMalloc(&t.d_inv[k], inv_bytes);
+      if (e == hipSuccess) e = hipMemsetAsync(t.d_inv[k], 0xff, inv_bytes, c->stream);
+    }
   }
   if (e == hipSuccess) e = hipMalloc(&t.d_cnt, R * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemsetAsync(t.d_cnt, 0, R * sizeof(int32_t), c->stream);

@@ -19,6 +19,7 @@
  *   psx_table_load_rows     AbstractRow::ResetRowData    src/petuum_ps_common/storage/numeric_store_row.hpp:142-145
  *   psx_table_read_rows     VectorStore::CopyToMem       src/petuum_ps_common/storage/vector_store.hpp:115-118
  *   psx_serialize_rows      ServerRow::Serialize         src/petuum_ps/server/server_row.hpp:65-71
+ *   psx_serialize_dirty     Server::CreateSendServerPushRowMsgs  src/petuum_ps/server/server.cpp:189-309
  *   psx_row_flags           ServerRow::IsDirty / FindRow src/petuum_ps/server/server_row.hpp:90-96,
  *                                                        src/petuum_ps/server/server_table.cpp:136-141
  *
@@ -155,6 +156,15 @@ psx_status psx_sync(psx_ctx *ctx);
  * skipped.  *used receives the bytes written. */
 psx_status psx_serialize_rows(psx_ctx *ctx, int32_t table_id, const int32_t *row_ids,
                               int32_t n, void *out, size_t cap, size_t *used);
+
+/* Server push body for every dirty row of every table (Server::CreateSendServerPushRowMsgs,
+ * server.cpp:189-309): per table (creation order) int32 table_id, the dirty rows as
+ * RecordBuff records in ascending row id, then int32 -1 between tables / -2 at the end
+ * (context.hpp:123-129).  clear_dirty resets the rows' dirty bit (server_table.cpp:229).
+ * On PSX_ERR_BUFFER_TOO_SMALL *used holds the bytes needed and nothing is cleared.
+ * out_on_device != 0: out is a 4-byte-aligned device buffer. */
+psx_status psx_serialize_dirty(psx_ctx *ctx, void *out, size_t cap, size_t *used,
+                               int32_t out_on_device, int32_t clear_dirty);
 
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);

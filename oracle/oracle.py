@@ -56,6 +56,8 @@ def lib():
         L.orc_row_inc.argtypes = [vp, i32, i32, i32, vp]
         L.orc_pack_stream.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, sz]
         L.orc_pack_stream.restype = sz
+        L.orc_serialize_dirty.argtypes = [vp, vp, ctypes.c_int, vp, sz, ctypes.c_int]
+        L.orc_serialize_dirty.restype = i64
         L.orc_partition_server.argtypes = [i32, i32, i32, i32]
         L.orc_partition_server.restype = i32
         _lib = L
@@ -145,6 +147,19 @@ class OracleServer:
         while True:
             out = np.zeros(nb, dtype=np.uint8)
             r = self._L.orc_serialize_records(self._s, table_id, _ptr(ids), ids.size, _ptr(out), nb)
+            if r == -2:
+                nb *= 4
+                continue
+            assert r >= 0, r
+            return out[:r].tobytes()
+
+    def serialize_dirty(self, table_ids, clear=True):
+        """Push-message body for every dirty row (server.cpp:189-309), tables in order."""
+        tids = np.ascontiguousarray(table_ids, dtype=np.int32)
+        nb = 1 << 16
+        while True:
+            out = np.zeros(nb, dtype=np.uint8)
+            r = self._L.orc_serialize_dirty(self._s, _ptr(tids), tids.size, _ptr(out), nb, 1 if clear else 0)
             if r == -2:
                 nb *= 4
                 continue

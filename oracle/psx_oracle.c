@@ -714,3 +714,46 @@ int64_t orc_serialize_records(orc_server *s, int32_t table_id, const int32_t *ro
   free(tmp);
   return (int64_t)used;
 }
+
+/* ---- serve-back push body (server.cpp:189-309) --------------------------------- */
+/* Server::CreateSendServerPushRowMsgs for one client that subscribes to every row:
+ * per table (in the given order) int32 table_id, then ServerTable::AppendTableToBuffs
+ * (server_table.cpp:197-261) = every dirty row as a RecordBuff record
+ * {int32 row_id; size_t size; ServerRow::Serialize bytes}, resetting dirty_ (:229);
+ * tables are separated by int32 -1 and the body ends with int32 -2
+ * (context.hpp:123-129).  The reference walks storage_ (a boost::unordered_map) in
+ * hash order; this restatement emits rows in ascending row id, the order the device
+ * path uses.  Returns bytes written, -2 if cap is too small. */
+static int cmp_i32(const void *a, const void *b) {
+  int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+  return (x > y) - (x < y);
+}
+
+int64_t orc_serialize_dirty(orc_server *s, const int32_t *table_ids, int ntables, void *out, size_t cap,
+                            int clear) {
+  uint8_t *o = (uint8_t *)out;
+  size_t used = 0;
+  for (int ti = 0; ti < ntables; ++ti) {
+    orc_table *t = find_table(s, table_ids[ti]);
+    if (!t) return -3;
+    if (used + 4 > cap) return -2;
+    memcpy(o + used, &table_ids[ti], 4);
+    used += 4;
+    int32_t *ids = (int32_t *)malloc((size_t)(t->nrows + 1) * 4);
+    int64_t nd = 0;
+    for (int64_t i = 0; i < t->index.cap; ++i)
+      if (t->index.used[i] == 1 && t->rows[t->index.vals[i]]->dirty) ids[nd++] = t->index.keys[i];
+    qsort(ids, (size_t)nd, 4, cmp_i32);
+    int64_t w = orc_serialize_records(s, table_ids[ti], ids, (int32_t)nd, o + used, cap - used);
+    if (w < 0) { free(ids); return w; }
+    used += (size_t)w;
+    if (clear)
+      for (int64_t k = 0; k < nd; ++k) find_row(t, ids[k])->dirty = 0;
+    free(ids);
+    if (used + 4 > cap) return -2;
+    int32_t sep = ti + 1 < ntables ? -1 : -2;
+    memcpy(o + used, &sep, 4);
+    used += 4;
+  }
+  return (int64_t)used;
+}

@@ -92,6 +92,7 @@ def load():
         "psx_apply_streams_device": ([vp, P(psx_stream), i32], ctypes.c_int),
         "psx_sync": ([vp], ctypes.c_int),
         "psx_serialize_rows": ([vp, i32, vp, i32, vp, sz, P(sz)], ctypes.c_int),
+        "psx_serialize_dirty": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),
         "psx_timing_enable": ([vp, i32], ctypes.c_int),

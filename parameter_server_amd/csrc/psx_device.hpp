@@ -116,4 +116,28 @@ struct OrdArgs {
   int force;              // replay: ignore the sticky duplicate flag
 };
 
+// Arguments of the serve-back kernels (psx_serve.hip).
+struct ServeArgs {
+  const uint8_t *flags;
+  const int32_t *nent;
+  const uint8_t *dense;      // dense rows
+  const uint8_t *entries;    // sorted/map entries
+  int kind;
+  int vsize;
+  int64_t row_cap;
+  int64_t max_entries;
+  int64_t row_offset, row_stride, max_rows;
+  int64_t *sizes;
+  int64_t *offs;
+  uint8_t *out;              // record region base (4-byte aligned)
+  uint8_t *flags_rw;         // non-null: clear bit1 (dirty) of every emitted row
+};
+
+// Write a few 4-byte words (table ids and separators) into the body.
+struct Words {
+  int32_t n;
+  int64_t pos[2 * kMaxTables + 1];
+  int32_t val[2 * kMaxTables + 1];
+};
+
 }  // namespace psx

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "psx_device.hpp"
+#include "psx_scan.hpp"
 
 namespace psx {
 
@@ -123,69 +124,6 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
       }
     }
   }
-}
-
-// Three-phase exclusive scan of cnt[0, n) into off[0, n]; tiles of 1024.
-__global__ void __launch_bounds__(256) scan_tiles_kernel(const int32_t *cnt, int64_t n, int32_t *off,
-                                                        int32_t *tsum) {
-  __shared__ int32_t wsum[4];
-  const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x * 4;
-  int32_t v[4];
-  int32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = base + j < n ? cnt[base + j] : 0;
-    s += v[j];
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t incl = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    int32_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int32_t wpre = 0;
-  for (int i = 0; i < w; ++i) wpre += wsum[i];
-  int32_t run = wpre + incl - s;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (base + j < n) off[base + j] = run;
-    run += v[j];
-  }
-  if (threadIdx.x == 255) tsum[blockIdx.x] = wpre + incl;
-}
-
-__global__ void __launch_bounds__(1024) scan_sums_kernel(int32_t *tsum, int64_t ntiles, int32_t *off, int64_t n) {
-  __shared__ int32_t carry;
-  __shared__ int32_t wsum[16];
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t c = 0; c < ntiles; c += 1024) {
-    const int64_t i = c + threadIdx.x;
-    const int32_t x = i < ntiles ? tsum[i] : 0;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int32_t incl = x;
-    for (int o = 1; o < 64; o <<= 1) {
-      int32_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    int32_t wpre = 0;
-    for (int k = 0; k < w; ++k) wpre += wsum[k];
-    const int32_t excl = carry + wpre + incl - x;
-    __syncthreads();
-    if (i < ntiles) tsum[i] = excl;
-    if (threadIdx.x == 1023) carry = excl + x;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) off[n] = carry;
-}
-
-__global__ void __launch_bounds__(256) scan_add_kernel(int32_t *off, int64_t n, const int32_t *tsum) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) off[i] += tsum[i >> 10];
 }
 
 __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
@@ -699,9 +637,7 @@ hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
   const int64_t n = a.max_rows;
   const int64_t ntiles = (n + 1023) / 1024;
   hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(scan_tiles_kernel, dim3((unsigned)ntiles), dim3(256), 0, st, a.cnt, n, a.off, a.tsum);
-  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(1024), 0, st, a.tsum, ntiles, a.off, n);
-  hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a.off, n, a.tsum);
+  launch_exclusive_scan<int32_t>(a.cnt, n, a.off, a.tsum, st);
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
   const int64_t tiles = (n + 63) / 64;
   if (a.kind != 0 && a.max_entries <= 1024) {

@@ -38,6 +38,9 @@ hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st);
 hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st);
 hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
                        uint32_t *call_status, hipStream_t st);
+hipError_t launch_serve_sizes(const ServeArgs &a, hipStream_t st);
+hipError_t launch_serve_emit(const ServeArgs &a, hipStream_t st);
+hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st);
 hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *entries, int64_t max_entries,
                                  const int64_t *slots, int32_t n, int32_t *out_n, uint8_t *out,
                                  hipStream_t st);
@@ -63,12 +66,14 @@ struct TableState {
   int32_t *d_off = nullptr;        // ordered path: exclusive prefix (max_rows + 1)
   int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
+  int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
+  int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
   bool fast() const { return cfg.row_kind == PSX_ROW_DENSE && cfg.oplog_dense_serialized; }
 };
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched};
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_srv_sizes, t.d_srv_offs};
   for (void *p : ptrs)
     if (p) hipFree(p);
 }
@@ -876,6 +881,83 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
     off += 12 + body;
   }
   *used = off;
+  return PSX_OK;
+}
+
+psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, int32_t out_on_device,
+                               int32_t clear_dirty) {
+  if (!c || !used) return PSX_ERR_INVALID_ARG;
+  *used = 0;
+  if (out_on_device && ((uintptr_t)out & 3)) return fail(c, PSX_ERR_INVALID_ARG, "device output must be 4-byte aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const size_t T = c->tables.size();
+  std::vector<psx::ServeArgs> args(T);
+  for (size_t i = 0; i < T; ++i) {
+    TableState &t = c->tables[i];
+    const int64_t R = t.cfg.max_rows;
+    if (!t.d_srv_sizes) {
+      HIP_TRY(c, hipMalloc(&t.d_srv_sizes, sizeof(int64_t) * R));
+      HIP_TRY(c, hipMalloc(&t.d_srv_offs, sizeof(int64_t) * (R + 1 + (R + 1023) / 1024)));
+    }
+    psx::ServeArgs &a = args[i];
+    a = psx::ServeArgs{};
+    a.flags = t.d_flags;
+    a.nent = t.d_nent;
+    a.dense = (const uint8_t *)t.d_data;
+    a.entries = t.d_entries;
+    a.kind = t.cfg.row_kind;
+    a.vsize = t.vsize;
+    a.row_cap = t.cfg.row_capacity;
+    a.max_entries = t.max_entries;
+    a.row_offset = t.cfg.row_offset;
+    a.row_stride = t.cfg.row_stride;
+    a.max_rows = R;
+    a.sizes = t.d_srv_sizes;
+    a.offs = t.d_srv_offs;
+    HIP_TRY(c, psx::launch_serve_sizes(a, c->stream));
+  }
+  // lay out {table_id, records..., -1 | -2} per table (server.cpp:189-309)
+  psx::Words w{};
+  std::vector<int64_t> base(T);
+  int64_t pos = 0;
+  for (size_t i = 0; i < T; ++i) {
+    int64_t total = 0;
+    HIP_TRY(c, hipMemcpyAsync(&total, args[i].offs + args[i].max_rows, sizeof(int64_t), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    w.pos[w.n] = pos;
+    w.val[w.n++] = c->tables[i].cfg.table_id;
+    pos += 4;
+    base[i] = pos;
+    pos += total;
+    w.pos[w.n] = pos;
+    w.val[w.n++] = i + 1 < T ? -1 : -2;
+    pos += 4;
+  }
+  *used = (size_t)pos;
+  if ((size_t)pos > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize_dirty: *used bytes needed");
+  if (pos == 0) return PSX_OK;
+  uint8_t *dst = (uint8_t *)out;
+  if (!out_on_device) {
+    if ((size_t)pos > c->staging_cap) {
+      if (c->d_staging) hipFree(c->d_staging);
+      c->d_staging = nullptr;
+      c->staging_cap = 0;
+      HIP_TRY(c, hipMalloc(&c->d_staging, (size_t)pos));
+      c->staging_cap = (size_t)pos;
+    }
+    dst = c->d_staging;
+  }
+  for (size_t i = 0; i < T; ++i) {
+    args[i].out = dst + base[i];
+    args[i].flags_rw = clear_dirty ? c->tables[i].d_flags : nullptr;
+    HIP_TRY(c, psx::launch_serve_emit(args[i], c->stream));
+  }
+  HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
+  if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return PSX_OK;
 }
 

@@ -1,0 +1,109 @@
+// psx_serve.hip — serve-back on the device: every dirty row of a table serialized as the
+// reference's push-message records.
+//
+// Server::CreateSendServerPushRowMsgs (server.cpp:189-309) writes, per table,
+// int32 table_id, then ServerTable::AppendTableToBuffs (server_table.cpp:197-261): every
+// dirty (and subscribed) row as a RecordBuff record {int32 row_id; size_t size;
+// ServerRow::Serialize bytes} (record_buff.hpp:41-53), resetting dirty_; tables are
+// separated by int32 -1 and the body ends with -2 (context.hpp:123-129).
+//
+//   serve_sizes  sizes[s] = 12 + body bytes for dirty rows, 0 otherwise
+//   scan         offs = exclusive prefix (int64, psx_scan.hpp)
+//   serve_emit   one wave per dirty row writes its record at base + offs[s]
+// Row bodies: DenseRow V[capacity] (vector_store.hpp:75-80); SortedVectorMapRow
+// Entry<V>[n] in store order (sorted_vector_map_store.hpp:148-152); SparseRow packed
+// {int32 col; V val}[n] (map_store.hpp:89-100).  Rows come out in ascending row id.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "psx_device.hpp"
+#include "psx_scan.hpp"
+
+namespace psx {
+
+
+__device__ __forceinline__ int64_t body_bytes(const ServeArgs &a, int64_t s) {
+  if (a.kind == 0) return a.row_cap * a.vsize;
+  const int64_t es = a.vsize == 4 ? 8 : 16;
+  const int64_t n = a.nent[s];
+  return a.kind == 1 ? n * es : n * (4 + a.vsize);
+}
+
+__global__ void __launch_bounds__(256) serve_sizes_kernel(ServeArgs a) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.max_rows) return;
+  a.sizes[s] = (a.flags[s] & 3) == 3 ? 12 + body_bytes(a, s) : 0;
+}
+
+__global__ void __launch_bounds__(256) serve_emit_kernel(ServeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t ntiles = (a.max_rows + 63) / 64;
+  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
+    const int64_t ms = tile * 64 + lane;
+    const bool dirty = ms < a.max_rows && a.sizes[ms] != 0;
+    uint64_t live = __ballot(dirty);
+    while (live) {
+      const int k = __builtin_ctzll(live);
+      live &= live - 1;
+      const int64_t s = tile * 64 + k;
+      uint8_t *rec = a.out + a.offs[s];
+      const int64_t body = a.sizes[s] - 12;
+      if (lane == 0) {
+        const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
+        reinterpret_cast<int32_t *>(rec)[0] = rid;
+        reinterpret_cast<uint32_t *>(rec)[1] = (uint32_t)(uint64_t)body;           // size_t, 4-aligned
+        reinterpret_cast<uint32_t *>(rec)[2] = (uint32_t)((uint64_t)body >> 32);
+      }
+      uint32_t *dst = reinterpret_cast<uint32_t *>(rec + 12);
+      if (a.kind == 0) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.dense + s * a.row_cap * a.vsize);
+        for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
+      } else if (a.kind == 1) {
+        const int64_t es = a.vsize == 4 ? 8 : 16;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.entries + s * a.max_entries * es);
+        for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
+      } else {
+        const int64_t es = a.vsize == 4 ? 8 : 16, vo = a.vsize == 4 ? 4 : 8;
+        const uint8_t *src = a.entries + s * a.max_entries * es;
+        const int32_t n = a.nent[s];
+        const int wpe = 1 + a.vsize / 4;                  // words per packed {int32, V}
+        for (int32_t e = lane; e < n; e += 64) {
+          uint32_t *d = dst + (int64_t)e * wpe;
+          d[0] = *reinterpret_cast<const uint32_t *>(src + e * es);
+          d[1] = *reinterpret_cast<const uint32_t *>(src + e * es + vo);
+          if (wpe == 3) d[2] = *reinterpret_cast<const uint32_t *>(src + e * es + vo + 4);
+        }
+      }
+      if (lane == 0 && a.flags_rw) a.flags_rw[s] &= (uint8_t)~2u;   // ResetDirty (server_table.cpp:229)
+    }
+  }
+}
+
+
+__global__ void put_words_kernel(uint8_t *out, Words w) {
+  for (int i = threadIdx.x; i < w.n; i += blockDim.x) *reinterpret_cast<int32_t *>(out + w.pos[i]) = w.val[i];
+}
+
+hipError_t launch_serve_sizes(const ServeArgs &a, hipStream_t st) {
+  const int64_t n = a.max_rows;
+  hipLaunchKernelGGL(serve_sizes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+  launch_exclusive_scan<int64_t>(a.sizes, n, a.offs, a.offs + n + 1, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_serve_emit(const ServeArgs &a, hipStream_t st) {
+  const int64_t tiles = (a.max_rows + 63) / 64;
+  int64_t blocks = (tiles + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(serve_emit_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st) {
+  if (w.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(put_words_kernel, dim3(1), dim3(128), 0, st, out, w);
+  return hipGetLastError();
+}
+
+}  // namespace psx

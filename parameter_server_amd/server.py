@@ -161,6 +161,17 @@ class Server:
             _check(self._L, self._ctx, st)
             return out[:used.value].tobytes()
 
+    def serialize_dirty(self, clear=True):
+        """Push body for every dirty row of every table (server.cpp:189-309); bytes."""
+        used = ctypes.c_size_t()
+        st = self._L.psx_serialize_dirty(self._ctx, None, 0, ctypes.byref(used), 0, 0)
+        if st not in (_abi.PSX_OK, 9):
+            _check(self._L, self._ctx, st)
+        out = np.zeros(max(used.value, 1), dtype=np.uint8)
+        _check(self._L, self._ctx, self._L.psx_serialize_dirty(
+            self._ctx, ctypes.c_void_p(out.ctypes.data), out.size, ctypes.byref(used), 0, 1 if clear else 0))
+        return out[:used.value].tobytes()
+
     # -- timing ------------------------------------------------------------------------
     def timing(self, on=True):
         _check(self._L, self._ctx, self._L.psx_timing_enable(self._ctx, 1 if on else 0))

@@ -67,3 +67,27 @@ def dense_stream_torch(table_id, row_ids, payload):
     recs[:, 0].copy_(row_ids.to(torch.int32))
     recs[:, 1:].copy_(payload.contiguous().view(torch.int32).view(n, words_per_rec - 1))
     return out.view(torch.uint8)
+
+
+def parse_push_body(body):
+    """Parse a push body ({table_id; records; -1|-2} per table, as read by the client's
+    SerializedRowReader, serialized_row_reader.hpp:49-93) into
+    {table_id: {row_id: row bytes}}."""
+    import struct
+    out, off, n = {}, 0, len(body)
+    while off + 4 <= n:
+        tid = struct.unpack_from("<i", body, off)[0]
+        off += 4
+        rows = out.setdefault(tid, {})
+        while True:
+            rid = struct.unpack_from("<i", body, off)[0]
+            off += 4
+            if rid == -1:
+                break
+            if rid == -2:
+                return out
+            size = struct.unpack_from("<Q", body, off)[0]
+            off += 8
+            rows[rid] = bytes(body[off:off + size])
+            off += size
+    return out

@@ -281,3 +281,55 @@ def test_sorted_map_wide_rows_lds_path(dt):
                for _ in range(4)]
     _apply(srv, orc, streams, [100, 101, 102, 103])
     assert srv.serialize_rows(3, list(range(rows))) == orc.serialize_records(3, list(range(rows)))
+
+
+def test_serve_back_push_body_matches_oracle():
+    """Serve-back of every dirty row of three tables (dense, sorted map, map) in the push
+    format of Server::CreateSendServerPushRowMsgs (server.cpp:189-309), then the dirty
+    bits are cleared (second body is empty tables only)."""
+    rng = np.random.RandomState(31)
+    rows, cap, K = 200, 20, 40
+    bgs = [100, 101]
+    srv = psa.Server(0, 1, bgs)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=F32, row_capacity=cap, max_rows=rows))
+    srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=I32, row_capacity=K,
+                                     oplog_dense_serialized=False, max_rows=rows, max_entries=K))
+    srv.CreateTable(4, psa.TableInfo(row_kind=psa.ROW_MAP, dtype=F64, row_capacity=K,
+                                     oplog_dense_serialized=False, max_rows=rows, max_entries=K))
+    orc = OracleServer(bgs)
+    orc.create_table(1, DENSE, F32, cap)
+    orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+    orc.create_table(4, MAP, F64, 0, oplog_dense_serialized=False)
+    init = rng.normal(size=(rows, cap)).astype(np.float32)
+    srv.load_rows(1, 0, init)
+    orc.load_dense_rows(1, 0, init)
+    streams = []
+    for b in range(2):
+        d_ids = rng.permutation(rows)[:60].astype(np.int32)
+        cnt = np.zeros((50, K), np.int32)
+        mp_ = np.zeros((30, K), np.float64)
+        for r in range(50):
+            c = rng.choice(K, size=rng.randint(1, 6), replace=False)
+            cnt[r, c] = rng.choice([-1, 1, 2], size=c.size)
+        for r in range(30):
+            c = rng.choice(K, size=rng.randint(1, 6), replace=False)
+            mp_[r, c] = rng.normal(size=c.size)
+        streams.append(np.frombuffer(pack_stream([
+            dict(table_id=1, dtype=F32, dense_serialized=True, row_ids=d_ids,
+                 oplogs=rng.normal(size=(60, cap)).astype(np.float32)),
+            dict(table_id=3, dtype=I32, dense_serialized=False,
+                 row_ids=rng.permutation(rows)[:50].astype(np.int32), oplogs=cnt),
+            dict(table_id=4, dtype=F64, dense_serialized=False,
+                 row_ids=rng.permutation(rows)[:30].astype(np.int32), oplogs=mp_)]), np.uint8))
+    _apply(srv, orc, streams, bgs)
+    got = srv.serialize_dirty()
+    want = orc.serialize_dirty([1, 3, 4])
+    gp, wp = wire.parse_push_body(got), wire.parse_push_body(want)
+    assert gp.keys() == wp.keys() == {1, 3, 4}
+    assert gp[1] == wp[1] and gp[3] == wp[3]                  # dense + sorted map: byte-exact
+    assert gp[4].keys() == wp[4].keys()
+    for r in gp[4]:
+        assert _as_map(gp[4][r], F64, True) == _as_map(wp[4][r], F64, True)
+    assert len(got) == len(want) and got[:4] == want[:4]
+    empty = srv.serialize_dirty()
+    assert empty == orc.serialize_dirty([1, 3, 4]) == np.array([1, -1, 3, -1, 4, -2], np.int32).tobytes()

@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=1 << 16)
     p.add_argument("--pmc-json", default=None,
                    help="per-launch HBM bytes of dense_apply from a rocprofv3 --pmc pass")
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows; "
                         "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange")
     p.add_argument("--c4-rows", type=int, default=10_000_000, help="C4 total rows (all shards)")
@@ -295,8 +295,78 @@ def run_pcie(args, srv, streams, rows, cap, bgs, ver):
             "what": "pinned H2D of all messages + fused apply + D2H of every row (served back), per step"}
 
 
+def run_c5(args):
+    """mixed dense + sparse tables, continuous stream with clocks.
+    Every clock, 8 workers each send one message carrying both tables (a C2-like dense
+    f32 table, 2^18 x 256, half the rows per worker; a C3-like SortedVectorMapRow<int32>
+    table, 100K x 1024, 1250 Zipf rows per worker); the server applies the 8 messages
+    (one fused call) and, as the min clock advances, serves every dirty row back to host
+    memory (Server::CreateSendServerPushRowMsgs, server.cpp:189-309).  SSP staleness 4
+    lets workers run ahead on the client side; the server sees the same continuous
+    stream.  Reports clocks/s and the apply + serve-back rate in algorithmic GB/s."""
+    import numpy as np
+    import torch
+    import parameter_server_amd as psa
+    from parameter_server_amd import wire
+    rows_d, cap, rows_s, K, B = 1 << 18, 256, 100_000, 1024, 8
+    rng = np.random.RandomState(77)
+    p = 1.0 / np.arange(1, rows_s + 1)
+    p /= p.sum()
+    msgs = []
+    for b in range(B):
+        ids_d = rng.permutation(rows_d)[: rows_d // 2].astype(np.int32)
+        upd = rng.normal(0, 0.01, size=(ids_d.size, cap)).astype(np.float32)
+        ids_s = rng.choice(rows_s, size=1250, replace=False, p=p).astype(np.int32)
+        cnt = np.zeros((ids_s.size, K), np.int32)
+        for r in range(ids_s.size):
+            c = rng.choice(K, size=rng.randint(1, 33), replace=False)
+            cnt[r, c] = rng.choice([-1, 1, 2], size=c.size)
+        msgs.append(wire.pack_np([
+            dict(table_id=1, dense_serialized=True, row_ids=ids_d, oplogs=upd),
+            dict(table_id=3, dense_serialized=False, row_ids=ids_s, oplogs=cnt)]))
+    dev = [torch.from_numpy(m).cuda() for m in msgs]
+    bgs = [100 + b for b in range(B)]
+    srv = psa.Server(0, 1, bgs)
+    srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows_d))
+    srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
+                                     oplog_dense_serialized=False, max_rows=rows_s, max_entries=K))
+    ver = [0]
+    served = [0]
+
+    def clock():
+        srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
+        ver[0] += 1
+        served[0] += len(srv.serialize_dirty(clear=True))
+
+    for _ in range(args.warmup):
+        clock()
+    served[0] = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        clock()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    msg_bytes = sum(m.size for m in msgs)
+    dirty_dense = rows_d                     # 8 half-coverage batches touch ~all rows
+    step_bytes = msg_bytes + 2 * dirty_dense * cap * 4 + served[0] / args.steps
+    print(json.dumps({
+        "metric": "C5 mixed dense+sparse clock (apply + serve-back to host)",
+        "value": round(args.steps / el, 2), "unit": "clocks/s",
+        "GBps_algorithmic": round(step_bytes * args.steps / el / 1e9, 2),
+        "ms_per_clock": round(el / args.steps * 1e3, 3),
+        "served_bytes_per_clock": int(served[0] / args.steps), "message_bytes_per_clock": msg_bytes,
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "dtype": "f32+int32",
+        "data": "synthetic", "config": {"workload": "C5: dense 2^18x256 f32 + sorted-map 100Kx1024 int32, 8 msgs/clock"},
+    }), flush=True)
+    srv.close()
+
+
 def main():
     args = parse()
+    if args.workload == "c5":
+        return run_c5(args)
     if args.workload == "c3":
         return run_c3(args)
     if args.workload == "c4":

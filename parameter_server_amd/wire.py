@@ -52,6 +52,31 @@ def sparse_stream_np(table_id, vsize, rows):
     return np.concatenate(parts)
 
 
+def pack_np(tables):
+    """One multi-table message, as CreateOpLogMsgs + OpLogSerializer lay it out
+    (abstract_bg_worker.cpp:590-649, oplog_serializer.hpp:12-37): tables in ascending id,
+    empty tables omitted.  tables: dicts {table_id, row_ids int32[n], oplogs V[n, cap],
+    dense_serialized}; sparse records keep the non-zero columns in ascending order
+    (DenseRowOpLog::SerializeSparse, dense_row_oplog.hpp:112-131)."""
+    parts = []
+    live = sorted((t for t in tables if len(t["row_ids"])), key=lambda t: t["table_id"])
+    if not live:
+        return np.zeros(0, dtype=np.uint8)
+    parts.append(np.array([len(live)], dtype=np.int32).view(np.uint8))
+    for t in live:
+        op = np.ascontiguousarray(t["oplogs"])
+        ids = np.asarray(t["row_ids"], dtype=np.int32)
+        if t["dense_serialized"]:
+            parts.append(dense_stream_np(t["table_id"], ids, op)[4:])
+        else:
+            rows = []
+            for r in range(ids.size):
+                nz = np.nonzero(op[r])[0].astype(np.int32)
+                rows.append((int(ids[r]), nz, op[r, nz]))
+            parts.append(sparse_stream_np(t["table_id"], op.dtype.itemsize, rows)[4:])
+    return np.concatenate(parts)
+
+
 def dense_stream_torch(table_id, row_ids, payload):
     """Device-side builder: row_ids int32[n] and payload V[n, cap] are torch tensors on the
     GPU; returns a uint8 CUDA tensor holding the stream (4-byte aligned)."""

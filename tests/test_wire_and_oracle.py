@@ -119,3 +119,16 @@ def test_oracle_serialize_records_framing(oracle_lib):
     assert np.frombuffer(raw[:4], np.int32)[0] == 3
     assert np.frombuffer(raw[4:12], np.uint64)[0] == 16
     assert np.frombuffer(raw[12:28], np.float32).tolist() == [0, 1, 2, 3]
+
+
+def test_multi_table_pack_matches_packer(oracle_lib):
+    rng = np.random.RandomState(8)
+    dense = rng.normal(size=(7, 12)).astype(np.float32)
+    cnt = np.zeros((5, 30), np.int32)
+    for r in range(5):
+        c = rng.choice(30, size=3, replace=False)
+        cnt[r, c] = rng.choice([-2, 1, 3], size=3)
+    tables = [dict(table_id=9, dtype=I32, dense_serialized=False, row_ids=np.arange(5, dtype=np.int32), oplogs=cnt),
+              dict(table_id=2, dtype=F32, dense_serialized=True, row_ids=np.arange(7, dtype=np.int32) * 3,
+                   oplogs=dense)]
+    assert wire.pack_np(tables).tobytes() == pack_stream(tables)

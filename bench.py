@@ -333,15 +333,20 @@ def run_c5(args):
                                      oplog_dense_serialized=False, max_rows=rows_s, max_entries=K))
     ver = [0]
     served = [0]
+    t_apply = [0.0]
 
     def clock():
+        t = time.perf_counter()
         srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
+        srv.sync()
+        t_apply[0] += time.perf_counter() - t
         ver[0] += 1
         served[0] += len(srv.serialize_dirty(clear=True))
 
     for _ in range(args.warmup):
         clock()
     served[0] = 0
+    t_apply[0] = 0.0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -356,6 +361,8 @@ def run_c5(args):
         "value": round(args.steps / el, 2), "unit": "clocks/s",
         "GBps_algorithmic": round(step_bytes * args.steps / el / 1e9, 2),
         "ms_per_clock": round(el / args.steps * 1e3, 3),
+        "apply_ms_per_clock": round(t_apply[0] / args.steps * 1e3, 3),
+        "serve_ms_per_clock": round((el - t_apply[0]) / args.steps * 1e3, 3),
         "served_bytes_per_clock": int(served[0] / args.steps), "message_bytes_per_clock": msg_bytes,
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "dtype": "f32+int32",
         "data": "synthetic", "config": {"workload": "C5: dense 2^18x256 f32 + sorted-map 100Kx1024 int32, 8 msgs/clock"},

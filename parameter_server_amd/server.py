@@ -161,16 +161,27 @@ class Server:
             _check(self._L, self._ctx, st)
             return out[:used.value].tobytes()
 
-    def serialize_dirty(self, clear=True):
-        """Push body for every dirty row of every table (server.cpp:189-309); bytes."""
+    def serialize_dirty(self, clear=True, out=None):
+        """Push body for every dirty row of every table (server.cpp:189-309).
+
+        Returns a numpy uint8 view of the body.  The body lands in page-locked host
+        memory (kept by this object and reused, so the view is valid until the next
+        call) unless `out` (a writable numpy uint8 array) is given."""
         used = ctypes.c_size_t()
         st = self._L.psx_serialize_dirty(self._ctx, None, 0, ctypes.byref(used), 0, 0)
         if st not in (_abi.PSX_OK, 9):
             _check(self._L, self._ctx, st)
-        out = np.zeros(max(used.value, 1), dtype=np.uint8)
+        need = max(used.value, 1)
+        if out is None:
+            buf = getattr(self, "_pinned", None)
+            if buf is None or buf.numel() < need:
+                import torch
+                self._pinned = buf = torch.empty(need + need // 4, dtype=torch.uint8, pin_memory=True)
+            out = buf.numpy()
+        assert out.dtype == np.uint8 and out.size >= need
         _check(self._L, self._ctx, self._L.psx_serialize_dirty(
             self._ctx, ctypes.c_void_p(out.ctypes.data), out.size, ctypes.byref(used), 0, 1 if clear else 0))
-        return out[:used.value].tobytes()
+        return out[:used.value]
 
     # -- timing ------------------------------------------------------------------------
     def timing(self, on=True):

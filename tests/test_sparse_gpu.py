@@ -322,7 +322,7 @@ def test_serve_back_push_body_matches_oracle():
             dict(table_id=4, dtype=F64, dense_serialized=False,
                  row_ids=rng.permutation(rows)[:30].astype(np.int32), oplogs=mp_)]), np.uint8))
     _apply(srv, orc, streams, bgs)
-    got = srv.serialize_dirty()
+    got = srv.serialize_dirty().tobytes()
     want = orc.serialize_dirty([1, 3, 4])
     gp, wp = wire.parse_push_body(got), wire.parse_push_body(want)
     assert gp.keys() == wp.keys() == {1, 3, 4}
@@ -332,4 +332,4 @@ def test_serve_back_push_body_matches_oracle():
         assert _as_map(gp[4][r], F64, True) == _as_map(wp[4][r], F64, True)
     assert len(got) == len(want) and got[:4] == want[:4]
     empty = srv.serialize_dirty()
-    assert empty == orc.serialize_dirty([1, 3, 4]) == np.array([1, -1, 3, -1, 4, -2], np.int32).tobytes()
+    assert empty.tobytes() == orc.serialize_dirty([1, 3, 4]) == np.array([1, -1, 3, -1, 4, -2], np.int32).tobytes()

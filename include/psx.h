@@ -22,6 +22,11 @@
  *   psx_serialize_dirty     Server::CreateSendServerPushRowMsgs  src/petuum_ps/server/server.cpp:189-309
  *   psx_row_flags           ServerRow::IsDirty / FindRow src/petuum_ps/server/server_row.hpp:90-96,
  *                                                        src/petuum_ps/server/server_table.cpp:136-141
+ *   psx_row_importance      ServerRow::get_importance    src/petuum_ps/server/server_row.hpp:120-130
+ *   psx_serialize_partial   Server::CreateSendServerPushRowMsgsPartial
+ *                                                        src/petuum_ps/server/server.cpp:311-420,
+ *                           ServerTable::GetPartialTableToSendRegular / AppendRowsToBuffsPartial
+ *                                                        src/petuum_ps/server/server_table.cpp:301-346,381-420
  *
  * Error behaviour: the reference aborts via glog CHECK on a version gap
  * (server.cpp:124-126) or an unknown table id (serialized_oplog_reader.hpp:112-120).
@@ -43,7 +48,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 1
+#define PSX_ABI_VERSION 2
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -97,6 +102,14 @@ typedef struct psx_table_config {
   int64_t row_stride;
   int64_t max_rows;
   int64_t max_entries;              /* sorted/map rows: device slots per row */
+  /* ABI 2: */
+  int32_t accum_importance;         /* 1: rows accumulate importance on apply, as ServerTable
+                                       selects under SSPAggr + RelativeMagnitude/FIFO_N_ReMag
+                                       (server_table.cpp:26-47; NSSumImpCalc,
+                                       ns_sum_imp_calc.hpp:57-98) */
+  int32_t reserved0;                /* must be 0 */
+  int64_t server_push_row_upper_bound; /* TableInfo.server_push_row_upper_bound (configs.hpp:181):
+                                       rows per table per partial push; 0 -> 100 (table_gflags.cpp:21) */
 } psx_table_config;
 
 /* One device-resident ClientSendOpLogMsg payload (ps_msgs.hpp:1003-1055 after its
@@ -137,6 +150,13 @@ psx_status psx_table_read_rows(psx_ctx *ctx, int32_t table_id, int64_t first_row
 psx_status psx_row_flags(psx_ctx *ctx, int32_t table_id, int64_t first_row,
                          int64_t num_rows, uint8_t *dst);
 psx_status psx_clear_dirty(psx_ctx *ctx, int32_t table_id);
+/* Accumulated importance of num_rows rows (same addressing as psx_row_flags): the
+ * f64 sum, since the row was last sent, of each applied record's NSSumImpCalc value —
+ * dense record: sum_i |u_i / v_i| (|u_i| where v_i == 0), v_i the value before the add;
+ * sparse record: sum_i |u_i|.  Zero for tables without accum_importance and for rows
+ * never applied (the reference leaves importance_ uninitialized, server_row.hpp:16-19). */
+psx_status psx_row_importance(psx_ctx *ctx, int32_t table_id, int64_t first_row,
+                              int64_t num_rows, double *dst);
 
 /* ---- apply (the hot path) -------------------------------------------------- */
 /* Server::ApplyOpLogUpdateVersion: host bytes, borrowed only for the call. */
@@ -160,11 +180,26 @@ psx_status psx_serialize_rows(psx_ctx *ctx, int32_t table_id, const int32_t *row
 /* Server push body for every dirty row of every table (Server::CreateSendServerPushRowMsgs,
  * server.cpp:189-309): per table (creation order) int32 table_id, the dirty rows as
  * RecordBuff records in ascending row id, then int32 -1 between tables / -2 at the end
- * (context.hpp:123-129).  clear_dirty resets the rows' dirty bit (server_table.cpp:229).
+ * (context.hpp:123-129).  clear_dirty resets the rows' dirty bit and importance (server_table.cpp:234-235).
  * On PSX_ERR_BUFFER_TOO_SMALL *used holds the bytes needed and nothing is cleared.
  * out_on_device != 0: out is a 4-byte-aligned device buffer. */
 psx_status psx_serialize_dirty(psx_ctx *ctx, void *out, size_t cap, size_t *used,
                                int32_t out_on_device, int32_t clear_dirty);
+
+/* Partial push body (Server::CreateSendServerPushRowMsgsPartial, server.cpp:311-420): the
+ * same framing as psx_serialize_dirty, but per table only the first
+ * server_push_row_upper_bound candidate rows, in send order.  Candidates are all dirty
+ * rows (the reference samples candidates with probability
+ * min(1, upper_bound*row_candidate_factor/rows) from a time-seeded generator,
+ * server_table.cpp:301-335; with that probability at 1 the sets coincide).  Importance
+ * tables send rows by importance, largest first, ties by ascending row id
+ * (SortCandidateVectorImportance, server_table.cpp:272-287); other tables in ascending
+ * row id (the reference shuffles them randomly, :263-270).  Sent rows have dirty and
+ * importance reset when clear_dirty != 0 (AppendRowsToBuffsPartial :398-399).  When no
+ * table has a row to send nothing is written and *used = 0 (server.cpp:348).
+ * On PSX_ERR_BUFFER_TOO_SMALL *used holds the bytes needed and nothing is cleared. */
+psx_status psx_serialize_partial(psx_ctx *ctx, void *out, size_t cap, size_t *used,
+                                 int32_t out_on_device, int32_t clear_dirty);
 
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);

@@ -35,6 +35,8 @@ struct TableInfo {
   int64_t row_stride = 1;
   int64_t max_rows = 0;
   int64_t max_entries = 0;
+  bool accum_importance = false;             // SSPAggr importance policies (server_table.cpp:26-47)
+  int64_t server_push_row_upper_bound = 0;   // configs.hpp:181; 0 -> 100
 };
 
 class Server {
@@ -65,6 +67,8 @@ class Server {
     c.row_stride = ti.row_stride;
     c.max_rows = ti.max_rows;
     c.max_entries = ti.max_entries;
+    c.accum_importance = ti.accum_importance ? 1 : 0;
+    c.server_push_row_upper_bound = ti.server_push_row_upper_bound;
     Check(psx_table_create(ctx_, &c));
   }
 
@@ -106,6 +110,18 @@ class Server {
       out.resize(used);
       return out;
     }
+  }
+
+  // Server::CreateSendServerPushRowMsgs / ...Partial (server.cpp:189-420): the push body.
+  std::vector<uint8_t> CreatePushBody(bool partial, bool clear_dirty = true) {
+    size_t used = 0;
+    auto fn = partial ? psx_serialize_partial : psx_serialize_dirty;
+    psx_status s = fn(ctx_, nullptr, 0, &used, 0, 0);
+    if (s != PSX_ERR_BUFFER_TOO_SMALL) Check(s);
+    std::vector<uint8_t> out(used);
+    if (used) Check(fn(ctx_, out.data(), used, &used, 0, clear_dirty ? 1 : 0));
+    out.resize(used);
+    return out;
   }
 
   psx_ctx *handle() const { return ctx_; }

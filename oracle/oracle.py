@@ -58,6 +58,10 @@ def lib():
         L.orc_pack_stream.restype = sz
         L.orc_serialize_dirty.argtypes = [vp, vp, ctypes.c_int, vp, sz, ctypes.c_int]
         L.orc_serialize_dirty.restype = i64
+        L.orc_table_set_importance.argtypes = [vp, i32, ctypes.c_int]
+        L.orc_row_importance.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_double)]
+        L.orc_serialize_partial.argtypes = [vp, vp, ctypes.c_int, vp, vp, sz, ctypes.c_int]
+        L.orc_serialize_partial.restype = i64
         L.orc_partition_server.argtypes = [i32, i32, i32, i32]
         L.orc_partition_server.restype = i32
         _lib = L
@@ -93,12 +97,19 @@ class OracleServer:
         assert self._L.orc_register_sender(self._s, bg) == ST_OK
 
     def create_table(self, table_id, kind, dtype, row_capacity, oplog_dense_serialized=True,
-                     dense_row_oplog_capacity=None):
+                     dense_row_oplog_capacity=None, accum_importance=False):
         cap = row_capacity if dense_row_oplog_capacity is None else dense_row_oplog_capacity
         st = self._L.orc_table_create(self._s, table_id, kind, dtype,
                                       1 if oplog_dense_serialized else 0, row_capacity, cap)
         assert st == ST_OK, st
+        if accum_importance:
+            assert self._L.orc_table_set_importance(self._s, table_id, 1) == ST_OK
         self.tables[table_id] = (kind, dtype, row_capacity)
+
+    def importance(self, table_id, row_id):
+        out = ctypes.c_double()
+        assert self._L.orc_row_importance(self._s, table_id, row_id, ctypes.byref(out)) == ST_OK
+        return out.value
 
     def apply_stream(self, data, bg, version):
         """Server::ApplyOpLogUpdateVersion; returns the status code."""
@@ -160,6 +171,21 @@ class OracleServer:
         while True:
             out = np.zeros(nb, dtype=np.uint8)
             r = self._L.orc_serialize_dirty(self._s, _ptr(tids), tids.size, _ptr(out), nb, 1 if clear else 0)
+            if r == -2:
+                nb *= 4
+                continue
+            assert r >= 0, r
+            return out[:r].tobytes()
+
+    def serialize_partial(self, table_ids, upper_bounds, clear=True):
+        """Partial push body (server.cpp:311-420); b"" when nothing is sent."""
+        tids = np.ascontiguousarray(table_ids, dtype=np.int32)
+        ub = np.ascontiguousarray(upper_bounds, dtype=np.int64)
+        nb = 1 << 16
+        while True:
+            out = np.zeros(nb, dtype=np.uint8)
+            r = self._L.orc_serialize_partial(self._s, _ptr(tids), tids.size, _ptr(ub), _ptr(out), nb,
+                                              1 if clear else 0)
             if r == -2:
                 nb *= 4
                 continue

@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 #define ORC_OK 0
 #define ORC_ERR_INVALID_ARG 1
@@ -148,6 +149,8 @@ typedef struct {
   /* map: MapStore<V> (map_store.hpp:45) col -> index into vals */
   imap_t map;
   int dirty;             /* ServerRow::dirty_ (server_row.hpp:133) */
+  double importance;     /* ServerRow::importance_ (server_row.hpp:143); the reference leaves it
+                            uninitialized (:16-19), this restatement starts it at 0 */
 } orc_row;
 
 typedef struct {
@@ -156,6 +159,7 @@ typedef struct {
   int dense_serialized;
   int64_t row_capacity;
   int64_t oplog_capacity;
+  int importance;        /* ApplyRow*AccumImportance selected (server_table.cpp:26-47) */
   imap_t index;          /* row_id -> row number */
   orc_row **rows;
   int64_t nrows, rows_cap;
@@ -318,9 +322,25 @@ static void map_inc(orc_row *r, int32_t col, val_t delta, int dt) {
 
 /* NumericStoreRow::ApplyBatchIncUnsafe (numeric_store_row.hpp:166-175) for one sparse
  * record, dispatched on the store type. */
+static double v_to_double(val_t v, int dt) {
+  switch (dt) {
+    case DT_F32: return (double)v.f;
+    case DT_F64: return v.d;
+    case DT_I32: return (double)v.i;
+    default: return (double)v.l;
+  }
+}
+
 static void apply_sparse_record(orc_table *t, orc_row *r, const int32_t *cols,
                                 const uint8_t *vals, int32_t n) {
   size_t vs = dt_size(t->dt);
+  if (t->importance) {
+    /* NSSumImpCalc::ApplyBatchIncGetImportance (ns_sum_imp_calc.hpp:57-77): the sum of
+     * |u_i| in record order, accumulated into importance_ (server_row.hpp:43-49,124-126) */
+    double acc = 0;
+    for (int32_t i = 0; i < n; ++i) acc += fabs(v_to_double(v_load(vals + (size_t)i * vs, t->dt), t->dt));
+    r->importance += acc;
+  }
   for (int32_t i = 0; i < n; ++i) {
     val_t d = v_load(vals + (size_t)i * vs, t->dt);
     if (t->kind == KIND_DENSE) {
@@ -352,8 +372,32 @@ static void apply_sparse_record(orc_table *t, orc_row *r, const int32_t *cols,
 #define ORC_I32ADD(a, b) ((int32_t)((uint32_t)(a) + (uint32_t)(b)))
 #define ORC_I64ADD(a, b) ((int64_t)((uint64_t)(a) + (uint64_t)(b)))
 
+/* NSSumImpCalc::ApplyDenseBatchIncGetImportance (ns_sum_imp_calc.hpp:79-98): per element,
+ * importance = (double(val) == 0) ? double(u) : double(u) / double(val) with val the value
+ * before the add, summed as |importance| in element order; then val += u. */
+#define ORC_DENSE_IMP_LOOP(T, ADD)                               \
+  do {                                                           \
+    T *val = (T *)r->dense;                                      \
+    double acc = 0;                                              \
+    for (int64_t i = 0; i < n; ++i) {                            \
+      T u;                                                       \
+      memcpy(&u, upd + (size_t)i * sizeof(T), sizeof(T));        \
+      double dv = (double)val[i], du = (double)u;                \
+      acc += fabs(dv == 0 ? du : du / dv);                       \
+      val[i] = ADD(val[i], u);                                   \
+    }                                                            \
+    r->importance += acc;                                        \
+  } while (0)
+
 static void apply_dense_record(orc_table *t, orc_row *r, const uint8_t *upd, int64_t n) {
-  if (t->kind == KIND_DENSE) {
+  if (t->kind == KIND_DENSE && t->importance) {
+    switch (t->dt) {
+      case DT_F32: ORC_DENSE_IMP_LOOP(float, ORC_FADD); break;
+      case DT_F64: ORC_DENSE_IMP_LOOP(double, ORC_FADD); break;
+      case DT_I32: ORC_DENSE_IMP_LOOP(int32_t, ORC_I32ADD); break;
+      default: ORC_DENSE_IMP_LOOP(int64_t, ORC_I64ADD); break;
+    }
+  } else if (t->kind == KIND_DENSE) {
     /* the typed `val[i] += upd[i]` loop of numeric_store_row.hpp:181-184 */
     switch (t->dt) {
       case DT_F32: ORC_DENSE_LOOP(float, ORC_FADD); break;
@@ -474,6 +518,25 @@ int orc_row_dirty(orc_server *s, int32_t table_id, int32_t row_id) {
 int64_t orc_num_rows(orc_server *s, int32_t table_id) {
   orc_table *t = find_table(s, table_id);
   return t ? t->nrows : -1;
+}
+
+/* ServerTable ctor's importance selection (server_table.cpp:26-47): under SSPAggr with a
+ * RelativeMagnitude / FIFO_N_ReMag update-sort policy the table applies through
+ * ApplyRow{Dense,}BatchIncAccumImportance and sorts push candidates by importance. */
+int orc_table_set_importance(orc_server *s, int32_t table_id, int on) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  t->importance = on ? 1 : 0;
+  return ORC_OK;
+}
+
+/* ServerRow::get_importance (server_row.hpp:120-122); absent rows read 0. */
+int orc_row_importance(orc_server *s, int32_t table_id, int32_t row_id, double *out) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  orc_row *r = find_row(t, row_id);
+  *out = r ? r->importance : 0.0;
+  return ORC_OK;
 }
 
 /* AbstractRow::ResetRowData (numeric_store_row.hpp:142-145 -> VectorStore::ResetData
@@ -747,8 +810,8 @@ int64_t orc_serialize_dirty(orc_server *s, const int32_t *table_ids, int ntables
     int64_t w = orc_serialize_records(s, table_ids[ti], ids, (int32_t)nd, o + used, cap - used);
     if (w < 0) { free(ids); return w; }
     used += (size_t)w;
-    if (clear)
-      for (int64_t k = 0; k < nd; ++k) find_row(t, ids[k])->dirty = 0;
+    if (clear)   /* ResetDirty + ResetImportance_ (server_table.cpp:234-235) */
+      for (int64_t k = 0; k < nd; ++k) { orc_row *r = find_row(t, ids[k]); r->dirty = 0; r->importance = 0; }
     free(ids);
     if (used + 4 > cap) return -2;
     int32_t sep = ti + 1 < ntables ? -1 : -2;
@@ -756,4 +819,71 @@ int64_t orc_serialize_dirty(orc_server *s, const int32_t *table_ids, int ntables
     used += 4;
   }
   return (int64_t)used;
+}
+
+/* ---- partial push (SSPAggr) ------------------------------------------------------ */
+/* Server::CreateSendServerPushRowMsgsPartial (server.cpp:311-420) for one client that
+ * subscribes to every row.  Per table: candidates = dirty rows
+ * (GetPartialTableToSendRegular, server_table.cpp:301-346, with select_prob = 1: the
+ * reference samples with a time-seeded generator, so only the all-candidates case is
+ * deterministic); importance tables order them by importance descending, ties by
+ * ascending row id (SortCandidateVectorImportance :272-287); other tables by ascending
+ * row id (the reference shuffles, :263-270); the first upper_bounds[ti] rows are sent
+ * through AppendRowsToBuffsPartial (:381-420): ResetDirty, ResetImportance, record.
+ * Body: per table int32 table_id, records, int32 -1 | -2.  Returns 0 when no table has
+ * a row to send (server.cpp:348), -2 if cap is too small. */
+static orc_table *g_sort_table;
+static int cmp_importance(const void *a, const void *b) {
+  int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+  double ix = find_row(g_sort_table, x)->importance, iy = find_row(g_sort_table, y)->importance;
+  if (ix == iy) return (x > y) - (x < y);
+  return ix > iy ? -1 : 1;
+}
+
+int64_t orc_serialize_partial(orc_server *s, const int32_t *table_ids, int ntables,
+                              const int64_t *upper_bounds, void *out, size_t cap, int clear) {
+  int32_t *sel[64];
+  int64_t nsel[64];
+  int any = 0;
+  if (ntables > 64) return -3;
+  for (int ti = 0; ti < ntables; ++ti) {
+    orc_table *t = find_table(s, table_ids[ti]);
+    if (!t) { for (int k = 0; k < ti; ++k) free(sel[k]); return -3; }
+    int32_t *ids = (int32_t *)malloc((size_t)(t->nrows + 1) * 4);
+    int64_t nd = 0;
+    for (int64_t i = 0; i < t->index.cap; ++i)
+      if (t->index.used[i] == 1 && t->rows[t->index.vals[i]]->dirty) ids[nd++] = t->index.keys[i];
+    qsort(ids, (size_t)nd, 4, cmp_i32);
+    if (t->importance) { g_sort_table = t; qsort(ids, (size_t)nd, 4, cmp_importance); }
+    if (nd > upper_bounds[ti]) nd = upper_bounds[ti];
+    sel[ti] = ids; nsel[ti] = nd;
+    if (nd) any = 1;
+  }
+  int64_t ret = 0;
+  if (any) {
+    uint8_t *o = (uint8_t *)out;
+    size_t used = 0;
+    for (int ti = 0; ti < ntables && ret >= 0; ++ti) {
+      if (used + 4 > cap) { ret = -2; break; }
+      memcpy(o + used, &table_ids[ti], 4);
+      used += 4;
+      int64_t w = orc_serialize_records(s, table_ids[ti], sel[ti], (int32_t)nsel[ti], o + used, cap - used);
+      if (w < 0) { ret = w; break; }
+      used += (size_t)w;
+      if (used + 4 > cap) { ret = -2; break; }
+      int32_t sep = ti + 1 < ntables ? -1 : -2;
+      memcpy(o + used, &sep, 4);
+      used += 4;
+    }
+    if (ret == 0) {
+      ret = (int64_t)used;
+      if (clear)
+        for (int ti = 0; ti < ntables; ++ti) {
+          orc_table *t = find_table(s, table_ids[ti]);
+          for (int64_t k = 0; k < nsel[ti]; ++k) { orc_row *r = find_row(t, sel[ti][k]); r->dirty = 0; r->importance = 0; }
+        }
+    }
+  }
+  for (int ti = 0; ti < ntables; ++ti) free(sel[ti]);
+  return ret;
 }

@@ -35,6 +35,9 @@ class psx_table_config(ctypes.Structure):
         ("row_stride", ctypes.c_int64),
         ("max_rows", ctypes.c_int64),
         ("max_entries", ctypes.c_int64),
+        ("accum_importance", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("server_push_row_upper_bound", ctypes.c_int64),
     ]
 
 
@@ -93,6 +96,8 @@ def load():
         "psx_sync": ([vp], ctypes.c_int),
         "psx_serialize_rows": ([vp, i32, vp, i32, vp, sz, P(sz)], ctypes.c_int),
         "psx_serialize_dirty": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
+        "psx_serialize_partial": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
+        "psx_row_importance": ([vp, i32, i64, i64, vp], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),
         "psx_timing_enable": ([vp, i32], ctypes.c_int),

@@ -79,6 +79,7 @@ struct DenseArgs {
   uint32_t *sticky;
   uint32_t *call_status;
   const uint8_t *zero_chunk;   // >= 2 KiB of zeros, stands in for absent messages
+  double *imp;                 // non-null: accumulate NSSumImpCalc importance per slot
 };
 
 // Fast-path dense tables of one call (for the duplicate-row gate).
@@ -114,6 +115,7 @@ struct OrdArgs {
   uint32_t *call_status;
   const uint32_t *sticky;
   int force;              // replay: ignore the sticky duplicate flag
+  double *imp;            // non-null: accumulate NSSumImpCalc importance per slot
 };
 
 // Arguments of the serve-back kernels (psx_serve.hip).
@@ -131,7 +133,31 @@ struct ServeArgs {
   int64_t *offs;
   uint8_t *out;              // record region base (4-byte aligned)
   uint8_t *flags_rw;         // non-null: clear bit1 (dirty) of every emitted row
+  double *imp_rw;            // non-null (with flags_rw): reset importance of every emitted row
+  // partial push (psx_serialize_partial)
+  const double *imp;         // importance per slot (null: no importance ordering)
+  double *keys;              // sort keys per slot: importance (or 0) if dirty, -1 otherwise
+  int32_t *vals;             // slot ids (sort payload)
+  uint32_t *ndirty;          // dirty-row count
+  const int32_t *sel;        // emit list: slots in send order
+  int64_t nsel;
+  int64_t *lsizes;           // record bytes per list entry
+  int64_t *loffs;            // exclusive prefix of lsizes + scan tile sums
 };
+
+// Importance term of one dense element (ns_sum_imp_calc.hpp:87-90), before the add.
+template <typename V>
+__device__ __forceinline__ double imp_term(V old, V u) {
+  const double dv = (double)old, du = (double)u;
+  return __builtin_fabs(dv == 0.0 ? du : du / dv);
+}
+
+// Butterfly sum over the 64 lanes of a wave; every lane receives the total.
+__device__ __forceinline__ double wave_sum_f64(double x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
 
 // Write a few 4-byte words (table ids and separators) into the body.
 struct Words {

@@ -316,7 +316,12 @@ template <> struct Elem<int64_t> {
 // inverse-index entries of slot k (and restores them to -1), writes the slot's flags,
 // then the wave walks the touched slots; for each, 4 elements per lane per 256-element
 // chunk: 1 table load + B record loads issued back to back, then the in-order sum.
-template <typename V, int BMAX>
+// IMP: also accumulate each record's NSSumImpCalc importance, sum_i |u_i / v_i| with v_i
+// the value before that record's add (ns_sum_imp_calc.hpp:79-98), into imp[slot] in
+// message order (ServerRow::AccumImportance, server_row.hpp:56-62,124-126).  Within a
+// record the f64 terms are summed lane-parallel (non-negative terms: the result is
+// within (cap-1)*2^-53 relative of the reference's element-order sum).
+template <typename V, int BMAX, bool IMP>
 __global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -376,6 +381,9 @@ __global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
       present[b] = (b < B) && i >= 0;
       rb[b] = present[b] ? a.ss.data[b] + rec0[b] + (int64_t)i * a.stride + 4 : a.zero_chunk;
     }
+    double ib[IMP ? BMAX : 1];
+#pragma unroll
+    for (int b = 0; b < (IMP ? BMAX : 1); ++b) ib[b] = 0.0;
     for (int64_t c0 = 0; c0 < a.cap; c0 += 256) {
       V t[4];
       V u[BMAX][4];
@@ -396,12 +404,24 @@ __global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         V acc = t[j];
+        const int64_t e = c0 + lane + 64 * j;
 #pragma unroll
         for (int b = 0; b < BMAX; ++b)
-          if (present[b]) acc = Elem<V>::add(acc, u[b][j]);
-        const int64_t e = c0 + lane + 64 * j;
+          if (present[b]) {
+            if constexpr (IMP) {
+              if (e < a.cap) ib[b] += imp_term<V>(acc, u[b][j]);
+            }
+            acc = Elem<V>::add(acc, u[b][j]);
+          }
         if (e < a.cap) trow[e] = acc;
       }
+    }
+    if constexpr (IMP) {
+      double tot = a.imp[slot];
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b)
+        if (present[b]) tot += wave_sum_f64(ib[b]);
+      if (lane == 0) a.imp[slot] = tot;
     }
   }
 }
@@ -750,7 +770,7 @@ static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
   switch (g_apply_variant) {
     case 0: {
       const int64_t tiles = (a.max_rows + 63) / 64;
-      hipLaunchKernelGGL((dense_apply_kernel<V, BMAX>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((dense_apply_kernel<V, BMAX, false>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, a);
       break;
     }
     case 1: launch_v2<V, BMAX, 64, false, 1>(a, st); break;
@@ -775,7 +795,14 @@ static void launch_adaptive(const DenseArgs &a, hipStream_t st) {
 
 template <typename V>
 static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
-  if (g_apply_variant == 6)
+  const int64_t tiles = (a.max_rows + 63) / 64;
+  const dim3 grid((unsigned)((tiles + 3) / 4));
+  if (a.imp) {   // importance tables (SSPAggr): the one-row-per-wave kernel with the f64 reduction
+    if (a.B <= 8)
+      hipLaunchKernelGGL((dense_apply_kernel<V, 8, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((dense_apply_kernel<V, 16, true>), grid, dim3(256), 0, st, a);
+  } else if (g_apply_variant == 6)
     launch_adaptive<V>(a, st);
   else if (a.B <= 8)
     launch_apply_bmax<V, 8>(a, st);

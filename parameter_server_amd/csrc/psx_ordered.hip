@@ -198,6 +198,15 @@ __device__ __forceinline__ int32_t wave_rank_sort(int32_t r, int L, int lane, in
   return out;
 }
 
+// NSSumImpCalc::ApplyBatchIncGetImportance (ns_sum_imp_calc.hpp:57-77): sum of |u_i|
+// over a sparse record's values, lane-parallel then a wave butterfly.
+template <typename V>
+__device__ __forceinline__ double sparse_importance(const uint8_t *vals, int32_t nn, int lane) {
+  double p = 0.0;
+  for (int32_t i = lane; i < nn; i += 64) p += __builtin_fabs((double)ldv<V>(vals + (int64_t)i * sizeof(V)));
+  return wave_sum_f64(p);
+}
+
 template <typename V, int KIND>
 __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
   extern __shared__ __align__(16) uint8_t dyn[];
@@ -250,6 +259,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
         wave_sync();
       }
       uint8_t *drow = reinterpret_cast<uint8_t *>(a.dense) + slot * a.row_cap * (int64_t)sizeof(V);
+      double impt = a.imp ? a.imp[slot] : 0.0;
 
       for (int32_t q = 0; q < L; ++q) {
         const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
@@ -259,16 +269,21 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
         const uint8_t *rec = a.ss.data[b] + roff;
         if (a.dense_records) {
           // duplicate-row replay of a dense record: row[e] += rec[e] (lane owns e)
+          double p = 0.0;
           for (int64_t e = lane; e < a.cap; e += 64) {
             V x = ldv<V>(drow + e * sizeof(V));
-            x = OV<V>::add(x, ldv<V>(rec + 4 + e * sizeof(V)));
+            const V u = ldv<V>(rec + 4 + e * sizeof(V));
+            if (a.imp) p += imp_term<V>(x, u);
+            x = OV<V>::add(x, u);
             stv<V>(drow + e * sizeof(V), x);
           }
+          if (a.imp) impt += wave_sum_f64(p);
           continue;
         }
         const int32_t nn = o_ld32(rec + 4);
         const uint8_t *cols = rec + 8;
         const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
+        if (a.imp) impt += sparse_importance<V>(vals, nn, lane);
         if (KIND == 0) {
           // VectorStore::Inc per (col, val), in record order.  Lanes run in parallel
           // when the record's columns are strictly ascending (what both reference
@@ -383,6 +398,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
         if (lane == 0) a.nent[slot] = n;
         wave_sync();
       }
+      if (a.imp && lane == 0) a.imp[slot] = impt;
     }
   }
 }
@@ -473,6 +489,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         key[j] = i < n ? o_ld32(row + (int64_t)i * ES) : 0;
         val[j] = i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
       }
+      double impt = a.imp ? a.imp[slot] : 0.0;
       for (int32_t q = 0; q < L; ++q) {
         const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
         int b;
@@ -482,6 +499,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         const int32_t nn = o_ld32(rec + 4);
         const uint8_t *cols = rec + 8;
         const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
+        if (a.imp) impt += sparse_importance<V>(vals, nn, lane);
         for (int32_t c0 = 0; c0 < nn; c0 += 64) {
           const int32_t pi = c0 + lane;
           const int32_t my_col = pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0;
@@ -613,6 +631,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         }
       }
       if (lane == 0) a.nent[slot] = n;
+      if (a.imp && lane == 0) a.imp[slot] = impt;
     }
   }
 }
@@ -635,7 +654,6 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 // ---------------------------------------------------------------------------
 hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
   const int64_t n = a.max_rows;
-  const int64_t ntiles = (n + 1023) / 1024;
   hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
   launch_exclusive_scan<int32_t>(a.cnt, n, a.off, a.tsum, st);
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);

@@ -41,6 +41,10 @@ hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMas
 hipError_t launch_serve_sizes(const ServeArgs &a, hipStream_t st);
 hipError_t launch_serve_emit(const ServeArgs &a, hipStream_t st);
 hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st);
+hipError_t launch_serve_list_sizes(const ServeArgs &a, hipStream_t st);
+hipError_t launch_serve_emit_list(const ServeArgs &a, hipStream_t st);
+hipError_t launch_sort_desc(void *temp, size_t *temp_bytes, const double *keys_in, double *keys_out,
+                            const int32_t *vals_in, int32_t *vals_out, int64_t n, hipStream_t st);
 hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *entries, int64_t max_entries,
                                  const int64_t *slots, int32_t n, int32_t *out_n, uint8_t *out,
                                  hipStream_t st);
@@ -68,12 +72,22 @@ struct TableState {
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
+  double *d_imp = nullptr;         // accum_importance: ServerRow::importance_ per slot
+  // partial push scratch (allocated on first psx_serialize_partial)
+  double *d_pkeys[2] = {nullptr, nullptr};
+  int32_t *d_pvals[2] = {nullptr, nullptr};
+  int64_t *d_lsizes = nullptr;
+  int64_t *d_loffs = nullptr;
+  void *d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   bool fast() const { return cfg.row_kind == PSX_ROW_DENSE && cfg.oplog_dense_serialized; }
 };
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_srv_sizes, t.d_srv_offs};
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_srv_sizes, t.d_srv_offs,
+                  t.d_imp, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
+                  t.d_lsizes, t.d_loffs, t.d_sort_tmp};
   for (void *p : ptrs)
     if (p) hipFree(p);
 }
@@ -108,6 +122,7 @@ struct psx_ctx {
   hipEvent_t ev_ready[2] = {nullptr, nullptr};    // slot's index stage done (side -> main)
   hipEvent_t ev_free[2] = {nullptr, nullptr};     // slot's apply stage done (main -> side)
   bool pipeline = false;                          // PSX_PIPELINE=1: overlap (no gain measured, DRAM-bound)
+  uint32_t *d_ndirty = nullptr;          // partial push: dirty-row count
   uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
   uint8_t *d_zero = nullptr;
   uint8_t *d_staging = nullptr;
@@ -397,6 +412,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.call_status = call_st;
     a.sticky = sticky;
     a.force = force_ordered ? 1 : 0;
+    a.imp = t.d_imp;
     st = timed(c, "ordered_apply", [&] { return psx::launch_ordered(t.cfg.dtype, a, c->stream); });
     if (st) return st;
   }
@@ -422,6 +438,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.sticky = sticky;
     a.call_status = call_st;
     a.zero_chunk = c->d_zero;
+    a.imp = t.d_imp;
     st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream); });
     if (st) return st;
   }
@@ -489,6 +506,31 @@ psx_status sync_impl(psx_ctx *c) {
   psx_status e = sticky_error(c, sticky & ~psx::kStDuplicateRow);
   if (e) return e;
   return sticky_error(c, replay_sticky);
+}
+
+// Serve-back kernel arguments for table t (allocates its size/offset scratch once).
+psx_status serve_args(psx_ctx *c, TableState &t, psx::ServeArgs *out) {
+  const int64_t R = t.cfg.max_rows;
+  if (!t.d_srv_sizes) {
+    HIP_TRY(c, hipMalloc(&t.d_srv_sizes, sizeof(int64_t) * R));
+    HIP_TRY(c, hipMalloc(&t.d_srv_offs, sizeof(int64_t) * (R + 1 + (R + 1023) / 1024)));
+  }
+  psx::ServeArgs a{};
+  a.flags = t.d_flags;
+  a.nent = t.d_nent;
+  a.dense = (const uint8_t *)t.d_data;
+  a.entries = t.d_entries;
+  a.kind = t.cfg.row_kind;
+  a.vsize = t.vsize;
+  a.row_cap = t.cfg.row_capacity;
+  a.max_entries = t.max_entries;
+  a.row_offset = t.cfg.row_offset;
+  a.row_stride = t.cfg.row_stride;
+  a.max_rows = R;
+  a.sizes = t.d_srv_sizes;
+  a.offs = t.d_srv_offs;
+  *out = a;
+  return PSX_OK;
 }
 
 }  // namespace
@@ -578,6 +620,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->side) hipStreamDestroy(c->side);
   if (c->d_status) hipFree(c->d_status);
   if (c->d_zero) hipFree(c->d_zero);
+  if (c->d_ndirty) hipFree(c->d_ndirty);
   if (c->d_staging) hipFree(c->d_staging);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
@@ -617,8 +660,12 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
   if (cfg->max_rows <= 0 || cfg->row_stride <= 0) return fail(c, PSX_ERR_INVALID_ARG, "bad shard geometry");
   if (cfg->max_rows > ((int64_t)1 << 31) - 2) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
+  if (cfg->reserved0 != 0 || cfg->server_push_row_upper_bound < 0 ||
+      (cfg->accum_importance != 0 && cfg->accum_importance != 1))
+    return fail(c, PSX_ERR_INVALID_ARG, "bad accum_importance / reserved0 / server_push_row_upper_bound");
   TableState t;
   t.cfg = *cfg;
+  if (t.cfg.server_push_row_upper_bound == 0) t.cfg.server_push_row_upper_bound = 100;   // table_gflags.cpp:21
   t.vsize = vsize_of(cfg->dtype);
   t.es = t.vsize == 4 ? 8 : 16;
   if (cfg->row_kind == PSX_ROW_DENSE) {
@@ -648,6 +695,10 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     e = hipMalloc(&t.d_nent, R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&t.d_entries, R * (size_t)t.max_entries * t.es);
     if (e == hipSuccess) e = hipMemsetAsync(t.d_nent, 0, R * sizeof(int32_t), c->stream);
+  }
+  if (e == hipSuccess && cfg->accum_importance) {
+    e = hipMalloc(&t.d_imp, R * sizeof(double));
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_imp, 0, R * sizeof(double), c->stream);
   }
   if (e == hipSuccess) e = hipMalloc(&t.d_flags, R);
   if (e == hipSuccess) e = hipMemsetAsync(t.d_flags, 0, R, c->stream);
@@ -736,6 +787,22 @@ psx_status psx_clear_dirty(psx_ctx *c, int32_t table_id) {
   if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, psx::launch_flags_and(t->d_flags, t->cfg.max_rows, (uint8_t)~2u, c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_row_importance(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows, double *dst) {
+  if (!c || (!dst && num_rows)) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  if (!t->d_imp) {
+    for (int64_t i = 0; i < num_rows; ++i) dst[i] = 0.0;
+    return PSX_OK;
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipMemcpyAsync(dst, t->d_imp + s, sizeof(double) * (size_t)num_rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return PSX_OK;
 }
 
@@ -896,27 +963,9 @@ psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, 
   std::vector<psx::ServeArgs> args(T);
   for (size_t i = 0; i < T; ++i) {
     TableState &t = c->tables[i];
-    const int64_t R = t.cfg.max_rows;
-    if (!t.d_srv_sizes) {
-      HIP_TRY(c, hipMalloc(&t.d_srv_sizes, sizeof(int64_t) * R));
-      HIP_TRY(c, hipMalloc(&t.d_srv_offs, sizeof(int64_t) * (R + 1 + (R + 1023) / 1024)));
-    }
-    psx::ServeArgs &a = args[i];
-    a = psx::ServeArgs{};
-    a.flags = t.d_flags;
-    a.nent = t.d_nent;
-    a.dense = (const uint8_t *)t.d_data;
-    a.entries = t.d_entries;
-    a.kind = t.cfg.row_kind;
-    a.vsize = t.vsize;
-    a.row_cap = t.cfg.row_capacity;
-    a.max_entries = t.max_entries;
-    a.row_offset = t.cfg.row_offset;
-    a.row_stride = t.cfg.row_stride;
-    a.max_rows = R;
-    a.sizes = t.d_srv_sizes;
-    a.offs = t.d_srv_offs;
-    HIP_TRY(c, psx::launch_serve_sizes(a, c->stream));
+    psx_status st = serve_args(c, t, &args[i]);
+    if (st) return st;
+    HIP_TRY(c, psx::launch_serve_sizes(args[i], c->stream));
   }
   // lay out {table_id, records..., -1 | -2} per table (server.cpp:189-309)
   psx::Words w{};
@@ -953,7 +1002,103 @@ psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, 
   for (size_t i = 0; i < T; ++i) {
     args[i].out = dst + base[i];
     args[i].flags_rw = clear_dirty ? c->tables[i].d_flags : nullptr;
+    args[i].imp_rw = clear_dirty ? c->tables[i].d_imp : nullptr;
     HIP_TRY(c, psx::launch_serve_emit(args[i], c->stream));
+  }
+  HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
+  if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used, int32_t out_on_device,
+                                 int32_t clear_dirty) {
+  if (!c || !used) return PSX_ERR_INVALID_ARG;
+  *used = 0;
+  if (out_on_device && ((uintptr_t)out & 3)) return fail(c, PSX_ERR_INVALID_ARG, "device output must be 4-byte aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (!c->d_ndirty) HIP_TRY(c, hipMalloc(&c->d_ndirty, sizeof(uint32_t)));
+  const size_t T = c->tables.size();
+  std::vector<psx::ServeArgs> args(T);
+  std::vector<int64_t> bytes(T, 0);
+  bool any = false;
+  for (size_t i = 0; i < T; ++i) {
+    TableState &t = c->tables[i];
+    const int64_t R = t.cfg.max_rows;
+    psx_status st = serve_args(c, t, &args[i]);
+    if (st) return st;
+    if (!t.d_pkeys[0]) {
+      for (int k = 0; k < 2; ++k) {
+        HIP_TRY(c, hipMalloc(&t.d_pkeys[k], sizeof(double) * R));
+        HIP_TRY(c, hipMalloc(&t.d_pvals[k], sizeof(int32_t) * R));
+      }
+      HIP_TRY(c, hipMalloc(&t.d_lsizes, sizeof(int64_t) * R));
+      HIP_TRY(c, hipMalloc(&t.d_loffs, sizeof(int64_t) * (R + 1 + (R + 1023) / 1024)));
+      size_t tb = 0;
+      HIP_TRY(c, psx::launch_sort_desc(nullptr, &tb, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1], R,
+                                       c->stream));
+      HIP_TRY(c, hipMalloc(&t.d_sort_tmp, tb ? tb : 1));
+      t.sort_tmp_bytes = tb;
+    }
+    psx::ServeArgs &a = args[i];
+    a.imp = t.d_imp;
+    a.keys = t.d_pkeys[0];
+    a.vals = t.d_pvals[0];
+    a.ndirty = c->d_ndirty;
+    HIP_TRY(c, hipMemsetAsync(c->d_ndirty, 0, sizeof(uint32_t), c->stream));
+    HIP_TRY(c, psx::launch_serve_sizes(a, c->stream));
+    size_t tb = t.sort_tmp_bytes;
+    HIP_TRY(c, psx::launch_sort_desc(t.d_sort_tmp, &tb, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1], R,
+                                     c->stream));
+    uint32_t nd = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nd, c->d_ndirty, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    a.keys = nullptr;
+    a.sel = t.d_pvals[1];
+    a.nsel = std::min<int64_t>((int64_t)nd, t.cfg.server_push_row_upper_bound);
+    a.lsizes = t.d_lsizes;
+    a.loffs = t.d_loffs;
+    if (a.nsel > 0) {
+      any = true;
+      HIP_TRY(c, psx::launch_serve_list_sizes(a, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(&bytes[i], a.loffs + a.nsel, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+  }
+  if (!any) return PSX_OK;   // nothing to send (server.cpp:348)
+  psx::Words w{};
+  std::vector<int64_t> base(T);
+  int64_t pos = 0;
+  for (size_t i = 0; i < T; ++i) {
+    w.pos[w.n] = pos;
+    w.val[w.n++] = c->tables[i].cfg.table_id;
+    pos += 4;
+    base[i] = pos;
+    pos += bytes[i];
+    w.pos[w.n] = pos;
+    w.val[w.n++] = i + 1 < T ? -1 : -2;
+    pos += 4;
+  }
+  *used = (size_t)pos;
+  if ((size_t)pos > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize_partial: *used bytes needed");
+  uint8_t *dst = (uint8_t *)out;
+  if (!out_on_device) {
+    if ((size_t)pos > c->staging_cap) {
+      if (c->d_staging) hipFree(c->d_staging);
+      c->d_staging = nullptr;
+      c->staging_cap = 0;
+      HIP_TRY(c, hipMalloc(&c->d_staging, (size_t)pos));
+      c->staging_cap = (size_t)pos;
+    }
+    dst = c->d_staging;
+  }
+  for (size_t i = 0; i < T; ++i) {
+    args[i].out = dst + base[i];
+    args[i].flags_rw = clear_dirty ? c->tables[i].d_flags : nullptr;
+    args[i].imp_rw = clear_dirty ? c->tables[i].d_imp : nullptr;
+    HIP_TRY(c, psx::launch_serve_emit_list(args[i], c->stream));
   }
   HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
   if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));

@@ -13,7 +13,13 @@
 // Row bodies: DenseRow V[capacity] (vector_store.hpp:75-80); SortedVectorMapRow
 // Entry<V>[n] in store order (sorted_vector_map_store.hpp:148-152); SparseRow packed
 // {int32 col; V val}[n] (map_store.hpp:89-100).  Rows come out in ascending row id.
+// Partial push (psx_serialize_partial, server.cpp:311-420): serve_sizes also writes a
+// sort key per slot (importance, or 0, for dirty rows; -1 otherwise); a stable
+// descending radix sort of (key, slot) puts the dirty rows in send order — importance
+// descending, ties by ascending slot = ascending row id (server_table.cpp:272-287); the
+// first upper_bound entries are the send list, emitted by serve_emit_list.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <cstdint>
 #include "psx_device.hpp"
 #include "psx_scan.hpp"
@@ -30,8 +36,58 @@ __device__ __forceinline__ int64_t body_bytes(const ServeArgs &a, int64_t s) {
 
 __global__ void __launch_bounds__(256) serve_sizes_kernel(ServeArgs a) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.max_rows) return;
-  a.sizes[s] = (a.flags[s] & 3) == 3 ? 12 + body_bytes(a, s) : 0;
+  const bool in = s < a.max_rows;
+  const bool dirty = in && (a.flags[s] & 3) == 3;
+  if (in) a.sizes[s] = dirty ? 12 + body_bytes(a, s) : 0;
+  if (a.keys) {
+    if (in) {
+      a.keys[s] = dirty ? (a.imp ? a.imp[s] : 0.0) : -1.0;
+      a.vals[s] = (int32_t)s;
+    }
+    const uint64_t bal = __ballot(dirty);
+    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(a.ndirty, (uint32_t)__builtin_popcountll(bal));
+  }
+}
+
+__global__ void __launch_bounds__(256) serve_list_sizes_kernel(ServeArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.nsel) a.lsizes[i] = a.sizes[a.sel[i]];
+}
+
+// One record {int32 row_id; size_t size; row bytes} for slot s at rec (one wave); with
+// flags_rw, ResetDirty and ResetImportance_ (server_table.cpp:234-235, :398-399).
+__device__ void emit_row(const ServeArgs &a, int64_t s, uint8_t *rec, int lane) {
+  const int64_t body = a.sizes[s] - 12;
+  if (lane == 0) {
+    const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
+    reinterpret_cast<int32_t *>(rec)[0] = rid;
+    reinterpret_cast<uint32_t *>(rec)[1] = (uint32_t)(uint64_t)body;           // size_t, 4-aligned
+    reinterpret_cast<uint32_t *>(rec)[2] = (uint32_t)((uint64_t)body >> 32);
+  }
+  uint32_t *dst = reinterpret_cast<uint32_t *>(rec + 12);
+  if (a.kind == 0) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.dense + s * a.row_cap * a.vsize);
+    for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
+  } else if (a.kind == 1) {
+    const int64_t es = a.vsize == 4 ? 8 : 16;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.entries + s * a.max_entries * es);
+    for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
+  } else {
+    const int64_t es = a.vsize == 4 ? 8 : 16, vo = a.vsize == 4 ? 4 : 8;
+    const uint8_t *src = a.entries + s * a.max_entries * es;
+    const int32_t n = a.nent[s];
+    const int wpe = 1 + a.vsize / 4;                  // words per packed {int32, V}
+    for (int32_t e = lane; e < n; e += 64) {
+      uint32_t *d = dst + (int64_t)e * wpe;
+      d[0] = *reinterpret_cast<const uint32_t *>(src + e * es);
+      d[1] = *reinterpret_cast<const uint32_t *>(src + e * es + vo);
+      if (wpe == 3) d[2] = *reinterpret_cast<const uint32_t *>(src + e * es + vo + 4);
+    }
+  }
+  if (lane == 0 && a.flags_rw) {
+    a.flags_rw[s] &= (uint8_t)~2u;
+    if (a.imp_rw) a.imp_rw[s] = 0.0;
+  }
 }
 
 __global__ void __launch_bounds__(256) serve_emit_kernel(ServeArgs a) {
@@ -47,39 +103,19 @@ __global__ void __launch_bounds__(256) serve_emit_kernel(ServeArgs a) {
       const int k = __builtin_ctzll(live);
       live &= live - 1;
       const int64_t s = tile * 64 + k;
-      uint8_t *rec = a.out + a.offs[s];
-      const int64_t body = a.sizes[s] - 12;
-      if (lane == 0) {
-        const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
-        reinterpret_cast<int32_t *>(rec)[0] = rid;
-        reinterpret_cast<uint32_t *>(rec)[1] = (uint32_t)(uint64_t)body;           // size_t, 4-aligned
-        reinterpret_cast<uint32_t *>(rec)[2] = (uint32_t)((uint64_t)body >> 32);
-      }
-      uint32_t *dst = reinterpret_cast<uint32_t *>(rec + 12);
-      if (a.kind == 0) {
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.dense + s * a.row_cap * a.vsize);
-        for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
-      } else if (a.kind == 1) {
-        const int64_t es = a.vsize == 4 ? 8 : 16;
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.entries + s * a.max_entries * es);
-        for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
-      } else {
-        const int64_t es = a.vsize == 4 ? 8 : 16, vo = a.vsize == 4 ? 4 : 8;
-        const uint8_t *src = a.entries + s * a.max_entries * es;
-        const int32_t n = a.nent[s];
-        const int wpe = 1 + a.vsize / 4;                  // words per packed {int32, V}
-        for (int32_t e = lane; e < n; e += 64) {
-          uint32_t *d = dst + (int64_t)e * wpe;
-          d[0] = *reinterpret_cast<const uint32_t *>(src + e * es);
-          d[1] = *reinterpret_cast<const uint32_t *>(src + e * es + vo);
-          if (wpe == 3) d[2] = *reinterpret_cast<const uint32_t *>(src + e * es + vo + 4);
-        }
-      }
-      if (lane == 0 && a.flags_rw) a.flags_rw[s] &= (uint8_t)~2u;   // ResetDirty (server_table.cpp:229)
+      emit_row(a, s, a.out + a.offs[s], lane);
     }
   }
 }
 
+
+// Emit the send list: one wave per entry, records in list order.
+__global__ void __launch_bounds__(256) serve_emit_list_kernel(ServeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave_g; i < a.nsel; i += nwaves) emit_row(a, a.sel[i], a.out + a.loffs[i], lane);
+}
 
 __global__ void put_words_kernel(uint8_t *out, Words w) {
   for (int i = threadIdx.x; i < w.n; i += blockDim.x) *reinterpret_cast<int32_t *>(out + w.pos[i]) = w.val[i];
@@ -98,6 +134,28 @@ hipError_t launch_serve_emit(const ServeArgs &a, hipStream_t st) {
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(serve_emit_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   return hipGetLastError();
+}
+
+hipError_t launch_serve_list_sizes(const ServeArgs &a, hipStream_t st) {
+  if (a.nsel <= 0) return hipSuccess;
+  hipLaunchKernelGGL(serve_list_sizes_kernel, dim3((unsigned)((a.nsel + 255) / 256)), dim3(256), 0, st, a);
+  launch_exclusive_scan<int64_t>(a.lsizes, a.nsel, a.loffs, a.loffs + a.nsel + 1, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_serve_emit_list(const ServeArgs &a, hipStream_t st) {
+  if (a.nsel <= 0) return hipSuccess;
+  int64_t blocks = (a.nsel + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(serve_emit_list_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// Stable descending sort of (key, slot) pairs.  temp == nullptr: *temp_bytes <- size.
+hipError_t launch_sort_desc(void *temp, size_t *temp_bytes, const double *keys_in, double *keys_out,
+                            const int32_t *vals_in, int32_t *vals_out, int64_t n, hipStream_t st) {
+  return hipcub::DeviceRadixSort::SortPairsDescending(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                                      (int)n, 0, 64, st);
 }
 
 hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st) {

@@ -28,6 +28,8 @@ class TableInfo:
     row_stride: int = 1
     max_rows: int = 0
     max_entries: int = 0
+    accum_importance: bool = False          # SSPAggr + RelativeMagnitude/FIFO_N_ReMag (server_table.cpp:26-47)
+    server_push_row_upper_bound: int = 0    # configs.hpp:181; 0 -> 100
 
 
 def _check(L, ctx, st):
@@ -84,7 +86,8 @@ class Server:
             row_capacity=info.row_capacity,
             dense_row_oplog_capacity=info.dense_row_oplog_capacity or info.row_capacity,
             row_offset=info.row_offset, row_stride=info.row_stride, max_rows=info.max_rows,
-            max_entries=info.max_entries)
+            max_entries=info.max_entries, accum_importance=1 if info.accum_importance else 0,
+            server_push_row_upper_bound=info.server_push_row_upper_bound)
         _check(self._L, self._ctx, self._L.psx_table_create(self._ctx, ctypes.byref(cfg)))
         self.tables[table_id] = info
 
@@ -143,6 +146,13 @@ class Server:
             self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data)))
         return out
 
+    def row_importance(self, table_id, first_row, num_rows):
+        """ServerRow::get_importance for a row range (server_row.hpp:120-122)."""
+        out = np.zeros(num_rows, dtype=np.float64)
+        _check(self._L, self._ctx, self._L.psx_row_importance(
+            self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data)))
+        return out
+
     def clear_dirty(self, table_id):
         _check(self._L, self._ctx, self._L.psx_clear_dirty(self._ctx, table_id))
 
@@ -167,8 +177,17 @@ class Server:
         Returns a numpy uint8 view of the body.  The body lands in page-locked host
         memory (kept by this object and reused, so the view is valid until the next
         call) unless `out` (a writable numpy uint8 array) is given."""
+        return self._serialize(self._L.psx_serialize_dirty, clear, out)
+
+    def serialize_partial(self, clear=True, out=None):
+        """Partial push body (Server::CreateSendServerPushRowMsgsPartial, server.cpp:311-420):
+        per table the first server_push_row_upper_bound dirty rows in send order.  An
+        empty array when no table has a row to send."""
+        return self._serialize(self._L.psx_serialize_partial, clear, out)
+
+    def _serialize(self, fn, clear, out):
         used = ctypes.c_size_t()
-        st = self._L.psx_serialize_dirty(self._ctx, None, 0, ctypes.byref(used), 0, 0)
+        st = fn(self._ctx, None, 0, ctypes.byref(used), 0, 0)
         if st not in (_abi.PSX_OK, 9):
             _check(self._L, self._ctx, st)
         need = max(used.value, 1)
@@ -179,8 +198,8 @@ class Server:
                 self._pinned = buf = torch.empty(need + need // 4, dtype=torch.uint8, pin_memory=True)
             out = buf.numpy()
         assert out.dtype == np.uint8 and out.size >= need
-        _check(self._L, self._ctx, self._L.psx_serialize_dirty(
-            self._ctx, ctypes.c_void_p(out.ctypes.data), out.size, ctypes.byref(used), 0, 1 if clear else 0))
+        _check(self._L, self._ctx, fn(self._ctx, ctypes.c_void_p(out.ctypes.data), out.size,
+                                      ctypes.byref(used), 0, 1 if clear else 0))
         return out[:used.value]
 
     # -- timing ------------------------------------------------------------------------

@@ -132,3 +132,38 @@ def test_multi_table_pack_matches_packer(oracle_lib):
               dict(table_id=2, dtype=F32, dense_serialized=True, row_ids=np.arange(7, dtype=np.int32) * 3,
                    oplogs=dense)]
     assert wire.pack_np(tables).tobytes() == pack_stream(tables)
+
+
+def test_oracle_dense_importance_hand_computed(oracle_lib):
+    """NSSumImpCalc::ApplyDenseBatchIncGetImportance (ns_sum_imp_calc.hpp:79-98):
+    sum_i |u_i / v_i|, |u_i| where v_i == 0, with v the value before the add;
+    accumulated per record into importance_ (server_row.hpp:56-62)."""
+    s = OracleServer([1])
+    s.create_table(1, DENSE, F32, 4, accum_importance=True)
+    s.load_dense_rows(1, 0, np.array([[1, 0, 2, -4]], np.float32))
+    upd = np.array([[1, 1, 1, 1]], np.float32)
+    assert s.apply_stream(wire.dense_stream_np(1, np.array([0], np.int32), upd), 1, 0) == 0
+    assert s.importance(1, 0) == 1 + 1 + 0.5 + 0.25
+    # second record sees the updated values [2, 1, 3, -3]
+    assert s.apply_stream(wire.dense_stream_np(1, np.array([0], np.int32), upd * -3), 1, 1) == 0
+    assert s.importance(1, 0) == 2.75 + 1.5 + 3 + 1 + 1
+
+
+def test_oracle_sparse_importance_and_partial_push(oracle_lib):
+    """Sparse records add sum |u| (ns_sum_imp_calc.hpp:57-77); the partial push sends the
+    most important dirty rows first, ties by row id (server_table.cpp:272-287), and
+    resets dirty + importance of what it sent (:398-399)."""
+    s = OracleServer([1])
+    s.create_table(2, SORTED_MAP, I32, 0, oplog_dense_serialized=False, accum_importance=True)
+    rows = [(5, np.array([1, 2], np.int32), np.array([3, -4], np.int32)),     # 7
+            (6, np.array([0], np.int32), np.array([-7], np.int32)),           # 7 (tie: 5 first)
+            (7, np.array([3], np.int32), np.array([9], np.int32)),            # 9
+            (8, np.array([3], np.int32), np.array([1], np.int32))]            # 1
+    assert s.apply_stream(wire.sparse_stream_np(2, 4, rows), 1, 0) == 0
+    assert [s.importance(2, r) for r in (5, 6, 7, 8)] == [7, 7, 9, 1]
+    body = s.serialize_partial([2], [3])
+    assert list(wire.parse_push_body(body)[2].keys()) == [7, 5, 6]
+    assert [s.row_dirty(2, r) for r in (5, 6, 7, 8)] == [False, False, False, True]
+    assert s.importance(2, 7) == 0 and s.importance(2, 8) == 1
+    assert list(wire.parse_push_body(s.serialize_partial([2], [3]))[2].keys()) == [8]
+    assert s.serialize_partial([2], [3]) == b""       # nothing dirty: no message (server.cpp:348)

@@ -44,6 +44,8 @@ def parse():
                    help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows; "
                         "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange")
     p.add_argument("--c4-rows", type=int, default=10_000_000, help="C4 total rows (all shards)")
+    p.add_argument("--importance", action="store_true",
+                   help="C2 with importance accumulation (SSPAggr RelativeMagnitude tables)")
     p.add_argument("--pcie", action="store_true",
                    help="also time the host-buffer form: pinned H2D of the 8 messages + apply + D2H of "
                         "every (dirty) row, i.e. the rate including PCIe (reported, never `value`)")
@@ -406,7 +408,7 @@ def main():
     srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
-                                     row_offset=base, max_rows=rows))
+                                     row_offset=base, max_rows=rows, accum_importance=args.importance))
     srv.load_rows(1, base, None, on_device_ptr=table0.data_ptr(), num_rows=rows)
     del table0
     torch.cuda.empty_cache()
@@ -480,6 +482,7 @@ def main():
                 "rows_per_gpu": rows, "cols": cap, "batches_per_step": B,
                 "algorithmic_bytes_per_step_per_gpu": step_bytes,
                 "parallelism": f"row-range shards x{world}, no collective",
+                "importance": bool(args.importance),
             },
             "roofline": {
                 "bound": "hbm",

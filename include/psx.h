@@ -22,6 +22,11 @@
  *   psx_serialize_dirty     Server::CreateSendServerPushRowMsgs  src/petuum_ps/server/server.cpp:189-309
  *   psx_row_flags           ServerRow::IsDirty / FindRow src/petuum_ps/server/server_row.hpp:90-96,
  *                                                        src/petuum_ps/server/server_table.cpp:136-141
+ *   psx_pack_stream         CreateOpLogMsgs + OpLogSerializer + RowOpLogSerializer (client pack)
+ *                                                        src/petuum_ps/thread/abstract_bg_worker.cpp:590-649,
+ *                                                        src/petuum_ps/client/oplog_serializer.hpp:12-37,
+ *                                                        src/petuum_ps/thread/row_oplog_serializer.hpp:139-166,
+ *                                                        src/petuum_ps_common/oplog/dense_row_oplog.hpp:112-136
  *   psx_row_importance      ServerRow::get_importance    src/petuum_ps/server/server_row.hpp:120-130
  *   psx_serialize_partial   Server::CreateSendServerPushRowMsgsPartial
  *                                                        src/petuum_ps/server/server.cpp:311-420,
@@ -200,6 +205,32 @@ psx_status psx_serialize_dirty(psx_ctx *ctx, void *out, size_t cap, size_t *used
  * On PSX_ERR_BUFFER_TOO_SMALL *used holds the bytes needed and nothing is cleared. */
 psx_status psx_serialize_partial(psx_ctx *ctx, void *out, size_t cap, size_t *used,
                                  int32_t out_on_device, int32_t clear_dirty);
+
+/* ---- client-side pack ------------------------------------------------------------ */
+/* One table's oplog rows for psx_pack_stream: row i's oplog is the `capacity` values at
+ * oplogs + i*capacity (a DenseRowOpLog's oplogs_, dense_row_oplog.hpp). Device memory. */
+typedef struct psx_pack_table {
+  int32_t table_id;
+  int32_t dtype;              /* psx_dtype */
+  int32_t dense_serialized;   /* TableInfo.oplog_dense_serialized: 1 SerializeDense, 0 SerializeSparse */
+  int32_t reserved0;          /* must be 0 */
+  int64_t capacity;           /* dense_row_oplog_capacity (values per row oplog) */
+  int64_t num_rows;
+  const int32_t *row_ids;     /* device, num_rows */
+  const void *oplogs;         /* device, num_rows * capacity values */
+} psx_pack_table;
+
+/* Pack n tables into one message payload (Appendix A) on the device, byte-identical to
+ * the reference client's CreateOpLogMsgs + OpLogSerializer + RowOpLogSerializer:
+ * tables in ascending id, tables with no rows omitted, records in the given row order;
+ * dense records V[capacity]; sparse records the non-zero (`!= 0`) columns ascending.
+ * No table with rows -> *used = 0 (an empty message, abstract_bg_worker.cpp:670-682).
+ * out: 4-byte-aligned device buffer of cap bytes (NULL to size: returns
+ * PSX_ERR_BUFFER_TOO_SMALL with *used).  record_offsets (optional, device): receives
+ * for every record, in message order, the byte offset of its row id — a producer-side
+ * record index.  Synchronous on the context stream. */
+psx_status psx_pack_stream(psx_ctx *ctx, const psx_pack_table *tables, int32_t n, void *out,
+                           size_t cap, size_t *used, uint64_t *record_offsets);
 
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);

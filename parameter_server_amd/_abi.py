@@ -50,6 +50,19 @@ class psx_stream(ctypes.Structure):
     ]
 
 
+class psx_pack_table(ctypes.Structure):
+    _fields_ = [
+        ("table_id", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("dense_serialized", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("capacity", ctypes.c_int64),
+        ("num_rows", ctypes.c_int64),
+        ("row_ids", ctypes.c_void_p),
+        ("oplogs", ctypes.c_void_p),
+    ]
+
+
 class PsxError(RuntimeError):
     def __init__(self, status, msg):
         self.status = status
@@ -98,6 +111,7 @@ def load():
         "psx_serialize_dirty": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
         "psx_serialize_partial": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
         "psx_row_importance": ([vp, i32, i64, i64, vp], ctypes.c_int),
+        "psx_pack_stream": ([vp, P(psx_pack_table), i32, vp, sz, P(sz), vp], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),
         "psx_timing_enable": ([vp, i32], ctypes.c_int),

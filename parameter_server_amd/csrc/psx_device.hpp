@@ -145,6 +145,29 @@ struct ServeArgs {
   int64_t *loffs;            // exclusive prefix of lsizes + scan tile sums
 };
 
+// One table of a device-side pack (psx_pack.hip).
+struct PackTab {
+  const int32_t *row_ids;
+  const uint8_t *oplogs;   // [nrows][cap] values
+  int64_t nrows;
+  int64_t cap;
+  int32_t vsize;
+  int32_t sparse;          // 1: SerializeSparse records
+  int32_t src16;           // 1: every oplog row starts 16-byte aligned (dense copies use 16-B loads)
+  int64_t rec0;            // byte offset of the table's first record in the message
+  int64_t rec_base;        // index of the table's first record in the record-offset index
+  int64_t *sizes;          // sparse: record bytes per row
+  int64_t *offs;           // sparse: exclusive prefix of sizes (+ scan tile sums)
+};
+
+// Message header words of a pack: num_tables and each table header.
+struct PackHdr {
+  int32_t n;
+  int64_t pos[kMaxTables + 1];
+  int32_t len[kMaxTables + 1];
+  uint32_t w[kMaxTables + 1][4];
+};
+
 // Importance term of one dense element (ns_sum_imp_calc.hpp:87-90), before the add.
 template <typename V>
 __device__ __forceinline__ double imp_term(V old, V u) {

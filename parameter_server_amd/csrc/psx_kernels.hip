@@ -487,7 +487,25 @@ template <> struct Vec<int64_t> {
   }
 };
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR>
+// Importance terms (ns_sum_imp_calc.hpp:87-90) of the 16/sizeof(V) elements of one lane
+// vector: old values a, record values b.
+template <typename V>
+__device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
+  double r = 0.0;
+  if constexpr (sizeof(V) == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r += imp_term<V>(__builtin_bit_cast(V, a[i]), __builtin_bit_cast(V, b[i]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      r += imp_term<V>(__builtin_bit_cast(V, ((uint64_t)a[2 * i + 1] << 32) | a[2 * i]),
+                       __builtin_bit_cast(V, ((uint64_t)b[2 * i + 1] << 32) | b[2 * i]));
+  }
+  return r;
+}
+
+// IMP: also accumulate each record's importance (see dense_apply_kernel) into imp[slot].
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP>
 __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;        // elements per 16-byte lane vector
@@ -562,6 +580,11 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           rp[q][b] = pres[q][b] ? pay0[b] + (int64_t)i * a.stride : a.zero_chunk;
         }
       }
+      double ib[IMP ? PAIR : 1][IMP ? BMAX : 1];
+#pragma unroll
+      for (int q = 0; q < (IMP ? PAIR : 1); ++q)
+#pragma unroll
+        for (int b = 0; b < (IMP ? BMAX : 1); ++b) ib[q][b] = 0.0;
       for (int64_t c0 = 0; c0 < vec_elems; c0 += CHUNK) {
         const int64_t e0 = c0 + (int64_t)lane * EPV;
         const bool full = e0 < vec_elems;
@@ -581,7 +604,12 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           u32x4 acc = t[q];
 #pragma unroll
           for (int b = 0; b < BMAX; ++b)
-            if (pres[q][b]) acc = Vec<V>::add(acc, u[q][b]);
+            if (pres[q][b]) {
+              if constexpr (IMP) {
+                if (full) ib[q][b] += vec_imp<V>(acc, u[q][b]);
+              }
+              acc = Vec<V>::add(acc, u[q][b]);
+            }
           if (full && has[q]) store16(trow[q] + e0 * VS, acc);
         }
       }
@@ -595,9 +623,26 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
             V acc = *reinterpret_cast<const V *>(trow[q] + e * VS);
 #pragma unroll
             for (int b = 0; b < BMAX; ++b)
-              if (pres[q][b]) acc = Elem<V>::add(acc, Elem<V>::load_rec(rp[q][b] + e * VS));
+              if (pres[q][b]) {
+                const V u = Elem<V>::load_rec(rp[q][b] + e * VS);
+                if constexpr (IMP) ib[q][b] += imp_term<V>(acc, u);
+                acc = Elem<V>::add(acc, u);
+              }
             *reinterpret_cast<V *>(trow[q] + e * VS) = acc;
           }
+        }
+      }
+      if constexpr (IMP) {
+        // ServerRow::AccumImportance per record, in message order (server_row.hpp:56-62)
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          if (!has[q]) continue;
+          double *ip = a.imp + s0 + ks[q];
+          double tot = *ip;
+#pragma unroll
+          for (int b = 0; b < BMAX; ++b)
+            if (pres[q][b]) tot += wave_sum_f64(ib[q][b]);
+          if (lane == 0) *ip = tot;
         }
       }
     }
@@ -757,9 +802,9 @@ static unsigned resident_blocks(K kernel, int64_t want) {
   return (unsigned)(cap < 1 ? 1 : cap);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false>
 static void launch_v2(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR>;
+  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
@@ -784,24 +829,28 @@ static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
 // Variant 6 (default): the message-count template BMAX is the next power of two >= B
 // and the number of rows in flight per wave grows as B shrinks, so every wave keeps
 // ~8-18 16-byte loads in flight whatever the batch width (B = 1 for a single message).
-template <typename V>
+template <typename V, bool IMP = false>
 static void launch_adaptive(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 1) launch_v2<V, 1, 16, true, 8>(a, st);
-  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4>(a, st);
-  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3>(a, st);
-  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2>(a, st);
-  else launch_v2<V, 16, 16, true, 1>(a, st);
+  if (a.B <= 1) launch_v2<V, 1, 16, true, 8, IMP>(a, st);
+  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4, IMP>(a, st);
+  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3, IMP>(a, st);
+  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2, IMP>(a, st);
+  else launch_v2<V, 16, 16, true, 1, IMP>(a, st);
 }
 
 template <typename V>
 static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
   const int64_t tiles = (a.max_rows + 63) / 64;
   const dim3 grid((unsigned)((tiles + 3) / 4));
-  if (a.imp) {   // importance tables (SSPAggr): the one-row-per-wave kernel with the f64 reduction
-    if (a.B <= 8)
-      hipLaunchKernelGGL((dense_apply_kernel<V, 8, true>), grid, dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((dense_apply_kernel<V, 16, true>), grid, dim3(256), 0, st, a);
+  if (a.imp) {   // importance tables (SSPAggr): same kernels plus the f64 importance sums
+    if (g_apply_variant == 0) {
+      if (a.B <= 8)
+        hipLaunchKernelGGL((dense_apply_kernel<V, 8, true>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((dense_apply_kernel<V, 16, true>), grid, dim3(256), 0, st, a);
+    } else {
+      launch_adaptive<V, true>(a, st);
+    }
   } else if (g_apply_variant == 6)
     launch_adaptive<V>(a, st);
   else if (a.B <= 8)

@@ -43,6 +43,9 @@ hipError_t launch_serve_emit(const ServeArgs &a, hipStream_t st);
 hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st);
 hipError_t launch_serve_list_sizes(const ServeArgs &a, hipStream_t st);
 hipError_t launch_serve_emit_list(const ServeArgs &a, hipStream_t st);
+hipError_t launch_pack_count(int dtype, PackTab t, hipStream_t st);
+hipError_t launch_pack_emit(int dtype, PackTab t, uint8_t *out, uint64_t *recoff, hipStream_t st);
+hipError_t launch_pack_header(uint8_t *out, const PackHdr &h, hipStream_t st);
 hipError_t launch_sort_desc(void *temp, size_t *temp_bytes, const double *keys_in, double *keys_out,
                             const int32_t *vals_in, int32_t *vals_out, int64_t n, hipStream_t st);
 hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *entries, int64_t max_entries,
@@ -123,6 +126,8 @@ struct psx_ctx {
   hipEvent_t ev_free[2] = {nullptr, nullptr};     // slot's apply stage done (main -> side)
   bool pipeline = false;                          // PSX_PIPELINE=1: overlap (no gain measured, DRAM-bound)
   uint32_t *d_ndirty = nullptr;          // partial push: dirty-row count
+  int64_t *d_pack = nullptr;             // psx_pack_stream: sparse record sizes + offsets
+  size_t pack_cap = 0;                   // entries
   uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
   uint8_t *d_zero = nullptr;
   uint8_t *d_staging = nullptr;
@@ -621,6 +626,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->d_status) hipFree(c->d_status);
   if (c->d_zero) hipFree(c->d_zero);
   if (c->d_ndirty) hipFree(c->d_ndirty);
+  if (c->d_pack) hipFree(c->d_pack);
   if (c->d_staging) hipFree(c->d_staging);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
@@ -1102,6 +1108,94 @@ psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used
   }
   HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
   if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_pack_stream(psx_ctx *c, const psx_pack_table *tables, int32_t n, void *out, size_t cap,
+                           size_t *used, uint64_t *record_offsets) {
+  if (!c || !used || n < 0 || n > PSX_MAX_TABLES || (n && !tables)) return PSX_ERR_INVALID_ARG;
+  *used = 0;
+  if (out && ((uintptr_t)out & 3)) return fail(c, PSX_ERR_INVALID_ARG, "pack output must be 4-byte aligned");
+  std::vector<const psx_pack_table *> live;
+  for (int32_t i = 0; i < n; ++i) {
+    const psx_pack_table &t = tables[i];
+    if (t.dtype < PSX_F32 || t.dtype > PSX_I64 || t.capacity <= 0 || t.num_rows < 0 || t.reserved0 ||
+        t.num_rows > INT32_MAX || (t.num_rows && (!t.row_ids || !t.oplogs)))
+      return fail(c, PSX_ERR_INVALID_ARG, "bad psx_pack_table " + std::to_string(i));
+    for (int32_t j = 0; j < i; ++j)
+      if (tables[j].table_id == t.table_id) return fail(c, PSX_ERR_INVALID_ARG, "table listed twice");
+    if (t.num_rows) live.push_back(&t);
+  }
+  // OpLogSerializer keeps tables in a std::map: ascending table id (oplog_serializer.hpp:12-37)
+  std::sort(live.begin(), live.end(),
+            [](const psx_pack_table *a, const psx_pack_table *b) { return a->table_id < b->table_id; });
+  if (live.empty()) return PSX_OK;   // empty message (abstract_bg_worker.cpp:670-682)
+  HIP_TRY(c, hipSetDevice(c->device));
+  // scratch: per sparse table sizes[n] + offs[n + 1 + tiles]
+  size_t need = 0;
+  for (auto *t : live)
+    if (!t->dense_serialized) need += 2 * (size_t)t->num_rows + 1 + ((size_t)t->num_rows + 1023) / 1024;
+  if (need > c->pack_cap) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->d_pack) hipFree(c->d_pack);
+    c->d_pack = nullptr;
+    c->pack_cap = 0;
+    HIP_TRY(c, hipMalloc(&c->d_pack, need * sizeof(int64_t)));
+    c->pack_cap = need;
+  }
+  std::vector<psx::PackTab> pt(live.size());
+  size_t sc = 0;
+  std::vector<int64_t> bytes(live.size(), 0);
+  for (size_t k = 0; k < live.size(); ++k) {
+    const psx_pack_table &t = *live[k];
+    psx::PackTab &p = pt[k];
+    p = psx::PackTab{};
+    p.row_ids = t.row_ids;
+    p.oplogs = (const uint8_t *)t.oplogs;
+    p.nrows = t.num_rows;
+    p.cap = t.capacity;
+    p.vsize = vsize_of(t.dtype);
+    p.sparse = t.dense_serialized ? 0 : 1;
+    p.src16 = ((uintptr_t)t.oplogs % 16 == 0 && (t.capacity * p.vsize) % 16 == 0) ? 1 : 0;
+    if (p.sparse) {
+      p.sizes = c->d_pack + sc;
+      p.offs = p.sizes + t.num_rows;
+      sc += 2 * (size_t)t.num_rows + 1 + ((size_t)t.num_rows + 1023) / 1024;
+      HIP_TRY(c, psx::launch_pack_count(t.dtype, p, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(&bytes[k], p.offs + t.num_rows, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    } else {
+      bytes[k] = t.num_rows * (4 + t.capacity * p.vsize);
+    }
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // layout: int32 num_tables; per table {int32 id; size_t update_size; int32 num_rows} + records
+  psx::PackHdr h{};
+  h.pos[0] = 0;
+  h.len[0] = 1;
+  h.w[0][0] = (uint32_t)live.size();
+  h.n = 1;
+  int64_t pos = 4, rec_base = 0;
+  for (size_t k = 0; k < live.size(); ++k) {
+    const psx_pack_table &t = *live[k];
+    h.pos[h.n] = pos;
+    h.len[h.n] = 4;
+    h.w[h.n][0] = (uint32_t)t.table_id;
+    h.w[h.n][1] = (uint32_t)pt[k].vsize;   // size_t update_size, little endian
+    h.w[h.n][2] = 0;
+    h.w[h.n][3] = (uint32_t)t.num_rows;
+    h.n++;
+    pos += 16;
+    pt[k].rec0 = pos;
+    pt[k].rec_base = rec_base;
+    rec_base += t.num_rows;
+    pos += bytes[k];
+  }
+  *used = (size_t)pos;
+  if (!out || (size_t)pos > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "pack: *used bytes needed");
+  for (size_t k = 0; k < live.size(); ++k)
+    HIP_TRY(c, psx::launch_pack_emit(live[k]->dtype, pt[k], (uint8_t *)out, record_offsets, c->stream));
+  HIP_TRY(c, psx::launch_pack_header((uint8_t *)out, h, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return PSX_OK;
 }

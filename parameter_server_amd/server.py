@@ -202,6 +202,46 @@ class Server:
                                       ctypes.byref(used), 0, 1 if clear else 0))
         return out[:used.value]
 
+    # -- client-side pack -------------------------------------------------------------
+    def pack_stream(self, tables, with_index=False):
+        """Pack per-table oplog rows into one message on the device (psx_pack_stream).
+
+        tables: dicts {table_id, dtype (psx dtype), dense_serialized, row_ids (CUDA int32
+        [n]), oplogs (CUDA [n, capacity])}.  Returns a CUDA uint8 tensor holding the
+        message (empty for an all-empty pack) and, with with_index, the CUDA int64 tensor
+        of record offsets."""
+        import torch
+        torch.cuda.current_stream(self.device).synchronize()   # inputs come from torch's stream
+        n = len(tables)
+        arr = (_abi.psx_pack_table * max(n, 1))()
+        nrec = 0
+        for i, t in enumerate(tables):
+            op = t["oplogs"]
+            assert op.is_cuda and op.is_contiguous() and op.dim() == 2
+            ids = t["row_ids"]
+            assert ids.is_cuda and ids.dtype == torch.int32 and ids.is_contiguous()
+            arr[i].table_id = t["table_id"]
+            arr[i].dtype = t["dtype"]
+            arr[i].dense_serialized = 1 if t["dense_serialized"] else 0
+            arr[i].capacity = op.shape[1]
+            arr[i].num_rows = op.shape[0]
+            arr[i].row_ids = ids.data_ptr() if op.shape[0] else None
+            arr[i].oplogs = op.data_ptr() if op.shape[0] else None
+            nrec += op.shape[0]
+        used = ctypes.c_size_t()
+        st = self._L.psx_pack_stream(self._ctx, arr, n, None, 0, ctypes.byref(used), None)
+        if st not in (_abi.PSX_OK, 9):
+            _check(self._L, self._ctx, st)
+        dev = torch.device("cuda", self.device)
+        out = torch.empty((used.value + 3) // 4, dtype=torch.int32, device=dev).view(torch.uint8)
+        idx = torch.empty(max(nrec, 1), dtype=torch.int64, device=dev) if with_index else None
+        if used.value:
+            _check(self._L, self._ctx, self._L.psx_pack_stream(
+                self._ctx, arr, n, out.data_ptr(), out.numel(), ctypes.byref(used),
+                idx.data_ptr() if idx is not None else None))
+        out = out[:used.value]
+        return (out, idx[:nrec]) if with_index else out
+
     # -- timing ------------------------------------------------------------------------
     def timing(self, on=True):
         _check(self._L, self._ctx, self._L.psx_timing_enable(self._ctx, 1 if on else 0))

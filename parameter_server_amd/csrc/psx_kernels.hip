@@ -494,7 +494,12 @@ __device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
   double r = 0.0;
   if constexpr (sizeof(V) == 4) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r += imp_term<V>(__builtin_bit_cast(V, a[i]), __builtin_bit_cast(V, b[i]));
+    for (int i = 0; i < 4; ++i) {
+      // copy the lanes out first: __builtin_bit_cast applied directly to a vector
+      // subscript a[i] reads element 0 for every i (observed with this clang)
+      const uint32_t ai = a[i], bi = b[i];
+      r += imp_term<V>(__builtin_bit_cast(V, ai), __builtin_bit_cast(V, bi));
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -504,7 +509,9 @@ __device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
   return r;
 }
 
-// IMP: also accumulate each record's importance (see dense_apply_kernel) into imp[slot].
+// IMP: also accumulate the rows' importance (see dense_apply_kernel) into imp[slot]; here
+// all of a row's terms of one call share one f64 accumulator (non-negative terms: within
+// (cap*B-1)*2^-53 relative of the reference's record-by-record sum).
 template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP>
 __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   constexpr int VS = (int)sizeof(V);
@@ -580,11 +587,14 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           rp[q][b] = pres[q][b] ? pay0[b] + (int64_t)i * a.stride : a.zero_chunk;
         }
       }
-      double ib[IMP ? PAIR : 1][IMP ? BMAX : 1];
+      // IMP: one f64 accumulator per row (all of its records this call) and the row's
+      // current importance fetched up front, so its latency hides under the row loads.
+      double ib[IMP ? PAIR : 1], imp0[IMP ? PAIR : 1];
 #pragma unroll
-      for (int q = 0; q < (IMP ? PAIR : 1); ++q)
-#pragma unroll
-        for (int b = 0; b < (IMP ? BMAX : 1); ++b) ib[q][b] = 0.0;
+      for (int q = 0; q < (IMP ? PAIR : 1); ++q) {
+        ib[q] = 0.0;
+        if constexpr (IMP) imp0[q] = has[q] ? a.imp[s0 + ks[q]] : 0.0;
+      }
       for (int64_t c0 = 0; c0 < vec_elems; c0 += CHUNK) {
         const int64_t e0 = c0 + (int64_t)lane * EPV;
         const bool full = e0 < vec_elems;
@@ -606,7 +616,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           for (int b = 0; b < BMAX; ++b)
             if (pres[q][b]) {
               if constexpr (IMP) {
-                if (full) ib[q][b] += vec_imp<V>(acc, u[q][b]);
+                if (full) ib[q] += vec_imp<V>(acc, u[q][b]);
               }
               acc = Vec<V>::add(acc, u[q][b]);
             }
@@ -625,7 +635,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
             for (int b = 0; b < BMAX; ++b)
               if (pres[q][b]) {
                 const V u = Elem<V>::load_rec(rp[q][b] + e * VS);
-                if constexpr (IMP) ib[q][b] += imp_term<V>(acc, u);
+                if constexpr (IMP) ib[q] += imp_term<V>(acc, u);
                 acc = Elem<V>::add(acc, u);
               }
             *reinterpret_cast<V *>(trow[q] + e * VS) = acc;
@@ -633,16 +643,11 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
         }
       }
       if constexpr (IMP) {
-        // ServerRow::AccumImportance per record, in message order (server_row.hpp:56-62)
+        // ServerRow::AccumImportance (server_row.hpp:56-62,124-126)
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
-          if (!has[q]) continue;
-          double *ip = a.imp + s0 + ks[q];
-          double tot = *ip;
-#pragma unroll
-          for (int b = 0; b < BMAX; ++b)
-            if (pres[q][b]) tot += wave_sum_f64(ib[q][b]);
-          if (lane == 0) *ip = tot;
+          const double tot = imp0[q] + wave_sum_f64(ib[q]);
+          if (has[q] && lane == 0) a.imp[s0 + ks[q]] = tot;
         }
       }
     }
@@ -829,13 +834,33 @@ static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
 // Variant 6 (default): the message-count template BMAX is the next power of two >= B
 // and the number of rows in flight per wave grows as B shrinks, so every wave keeps
 // ~8-18 16-byte loads in flight whatever the batch width (B = 1 for a single message).
-template <typename V, bool IMP = false>
+template <typename V>
 static void launch_adaptive(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 1) launch_v2<V, 1, 16, true, 8, IMP>(a, st);
-  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4, IMP>(a, st);
-  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3, IMP>(a, st);
-  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2, IMP>(a, st);
-  else launch_v2<V, 16, 16, true, 1, IMP>(a, st);
+  if (a.B <= 1) launch_v2<V, 1, 16, true, 8>(a, st);
+  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4>(a, st);
+  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3>(a, st);
+  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2>(a, st);
+  else launch_v2<V, 16, 16, true, 1>(a, st);
+}
+
+// Importance tables: the f64 terms cost registers, so fewer rows in flight per wave
+// buys back occupancy (PSX_IMP_PAIR=2 selects the plain table's pairing for A/B).
+int g_imp_pair = 1;
+template <typename V>
+static void launch_adaptive_imp(const DenseArgs &a, hipStream_t st) {
+  if (g_imp_pair >= 2) {
+    if (a.B <= 1) launch_v2<V, 1, 16, true, 8, true>(a, st);
+    else if (a.B <= 2) launch_v2<V, 2, 16, true, 4, true>(a, st);
+    else if (a.B <= 4) launch_v2<V, 4, 16, true, 3, true>(a, st);
+    else if (a.B <= 8) launch_v2<V, 8, 16, true, 2, true>(a, st);
+    else launch_v2<V, 16, 16, true, 1, true>(a, st);
+  } else {
+    if (a.B <= 1) launch_v2<V, 1, 16, true, 4, true>(a, st);
+    else if (a.B <= 2) launch_v2<V, 2, 16, true, 2, true>(a, st);
+    else if (a.B <= 4) launch_v2<V, 4, 16, true, 2, true>(a, st);
+    else if (a.B <= 8) launch_v2<V, 8, 16, true, 1, true>(a, st);
+    else launch_v2<V, 16, 16, true, 1, true>(a, st);
+  }
 }
 
 template <typename V>
@@ -849,7 +874,7 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
       else
         hipLaunchKernelGGL((dense_apply_kernel<V, 16, true>), grid, dim3(256), 0, st, a);
     } else {
-      launch_adaptive<V, true>(a, st);
+      launch_adaptive_imp<V>(a, st);
     }
   } else if (g_apply_variant == 6)
     launch_adaptive<V>(a, st);

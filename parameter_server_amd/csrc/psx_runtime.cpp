@@ -1236,6 +1236,7 @@ namespace psx {
 extern int g_index_variant;
 extern int g_apply_variant;
 extern int g_inv_layout;
+extern int g_imp_pair;
 }  // namespace psx
 
 extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
@@ -1263,6 +1264,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_INDEX_VARIANT")) psx::g_index_variant = atoi(v);
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_INV_LAYOUT")) psx::g_inv_layout = atoi(v);
+    if (const char *v = getenv("PSX_IMP_PAIR")) psx::g_imp_pair = atoi(v);
   }
 } variant_env;
 }  // namespace

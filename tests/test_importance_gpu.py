@@ -7,9 +7,11 @@ NSSumImpCalc importance (ns_sum_imp_calc.hpp:57-98) to ServerRow::importance_
 first (server_table.cpp:272-346, server.cpp:311-420).
 
 Tolerances: row values bit-exact (the add order is the reference's).  Importance is an
-f64 sum of non-negative terms; the device sums a record's terms lane-parallel, so it is
-within (cap-1) * 2^-53 relative of the reference's element-order sum per record; the
-tests allow rel 1e-12.  Partial push bodies are compared byte-for-byte (the data keeps
+f64 sum of non-negative terms; the device reassociates the sum (lane-parallel within a
+record; the vectorised kernel also across the records of one call) and builds f32
+quotients from an f32 reciprocal plus an exact f64 remainder step (rel < 2^-45 per
+term), so it is within (cap*B)*2^-53 + 2^-45 relative of the reference's
+element-by-element sum; the tests allow rel 1e-12 (cap*B <= 2700 here).  Partial push bodies are compared byte-for-byte (the data keeps
 row importances far apart relative to that tolerance, so the send order is the same)."""
 import numpy as np
 import pytest
@@ -98,6 +100,27 @@ def _dense_importance_case(dt, B):
     assert np.array_equal(got.view(np.uint8), orc.read_dense_rows(1, 0, rows).view(np.uint8))
     imp = _check_importance(srv, orc, 1, rows)
     assert (imp > 0).sum() >= rows // 2
+
+
+def test_dense_importance_special_values():
+    """Zeros, signed zeros, denormals, huge/tiny quotients, inf and NaN in the old
+    values and the updates (the f32 fast quotient falls back to the exact division
+    outside the normal range)."""
+    specials = np.array([0.0, -0.0, 1e-45, -3e-39, 1.2e-38, 1.0, -2.5, 3e38, -3.4e38, np.inf, -np.inf, np.nan,
+                         7e-20, 6e19, 1e-30, 123456.7], np.float32)
+    n = specials.size
+    rows, cap = n, n
+    init = np.stack([np.roll(specials, k) for k in range(rows)])
+    upd = np.stack([np.roll(specials[::-1], 3 * k) for k in range(rows)])
+    srv, orc = _dense_pair(F32, rows, cap, [1])
+    srv.load_rows(1, 0, init)
+    orc.load_dense_rows(1, 0, init)
+    st = wire.dense_stream_np(1, np.arange(rows, dtype=np.int32), upd)
+    _apply_dev(srv, orc, [st], [1])
+    assert np.array_equal(srv.read_rows(1, 0, rows).view(np.uint8), orc.read_dense_rows(1, 0, rows).view(np.uint8))
+    got = srv.row_importance(1, 0, rows)
+    want = np.array([orc.importance(1, r) for r in range(rows)])
+    np.testing.assert_allclose(got, want, rtol=IMP_RTOL, atol=0, equal_nan=True)
 
 
 def test_dense_importance_accumulates_across_calls_and_host_path():

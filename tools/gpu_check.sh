@@ -19,7 +19,7 @@ run() {  # name timeout cmd...
   return 0
 }
 python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { echo build failed; tail -20 "$OUT/build.log"; exit 1; }
-[ "${SKIP_TESTS:-0}" = 1 ] || run gpu_tests 600 python -m pytest tests -m gpu -x -q
+[ "${SKIP_TESTS:-0}" = 1 ] || run gpu_tests 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 [ "${SKIP_BENCH:-0}" = 1 ] || run bench 400 python bench.py --steps "$STEPS" --warmup 2 --cpu-seconds "${CPU_SECONDS:-8}" ${BENCH_ARGS:-}
 [ "${RUN_C4:-0}" = 1 ] && run bench_c4 500 python bench.py --workload c4 --steps 5 --warmup 1
 [ "${SKIP_C3:-0}" = 1 ] || run bench_c3 400 python bench.py --workload c3 --steps "$STEPS" --warmup 2 --cpu-seconds "${CPU_SECONDS:-8}"

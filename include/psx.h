@@ -28,6 +28,7 @@
  *                                                        src/petuum_ps/thread/row_oplog_serializer.hpp:139-166,
  *                                                        src/petuum_ps_common/oplog/dense_row_oplog.hpp:112-136
  *   psx_row_importance      ServerRow::get_importance    src/petuum_ps/server/server_row.hpp:120-130
+ *   psx_row_versions        VersionServerRow::get_version src/petuum_ps/server/version_server_row.hpp:66
  *   psx_serialize_partial   Server::CreateSendServerPushRowMsgsPartial
  *                                                        src/petuum_ps/server/server.cpp:311-420,
  *                           ServerTable::GetPartialTableToSendRegular / AppendRowsToBuffsPartial
@@ -53,7 +54,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 2
+#define PSX_ABI_VERSION 3
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -112,9 +113,22 @@ typedef struct psx_table_config {
                                        selects under SSPAggr + RelativeMagnitude/FIFO_N_ReMag
                                        (server_table.cpp:26-47; NSSumImpCalc,
                                        ns_sum_imp_calc.hpp:57-98) */
-  int32_t reserved0;                /* must be 0 */
+  int32_t version_maintain;         /* ABI 3 (was reserved0): TableInfo.version_maintain (configs.hpp:207).
+                                       Dense records carry VersionDenseRowOpLog's trailer
+                                       {uint64 version; bool end_of_version} (version_dense_row_oplog.hpp:161-180,
+                                       parsed and not otherwise used without a server logic); rows are
+                                       VersionServerRow: version_ = 1 at creation, +1 per applied record,
+                                       appended to every serialized row (version_server_row.hpp:11-71).
+                                       Dense rows with dense-serialized kDenseRowOpLog records only. */
   int64_t server_push_row_upper_bound; /* TableInfo.server_push_row_upper_bound (configs.hpp:181):
                                        rows per table per partial push; 0 -> 100 (table_gflags.cpp:21) */
+  /* ABI 3: */
+  int32_t row_oplog_type;           /* TableInfo.row_oplog_type (configs.hpp:35-40): 0 kDenseRowOpLog;
+                                       3 kDenseRowOpLogFloat16 = dense records uint16[cap] binary16,
+                                       decompressed to f32 before the add (dense_row_oplog_float16.hpp:144-157;
+                                       f32 tables only).  1/2 select sparse row oplogs, which change nothing on
+                                       the server for sparse-serialized tables (abstract_row_oplog.hpp:64-78). */
+  int32_t reserved1;                /* must be 0 */
 } psx_table_config;
 
 /* One device-resident ClientSendOpLogMsg payload (ps_msgs.hpp:1003-1055 after its
@@ -163,6 +177,13 @@ psx_status psx_clear_dirty(psx_ctx *ctx, int32_t table_id);
 psx_status psx_row_importance(psx_ctx *ctx, int32_t table_id, int64_t first_row,
                               int64_t num_rows, double *dst);
 
+/* VersionServerRow::get_version (version_server_row.hpp:66) of num_rows rows (same
+ * addressing as psx_row_flags): 1 + records applied since creation for version tables;
+ * 0 for rows that do not exist and for tables without version_maintain
+ * (abstract_server_row.hpp:71). */
+psx_status psx_row_versions(psx_ctx *ctx, int32_t table_id, int64_t first_row,
+                            int64_t num_rows, uint64_t *dst);
+
 /* ---- apply (the hot path) -------------------------------------------------- */
 /* Server::ApplyOpLogUpdateVersion: host bytes, borrowed only for the call. */
 psx_status psx_apply_stream(psx_ctx *ctx, const void *oplog, size_t oplog_size,
@@ -176,7 +197,8 @@ psx_status psx_sync(psx_ctx *ctx);
 
 /* ---- serve-back -------------------------------------------------------------- */
 /* Serialize rows exactly as ServerRow::Serialize (dense: V[capacity]; sorted map:
- * Entry{int32,V}[n] in store order; map: {int32,V}[n]) framed as RecordBuff records
+ * Entry{int32,V}[n] in store order; map: {int32,V}[n]; version tables append
+ * uint64 version, VersionServerRow::Serialize) framed as RecordBuff records
  * {int32 row_id; size_t size; bytes} (record_buff.hpp:41-53).  Absent rows are
  * skipped.  *used receives the bytes written. */
 psx_status psx_serialize_rows(psx_ctx *ctx, int32_t table_id, const int32_t *row_ids,

@@ -37,6 +37,8 @@ struct TableInfo {
   int64_t max_entries = 0;
   bool accum_importance = false;             // SSPAggr importance policies (server_table.cpp:26-47)
   int64_t server_push_row_upper_bound = 0;   // configs.hpp:181; 0 -> 100
+  bool version_maintain = false;             // configs.hpp:207 (VersionDenseRowOpLog / VersionServerRow)
+  int32_t row_oplog_type = 0;                // configs.hpp:35-40 (3: float16 dense records)
 };
 
 class Server {
@@ -69,6 +71,8 @@ class Server {
     c.max_entries = ti.max_entries;
     c.accum_importance = ti.accum_importance ? 1 : 0;
     c.server_push_row_upper_bound = ti.server_push_row_upper_bound;
+    c.version_maintain = ti.version_maintain ? 1 : 0;
+    c.row_oplog_type = ti.row_oplog_type;
     Check(psx_table_create(ctx_, &c));
   }
 

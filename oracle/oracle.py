@@ -59,6 +59,9 @@ def lib():
         L.orc_serialize_dirty.argtypes = [vp, vp, ctypes.c_int, vp, sz, ctypes.c_int]
         L.orc_serialize_dirty.restype = i64
         L.orc_table_set_importance.argtypes = [vp, i32, ctypes.c_int]
+        L.orc_table_set_version_maintain.argtypes = [vp, i32, ctypes.c_int]
+        L.orc_table_set_f16_records.argtypes = [vp, i32, ctypes.c_int]
+        L.orc_row_version.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_uint64)]
         L.orc_row_importance.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_double)]
         L.orc_serialize_partial.argtypes = [vp, vp, ctypes.c_int, vp, vp, sz, ctypes.c_int]
         L.orc_serialize_partial.restype = i64
@@ -97,18 +100,29 @@ class OracleServer:
         assert self._L.orc_register_sender(self._s, bg) == ST_OK
 
     def create_table(self, table_id, kind, dtype, row_capacity, oplog_dense_serialized=True,
-                     dense_row_oplog_capacity=None, accum_importance=False):
+                     dense_row_oplog_capacity=None, accum_importance=False, version_maintain=False,
+                     f16_records=False):
         cap = row_capacity if dense_row_oplog_capacity is None else dense_row_oplog_capacity
         st = self._L.orc_table_create(self._s, table_id, kind, dtype,
                                       1 if oplog_dense_serialized else 0, row_capacity, cap)
         assert st == ST_OK, st
         if accum_importance:
             assert self._L.orc_table_set_importance(self._s, table_id, 1) == ST_OK
+        if version_maintain:
+            assert self._L.orc_table_set_version_maintain(self._s, table_id, 1) == ST_OK
+        if f16_records:
+            assert self._L.orc_table_set_f16_records(self._s, table_id, 1) == ST_OK
         self.tables[table_id] = (kind, dtype, row_capacity)
 
     def importance(self, table_id, row_id):
         out = ctypes.c_double()
         assert self._L.orc_row_importance(self._s, table_id, row_id, ctypes.byref(out)) == ST_OK
+        return out.value
+
+    def row_version(self, table_id, row_id):
+        """VersionServerRow::get_version (version_server_row.hpp:66); 0 otherwise."""
+        out = ctypes.c_uint64()
+        assert self._L.orc_row_version(self._s, table_id, row_id, ctypes.byref(out)) == ST_OK
         return out.value
 
     def apply_stream(self, data, bg, version):

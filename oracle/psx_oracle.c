@@ -151,6 +151,8 @@ typedef struct {
   int dirty;             /* ServerRow::dirty_ (server_row.hpp:133) */
   double importance;     /* ServerRow::importance_ (server_row.hpp:143); the reference leaves it
                             uninitialized (:16-19), this restatement starts it at 0 */
+  uint64_t version;      /* VersionServerRow::version_ (version_server_row.hpp:13-19,69): 1 at
+                            creation, +1 per applied record; read only for version tables */
 } orc_row;
 
 typedef struct {
@@ -160,6 +162,8 @@ typedef struct {
   int64_t row_capacity;
   int64_t oplog_capacity;
   int importance;        /* ApplyRow*AccumImportance selected (server_table.cpp:26-47) */
+  int version_maintain;  /* TableInfo.version_maintain (configs.hpp:207) */
+  int f16_records;       /* row_oplog_type kDenseRowOpLogFloat16 (configs.hpp:39) */
   imap_t index;          /* row_id -> row number */
   orc_row **rows;
   int64_t nrows, rows_cap;
@@ -227,6 +231,7 @@ int orc_table_create(orc_server *s, int32_t table_id, int kind, int dt, int dens
 /* ServerTable::CreateRow -> AbstractRow::Init(row_capacity) (server_table.cpp:143-162). */
 static orc_row *create_row(orc_table *t, int32_t row_id) {
   orc_row *r = (orc_row *)calloc(1, sizeof(orc_row));
+  r->version = 1;   /* VersionServerRow(row_data): version_(1) (version_server_row.hpp:17-19) */
   if (t->kind == KIND_DENSE) {
     r->dense = (uint8_t *)calloc((size_t)(t->row_capacity ? t->row_capacity : 1), dt_size(t->dt));
   } else if (t->kind == KIND_SORTED_MAP) {
@@ -417,6 +422,40 @@ static void apply_dense_record(orc_table *t, orc_row *r, const uint8_t *upd, int
 static int32_t rd32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
 static uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
 
+/* Float16Compressor::decompress, called by DenseRowOpLogFloat16::ParseDenseSerializedOpLog
+ * (dense_row_oplog_float16.hpp:144-157).  float16_compressor.hpp is fetched by
+ * third_party/third_party.mk:281-290 with no pinned version and is absent here, so this
+ * restates IEEE-754 binary16 -> binary32, which is exact (a unique result) for every
+ * finite value and infinity; NaNs keep their payload shifted into the binary32 mantissa
+ * (no quieting).  Parity for the fp16 record format is "unpinned". */
+static float half_to_float(uint16_t h) {
+  uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu, bits;
+  if (e == 0x1f) {
+    bits = sign | 0x7f800000u | (m << 13);
+  } else if (e != 0) {
+    bits = sign | ((e + 112u) << 23) | (m << 13);
+  } else if (m == 0) {
+    bits = sign;
+  } else {                       /* subnormal half: normalise */
+    uint32_t k = 0;
+    while (!(m & 0x400u)) { m <<= 1; ++k; }
+    bits = sign | ((113u - k) << 23) | ((m & 0x3ffu) << 13);
+  }
+  float f;
+  memcpy(&f, &bits, 4);
+  return f;
+}
+
+/* Bytes of one dense record body after its row id: DenseRowOpLog V[cap]
+ * (dense_row_oplog.hpp:138-144), VersionDenseRowOpLog V[cap] + uint64 version + bool
+ * end_of_version (version_dense_row_oplog.hpp:173-180), DenseRowOpLogFloat16
+ * uint16[cap] (dense_row_oplog_float16.hpp:144-157). */
+static size_t dense_body_bytes(const orc_table *t) {
+  if (t->f16_records) return (size_t)t->oplog_capacity * 2;
+  return (size_t)t->oplog_capacity * dt_size(t->dt) + (t->version_maintain ? 9 : 0);
+}
+
 /* Walk the stream exactly as SerializedOpLogReader::Restart/Next/StartNewTable
  * (serialized_oplog_reader.hpp:30-133) with AbstractRowOpLog::ParseSparseSerializedOpLog
  * (abstract_row_oplog.hpp:64-78) / DenseRowOpLog::ParseDenseSerializedOpLog
@@ -446,13 +485,26 @@ static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) 
       int32_t row_id = rd32(b + off);
       off += 4;
       if (t->dense_serialized) {
-        size_t rs = (size_t)t->oplog_capacity * vs;
+        size_t rs = dense_body_bytes(t);
         if (off + rs > size) return ORC_ERR_MALFORMED;
         if (apply) {
           orc_row *r = find_row(t, row_id);
           if (!r) r = create_row(t, row_id);
-          apply_dense_record(t, r, b + off, t->oplog_capacity);
+          if (t->f16_records) {
+            /* ParseDenseSerializedOpLog decompresses into the sample oplog's f32 buffer,
+             * which is then applied as a dense float record */
+            float *tmp = (float *)malloc((size_t)t->oplog_capacity * sizeof(float));
+            for (int64_t i = 0; i < t->oplog_capacity; ++i) {
+              uint16_t h; memcpy(&h, b + off + (size_t)i * 2, 2);
+              tmp[i] = half_to_float(h);
+            }
+            apply_dense_record(t, r, (const uint8_t *)tmp, t->oplog_capacity);
+            free(tmp);
+          } else {
+            apply_dense_record(t, r, b + off, t->oplog_capacity);
+          }
           r->dirty = 1;
+          r->version++;   /* VersionServerRow::ApplyDenseBatchInc* (version_server_row.hpp:44-53) */
         }
         off += rs;
       } else {
@@ -477,6 +529,7 @@ static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) 
           apply_sparse_record(t, r, cc, b + off + 4 + (size_t)n * 4, n);
           free(cc);
           r->dirty = 1;
+          r->version++;   /* VersionServerRow::ApplyBatchInc* (version_server_row.hpp:28-42) */
         }
         off += rs;
       }
@@ -527,6 +580,41 @@ int orc_table_set_importance(orc_server *s, int32_t table_id, int on) {
   orc_table *t = find_table(s, table_id);
   if (!t) return ORC_ERR_INVALID_ARG;
   t->importance = on ? 1 : 0;
+  return ORC_OK;
+}
+
+/* TableInfo.version_maintain (configs.hpp:207): records are VersionDenseRowOpLog
+ * (server_table.cpp:56-61) and rows VersionServerRow (server_table.cpp:149-153).  Only
+ * dense-serialized DenseRowOpLog tables: the reference writes a sparse version record's
+ * trailer at the wrong offset (version_dense_row_oplog.hpp:133-159) and parses sparse
+ * records without it (abstract_row_oplog.hpp:64-78), and the version sample oplog exists
+ * only for row_oplog_type kDenseRowOpLog (server_table.cpp:56-67). */
+int orc_table_set_version_maintain(orc_server *s, int32_t table_id, int on) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  if (on && (!t->dense_serialized || t->f16_records)) return ORC_ERR_UNSUPPORTED;
+  t->version_maintain = on ? 1 : 0;
+  return ORC_OK;
+}
+
+/* row_oplog_type kDenseRowOpLogFloat16 (server_table.cpp:68-72): dense records are
+ * uint16[cap]; float tables only (CHECK(update_size == sizeof(float)),
+ * dense_row_oplog_float16.hpp:28). */
+int orc_table_set_f16_records(orc_server *s, int32_t table_id, int on) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  if (on && (t->dt != DT_F32 || t->version_maintain)) return ORC_ERR_UNSUPPORTED;
+  t->f16_records = on ? 1 : 0;
+  return ORC_OK;
+}
+
+/* VersionServerRow::get_version (version_server_row.hpp:66); 0 for a plain ServerRow
+ * (abstract_server_row.hpp:71) and for absent rows. */
+int orc_row_version(orc_server *s, int32_t table_id, int32_t row_id, uint64_t *out) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  orc_row *r = find_row(t, row_id);
+  *out = (r && t->version_maintain) ? r->version : 0;
   return ORC_OK;
 }
 
@@ -582,11 +670,21 @@ int orc_read_dense_rows(orc_server *s, int32_t table_id, int64_t first_row, int6
  * SortedVectorMapStore (:148-152, entries in store order), MapStore (map_store.hpp:89-100;
  * the reference emits unordered_map order, this oracle emits ascending column order —
  * parity for MapStore rows is defined on the {col -> value} map).
+ * Version tables append VersionServerRow's uint64 version_ (version_server_row.hpp:55-64).
  * Returns the byte count, or -1 if the row is absent, or -2 if cap is too small. */
+static int64_t serialize_row_body(orc_table *t, orc_row *r, void *out, size_t cap);
 int64_t orc_serialize_row(orc_server *s, int32_t table_id, int32_t row_id, void *out, size_t cap) {
   orc_table *t = find_table(s, table_id);
   orc_row *r = t ? find_row(t, row_id) : NULL;
   if (!r) return -1;
+  int64_t nb = serialize_row_body(t, r, out, cap);
+  if (nb < 0 || !t->version_maintain) return nb;
+  if ((size_t)nb + 8 > cap) return -2;
+  memcpy((uint8_t *)out + nb, &r->version, 8);
+  return nb + 8;
+}
+
+static int64_t serialize_row_body(orc_table *t, orc_row *r, void *out, size_t cap) {
   size_t vs = dt_size(t->dt);
   if (t->kind == KIND_DENSE) {
     size_t nb = (size_t)t->row_capacity * vs;
@@ -764,7 +862,7 @@ int64_t orc_serialize_records(orc_server *s, int32_t table_id, const int32_t *ro
     orc_row *r = t ? find_row(t, row_ids[i]) : NULL;
     if (!r) continue;
     size_t need = (size_t)t->row_capacity * 16 + (size_t)r->num_entries * 16 +
-                  (size_t)(t->kind == KIND_MAP ? r->map.count : 0) * 16 + 16;
+                  (size_t)(t->kind == KIND_MAP ? r->map.count : 0) * 16 + 24;
     if (need > tmp_cap) { free(tmp); tmp_cap = need; tmp = (uint8_t *)malloc(tmp_cap); }
     int64_t nb = orc_serialize_row(s, table_id, row_ids[i], tmp, tmp_cap);
     if (nb < 0) { free(tmp); return -3; }

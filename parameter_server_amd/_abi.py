@@ -21,6 +21,8 @@ STATUS_NAMES = {
 ROW_DENSE, ROW_SORTED_MAP, ROW_MAP = 0, 1, 2
 F32, F64, I32, I64 = 0, 1, 2, 3
 MAX_FUSED_STREAMS = 16
+# TableInfo.row_oplog_type (configs.hpp:35-40)
+DENSE_ROW_OPLOG, SPARSE_ROW_OPLOG, SPARSE_VECTOR_ROW_OPLOG, DENSE_ROW_OPLOG_FLOAT16 = 0, 1, 2, 3
 
 
 class psx_table_config(ctypes.Structure):
@@ -36,8 +38,10 @@ class psx_table_config(ctypes.Structure):
         ("max_rows", ctypes.c_int64),
         ("max_entries", ctypes.c_int64),
         ("accum_importance", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("version_maintain", ctypes.c_int32),
         ("server_push_row_upper_bound", ctypes.c_int64),
+        ("row_oplog_type", ctypes.c_int32),
+        ("reserved1", ctypes.c_int32),
     ]
 
 
@@ -111,6 +115,7 @@ def load():
         "psx_serialize_dirty": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
         "psx_serialize_partial": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
         "psx_row_importance": ([vp, i32, i64, i64, vp], ctypes.c_int),
+        "psx_row_versions": ([vp, i32, i64, i64, vp], ctypes.c_int),
         "psx_pack_stream": ([vp, P(psx_pack_table), i32, vp, sz, P(sz), vp], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),

@@ -34,7 +34,7 @@ struct TableDir {
   int32_t table_id[kMaxTables];
   int32_t vsize[kMaxTables];
   int32_t dense_serialized[kMaxTables];
-  int64_t oplog_cap[kMaxTables];
+  int64_t dense_body[kMaxTables];   // bytes of a dense record after its row id (dense_body_bytes)
 };
 
 // Device-resident messages of one fused call, passed by value.
@@ -80,6 +80,7 @@ struct DenseArgs {
   uint32_t *call_status;
   const uint8_t *zero_chunk;   // >= 2 KiB of zeros, stands in for absent messages
   double *imp;                 // non-null: accumulate NSSumImpCalc importance per slot
+  uint64_t *ver;               // non-null: VersionServerRow::version_ per slot (+1 per record)
 };
 
 // Fast-path dense tables of one call (for the duplicate-row gate).
@@ -116,6 +117,8 @@ struct OrdArgs {
   const uint32_t *sticky;
   int force;              // replay: ignore the sticky duplicate flag
   double *imp;            // non-null: accumulate NSSumImpCalc importance per slot
+  uint64_t *ver;          // non-null: VersionServerRow::version_ per slot (+1 per record)
+  int rec_f16;            // dense records are binary16 (kDenseRowOpLogFloat16)
 };
 
 // Arguments of the serve-back kernels (psx_serve.hip).
@@ -134,6 +137,7 @@ struct ServeArgs {
   uint8_t *out;              // record region base (4-byte aligned)
   uint8_t *flags_rw;         // non-null: clear bit1 (dirty) of every emitted row
   double *imp_rw;            // non-null (with flags_rw): reset importance of every emitted row
+  const uint64_t *ver;       // non-null: version table, append uint64 version to every row body
   // partial push (psx_serialize_partial)
   const double *imp;         // importance per slot (null: no importance ordering)
   double *keys;              // sort keys per slot: importance (or 0) if dirty, -1 otherwise
@@ -196,6 +200,16 @@ __device__ __forceinline__ double imp_term<float>(float old, float u) {
     return __builtin_fabs(__builtin_fma(rem, (double)r0, dq0));
   }
   return __builtin_fabs((double)u / (double)old);
+}
+
+// Float16Compressor::decompress (dense_row_oplog_float16.hpp:144-157; third-party header,
+// unpinned): binary16 -> binary32 bits, exact for every finite value and infinity (the
+// hardware conversion); NaNs keep their payload shifted into the mantissa, unquieted, as
+// the oracle's restatement does.
+__device__ __forceinline__ uint32_t half_to_f32_bits(uint32_t h) {
+  const uint32_t hw = __builtin_bit_cast(uint32_t, (float)__builtin_bit_cast(_Float16, (uint16_t)h));
+  const bool nan = (h & 0x7fffu) > 0x7c00u;
+  return nan ? (((h & 0x8000u) << 16) | 0x7f800000u | ((h & 0x3ffu) << 13)) : hw;
 }
 
 // Butterfly sum over the 64 lanes of a wave; every lane receives the total.

@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
         Seg *sg = &segs[b * kMaxTables + t];
         if (sg->rec0 >= 0) { atomicOr(call_status, kStUnsupported); sh_state = 2; break; }
         if (dir.dense_serialized[t]) {
-          const uint64_t stride = 4 + (uint64_t)dir.oplog_cap[t] * dir.vsize[t];
+          const uint64_t stride = 4 + (uint64_t)dir.dense_body[t];
           const uint64_t need = (uint64_t)nrows * stride;
           if (off + need > size) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
           sg->rec0 = (int64_t)off;
@@ -107,6 +107,10 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
           sg->sparse = 0;
           sh_off = off + need;
           sh_k = sh_k + 1;
+        } else if (off & 3) {
+          // the sparse walk stages 4-byte words: a sparse table behind a version table's
+          // odd-sized records (9-byte trailers) is not supported
+          atomicOr(call_status, kStUnsupported); sh_state = 2; break;
         } else {
           sg->rec0 = (int64_t)sh_rk;   // index of the first record offset
           sg->num_rows = nrows;
@@ -364,7 +368,15 @@ __global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
     }
   }
   if (skip) return;
-  if (touched) a.flags[my_slot] = 3;   // exists | dirty
+  if (touched) {
+    a.flags[my_slot] = 3;   // exists | dirty
+    if (a.ver) {            // VersionServerRow: version_++ per applied record (version_server_row.hpp:44-53)
+      uint64_t n = 0;
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) n += idx[b] >= 0 ? 1u : 0u;
+      a.ver[my_slot] += n;
+    }
+  }
 
   uint64_t live = __ballot(touched);
   V *table = reinterpret_cast<V *>(a.table);
@@ -448,6 +460,23 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p) {
 }
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
 
+// Four binary16 record values (8 bytes, 2-byte aligned) -> four f32 bit patterns.
+typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
+template <bool NT>
+__device__ __forceinline__ u32x4 load_h4(const uint8_t *p) {
+  uint32_t w0, w1;
+  if constexpr (NT) {
+    const u32x2_a2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_a2 *>(p));
+    w0 = v[0];
+    w1 = v[1];
+  } else {
+    __builtin_memcpy(&w0, p, 4);
+    __builtin_memcpy(&w1, p + 4, 4);
+  }
+  return u32x4{half_to_f32_bits(w0 & 0xffffu), half_to_f32_bits(w0 >> 16), half_to_f32_bits(w1 & 0xffffu),
+               half_to_f32_bits(w1 >> 16)};
+}
+
 template <typename V> struct Vec;
 template <> struct Vec<float> {
   __device__ static u32x4 add(u32x4 a, u32x4 b) {
@@ -512,7 +541,9 @@ __device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
 // IMP: also accumulate the rows' importance (see dense_apply_kernel) into imp[slot]; here
 // all of a row's terms of one call share one f64 accumulator (non-negative terms: within
 // (cap*B-1)*2^-53 relative of the reference's record-by-record sum).
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP>
+// H16 (f32 tables with kDenseRowOpLogFloat16 records): record payloads are binary16, so a
+// lane's 4 elements come from one 8-byte load and are decompressed before the add.
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, bool H16 = false>
 __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;        // elements per 16-byte lane vector
@@ -562,7 +593,15 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
       }
     }
     if (skip) continue;
-    if (touched) a.flags[my_slot] = 3;   // exists | dirty
+    if (touched) {
+      a.flags[my_slot] = 3;   // exists | dirty
+      if (a.ver) {            // VersionServerRow: version_++ per applied record (version_server_row.hpp:44-53)
+        uint64_t n = 0;
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) n += idx[b] >= 0 ? 1u : 0u;
+        a.ver[my_slot] += n;
+      }
+    }
     uint64_t live = __ballot(touched);
 
     while (live) {
@@ -605,8 +644,13 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           t[q] = (full && has[q]) ? load16<false>(trow[q] + e0 * VS) : u32x4{0, 0, 0, 0};
 #pragma unroll
           for (int b = 0; b < BMAX; ++b) {
-            const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * VS : a.zero_chunk + lane * 16;
-            u[q][b] = full ? load16<NT>(src) : u32x4{0, 0, 0, 0};
+            if constexpr (H16) {
+              const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * 2 : a.zero_chunk + lane * 8;
+              u[q][b] = full ? load_h4<NT>(src) : u32x4{0, 0, 0, 0};
+            } else {
+              const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * VS : a.zero_chunk + lane * 16;
+              u[q][b] = full ? load16<NT>(src) : u32x4{0, 0, 0, 0};
+            }
           }
         }
 #pragma unroll
@@ -634,7 +678,14 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
 #pragma unroll
             for (int b = 0; b < BMAX; ++b)
               if (pres[q][b]) {
-                const V u = Elem<V>::load_rec(rp[q][b] + e * VS);
+                V u;
+                if constexpr (H16) {
+                  uint16_t h;
+                  __builtin_memcpy(&h, rp[q][b] + e * 2, 2);
+                  u = __builtin_bit_cast(V, half_to_f32_bits(h));
+                } else {
+                  u = Elem<V>::load_rec(rp[q][b] + e * VS);
+                }
                 if constexpr (IMP) ib[q] += imp_term<V>(acc, u);
                 acc = Elem<V>::add(acc, u);
               }
@@ -709,6 +760,43 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
   }
 }
 
+// dense_index_xcd: message b's records go to the blocks of XCD group b % 8 (blocks are
+// dealt round-robin over the 8 XCDs, MI355X_MICROARCH.md "Workgroup dispatch"), so one
+// message's scattered 4-byte stores land in one XCD's L2 (its max_rows*4-byte window of
+// the batch-major index) and can merge there before they are written back, instead of
+// leaving as one 64-byte write request each.  Used when B is a multiple of 8.
+template <int UNROLL>
+__global__ void __launch_bounds__(256) dense_index_xcd_kernel(StreamSet ss, const Seg *segs, int t, int B,
+                                                             int64_t stride, Geo g, int32_t *inv, InvLayout L,
+                                                             uint32_t *call_status) {
+  const int grp = blockIdx.x & 7;
+  const int64_t G = (int64_t)(gridDim.x >> 3) * blockDim.x;   // threads per XCD group
+  const int64_t tid = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+  for (int b = grp; b < B; b += 8) {
+    const Seg sg = segs[b * kMaxTables + t];
+    if (sg.rec0 < 0 || sg.sparse) continue;
+    const uint8_t *base = ss.data[b] + sg.rec0;
+    const int64_t n = sg.num_rows;
+    int32_t *invb = inv + b * L.sb;
+    for (int64_t r0 = tid; r0 < n; r0 += G * UNROLL) {
+      int32_t rid[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int64_t r = r0 + u * G;
+        rid[u] = r < n ? __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(base + r * stride)) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int64_t r = r0 + u * G;
+        if (r >= n) continue;
+        const int64_t sl = slot_of(rid[u], g);
+        if (sl < 0) { atomicOr(call_status, kStRowRange); continue; }
+        invb[sl * L.ss] = (int32_t)r;
+      }
+    }
+  }
+}
+
 // finish_call: fold the per-call status into the sticky word and free the ring slot.
 __global__ void finish_call_kernel(uint32_t *sticky, uint32_t *call_status, uint32_t *call_log) {
   if (threadIdx.x == 0) {
@@ -738,6 +826,16 @@ __global__ void gather_rows_kernel(const V *table, const int64_t *slots, int32_t
   const int64_t s = slots[r];
   for (int64_t e = threadIdx.x; e < row_cap; e += blockDim.x)
     out[(int64_t)r * row_cap + e] = s >= 0 ? table[s * row_cap + e] : V(0);
+}
+
+__global__ void fill_u64_kernel(uint64_t *p, int64_t n, uint64_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void gather_u64_kernel(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = slots[i] >= 0 ? src[slots[i]] : 0;
 }
 
 __global__ void gather_flags_kernel(const uint8_t *flags, const int64_t *slots, int32_t n, uint8_t *out) {
@@ -771,6 +869,13 @@ hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64
       hipLaunchKernelGGL((dense_index_v2_kernel<8, false>), dim3(2048), dim3(256), 0, st, ss, segs, t, B,
                          stride, g, inv, L, call_status);
       break;
+    case 3:
+      if (B % 8 == 0) {
+        hipLaunchKernelGGL((dense_index_xcd_kernel<8>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g,
+                           inv, L, call_status);
+        break;
+      }
+      [[fallthrough]];
     default:
       hipLaunchKernelGGL((dense_index_v2_kernel<8, true>), dim3(2048), dim3(256), 0, st, ss, segs, t, B,
                          stride, g, inv, L, call_status);
@@ -807,9 +912,9 @@ static unsigned resident_blocks(K kernel, int64_t want) {
   return (unsigned)(cap < 1 ? 1 : cap);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, bool H16 = false>
 static void launch_v2(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP>;
+  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
@@ -863,6 +968,17 @@ static void launch_adaptive_imp(const DenseArgs &a, hipStream_t st) {
   }
 }
 
+// f32 tables with binary16 records (kDenseRowOpLogFloat16): half the record bytes per
+// element, so more rows in flight per wave at the same load count.
+template <bool IMP>
+static void launch_adaptive_h16(const DenseArgs &a, hipStream_t st) {
+  if (a.B <= 1) launch_v2<float, 1, 16, true, 8, IMP, true>(a, st);
+  else if (a.B <= 2) launch_v2<float, 2, 16, true, 4, IMP, true>(a, st);
+  else if (a.B <= 4) launch_v2<float, 4, 16, true, 3, IMP, true>(a, st);
+  else if (a.B <= 8) launch_v2<float, 8, 16, true, 2, IMP, true>(a, st);
+  else launch_v2<float, 16, 16, true, 1, IMP, true>(a, st);
+}
+
 template <typename V>
 static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
   const int64_t tiles = (a.max_rows + 63) / 64;
@@ -885,7 +1001,12 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st) {
+hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st, bool rec_f16) {
+  if (rec_f16) {   // f32 tables only (checked at table creation)
+    if (a.imp) launch_adaptive_h16<true>(a, st);
+    else launch_adaptive_h16<false>(a, st);
+    return hipGetLastError();
+  }
   switch (dtype) {
     case 0: return launch_dense_apply_t<float>(a, st);
     case 1: return launch_dense_apply_t<double>(a, st);
@@ -926,6 +1047,18 @@ hipError_t launch_gather_rows(int dtype, const void *table, const int64_t *slots
     default: hipLaunchKernelGGL(gather_rows_kernel<int64_t>, dim3(n), dim3(256), 0, st,
                                 (const int64_t *)table, slots, n, row_cap, (int64_t *)out); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, n, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_u64_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, slots, n, out);
   return hipGetLastError();
 }
 

@@ -177,6 +177,20 @@ __device__ __forceinline__ void stv(uint8_t *p, V v) {
   __builtin_memcpy(p, &v, sizeof(V));
 }
 
+// Element e of a dense record body: V, or binary16 for kDenseRowOpLogFloat16 records
+// (f32 tables only; dense_row_oplog_float16.hpp:144-157).
+template <typename V>
+__device__ __forceinline__ V rec_val(const uint8_t *body, int64_t e, int f16) {
+  if constexpr (sizeof(V) == 4) {
+    if (f16) {
+      uint16_t h;
+      __builtin_memcpy(&h, body + e * 2, 2);
+      return __builtin_bit_cast(V, half_to_f32_bits(h));
+    }
+  }
+  return ldv<V>(body + e * (int64_t)sizeof(V));
+}
+
 // Entry<V>{int32 first; V second} with the C++ layout: 8 bytes, or 16 with 4 pad bytes.
 template <typename V> struct Ent {
   static constexpr int ES = sizeof(V) == 4 ? 8 : 16;
@@ -272,7 +286,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
           double p = 0.0;
           for (int64_t e = lane; e < a.cap; e += 64) {
             V x = ldv<V>(drow + e * sizeof(V));
-            const V u = ldv<V>(rec + 4 + e * sizeof(V));
+            const V u = rec_val<V>(rec + 4, e, a.rec_f16);
             if (a.imp) p += imp_term<V>(x, u);
             x = OV<V>::add(x, u);
             stv<V>(drow + e * sizeof(V), x);
@@ -399,6 +413,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
         wave_sync();
       }
       if (a.imp && lane == 0) a.imp[slot] = impt;
+      if (a.ver && lane == 0) a.ver[slot] += (uint64_t)L;   // VersionServerRow: +1 per record
     }
   }
 }
@@ -632,6 +647,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
       }
       if (lane == 0) a.nent[slot] = n;
       if (a.imp && lane == 0) a.imp[slot] = impt;
+      if (a.ver && lane == 0) a.ver[slot] += (uint64_t)L;
     }
   }
 }

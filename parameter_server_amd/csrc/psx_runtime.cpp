@@ -34,7 +34,9 @@ hipError_t launch_gather_rows(int dtype, const void *table, const int64_t *slots
 hipError_t launch_gather_flags(const uint8_t *flags, const int64_t *slots, int32_t n, uint8_t *out,
                                hipStream_t st);
 
-hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st);
+hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st, bool rec_f16);
+hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t st);
+hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
 hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st);
 hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
                        uint32_t *call_status, hipStream_t st);
@@ -76,6 +78,7 @@ struct TableState {
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
   double *d_imp = nullptr;         // accum_importance: ServerRow::importance_ per slot
+  uint64_t *d_ver = nullptr;       // version_maintain: VersionServerRow::version_ per slot (1 at creation)
   // partial push scratch (allocated on first psx_serialize_partial)
   double *d_pkeys[2] = {nullptr, nullptr};
   int32_t *d_pvals[2] = {nullptr, nullptr};
@@ -84,12 +87,21 @@ struct TableState {
   void *d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   bool fast() const { return cfg.row_kind == PSX_ROW_DENSE && cfg.oplog_dense_serialized; }
+  bool rec_f16() const { return cfg.row_oplog_type == 3; }
+  // Bytes of a dense record after its row id: V[cap] (dense_row_oplog.hpp:138-144), plus
+  // {uint64 version; bool end_of_version} for version tables (version_dense_row_oplog.hpp:173-180),
+  // or uint16[cap] for kDenseRowOpLogFloat16 (dense_row_oplog_float16.hpp:144-157).
+  int64_t dense_body() const {
+    if (rec_f16()) return cfg.dense_row_oplog_capacity * 2;
+    return cfg.dense_row_oplog_capacity * vsize + (cfg.version_maintain ? 9 : 0);
+  }
+  int64_t dense_stride() const { return 4 + dense_body(); }
 };
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
                   t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_srv_sizes, t.d_srv_offs,
-                  t.d_imp, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
+                  t.d_imp, t.d_ver, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -259,6 +271,8 @@ psx_status host_validate(psx_ctx *c, const uint8_t *p, size_t size) {
     if (usz != (uint64_t)t->vsize || nrows < 0) return fail(c, PSX_ERR_MALFORMED, "bad update_size/num_rows");
     if (std::find(seen.begin(), seen.end(), tid) != seen.end())
       return fail(c, PSX_ERR_UNSUPPORTED, "table appears twice in one message");
+    if (!t->cfg.oplog_dense_serialized && (off & 3))
+      return fail(c, PSX_ERR_UNSUPPORTED, "sparse table at an unaligned offset (behind odd-sized version records)");
     seen.push_back(tid);
     for (int32_t r = 0; r < nrows; ++r) {
       if (off + 4 > size) return fail(c, PSX_ERR_MALFORMED, "truncated record");
@@ -267,7 +281,7 @@ psx_status host_validate(psx_ctx *c, const uint8_t *p, size_t size) {
         return fail(c, PSX_ERR_ROW_RANGE, "row " + std::to_string(rid) + " not owned by this shard");
       off += 4;
       if (t->cfg.oplog_dense_serialized) {
-        size_t rs = (size_t)t->cfg.dense_row_oplog_capacity * t->vsize;
+        size_t rs = (size_t)t->dense_body();
         if (off + rs > size) return fail(c, PSX_ERR_MALFORMED, "truncated dense record");
         off += rs;
       } else {
@@ -332,7 +346,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     dir.table_id[i] = c->tables[i].cfg.table_id;
     dir.vsize[i] = c->tables[i].vsize;
     dir.dense_serialized[i] = c->tables[i].cfg.oplog_dense_serialized;
-    dir.oplog_cap[i] = c->tables[i].cfg.dense_row_oplog_capacity;
+    dir.dense_body[i] = c->tables[i].dense_body();
   }
   const int ring = (int)(c->call_seq % kRing);
   uint32_t *sticky = c->d_status;
@@ -356,7 +370,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     TableState &t = c->tables[ti];
     if (!t.fast() || force_ordered) continue;
     fast.t[fast.n++] = (int32_t)ti;
-    const int64_t stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
+    const int64_t stride = t.dense_stride();
     // 0: slot-major [s][b]; 1: batch-major [b][s] (default)
     const psx::InvLayout L = psx::g_inv_layout ? psx::InvLayout{1, t.cfg.max_rows} : psx::InvLayout{n, 1};
     layouts[ti] = L;
@@ -396,7 +410,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.B = n;
     a.kind = t.cfg.row_kind;
     a.dense_records = t.cfg.oplog_dense_serialized;
-    a.stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
+    a.stride = t.dense_stride();
+    a.ver = t.d_ver;
+    a.rec_f16 = t.rec_f16() ? 1 : 0;
     a.cap = t.cfg.dense_row_oplog_capacity;
     a.row_cap = t.cfg.row_capacity;
     a.row_offset = t.cfg.row_offset;
@@ -430,11 +446,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.segs = segs;
     a.t = ti;
     a.B = n;
-    a.stride = 4 + t.cfg.dense_row_oplog_capacity * t.vsize;
+    a.stride = t.dense_stride();
     a.cap = t.cfg.dense_row_oplog_capacity;
     a.row_cap = t.cfg.row_capacity;
     a.max_rows = t.cfg.max_rows;
     a.table = t.d_data;
+    a.ver = t.d_ver;
     a.flags = t.d_flags;
     a.inv = t.d_inv[slot];
     a.inv_ss = layouts[ti].ss;
@@ -444,7 +461,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.call_status = call_st;
     a.zero_chunk = c->d_zero;
     a.imp = t.d_imp;
-    st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream); });
+    st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream, t.rec_f16()); });
     if (st) return st;
   }
   st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
@@ -534,6 +551,7 @@ psx_status serve_args(psx_ctx *c, TableState &t, psx::ServeArgs *out) {
   a.max_rows = R;
   a.sizes = t.d_srv_sizes;
   a.offs = t.d_srv_offs;
+  a.ver = t.d_ver;
   *out = a;
   return PSX_OK;
 }
@@ -666,11 +684,23 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
   if (cfg->max_rows <= 0 || cfg->row_stride <= 0) return fail(c, PSX_ERR_INVALID_ARG, "bad shard geometry");
   if (cfg->max_rows > ((int64_t)1 << 31) - 2) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
-  if (cfg->reserved0 != 0 || cfg->server_push_row_upper_bound < 0 ||
-      (cfg->accum_importance != 0 && cfg->accum_importance != 1))
-    return fail(c, PSX_ERR_INVALID_ARG, "bad accum_importance / reserved0 / server_push_row_upper_bound");
+  if (cfg->reserved1 != 0 || cfg->server_push_row_upper_bound < 0 ||
+      (cfg->accum_importance != 0 && cfg->accum_importance != 1) ||
+      (cfg->version_maintain != 0 && cfg->version_maintain != 1) || cfg->row_oplog_type < 0 ||
+      cfg->row_oplog_type > 3)
+    return fail(c, PSX_ERR_INVALID_ARG,
+                "bad accum_importance / version_maintain / row_oplog_type / reserved1 / server_push_row_upper_bound");
+  const bool f16 = cfg->row_oplog_type == 3 && cfg->oplog_dense_serialized;
+  if (cfg->version_maintain && (cfg->row_kind != PSX_ROW_DENSE || !cfg->oplog_dense_serialized || f16))
+    // the reference's sparse version records are inconsistent between writer and reader
+    // (version_dense_row_oplog.hpp:133-159 vs abstract_row_oplog.hpp:64-78), and the version
+    // sample oplog exists only for kDenseRowOpLog (server_table.cpp:56-67)
+    return fail(c, PSX_ERR_UNSUPPORTED, "version_maintain needs dense rows with dense-serialized kDenseRowOpLog records");
+  if (f16 && cfg->dtype != PSX_F32)
+    return fail(c, PSX_ERR_UNSUPPORTED, "float16 records need f32 rows (dense_row_oplog_float16.hpp:28)");
   TableState t;
   t.cfg = *cfg;
+  if (!f16) t.cfg.row_oplog_type = 0;   // kSparse*RowOpLog: no server-side difference for sparse records
   if (t.cfg.server_push_row_upper_bound == 0) t.cfg.server_push_row_upper_bound = 100;   // table_gflags.cpp:21
   t.vsize = vsize_of(cfg->dtype);
   t.es = t.vsize == 4 ? 8 : 16;
@@ -705,6 +735,10 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (e == hipSuccess && cfg->accum_importance) {
     e = hipMalloc(&t.d_imp, R * sizeof(double));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_imp, 0, R * sizeof(double), c->stream);
+  }
+  if (e == hipSuccess && cfg->version_maintain) {
+    e = hipMalloc(&t.d_ver, R * sizeof(uint64_t));
+    if (e == hipSuccess) e = psx::launch_fill_u64(t.d_ver, (int64_t)R, 1, c->stream);
   }
   if (e == hipSuccess) e = hipMalloc(&t.d_flags, R);
   if (e == hipSuccess) e = hipMemsetAsync(t.d_flags, 0, R, c->stream);
@@ -812,6 +846,24 @@ psx_status psx_row_importance(psx_ctx *c, int32_t table_id, int64_t first_row, i
   return PSX_OK;
 }
 
+psx_status psx_row_versions(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows, uint64_t *dst) {
+  if (!c || (!dst && num_rows)) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  for (int64_t i = 0; i < num_rows; ++i) dst[i] = 0;
+  if (!t->d_ver || num_rows == 0) return PSX_OK;
+  std::vector<uint8_t> flags((size_t)num_rows);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipMemcpyAsync(dst, t->d_ver + s, sizeof(uint64_t) * (size_t)num_rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(flags.data(), t->d_flags + s, (size_t)num_rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int64_t i = 0; i < num_rows; ++i)
+    if (!(flags[i] & 1)) dst[i] = 0;   // no ServerRow: nothing to report
+  return PSX_OK;
+}
+
 psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) {
   if (!c || !s || n <= 0 || n > PSX_MAX_FUSED_STREAMS) return PSX_ERR_INVALID_ARG;
   // Version rule of Server::ApplyOpLogUpdateVersion (server.cpp:124-126), checked for
@@ -900,10 +952,13 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
   uint8_t *d_out = nullptr;
   int32_t *d_cnt = nullptr;
   uint8_t *d_flags = nullptr;
+  uint64_t *d_vers = nullptr;
   std::vector<uint8_t> rows(rb * n);
   std::vector<int32_t> counts(n, 0);
   std::vector<uint8_t> flags(n, 0);
+  std::vector<uint64_t> vers(n, 0);
   hipError_t e = hipMalloc(&d_slots, sizeof(int64_t) * n);
+  if (e == hipSuccess && t->d_ver) e = hipMalloc(&d_vers, sizeof(uint64_t) * n);
   if (e == hipSuccess) e = hipMalloc(&d_out, rb * n);
   if (e == hipSuccess) e = hipMalloc(&d_cnt, sizeof(int32_t) * n);
   if (e == hipSuccess) e = hipMalloc(&d_flags, n);
@@ -913,6 +968,9 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
               : psx::launch_gather_entries(t->cfg.dtype, t->d_nent, t->d_entries, t->max_entries, d_slots, n, d_cnt,
                                            d_out, c->stream);
   if (e == hipSuccess) e = psx::launch_gather_flags(t->d_flags, d_slots, n, d_flags, c->stream);
+  if (e == hipSuccess && d_vers) e = psx::launch_gather_u64(t->d_ver, d_slots, n, d_vers, c->stream);
+  if (e == hipSuccess && d_vers)
+    e = hipMemcpyAsync(vers.data(), d_vers, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(rows.data(), d_out, rb * n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess && !dense) e = hipMemcpyAsync(counts.data(), d_cnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flags, n, hipMemcpyDeviceToHost, c->stream);
@@ -921,6 +979,7 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
   if (d_out) hipFree(d_out);
   if (d_cnt) hipFree(d_cnt);
   if (d_flags) hipFree(d_flags);
+  if (d_vers) hipFree(d_vers);
   if (e != hipSuccess) return hip_fail(c, e, "serialize gather");
   // RecordBuff::Append framing {int32 row_id; size_t size; bytes} (record_buff.hpp:41-53);
   // rows absent from the shard's storage are skipped, as ServerTable only holds created rows.
@@ -937,8 +996,9 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
     } else {
       body = (size_t)counts[i] * (4 + t->vsize);          // MapStore::Serialize packs {int32, V}
     }
-    if (off + 12 + body > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize: output buffer too small");
-    uint64_t sz = body;
+    const size_t trailer = t->d_ver ? 8 : 0;   // VersionServerRow::Serialize (version_server_row.hpp:59-64)
+    if (off + 12 + body + trailer > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize: output buffer too small");
+    uint64_t sz = body + trailer;
     memcpy(o + off, &row_ids[i], 4);
     memcpy(o + off + 4, &sz, 8);
     if (t->cfg.row_kind == PSX_ROW_MAP) {
@@ -951,7 +1011,8 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
     } else {
       memcpy(o + off + 12, src, body);
     }
-    off += 12 + body;
+    if (trailer) memcpy(o + off + 12 + body, &vers[i], 8);
+    off += 12 + body + trailer;
   }
   *used = off;
   return PSX_OK;

@@ -27,11 +27,15 @@
 namespace psx {
 
 
-__device__ __forceinline__ int64_t body_bytes(const ServeArgs &a, int64_t s) {
+__device__ __forceinline__ int64_t row_bytes(const ServeArgs &a, int64_t s) {
   if (a.kind == 0) return a.row_cap * a.vsize;
   const int64_t es = a.vsize == 4 ? 8 : 16;
   const int64_t n = a.nent[s];
   return a.kind == 1 ? n * es : n * (4 + a.vsize);
+}
+// VersionServerRow::Serialize appends uint64 version_ (version_server_row.hpp:55-64).
+__device__ __forceinline__ int64_t body_bytes(const ServeArgs &a, int64_t s) {
+  return row_bytes(a, s) + (a.ver ? 8 : 0);
 }
 
 __global__ void __launch_bounds__(256) serve_sizes_kernel(ServeArgs a) {
@@ -57,12 +61,18 @@ __global__ void __launch_bounds__(256) serve_list_sizes_kernel(ServeArgs a) {
 // One record {int32 row_id; size_t size; row bytes} for slot s at rec (one wave); with
 // flags_rw, ResetDirty and ResetImportance_ (server_table.cpp:234-235, :398-399).
 __device__ void emit_row(const ServeArgs &a, int64_t s, uint8_t *rec, int lane) {
-  const int64_t body = a.sizes[s] - 12;
+  const int64_t total = a.sizes[s] - 12;
+  const int64_t body = total - (a.ver ? 8 : 0);   // row bytes before the version trailer
   if (lane == 0) {
     const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
     reinterpret_cast<int32_t *>(rec)[0] = rid;
-    reinterpret_cast<uint32_t *>(rec)[1] = (uint32_t)(uint64_t)body;           // size_t, 4-aligned
-    reinterpret_cast<uint32_t *>(rec)[2] = (uint32_t)((uint64_t)body >> 32);
+    reinterpret_cast<uint32_t *>(rec)[1] = (uint32_t)(uint64_t)total;          // size_t, 4-aligned
+    reinterpret_cast<uint32_t *>(rec)[2] = (uint32_t)((uint64_t)total >> 32);
+    if (a.ver) {
+      const uint64_t v = a.ver[s];
+      reinterpret_cast<uint32_t *>(rec + 12 + body)[0] = (uint32_t)v;
+      reinterpret_cast<uint32_t *>(rec + 12 + body)[1] = (uint32_t)(v >> 32);
+    }
   }
   uint32_t *dst = reinterpret_cast<uint32_t *>(rec + 12);
   if (a.kind == 0) {

@@ -30,6 +30,8 @@ class TableInfo:
     max_entries: int = 0
     accum_importance: bool = False          # SSPAggr + RelativeMagnitude/FIFO_N_ReMag (server_table.cpp:26-47)
     server_push_row_upper_bound: int = 0    # configs.hpp:181; 0 -> 100
+    version_maintain: bool = False          # VersionDenseRowOpLog records + VersionServerRow rows (configs.hpp:207)
+    row_oplog_type: int = 0                 # RowOpLogType (configs.hpp:35-40); 3 = float16 dense records
 
 
 def _check(L, ctx, st):
@@ -87,7 +89,8 @@ class Server:
             dense_row_oplog_capacity=info.dense_row_oplog_capacity or info.row_capacity,
             row_offset=info.row_offset, row_stride=info.row_stride, max_rows=info.max_rows,
             max_entries=info.max_entries, accum_importance=1 if info.accum_importance else 0,
-            server_push_row_upper_bound=info.server_push_row_upper_bound)
+            server_push_row_upper_bound=info.server_push_row_upper_bound,
+            version_maintain=1 if info.version_maintain else 0, row_oplog_type=info.row_oplog_type)
         _check(self._L, self._ctx, self._L.psx_table_create(self._ctx, ctypes.byref(cfg)))
         self.tables[table_id] = info
 
@@ -150,6 +153,13 @@ class Server:
         """ServerRow::get_importance for a row range (server_row.hpp:120-122)."""
         out = np.zeros(num_rows, dtype=np.float64)
         _check(self._L, self._ctx, self._L.psx_row_importance(
+            self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+    def row_versions(self, table_id, first_row, num_rows):
+        """VersionServerRow::get_version for a row range (version_server_row.hpp:66)."""
+        out = np.zeros(num_rows, dtype=np.uint64)
+        _check(self._L, self._ctx, self._L.psx_row_versions(
             self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data)))
         return out
 

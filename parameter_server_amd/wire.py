@@ -40,6 +40,35 @@ def dense_stream_np(table_id, row_ids, payload):
     return out
 
 
+def dense_variant_stream_np(table_id, row_ids, payload, versions=None, end_of_version=None, f16=False):
+    """One single-table stream of the variant dense record formats (records are only
+    byte-aligned here, so they are assembled bytewise):
+      versions given : VersionDenseRowOpLog::SerializeDense = V[cap] + uint64 version +
+                       bool end_of_version (version_dense_row_oplog.hpp:161-171)
+      f16            : DenseRowOpLogFloat16::SerializeDense = uint16[cap] (binary16 bits,
+                       dense_row_oplog_float16.hpp:135-142); payload is uint16 bits or
+                       float16, and update_size in the table header stays sizeof(float)."""
+    payload = np.ascontiguousarray(payload)
+    n, cap = payload.shape
+    if f16:
+        body = payload.view(np.uint16).view(np.uint8).reshape(n, 2 * cap)
+        vsize = 4
+    else:
+        vsize = payload.dtype.itemsize
+        body = payload.view(np.uint8).reshape(n, cap * vsize)
+    cols = [np.asarray(row_ids, dtype="<i4").view(np.uint8).reshape(n, 4), body]
+    if versions is not None:
+        cols.append(np.asarray(versions, dtype="<u8").view(np.uint8).reshape(n, 8))
+        eov = np.zeros(n, bool) if end_of_version is None else np.asarray(end_of_version, bool)
+        cols.append(eov.astype(np.uint8).reshape(n, 1))
+    recs = np.concatenate(cols, axis=1)
+    hdr = np.zeros(20, np.uint8)
+    hdr[:8].view(np.int32)[:] = [1, table_id]
+    hdr[8:16].view(np.uint64)[0] = vsize
+    hdr[16:20].view(np.int32)[0] = n
+    return np.concatenate([hdr, recs.reshape(-1)])
+
+
 def sparse_stream_np(table_id, vsize, rows):
     """rows: list of (row_id, cols int32[n], vals V[n]); one single-table sparse stream."""
     parts = [np.array([1, table_id], dtype=np.int32).view(np.uint8),
@@ -66,7 +95,10 @@ def pack_np(tables):
     for t in live:
         op = np.ascontiguousarray(t["oplogs"])
         ids = np.asarray(t["row_ids"], dtype=np.int32)
-        if t["dense_serialized"]:
+        if t["dense_serialized"] and (t.get("f16") or t.get("versions") is not None):
+            parts.append(dense_variant_stream_np(t["table_id"], ids, op, versions=t.get("versions"),
+                                                 end_of_version=t.get("end_of_version"), f16=t.get("f16", False))[4:])
+        elif t["dense_serialized"]:
             parts.append(dense_stream_np(t["table_id"], ids, op)[4:])
         else:
             rows = []

@@ -14,7 +14,7 @@ def test_lib_exports_every_header_symbol(built_lib):
 
 
 def test_abi_version_and_status_strings(built_lib):
-    assert built_lib.psx_abi_version() == 2
+    assert built_lib.psx_abi_version() == 3
     assert built_lib.psx_status_string(0) == b"ok"
     assert built_lib.psx_status_string(2) == b"version gap"
 
@@ -60,9 +60,9 @@ def test_table_config_layout_matches_header(tmp_path):
 #include <stddef.h>
 #include "psx.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu\\n", sizeof(psx_table_config), offsetof(psx_table_config, max_entries),
+  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(psx_table_config), offsetof(psx_table_config, max_entries),
          offsetof(psx_table_config, accum_importance), offsetof(psx_table_config, server_push_row_upper_bound),
-         sizeof(psx_stream));
+         sizeof(psx_stream), offsetof(psx_table_config, version_maintain), offsetof(psx_table_config, row_oplog_type));
   return 0;
 }
 """)
@@ -71,5 +71,6 @@ int main(void) {
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     c = _abi.psx_table_config
     want = [ctypes.sizeof(c), c.max_entries.offset, c.accum_importance.offset,
-            c.server_push_row_upper_bound.offset, ctypes.sizeof(_abi.psx_stream)]
+            c.server_push_row_upper_bound.offset, ctypes.sizeof(_abi.psx_stream), c.version_maintain.offset,
+            c.row_oplog_type.offset]
     assert got == want

@@ -167,3 +167,49 @@ def test_oracle_sparse_importance_and_partial_push(oracle_lib):
     assert s.importance(2, 7) == 0 and s.importance(2, 8) == 1
     assert list(wire.parse_push_body(s.serialize_partial([2], [3]))[2].keys()) == [8]
     assert s.serialize_partial([2], [3]) == b""       # nothing dirty: no message (server.cpp:348)
+
+
+def test_oracle_version_records_and_rows(oracle_lib):
+    """VersionDenseRowOpLog records (V[cap] + uint64 version + bool end_of_version,
+    version_dense_row_oplog.hpp:161-180) and VersionServerRow (version 1 at creation, +1
+    per applied record, uint64 appended to Serialize; version_server_row.hpp:11-71)."""
+    o = OracleServer([1, 2])
+    o.create_table(1, DENSE, F32, 4, version_maintain=True)
+    ids = np.array([3, 5, 3], np.int32)
+    s = wire.dense_variant_stream_np(1, ids, np.arange(12, dtype=np.float32).reshape(3, 4),
+                                     versions=[7, 8, 9], end_of_version=[1, 0, 1])
+    assert s.size == 20 + 3 * (4 + 16 + 9)
+    assert o.apply_stream(s, 1, 0) == 0
+    assert [o.row_version(1, r) for r in (3, 5, 4)] == [3, 2, 0]
+    row3 = o.serialize_row(1, 3)
+    assert len(row3) == 16 + 8
+    assert np.frombuffer(row3[:16], np.float32).tolist() == [8.0, 10.0, 12.0, 14.0]
+    assert np.frombuffer(row3[16:], np.uint64)[0] == 3
+    # a truncated trailer is a malformed stream
+    assert o.apply_stream(s[:-1], 2, 0) == 4
+
+
+def test_oracle_version_needs_dense_serialized(oracle_lib):
+    o = OracleServer([1])
+    o.create_table(2, DENSE, F32, 4, oplog_dense_serialized=False)
+    assert o._L.orc_table_set_version_maintain(o._s, 2, 1) == 10
+
+
+def test_oracle_half_decompression_all_values(oracle_lib):
+    """The fp16 record restatement (IEEE binary16 -> binary32; Float16Compressor is not
+    vendored, parity unpinned) agrees with numpy's conversion for all 63488 non-NaN
+    halves and keeps NaN payloads."""
+    h = np.arange(1 << 16, dtype=np.uint32).astype(np.uint16)
+    cap = h.size
+    o = OracleServer([1])
+    o.create_table(1, DENSE, F32, cap, f16_records=True)
+    s = wire.dense_variant_stream_np(1, np.array([0], np.int32), h.reshape(1, cap), f16=True)
+    assert o.apply_stream(s, 1, 0) == 0
+    got = o.read_dense_rows(1, 0, 1)[0]
+    want = h.view(np.float16).astype(np.float32)
+    nan = np.isnan(want)
+    assert nan.sum() == 2046
+    # 0 + x: exact for every non-NaN value (signed zeros: -0 + 0 = +0 in the table add)
+    assert np.array_equal(got[~nan], (np.float32(0) + want[~nan]))
+    gb = got[nan].view(np.uint32)   # the add quiets the NaN (bit 22); the rest of the payload survives
+    assert np.array_equal(gb & 0x003fe000, (h[nan].astype(np.uint32) & 0x1ff) << 13)

@@ -15,7 +15,10 @@ What it restates (reference file:line):
     L(i,k) += -step * (grad_coeff R(k,j) + 2 lambda / nnz_per_row L(i,k)), then the R
     update -step * (grad_coeff L(i,k) + 2 lambda / nnz_per_col R(k,j)) goes to
     R_table.DenseBatchInc(j, ...);
-  * step_size = init_step_size * (100 + iter)^-0.5 (:475-478); one clock per iteration;
+  * step_size = init_step_size * step_dec^iter (use_step_dec, :473-476, with the run
+    script's single-machine init_step_size 8e-3, step_dec 0.995 and lambda 0.05,
+    run_matrixfact_split.sh:50-58); one clock
+    per iteration;
   * client side of DenseBatchInc (ssp_consistency_controller.cpp:129-187): the row oplog
     is overwritten on first touch, then accumulated `oplog[c] += u[c]`, and the update is
     applied to the process-cache row at once;
@@ -112,7 +115,7 @@ class Client:
             self.R[rid] = np.frombuffer(data, np.float32).copy()
 
 
-def run(server, path, k=16, iters=4, workers=2, bg_id=0, init_step=0.5, lam=0.001, seed=1234):
+def run(server, path, k=16, iters=4, workers=2, bg_id=0, init_step=8e-3, step_dec=0.995, lam=0.05, seed=1234):
     """Returns per-iteration (loss, message, push body) for the given server."""
     x_row, x_col, x_val, n_rows, n_cols = read_split(path)
     starts = partition_workload(x_row, workers)
@@ -133,7 +136,7 @@ def run(server, path, k=16, iters=4, workers=2, bg_id=0, init_step=0.5, lam=0.00
     two_lam = np.float32(lam * 2)
     out = []
     for it in range(iters):
-        step = np.float32(init_step * (100.0 + it) ** -0.5)
+        step = np.float32(init_step * step_dec ** it)       # use_step_dec (:473-476, run script)
         for w in range(workers):
             for a in range(starts[w], ends[w]):
                 i, j, xij = int(x_row[a]), int(x_col[a]), x_val[a]

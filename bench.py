@@ -38,8 +38,13 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of the cpu_baseline sample (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 16)
-    p.add_argument("--pmc-json", default=None,
-                   help="per-launch HBM bytes of dense_apply from a rocprofv3 --pmc pass")
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="server threads of the cpu_baseline (capped at the visible CPUs; the GPU box's share is 16)")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_dense_apply.json"),
+                   help="per-launch HBM bytes of dense_apply from the rocprofv3 --pmc passes "
+                        "(tools/pmc_summary.py); used for roofline.traffic on the default C2 configuration")
+    p.add_argument("--f16-records", action="store_true",
+                   help="C2 with kDenseRowOpLogFloat16 records (binary16 payloads, row_oplog_type 3)")
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows; "
                         "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange")
@@ -53,35 +58,63 @@ def parse():
 
 
 def cpu_baseline(args):
-    """Oracle (CPU restatement of the reference apply loop) on a bounded sample."""
+    """Oracle (CPU restatement of the reference apply loop) on a bounded sample, run as T
+    server threads: rows are sharded row_id % T (the reference's comm-channel placement,
+    context.hpp:291-304) and each thread applies its own shard's messages, as T reference
+    ServerThreads would (the client already splits its oplog per server,
+    abstract_bg_worker.cpp:590-649).  ctypes releases the GIL, so shards run in parallel.
+    A single-thread pass (one reference server thread) is timed beside it."""
     import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
     from oracle.oracle import OracleServer, DENSE, F32
     from parameter_server_amd import wire
     rows, cap, B = args.cpu_rows, args.cols, args.batches
+    T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     rng = np.random.RandomState(1234)
     init = rng.normal(0, 0.1, size=(rows, cap)).astype(np.float32)
-    streams = []
+    perms, upds = [], []
     for b in range(B):
         r = np.random.RandomState(1234 + b)
-        streams.append(wire.dense_stream_np(1, r.permutation(rows).astype(np.int32),
-                                            r.normal(0, 0.01, size=(rows, cap)).astype(np.float32)))
+        perms.append(r.permutation(rows).astype(np.int32))
+        upds.append(r.normal(0, 0.01, size=(rows, cap)).astype(np.float32))
     bgs = list(range(100, 100 + B))
-    orc = OracleServer(bgs)
-    orc.create_table(1, DENSE, F32, cap)
-    orc.load_dense_rows(1, 0, init)
-    step_bytes = sum(s.size for s in streams) + 2 * rows * cap * 4
-    steps, elapsed, ver = 0, 0.0, 0
-    while elapsed < args.cpu_seconds or steps == 0:
-        t0 = time.perf_counter()
-        for b in range(B):
-            assert orc.apply_stream(streams[b], bgs[b], ver) == 0
-        elapsed += time.perf_counter() - t0
-        steps += 1
-        ver += 1
-    orc.close()
-    return {"value": step_bytes * steps / elapsed / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{rows} rows x {cap} f32, {B} batches/step, {steps} steps in {elapsed:.1f} s "
-                      f"(oracle/psx_oracle.c restatement of server.cpp:120-179, 1 thread)"}
+
+    def timed_run(nthreads, seconds):
+        shards = []
+        for t in range(nthreads):
+            o = OracleServer(bgs)
+            o.create_table(1, DENSE, F32, cap)
+            o.load_dense_rows(1, t, init[t::nthreads], stride=nthreads)
+            msgs = []
+            for b in range(B):
+                m = (perms[b] % nthreads) == t
+                msgs.append(wire.dense_stream_np(1, perms[b][m], upds[b][m]))
+            shards.append((o, msgs))
+        step_bytes = sum(m.size for _, ms in shards for m in ms) + 2 * rows * cap * 4
+
+        def one(t, ver):
+            o, msgs = shards[t]
+            for b in range(B):
+                assert o.apply_stream(msgs[b], bgs[b], ver) == 0
+
+        steps, elapsed = 0, 0.0
+        with ThreadPoolExecutor(nthreads) as ex:
+            while elapsed < seconds or steps == 0:
+                t0 = time.perf_counter()
+                list(ex.map(one, range(nthreads), [steps] * nthreads))
+                elapsed += time.perf_counter() - t0
+                steps += 1
+        for o, _ in shards:
+            o.close()
+        return step_bytes * steps / elapsed / 1e9, steps, elapsed
+
+    v1, n1, e1 = timed_run(1, args.cpu_seconds / 3)
+    vt, nt, et = timed_run(T, args.cpu_seconds * 2 / 3) if T > 1 else (v1, n1, e1)
+    return {"value": round(vt, 3), "unit": "GB/s", "cores": T, "kind": "port",
+            "single_thread_GBps": round(v1, 3),
+            "sample": f"{rows} rows x {cap} f32, {B} batches/step; {T} threads (rows % {T} shards): {nt} steps in "
+                      f"{et:.1f} s; 1 thread: {n1} steps in {e1:.1f} s (oracle/psx_oracle.c restatement of "
+                      f"server.cpp:120-179)"}
 
 
 def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234):
@@ -400,7 +433,10 @@ def main():
     for b in range(B):
         perm = torch.randperm(rows, device="cuda", generator=g).to(torch.int32) + base
         upd = torch.randn(rows, cap, device="cuda", generator=g) * 0.01
-        streams.append(wire.dense_stream_torch(1, perm, upd))
+        if args.f16_records:
+            streams.append(wire.dense_stream_torch_f16(1, perm, upd.half()))
+        else:
+            streams.append(wire.dense_stream_torch(1, perm, upd))
         del upd, perm
     torch.cuda.synchronize()
 
@@ -408,7 +444,8 @@ def main():
     srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
-                                     row_offset=base, max_rows=rows, accum_importance=args.importance))
+                                     row_offset=base, max_rows=rows, accum_importance=args.importance,
+                                     row_oplog_type=3 if args.f16_records else 0))
     srv.load_rows(1, base, None, on_device_ptr=table0.data_ptr(), num_rows=rows)
     del table0
     torch.cuda.empty_cache()
@@ -455,7 +492,8 @@ def main():
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
     traffic = None
-    if args.pmc_json and os.path.exists(args.pmc_json):
+    default_cfg = (rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
+    if default_cfg and args.pmc_json and os.path.exists(args.pmc_json):
         traffic = json.load(open(args.pmc_json)).get("dense_apply_hbm_bytes_per_launch")
 
     pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie else None
@@ -464,7 +502,8 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(args)
         line = {
-            "metric": "row-update apply GB/s (device-resident), dense float rows",
+            "metric": "row-update apply GB/s (device-resident), dense float rows"
+                      + (", float16 records" if args.f16_records else ""),
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -483,6 +522,7 @@ def main():
                 "algorithmic_bytes_per_step_per_gpu": step_bytes,
                 "parallelism": f"row-range shards x{world}, no collective",
                 "importance": bool(args.importance),
+                "record_format": "float16 (row_oplog_type 3)" if args.f16_records else "V[cap] (DenseRowOpLog)",
             },
             "roofline": {
                 "bound": "hbm",
@@ -492,6 +532,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": os.path.relpath(args.pmc_json, ROOT) if traffic else None,
+                "dram_GBps": round(traffic / apply_avg_s / 1e9, 1) if traffic and apply_avg_s > 0 else None,
                 "avg_launch_ms": round(apply_avg_s * 1e3, 4),
             },
             "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},

@@ -543,7 +543,8 @@ __device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
 // (cap*B-1)*2^-53 relative of the reference's record-by-record sum).
 // H16 (f32 tables with kDenseRowOpLogFloat16 records): record payloads are binary16, so a
 // lane's 4 elements come from one 8-byte load and are decompressed before the add.
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, bool H16 = false>
+// STNT: the updated table row is written with non-temporal stores (rows 16-byte aligned).
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, bool H16 = false, bool STNT = false>
 __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;        // elements per 16-byte lane vector
@@ -664,7 +665,12 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
               }
               acc = Vec<V>::add(acc, u[q][b]);
             }
-          if (full && has[q]) store16(trow[q] + e0 * VS, acc);
+          if (full && has[q]) {
+            if constexpr (STNT)
+              __builtin_nontemporal_store(acc, reinterpret_cast<u32x4 *>(trow[q] + e0 * VS));
+            else
+              store16(trow[q] + e0 * VS, acc);
+          }
         }
       }
       // ragged tail (cap % EPV elements): element-wise on the first lanes
@@ -912,9 +918,9 @@ static unsigned resident_blocks(K kernel, int64_t want) {
   return (unsigned)(cap < 1 ? 1 : cap);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, bool H16 = false>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, bool H16 = false, bool STNT = false>
 static void launch_v2(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
+  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16, STNT>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
@@ -932,6 +938,12 @@ static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
     case 2: launch_v2<V, BMAX, 64, true, 1>(a, st); break;
     case 3: launch_v2<V, BMAX, 16, true, 1>(a, st); break;
     case 4: launch_v2<V, BMAX, 16, true, 2>(a, st); break;
+    case 7:   // non-temporal table stores (16-byte aligned rows only)
+      if ((a.row_cap * (int64_t)sizeof(V)) % 16 == 0) launch_v2<V, BMAX, 16, true, 2, false, false, true>(a, st);
+      else launch_v2<V, BMAX, 16, true, 2>(a, st);
+      break;
+    case 8: launch_v2<V, BMAX, 16, true, 3>(a, st); break;
+    case 9: launch_v2<V, BMAX, 32, true, 2>(a, st); break;
     default: launch_v2<V, BMAX, 64, true, 2>(a, st); break;
   }
 }

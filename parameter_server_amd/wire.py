@@ -126,6 +126,21 @@ def dense_stream_torch(table_id, row_ids, payload):
     return out.view(torch.uint8)
 
 
+def dense_stream_torch_f16(table_id, row_ids, payload16):
+    """Device-side builder of a kDenseRowOpLogFloat16 stream (int32 row_id; uint16[cap],
+    dense_row_oplog_float16.hpp:135-142; update_size stays sizeof(float)); cap even."""
+    import torch
+    n, cap = payload16.shape
+    assert cap % 2 == 0 and payload16.element_size() == 2
+    words = 1 + cap // 2
+    out = torch.empty(5 + n * words, dtype=torch.int32, device=payload16.device)
+    out[:5].copy_(torch.tensor([1, table_id, 4, 0, n], dtype=torch.int32))
+    recs = out[5:].view(n, words)
+    recs[:, 0].copy_(row_ids.to(torch.int32))
+    recs[:, 1:].copy_(payload16.contiguous().view(torch.int16).view(torch.int32).view(n, cap // 2))
+    return out.view(torch.uint8)
+
+
 def parse_push_body(body):
     """Parse a push body ({table_id; records; -1|-2} per table, as read by the client's
     SerializedRowReader, serialized_row_reader.hpp:49-93) into

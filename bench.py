@@ -37,7 +37,8 @@ def parse():
     p.add_argument("--batches", type=int, default=8)
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of the cpu_baseline sample (0 disables)")
-    p.add_argument("--cpu-rows", type=int, default=1 << 16)
+    p.add_argument("--cpu-rows", type=int, default=1 << 18,
+                   help="rows of the cpu_baseline sample (a quarter of C2: table and streams far larger than the caches)")
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="server threads of the cpu_baseline (capped at the visible CPUs; the GPU box's share is 16)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_dense_apply.json"),
@@ -70,13 +71,13 @@ def cpu_baseline(args):
     from parameter_server_amd import wire
     rows, cap, B = args.cpu_rows, args.cols, args.batches
     T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    rng = np.random.RandomState(1234)
-    init = rng.normal(0, 0.1, size=(rows, cap)).astype(np.float32)
+    rng = np.random.default_rng(1234)
+    init = rng.standard_normal((rows, cap), dtype=np.float32) * np.float32(0.1)
     perms, upds = [], []
     for b in range(B):
-        r = np.random.RandomState(1234 + b)
+        r = np.random.default_rng(1235 + b)
         perms.append(r.permutation(rows).astype(np.int32))
-        upds.append(r.normal(0, 0.01, size=(rows, cap)).astype(np.float32))
+        upds.append(r.standard_normal((rows, cap), dtype=np.float32) * np.float32(0.01))
     bgs = list(range(100, 100 + B))
 
     def timed_run(nthreads, seconds):
@@ -99,9 +100,10 @@ def cpu_baseline(args):
 
         steps, elapsed = 0, 0.0
         with ThreadPoolExecutor(nthreads) as ex:
+            list(ex.map(one, range(nthreads), [0] * nthreads))      # untimed warm-up step
             while elapsed < seconds or steps == 0:
                 t0 = time.perf_counter()
-                list(ex.map(one, range(nthreads), [steps] * nthreads))
+                list(ex.map(one, range(nthreads), [steps + 1] * nthreads))
                 elapsed += time.perf_counter() - t0
                 steps += 1
         for o, _ in shards:

@@ -62,6 +62,12 @@ def lib():
         L.orc_table_set_version_maintain.argtypes = [vp, i32, ctypes.c_int]
         L.orc_table_set_f16_records.argtypes = [vp, i32, ctypes.c_int]
         L.orc_row_version.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_table_set_adarevision.argtypes = [vp, i32, ctypes.c_float, ctypes.c_int, ctypes.c_uint64, i32]
+        L.orc_row_sent.argtypes = [vp, i32, i32, i32]
+        L.orc_ada_state.argtypes = [vp, i32, i32, vp, vp, vp]
+        L.orc_ada_num_snapshots.argtypes = [vp, i32]
+        L.orc_ada_num_snapshots.restype = i64
+        L.orc_rng_normals.argtypes = [ctypes.c_uint32, ctypes.c_float, ctypes.c_float, i64, vp]
         L.orc_row_importance.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_double)]
         L.orc_serialize_partial.argtypes = [vp, vp, ctypes.c_int, vp, vp, sz, ctypes.c_int]
         L.orc_serialize_partial.restype = i64
@@ -124,6 +130,27 @@ class OracleServer:
         out = ctypes.c_uint64()
         assert self._L.orc_row_version(self._s, table_id, row_id, ctypes.byref(out)) == ST_OK
         return out.value
+
+    def set_adarevision(self, table_id, init_step_size=0.1, gaussian_init=True, old_grad_upper_bound=10000,
+                        push_clients=1):
+        """AdaRevisionServerTableLogic on a table (adarevision_server_table_logic.cpp); returns the status."""
+        return self._L.orc_table_set_adarevision(self._s, table_id, init_step_size, 1 if gaussian_init else 0,
+                                                 old_grad_upper_bound, push_clients)
+
+    def row_sent(self, table_id, row_id, num_clients=1):
+        """Server::RowSent (server.cpp:436-441)."""
+        return self._L.orc_row_sent(self._s, table_id, row_id, num_clients)
+
+    def ada_state(self, table_id, row_id):
+        """(accum_gradients_, z_, z_max_) of a row, or None if the row does not exist."""
+        cap = self.tables[table_id][2]
+        a, z, m = (np.zeros(cap, np.float32) for _ in range(3))
+        if self._L.orc_ada_state(self._s, table_id, row_id, _ptr(a), _ptr(z), _ptr(m)) != ST_OK:
+            return None
+        return a, z, m
+
+    def ada_num_snapshots(self, table_id):
+        return self._L.orc_ada_num_snapshots(self._s, table_id)
 
     def apply_stream(self, data, bg, version):
         """Server::ApplyOpLogUpdateVersion; returns the status code."""
@@ -248,6 +275,14 @@ def pack_stream(tables):
                           ctypes.cast(op_ptrs, ctypes.c_void_p), _ptr(out), total)
     assert w == total
     return out.tobytes()
+
+
+def rng_normals(seed, mean, stddev, n):
+    """First n draws of the restated std::normal_distribution<float>(mean, stddev) on
+    std::mt19937(seed) (the generator AdaRevisionServerTableLogic uses)."""
+    out = np.zeros(n, np.float32)
+    lib().orc_rng_normals(seed, mean, stddev, n, _ptr(out))
+    return out
 
 
 def partition_server(row_id, num_channels, num_clients, channel):

@@ -32,6 +32,7 @@
 #define ORC_ERR_CAPACITY 6
 #define ORC_ERR_UNSUPPORTED 10
 #define ORC_ERR_SENDER 11
+#define ORC_ERR_STATE 13
 
 enum { KIND_DENSE = 0, KIND_SORTED_MAP = 1, KIND_MAP = 2 };
 enum { DT_F32 = 0, DT_F64 = 1, DT_I32 = 2, DT_I64 = 3 };
@@ -138,6 +139,73 @@ static int imap_grow(imap_t *m) {
 static void imap_erase_at(imap_t *m, int64_t slot) { m->used[slot] = 2; m->count--; m->tombs++; }
 
 /* ------------------------------------------------------------------------ */
+/* std::mt19937 ([rand.eng.mers], C++11) and libstdc++'s normal_distribution<float>
+ * (bits/random.tcc: Marsaglia's polar method on generate_canonical<float, 24> draws, the
+ * second value of each pair cached): AdaRevisionServerTableLogic draws every row it creates
+ * from one mt19937(12345) through normal_distribution<float>(0, 0.1)
+ * (adarevision_server_table_logic.cpp:30-34,43-46).  Restated here (the product uses
+ * <random> itself); pinned to libstdc++ by tests/golden/make_rng_golden.cpp. */
+typedef struct { uint32_t mt[624]; int idx; int saved_ok; float saved; } orc_rng;
+
+static void rng_seed(orc_rng *g, uint32_t s) {
+  g->mt[0] = s;
+  for (int i = 1; i < 624; ++i) g->mt[i] = 1812433253u * (g->mt[i - 1] ^ (g->mt[i - 1] >> 30)) + (uint32_t)i;
+  g->idx = 624;
+  g->saved_ok = 0;
+  g->saved = 0.0f;
+}
+static uint32_t rng_u32(orc_rng *g) {
+  if (g->idx >= 624) {
+    for (int i = 0; i < 624; ++i) {
+      uint32_t y = (g->mt[i] & 0x80000000u) | (g->mt[(i + 1) % 624] & 0x7fffffffu);
+      g->mt[i] = g->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    g->idx = 0;
+  }
+  uint32_t y = g->mt[g->idx++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+/* generate_canonical<float, 24>: one 32-bit draw, (float)x / 2^32, kept below 1 */
+static float rng_canonical(orc_rng *g) {
+  float r = (float)rng_u32(g) / 4294967296.0f;
+  return r >= 1.0f ? nextafterf(1.0f, 0.0f) : r;
+}
+static float rng_normal(orc_rng *g, float mean, float stddev) {
+  float ret;
+  if (g->saved_ok) {
+    g->saved_ok = 0;
+    ret = g->saved;
+  } else {
+    float x, y, r2;
+    do {
+      x = (float)(2.0f * rng_canonical(g) - 1.0);   /* result_type(2.0) * u - 1.0: a double subtraction */
+      y = (float)(2.0f * rng_canonical(g) - 1.0);
+      r2 = x * x + y * y;
+    } while (r2 > 1.0 || r2 == 0.0);
+    const float mult = sqrtf(-2 * logf(r2) / r2);
+    g->saved = x * mult;
+    g->saved_ok = 1;
+    ret = y * mult;
+  }
+  return ret * stddev + mean;
+}
+
+/* Test hook: the first n draws of normal_distribution<float>(mean, stddev) on mt19937(seed). */
+void orc_rng_normals(uint32_t seed, float mean, float stddev, int64_t n, float *out) {
+  orc_rng g;
+  rng_seed(&g, seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = rng_normal(&g, mean, stddev);
+}
+
+/* old_accum_gradients_ entry: (row, version) -> (accum_gradients_, clients left)
+ * (adarevision_server_table_logic.hpp:64-67) */
+typedef struct { int32_t row; uint64_t version; float *acc; size_t count; } orc_snap;
+
+/* ------------------------------------------------------------------------ */
 /* Rows. */
 typedef struct {
   /* dense: VectorStore<V> (vector_store.hpp:64-102), zeroed at Init */
@@ -153,6 +221,7 @@ typedef struct {
                             uninitialized (:16-19), this restatement starts it at 0 */
   uint64_t version;      /* VersionServerRow::version_ (version_server_row.hpp:13-19,69): 1 at
                             creation, +1 per applied record; read only for version tables */
+  float *ada_acc, *ada_z, *ada_zmax;   /* AdaRevisionRow (adarevision_server_table_logic.hpp:11-22) */
 } orc_row;
 
 typedef struct {
@@ -164,6 +233,14 @@ typedef struct {
   int importance;        /* ApplyRow*AccumImportance selected (server_table.cpp:26-47) */
   int version_maintain;  /* TableInfo.version_maintain (configs.hpp:207) */
   int f16_records;       /* row_oplog_type kDenseRowOpLogFloat16 (configs.hpp:39) */
+  int ada;               /* AdaRevisionServerTableLogic attached (server_table.cpp:83-93) */
+  float ada_step;        /* FLAGS_init_step_size (adarevision_server_table_logic.cpp:8,22) */
+  uint64_t ada_upper;    /* FLAGS_old_grad_upper_bound (:9,192-197) */
+  int ada_gauss;         /* FLAGS_random_init == "guassian" (:10,30-34) */
+  size_t ada_clients;    /* clients a pushed row goes to (ServerRowSent's num_clients) */
+  orc_rng ada_rng;
+  orc_snap *snaps;       /* old_accum_gradients_ */
+  int64_t nsnaps, snaps_cap;
   imap_t index;          /* row_id -> row number */
   orc_row **rows;
   int64_t nrows, rows_cap;
@@ -185,6 +262,7 @@ orc_server *orc_server_create(void) { return (orc_server *)calloc(1, sizeof(orc_
 
 static void row_free(orc_table *t, orc_row *r) {
   free(r->dense); free(r->entries);
+  free(r->ada_acc); free(r->ada_z); free(r->ada_zmax);
   if (t->kind == KIND_MAP) imap_free(&r->map);
   free(r);
 }
@@ -194,6 +272,8 @@ void orc_server_destroy(orc_server *s) {
   for (int i = 0; i < s->ntables; ++i) {
     orc_table *t = s->tables[i];
     for (int64_t r = 0; r < t->nrows; ++r) row_free(t, t->rows[r]);
+    for (int64_t k = 0; k < t->nsnaps; ++k) free(t->snaps[k].acc);
+    free(t->snaps);
     free(t->rows); imap_free(&t->index); free(t);
   }
   free(s);
@@ -232,6 +312,13 @@ int orc_table_create(orc_server *s, int32_t table_id, int kind, int dt, int dens
 static orc_row *create_row(orc_table *t, int32_t row_id) {
   orc_row *r = (orc_row *)calloc(1, sizeof(orc_row));
   r->version = 1;   /* VersionServerRow(row_data): version_(1) (version_server_row.hpp:17-19) */
+  if (t->ada) {     /* AdaRevisionRow(row_size): accum 0, z 1, z_max 1 (adarevision_server_table_logic.hpp:12-16) */
+    size_t n = (size_t)(t->row_capacity ? t->row_capacity : 1);
+    r->ada_acc = (float *)calloc(n, sizeof(float));
+    r->ada_z = (float *)malloc(n * sizeof(float));
+    r->ada_zmax = (float *)malloc(n * sizeof(float));
+    for (size_t i = 0; i < n; ++i) { r->ada_z[i] = 1.0f; r->ada_zmax[i] = 1.0f; }
+  }
   if (t->kind == KIND_DENSE) {
     r->dense = (uint8_t *)calloc((size_t)(t->row_capacity ? t->row_capacity : 1), dt_size(t->dt));
   } else if (t->kind == KIND_SORTED_MAP) {
@@ -419,6 +506,122 @@ static void apply_dense_record(orc_table *t, orc_row *r, const uint8_t *upd, int
   }
 }
 
+/* ---- AdaRevision server-table logic (adarevision_server_table_logic.cpp) ---------- */
+/* Init (:19-36): attached to a table as TableInfo.server_table_logic selects it
+ * (server_table.cpp:83-93).  AdaRevision treats updates as a dense float row of
+ * row_capacity values (:65-68). */
+int orc_table_set_adarevision(orc_server *s, int32_t table_id, float init_step, int gaussian,
+                              uint64_t upper_bound, int32_t push_clients) {
+  orc_table *t = find_table(s, table_id);
+  if (!t || push_clients <= 0) return ORC_ERR_INVALID_ARG;
+  if (t->kind != KIND_DENSE || t->dt != DT_F32 || !t->dense_serialized || t->f16_records ||
+      t->oplog_capacity != t->row_capacity || t->nrows)
+    return ORC_ERR_UNSUPPORTED;
+  t->ada = 1;
+  t->ada_step = init_step;
+  t->ada_gauss = gaussian ? 1 : 0;
+  t->ada_upper = upper_bound;
+  t->ada_clients = (size_t)push_clients;
+  rng_seed(&t->ada_rng, 12345);   /* gen_ = new std::mt19937(12345) (:32) */
+  return ORC_OK;
+}
+
+static void apply_dense_record(orc_table *t, orc_row *r, const uint8_t *upd, int64_t n);
+
+/* ServerRowCreated (:38-50) for a row CreateRow makes on first touch (server.cpp:163-166):
+ * with random_init "guassian", row_capacity N(0, 0.1) draws go through RowBatchInc_. */
+static void ada_row_created(orc_table *t, orc_row *r) {
+  if (!t->ada_gauss) return;
+  int64_t n = t->row_capacity;
+  float *d = (float *)malloc((size_t)n * sizeof(float));
+  for (int64_t i = 0; i < n; ++i) d[i] = rng_normal(&t->ada_rng, 0.0f, 0.1f);
+  apply_dense_record(t, r, (const uint8_t *)d, n);
+  r->dirty = 1;
+  r->version++;
+  free(d);
+}
+
+static orc_snap *ada_find(orc_table *t, int32_t row, uint64_t version) {
+  for (int64_t k = 0; k < t->nsnaps; ++k)
+    if (t->snaps[k].row == row && t->snaps[k].version == version) return &t->snaps[k];
+  return NULL;
+}
+
+/* ApplyRowOpLog (:52-175): per element, in float, the AdaRevision step against the
+ * accumulated gradient as of the record's row version (0: none), then RowBatchInc_ of the
+ * deltas (:173-174).  A version without a snapshot is the reference's CHECK (:116). */
+static int ada_apply(orc_table *t, orc_row *r, int32_t row_id, const uint8_t *upd, uint64_t rv, int eov) {
+  int64_t n = t->row_capacity;
+  orc_snap *sn = NULL;
+  if (rv != 0) {
+    sn = ada_find(t, row_id, rv);
+    if (!sn) return ORC_ERR_STATE;
+  }
+  float *d = (float *)malloc((size_t)n * sizeof(float));
+  const float step = t->ada_step;
+  for (int64_t i = 0; i < n; ++i) {
+    float u;
+    memcpy(&u, upd + (size_t)i * 4, 4);
+    float g_bck = r->ada_acc[i] - (sn ? sn->acc[i] : 0.0f);
+    float eta_old = step / sqrtf(r->ada_zmax[i]);
+    r->ada_z[i] += u * (u + 2 * g_bck);
+    r->ada_zmax[i] = (r->ada_z[i] < r->ada_zmax[i]) ? r->ada_zmax[i] : r->ada_z[i];   /* std::max */
+    float eta = step / sqrtf(r->ada_zmax[i]);
+    d[i] = -(eta * u) + (eta_old - eta) * g_bck;
+    r->ada_acc[i] += u;
+  }
+  if (sn && eov && --sn->count == 0) {   /* :165-170 */
+    free(sn->acc);
+    *sn = t->snaps[--t->nsnaps];
+  }
+  apply_dense_record(t, r, (const uint8_t *)d, n);
+  free(d);
+  return ORC_OK;
+}
+
+/* ServerRowSent (:177-190): old_accum_gradients_.insert({(row, get_version()),
+ * (accum_gradients_, num_clients)}); an existing key is kept (std::map::insert). */
+static void ada_row_sent(orc_table *t, int32_t row_id, orc_row *r, size_t num_clients) {
+  uint64_t v = t->version_maintain ? r->version : 0;
+  if (ada_find(t, row_id, v)) return;
+  if (t->nsnaps == t->snaps_cap) {
+    t->snaps_cap = t->snaps_cap ? 2 * t->snaps_cap : 64;
+    t->snaps = (orc_snap *)realloc(t->snaps, (size_t)t->snaps_cap * sizeof(orc_snap));
+  }
+  orc_snap *sn = &t->snaps[t->nsnaps++];
+  sn->row = row_id;
+  sn->version = v;
+  sn->count = num_clients;
+  sn->acc = (float *)malloc((size_t)t->row_capacity * sizeof(float));
+  memcpy(sn->acc, r->ada_acc, (size_t)t->row_capacity * sizeof(float));
+}
+
+/* Server::RowSent (server.cpp:436-441) -> ServerTable::RowSent (server_table.cpp:191-195):
+ * what ServerThread::ReplyRowRequest does after serving a row (server_thread.cpp:221). */
+int orc_row_sent(orc_server *s, int32_t table_id, int32_t row_id, int32_t num_clients) {
+  orc_table *t = find_table(s, table_id);
+  orc_row *r = t ? find_row(t, row_id) : NULL;
+  if (!r || num_clients <= 0) return ORC_ERR_INVALID_ARG;
+  if (t->ada) ada_row_sent(t, row_id, r, (size_t)num_clients);
+  return ORC_OK;
+}
+
+/* AdaRevisionRow state of a row and the number of live old_accum_gradients_ entries. */
+int orc_ada_state(orc_server *s, int32_t table_id, int32_t row_id, float *acc, float *z, float *zmax) {
+  orc_table *t = find_table(s, table_id);
+  orc_row *r = t ? find_row(t, row_id) : NULL;
+  if (!r || !t->ada) return ORC_ERR_INVALID_ARG;
+  size_t nb = (size_t)t->row_capacity * sizeof(float);
+  memcpy(acc, r->ada_acc, nb);
+  memcpy(z, r->ada_z, nb);
+  memcpy(zmax, r->ada_zmax, nb);
+  return ORC_OK;
+}
+int64_t orc_ada_num_snapshots(orc_server *s, int32_t table_id) {
+  orc_table *t = find_table(s, table_id);
+  return t ? t->nsnaps : -1;
+}
+
 static int32_t rd32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
 static uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
 
@@ -489,8 +692,21 @@ static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) 
         if (off + rs > size) return ORC_ERR_MALFORMED;
         if (apply) {
           orc_row *r = find_row(t, row_id);
-          if (!r) r = create_row(t, row_id);
-          if (t->f16_records) {
+          if (!r) {
+            r = create_row(t, row_id);
+            if (t->ada) ada_row_created(t, r);
+          }
+          if (t->ada) {
+            uint64_t rv = 0;
+            int eov = 0;
+            if (t->version_maintain) {   /* ExtractOpLogVersion (server_table.cpp:527-535) */
+              size_t vo = (size_t)t->oplog_capacity * dt_size(t->dt);
+              rv = rd64(b + off + vo);
+              eov = b[off + vo + 8] != 0;
+            }
+            int st = ada_apply(t, r, row_id, b + off, rv, eov);
+            if (st) return st;
+          } else if (t->f16_records) {
             /* ParseDenseSerializedOpLog decompresses into the sample oplog's f32 buffer,
              * which is then applied as a dense float record */
             float *tmp = (float *)malloc((size_t)t->oplog_capacity * sizeof(float));
@@ -908,8 +1124,12 @@ int64_t orc_serialize_dirty(orc_server *s, const int32_t *table_ids, int ntables
     int64_t w = orc_serialize_records(s, table_ids[ti], ids, (int32_t)nd, o + used, cap - used);
     if (w < 0) { free(ids); return w; }
     used += (size_t)w;
-    if (clear)   /* ResetDirty + ResetImportance_ (server_table.cpp:234-235) */
-      for (int64_t k = 0; k < nd; ++k) { orc_row *r = find_row(t, ids[k]); r->dirty = 0; r->importance = 0; }
+    if (clear)   /* ResetDirty + ResetImportance_ (server_table.cpp:234-235), ServerRowSent (:252-255) */
+      for (int64_t k = 0; k < nd; ++k) {
+        orc_row *r = find_row(t, ids[k]);
+        r->dirty = 0; r->importance = 0;
+        if (t->ada) ada_row_sent(t, ids[k], r, t->ada_clients);
+      }
     free(ids);
     if (used + 4 > cap) return -2;
     int32_t sep = ti + 1 < ntables ? -1 : -2;
@@ -954,6 +1174,7 @@ int64_t orc_serialize_partial(orc_server *s, const int32_t *table_ids, int ntabl
     qsort(ids, (size_t)nd, 4, cmp_i32);
     if (t->importance) { g_sort_table = t; qsort(ids, (size_t)nd, 4, cmp_importance); }
     if (nd > upper_bounds[ti]) nd = upper_bounds[ti];
+    if (t->ada && (uint64_t)t->nsnaps >= t->ada_upper) nd = 0;   /* !AllowSend() (server_table.cpp:293-295) */
     sel[ti] = ids; nsel[ti] = nd;
     if (nd) any = 1;
   }
@@ -978,7 +1199,11 @@ int64_t orc_serialize_partial(orc_server *s, const int32_t *table_ids, int ntabl
       if (clear)
         for (int ti = 0; ti < ntables; ++ti) {
           orc_table *t = find_table(s, table_ids[ti]);
-          for (int64_t k = 0; k < nsel[ti]; ++k) { orc_row *r = find_row(t, sel[ti][k]); r->dirty = 0; r->importance = 0; }
+          for (int64_t k = 0; k < nsel[ti]; ++k) {   /* AppendRowsToBuffsPartial (server_table.cpp:398-416) */
+            orc_row *r = find_row(t, sel[ti][k]);
+            r->dirty = 0; r->importance = 0;
+            if (t->ada) ada_row_sent(t, sel[ti][k], r, t->ada_clients);
+          }
         }
     }
   }

@@ -29,6 +29,12 @@
  *                                                        src/petuum_ps_common/oplog/dense_row_oplog.hpp:112-136
  *   psx_row_importance      ServerRow::get_importance    src/petuum_ps/server/server_row.hpp:120-130
  *   psx_row_versions        VersionServerRow::get_version src/petuum_ps/server/version_server_row.hpp:66
+ *   psx_table_set_adarevision  AdaRevisionServerTableLogic::Init (server_table_logic = AdaRevision)
+ *                                                        src/petuum_ps/server/adarevision_server_table_logic.cpp:19-36,
+ *                                                        src/petuum_ps/server/server_table.cpp:83-93
+ *   psx_row_sent            Server::RowSent -> ServerRowSent  src/petuum_ps/server/server.cpp:436-441,
+ *                                                        src/petuum_ps/server/server_thread.cpp:221
+ *   psx_adarevision_state   AdaRevisionRow               src/petuum_ps/server/adarevision_server_table_logic.hpp:11-22
  *   psx_serialize_partial   Server::CreateSendServerPushRowMsgsPartial
  *                                                        src/petuum_ps/server/server.cpp:311-420,
  *                           ServerTable::GetPartialTableToSendRegular / AppendRowsToBuffsPartial
@@ -74,7 +80,11 @@ typedef enum psx_status {
   PSX_ERR_BUFFER_TOO_SMALL = 9,
   PSX_ERR_UNSUPPORTED = 10,   /* e.g. the same table twice inside one message */
   PSX_ERR_SENDER = 11,        /* bg id never registered (Server::Init bg_ids) */
-  PSX_ERR_NO_DEVICE = 12      /* no HIP device visible */
+  PSX_ERR_NO_DEVICE = 12,     /* no HIP device visible */
+  PSX_ERR_STATE = 13          /* server-logic state missing: an AdaRevision record names a
+                                 (row, version) with no accum_gradients_ snapshot (CHECK,
+                                 adarevision_server_table_logic.cpp:114-116); the call is
+                                 partially applied */
 } psx_status;
 
 /* Row storage kinds (TableInfo.row_type -> registered AbstractRow). */
@@ -227,6 +237,45 @@ psx_status psx_serialize_dirty(psx_ctx *ctx, void *out, size_t cap, size_t *used
  * On PSX_ERR_BUFFER_TOO_SMALL *used holds the bytes needed and nothing is cleared. */
 psx_status psx_serialize_partial(psx_ctx *ctx, void *out, size_t cap, size_t *used,
                                  int32_t out_on_device, int32_t clear_dirty);
+
+/* ---- AdaRevision server-table logic ------------------------------------------------ */
+/* AdaRevisionServerTableLogic (src/petuum_ps/server/adarevision_server_table_logic.cpp),
+ * the server-table logic apps register as TableInfo.server_table_logic
+ * (apps/matrixfact/src/matrixfact_adarevision.cpp:633-635; its run script sets
+ * server_table_logic=1 and version_maintain=true).  Per record, per element, in f32:
+ * g_bck = accum - accum_at(record's row version, 0 if none); eta_old = step/sqrt(z_max);
+ * z += u*(u + 2*g_bck); z_max = max(z, z_max); eta = step/sqrt(z_max);
+ * delta = -(eta*u) + (eta_old - eta)*g_bck; accum += u; then the row gets += delta through
+ * the table's ordinary apply (dirty, importance, version).  A push (psx_serialize_dirty /
+ * _partial with clear_dirty) and psx_row_sent snapshot accum under (row, row version) for
+ * num_clients clients; a record with end_of_version releases one client. */
+typedef struct psx_adarevision_config {
+  float init_step_size;            /* FLAGS_init_step_size (:8; reference default 0.1) */
+  int32_t gaussian_init;           /* FLAGS_random_init == "guassian" (:10,30-34,43-49; the default):
+                                      a row created by an apply first gets row_capacity N(0, 0.1)
+                                      draws of one mt19937(12345), in creation order */
+  uint64_t old_grad_upper_bound;   /* FLAGS_old_grad_upper_bound (:9; default 10000): the partial push
+                                      sends nothing from the table while that many snapshots are live
+                                      (AllowSend, :192-197; server_table.cpp:293-295) */
+  int32_t push_clients;            /* num_clients of ServerRowSent for the push paths = clients subscribed
+                                      to the pushed rows (server_table.cpp:253-254,413-414); 0 -> 1 */
+  int32_t max_snapshots_per_row;   /* HBM slots per row for live snapshots, 1..8; 0 -> 4.  Exceeding it is
+                                      PSX_ERR_CAPACITY (the reference's map is unbounded) */
+} psx_adarevision_config;
+
+/* Attach the logic to a table before its first apply: f32 dense rows, dense-serialized
+ * kDenseRowOpLog records of row_capacity values (:65-68).  A context with an AdaRevision
+ * table takes dense-serialized tables only and rejects a row twice in one message
+ * (PSX_ERR_UNSUPPORTED at psx_sync): there is no ordered replay for the logic. */
+psx_status psx_table_set_adarevision(psx_ctx *ctx, int32_t table_id, const psx_adarevision_config *cfg);
+/* Server::RowSent after a row request reply (server_thread.cpp:221, server.cpp:436-441):
+ * ServerRowSent for the listed rows; a no-op for tables without a logic. */
+psx_status psx_row_sent(psx_ctx *ctx, int32_t table_id, const int32_t *row_ids, int32_t n,
+                        int32_t num_clients);
+/* AdaRevisionRow state of num_rows rows (accum_gradients_, z_, z_max_; [num_rows][row_capacity]
+ * each, any may be NULL) and the number of live snapshots (old_accum_gradients_.size()). */
+psx_status psx_adarevision_state(psx_ctx *ctx, int32_t table_id, int64_t first_row, int64_t num_rows,
+                                 float *accum, float *z, float *z_max, uint64_t *live_snapshots);
 
 /* ---- client-side pack ------------------------------------------------------------ */
 /* One table's oplog rows for psx_pack_stream: row i's oplog is the `capacity` values at

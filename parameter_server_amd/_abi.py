@@ -16,7 +16,7 @@ STATUS_NAMES = {
     0: "PSX_OK", 1: "PSX_ERR_INVALID_ARG", 2: "PSX_ERR_VERSION", 3: "PSX_ERR_UNKNOWN_TABLE",
     4: "PSX_ERR_MALFORMED", 5: "PSX_ERR_ROW_RANGE", 6: "PSX_ERR_CAPACITY", 7: "PSX_ERR_DEVICE",
     8: "PSX_ERR_OOM", 9: "PSX_ERR_BUFFER_TOO_SMALL", 10: "PSX_ERR_UNSUPPORTED",
-    11: "PSX_ERR_SENDER", 12: "PSX_ERR_NO_DEVICE",
+    11: "PSX_ERR_SENDER", 12: "PSX_ERR_NO_DEVICE", 13: "PSX_ERR_STATE",
 }
 ROW_DENSE, ROW_SORTED_MAP, ROW_MAP = 0, 1, 2
 F32, F64, I32, I64 = 0, 1, 2, 3
@@ -64,6 +64,16 @@ class psx_pack_table(ctypes.Structure):
         ("num_rows", ctypes.c_int64),
         ("row_ids", ctypes.c_void_p),
         ("oplogs", ctypes.c_void_p),
+    ]
+
+
+class psx_adarevision_config(ctypes.Structure):
+    _fields_ = [
+        ("init_step_size", ctypes.c_float),
+        ("gaussian_init", ctypes.c_int32),
+        ("old_grad_upper_bound", ctypes.c_uint64),
+        ("push_clients", ctypes.c_int32),
+        ("max_snapshots_per_row", ctypes.c_int32),
     ]
 
 
@@ -116,6 +126,9 @@ def load():
         "psx_serialize_partial": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
         "psx_row_importance": ([vp, i32, i64, i64, vp], ctypes.c_int),
         "psx_row_versions": ([vp, i32, i64, i64, vp], ctypes.c_int),
+        "psx_table_set_adarevision": ([vp, i32, P(psx_adarevision_config)], ctypes.c_int),
+        "psx_row_sent": ([vp, i32, vp, i32, i32], ctypes.c_int),
+        "psx_adarevision_state": ([vp, i32, i64, i64, vp, vp, vp, P(ctypes.c_uint64)], ctypes.c_int),
         "psx_pack_stream": ([vp, P(psx_pack_table), i32, vp, sz, P(sz), vp], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),

@@ -1,0 +1,313 @@
+// psx_ada.hip — AdaRevision server-table logic on the device
+// (src/petuum_ps/server/adarevision_server_table_logic.cpp:14-197; apps register it as
+// TableInfo.server_table_logic, apps/matrixfact/src/matrixfact_adarevision.cpp:633-635).
+//
+// The per-row state (AdaRevisionRow, adarevision_server_table_logic.hpp:11-22:
+// accum_gradients_, z_, z_max_, f32 [row_capacity] each) lives in HBM beside the table
+// row; old_accum_gradients_ ((row, version) -> (accum_gradients_ when that version was
+// sent, clients left), :64-67) is S slots per row: {version, count} + an f32 row image.
+//
+//   ada_new_rows   rows this call creates (touched, not present before), keyed by their
+//                  first record (message, position): the order CreateRow runs in
+//                  (server.cpp:154-178).  The host sorts the keys and draws each new row's
+//                  N(0, 0.1) initial deltas from the table's mt19937(12345) (:30-34,43-46).
+//   ada_init_rows  ServerRowCreated (:38-50): RowBatchInc_(deltas) into the zero row.
+//   ada_apply      ApplyRowOpLog (:52-175): one wave per touched row, its records in
+//                  message order; per element the AdaRevision step, then RowBatchInc_ of
+//                  the delta (the row add, importance, VersionServerRow version_++).
+//   ada_sent       ServerRowSent (:177-190): snapshot accum_gradients_ under
+//                  (row, get_version()) unless that key is live (std::map::insert).
+// Every f32 operation is the reference's, in its order (no contraction:
+// -ffp-contract=off; sqrtf and division correctly rounded), so rows and state are
+// bit-identical to the sequential reference.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <cstdint>
+#include "psx_device.hpp"
+
+namespace psx {
+
+__device__ __forceinline__ bool ada_go(const AdaArgs &a) {
+  return !(*a.call_status & (kStFatal | kStDuplicateRow)) && !(*a.sticky & kStDuplicateRow);
+}
+
+// Rows created by this call: touched by some message and not present before it.
+__global__ void __launch_bounds__(256) ada_new_rows_kernel(AdaArgs a) {
+  const int lane = threadIdx.x & 63;
+  const bool go = ada_go(a);
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < a.max_rows; base += G) {
+    const int64_t s = base + lane;
+    bool fresh = false;
+    uint64_t key = 0;
+    if (go && s < a.max_rows && !(a.flags[s] & 1)) {
+      for (int b = 0; b < a.B; ++b) {
+        const int32_t i = a.inv[s * a.inv_ss + b * a.inv_sb];
+        if (i >= 0) {
+          fresh = true;
+          key = ((uint64_t)b << 32) | (uint32_t)i;
+          break;
+        }
+      }
+    }
+    const uint64_t m = __ballot(fresh);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      uint32_t pos = 0;
+      if (lane == leader) pos = atomicAdd(a.words + 1, (uint32_t)__builtin_popcountll(m));
+      pos = __builtin_amdgcn_readlane(pos, leader);
+      if (fresh) {
+        const uint32_t r = pos + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+        a.new_keys[r] = key;
+        a.new_slots[r] = (int32_t)s;
+      }
+    }
+  }
+}
+
+// ServerRowCreated's RowBatchInc_ (:47-48): the new (zeroed) row += its initial deltas.
+__global__ void __launch_bounds__(256) ada_init_rows_kernel(AdaArgs a, const int32_t *slots, const float *deltas,
+                                                           int32_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = w0; r < n; r += nw) {
+    const int64_t s = slots[r];
+    float *row = a.table + s * a.cap;
+    const float *d = deltas + r * a.cap;
+    double p = 0.0;
+    for (int64_t e = lane; e < a.cap; e += 64) {
+      const float x = row[e], u = d[e];
+      if (a.imp) p += imp_term<float>(x, u);
+      row[e] = x + u;
+    }
+    if (a.imp) {
+      const double tot = a.imp[s] + wave_sum_f64(p);
+      if (lane == 0) a.imp[s] = tot;
+    }
+    if (lane == 0) {
+      if (a.ver) a.ver[s] += 1;
+      a.flags[s] = 3;   // exists | dirty
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t *p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+
+// ApplyRowOpLog (:52-175) for every record of the call, per row in message order.
+template <bool IMP>
+__global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const bool skip = !ada_go(a);
+  const uint8_t *pay0[kMaxFused];   // payload of record 0 of message b
+#pragma unroll
+  for (int b = 0; b < kMaxFused; ++b) {
+    pay0[b] = nullptr;
+    if (b < a.B) {
+      const Seg sg = a.segs[b * kMaxTables + a.t];
+      if (sg.rec0 >= 0 && !sg.sparse) pay0[b] = a.ss.data[b] + sg.rec0 + 4;
+    }
+  }
+  const int S = a.S;
+  const int64_t ntiles = (a.max_rows + 63) / 64;
+  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
+    const int64_t my = tile * 64 + lane;
+    const bool mine = my < a.max_rows;
+    int32_t idx[kMaxFused];
+    bool touched = false;
+    uint64_t nrec = 0;
+#pragma unroll
+    for (int b = 0; b < kMaxFused; ++b) {
+      idx[b] = -1;
+      if (b < a.B && mine) {
+        int32_t *p = a.inv + my * a.inv_ss + b * a.inv_sb;
+        idx[b] = *p;
+        if (idx[b] >= 0) {
+          touched = true;
+          ++nrec;
+          *p = -1;   // restore the index for the next call
+        }
+      }
+    }
+    if (skip) continue;
+    if (touched) {
+      a.flags[my] = 3;
+      if (a.ver) a.ver[my] += nrec;   // VersionServerRow: version_++ per RowBatchInc_
+    }
+    uint64_t live = __ballot(touched);
+    while (live) {
+      const int k = __builtin_ctzll(live);
+      live &= live - 1;
+      const int64_t s = tile * 64 + k;
+      float *row = a.table + s * a.cap;
+      float *acc = a.acc + s * a.cap, *z = a.z + s * a.cap, *zmax = a.zmax + s * a.cap;
+      uint64_t sv[kAdaMaxS], sc[kAdaMaxS];   // the row's snapshot slots, wave-uniform
+#pragma unroll
+      for (int q = 0; q < kAdaMaxS; ++q) {
+        sv[q] = q < S ? a.snap_ver[s * S + q] : 0;
+        sc[q] = q < S ? a.snap_cnt[s * S + q] : 0;
+      }
+      bool snap_dirty = false;
+      double impt = IMP ? a.imp[s] : 0.0;
+      for (int b = 0; b < a.B; ++b) {
+        const int32_t i = __builtin_amdgcn_readlane(idx[b], k);
+        if (i < 0) continue;
+        const uint8_t *rec = pay0[b] + (int64_t)i * a.stride;
+        uint64_t rv = 0;
+        bool eov = false;
+        if (a.version_records) {   // ExtractOpLogVersion (server_table.cpp:527-535)
+          rv = ld_u64(rec + a.cap * 4);
+          eov = rec[a.cap * 4 + 8] != 0;
+        }
+        int q0 = -1;
+        if (rv) {   // old_accum_gradients_.find((row, version)) (:114-116)
+#pragma unroll
+          for (int q = 0; q < kAdaMaxS; ++q)
+            if (q0 < 0 && q < S && sc[q] && sv[q] == rv) q0 = q;
+          if (q0 < 0) {
+            if (lane == 0) atomicOr(a.call_status, kStState);
+            continue;
+          }
+        }
+        const float *old = q0 >= 0 ? a.snap_acc + (s * S + q0) * a.cap : nullptr;
+        double p = 0.0;
+        for (int64_t e = lane; e < a.cap; e += 64) {
+          float u;
+          __builtin_memcpy(&u, rec + e * 4, 4);
+          const float ac = acc[e];
+          const float g_bck = ac - (old ? old[e] : 0.0f);
+          const float zm0 = zmax[e];
+          const float eta_old = a.step / sqrtf(zm0);
+          const float zz = z[e] + u * (u + 2.0f * g_bck);
+          const float zm = zz < zm0 ? zm0 : zz;   // std::max(z_, z_max_)
+          const float eta = a.step / sqrtf(zm);
+          const float d = -(eta * u) + (eta_old - eta) * g_bck;
+          z[e] = zz;
+          zmax[e] = zm;
+          acc[e] = ac + u;
+          const float x = row[e];   // RowBatchInc_(deltas) (:173-174)
+          if constexpr (IMP) p += imp_term<float>(x, d);
+          row[e] = x + d;
+        }
+        if constexpr (IMP) impt += wave_sum_f64(p);
+        if (q0 >= 0 && eov) {   // the client is done with this version (:165-170)
+#pragma unroll
+          for (int q = 0; q < kAdaMaxS; ++q)
+            if (q == q0) {
+              sc[q] -= 1;
+              if (sc[q] == 0 && lane == 0) atomicSub(a.words, 1u);
+            }
+          snap_dirty = true;
+        }
+      }
+      if (snap_dirty) {
+#pragma unroll
+        for (int q = 0; q < kAdaMaxS; ++q)
+          if (q < S && lane == q) a.snap_cnt[s * S + q] = sc[q];
+      }
+      if (IMP && lane == 0) a.imp[s] = impt;
+    }
+  }
+}
+
+// ServerRowSent (:177-190) for the rows in `list` (n entries) or, with list == nullptr,
+// for every slot s < n whose serve-back size is non-zero (the rows a push just sent).
+__global__ void __launch_bounds__(256) ada_sent_kernel(AdaArgs a, const int32_t *list, const int64_t *sizes,
+                                                      int64_t n, uint64_t clients) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int S = a.S;
+  for (int64_t base = wave_g * 64; base < n; base += nwaves * 64) {
+    const int64_t i = base + lane;
+    int64_t mys = -1;
+    if (i < n) mys = list ? (int64_t)list[i] : ((sizes[i] != 0) ? i : -1);
+    uint64_t live = __ballot(mys >= 0);
+    while (live) {
+      const int k = __builtin_ctzll(live);
+      live &= live - 1;
+      const int64_t s = (int64_t)__builtin_amdgcn_readlane((int32_t)mys, k);
+      const uint64_t v = a.ver ? a.ver[s] : 0;   // row->get_version() (abstract_server_row.hpp:71)
+      int hit = -1, fr = -1;
+      for (int q = 0; q < S; ++q) {
+        const uint64_t c = a.snap_cnt[s * S + q];
+        if (c && a.snap_ver[s * S + q] == v) hit = q;
+        if (!c && fr < 0) fr = q;
+      }
+      if (hit >= 0) continue;   // std::map::insert keeps the live entry
+      if (fr < 0) {
+        if (lane == 0) atomicOr(a.words + 2, kStCapacity);
+        continue;
+      }
+      float *dst = a.snap_acc + (s * S + fr) * a.cap;
+      const float *src = a.acc + s * a.cap;
+      for (int64_t e = lane; e < a.cap; e += 64) dst[e] = src[e];
+      if (lane == 0) {
+        a.snap_ver[s * S + fr] = v;
+        a.snap_cnt[s * S + fr] = clients;
+        atomicAdd(a.words, 1u);
+      }
+    }
+  }
+}
+
+__global__ void fill_f32_kernel(float *p, int64_t n, float v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+hipError_t launch_fill_f32(float *p, int64_t n, float v, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, n, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_ada_new_rows(const AdaArgs &a, hipStream_t st) {
+  int64_t blocks = (a.max_rows + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(ada_new_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ada_sort(void *tmp, size_t *bytes, const uint64_t *kin, uint64_t *kout, const int32_t *vin,
+                           int32_t *vout, int n, hipStream_t st) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, *bytes, kin, kout, vin, vout, n, 0, 64, st);
+}
+
+hipError_t launch_ada_init_rows(const AdaArgs &a, const int32_t *slots, const float *deltas, int32_t n,
+                                hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = ((int64_t)n + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(ada_init_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, slots, deltas, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st) {
+  const int64_t tiles = (a.max_rows + 63) / 64;
+  int64_t blocks = (tiles + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  if (a.imp)
+    hipLaunchKernelGGL(ada_apply_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(ada_apply_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t *sizes, int64_t n,
+                           uint64_t clients, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(ada_sent_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, list, sizes, n, clients);
+  return hipGetLastError();
+}
+
+}  // namespace psx

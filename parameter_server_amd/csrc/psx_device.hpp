@@ -24,9 +24,11 @@ enum : uint32_t {
   kStCapacity = 1u << 3,
   kStUnsupported = 1u << 4,
   kStDuplicateRow = 1u << 5,   // a row appears twice in one message: replay on the ordered path
+  kStState = 1u << 6,          // AdaRevision: a record names a (row, version) with no snapshot
 };
 constexpr uint32_t kStFatal = kStMalformed | kStUnknownTable | kStRowRange | kStCapacity |
-                              kStUnsupported;
+                              kStUnsupported | kStState;
+constexpr int kAdaMaxS = 8;     // AdaRevision snapshot slots per row (psx_adarevision_config)
 
 // Table directory passed by value to the decoder.
 struct TableDir {
@@ -81,6 +83,35 @@ struct DenseArgs {
   const uint8_t *zero_chunk;   // >= 2 KiB of zeros, stands in for absent messages
   double *imp;                 // non-null: accumulate NSSumImpCalc importance per slot
   uint64_t *ver;               // non-null: VersionServerRow::version_ per slot (+1 per record)
+};
+
+// AdaRevision server-table logic on one f32 dense table (psx_ada.hip).
+struct AdaArgs {
+  StreamSet ss;
+  const Seg *segs;
+  int t;
+  int B;
+  int64_t stride;              // dense record stride in bytes
+  int64_t cap;                 // row_capacity == dense_row_oplog_capacity
+  int64_t max_rows;
+  float *table;
+  uint8_t *flags;
+  int32_t *inv;
+  int64_t inv_ss, inv_sb;
+  const uint32_t *counters;
+  const uint32_t *sticky;
+  uint32_t *call_status;
+  double *imp;                 // importance tables (SSPAggr)
+  uint64_t *ver;               // version tables
+  float *acc, *z, *zmax;       // AdaRevisionRow per slot [max_rows][cap]
+  int version_records;         // records carry {uint64 version; bool end_of_version}
+  float step;                  // init_step_size_
+  int S;                       // snapshot slots per row (<= kAdaMaxS)
+  uint64_t *snap_ver, *snap_cnt;   // [max_rows][S]; count 0 = free
+  float *snap_acc;             // [max_rows][S][cap]
+  uint32_t *words;             // [0] live snapshots, [1] rows created this call, [2] error bits
+  uint64_t *new_keys;          // rows created this call: (message << 32 | record), slot
+  int32_t *new_slots;
 };
 
 // Fast-path dense tables of one call (for the duplicate-row gate).

@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -36,6 +38,15 @@ hipError_t launch_gather_flags(const uint8_t *flags, const int64_t *slots, int32
 
 hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st, bool rec_f16);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t st);
+hipError_t launch_fill_f32(float *p, int64_t n, float v, hipStream_t st);
+hipError_t launch_ada_new_rows(const AdaArgs &a, hipStream_t st);
+hipError_t launch_ada_sort(void *tmp, size_t *bytes, const uint64_t *kin, uint64_t *kout, const int32_t *vin,
+                           int32_t *vout, int n, hipStream_t st);
+hipError_t launch_ada_init_rows(const AdaArgs &a, const int32_t *slots, const float *deltas, int32_t n,
+                                hipStream_t st);
+hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st);
+hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t *sizes, int64_t n,
+                           uint64_t clients, hipStream_t st);
 hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
 hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st);
 hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
@@ -79,6 +90,21 @@ struct TableState {
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
   double *d_imp = nullptr;         // accum_importance: ServerRow::importance_ per slot
   uint64_t *d_ver = nullptr;       // version_maintain: VersionServerRow::version_ per slot (1 at creation)
+  // AdaRevision server-table logic (psx_table_set_adarevision)
+  bool ada = false;
+  psx_adarevision_config ada_cfg{};
+  float *d_acc = nullptr, *d_z = nullptr, *d_zmax = nullptr;   // AdaRevisionRow [max_rows][row_capacity]
+  uint64_t *d_snap_ver = nullptr, *d_snap_cnt = nullptr;       // old_accum_gradients_ slots [max_rows][S]
+  float *d_snap_acc = nullptr;                                 // [max_rows][S][row_capacity]
+  uint32_t *d_ada_words = nullptr;                             // [0] live snapshots [1] new rows [2] errors
+  uint64_t *d_new_keys = nullptr;                              // [2][max_rows]: unsorted, sorted
+  int32_t *d_new_slots = nullptr;                              // [2][max_rows]
+  void *d_new_tmp = nullptr;
+  size_t new_tmp_bytes = 0;
+  float *d_init = nullptr;                                     // initial deltas of new rows
+  size_t init_cap = 0;
+  std::shared_ptr<std::mt19937> ada_gen;                       // gen_ (adarevision_server_table_logic.cpp:32)
+  std::shared_ptr<std::normal_distribution<float>> ada_dist;   // dist_ (:33)
   // partial push scratch (allocated on first psx_serialize_partial)
   double *d_pkeys[2] = {nullptr, nullptr};
   int32_t *d_pvals[2] = {nullptr, nullptr};
@@ -101,7 +127,8 @@ struct TableState {
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
                   t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_srv_sizes, t.d_srv_offs,
-                  t.d_imp, t.d_ver, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
+                  t.d_imp, t.d_ver, t.d_acc, t.d_z, t.d_zmax, t.d_snap_ver, t.d_snap_cnt, t.d_snap_acc,
+                  t.d_ada_words, t.d_new_keys, t.d_new_slots, t.d_new_tmp, t.d_init, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -126,6 +153,7 @@ struct psx_ctx {
   hipStream_t stream = nullptr;
   std::map<int32_t, int64_t> versions;   // bg_version_map_
   std::vector<TableState> tables;
+  bool has_ada = false;                  // some table runs the AdaRevision logic
   // Per-call state lives in two slots (call k uses slot k & 1) so that the decode/index
   // stage of call k+1 can run on the side stream while call k applies on the main stream.
   psx::Seg *d_segs[2] = {nullptr, nullptr};
@@ -297,6 +325,34 @@ psx_status host_validate(psx_ctx *c, const uint8_t *p, size_t size) {
   return PSX_OK;
 }
 
+// Kernel arguments of the AdaRevision kernels for table t (index ti).
+psx::AdaArgs ada_args(TableState &t, int ti) {
+  psx::AdaArgs a{};
+  a.t = ti;
+  a.stride = t.dense_stride();
+  a.cap = t.cfg.row_capacity;
+  a.max_rows = t.cfg.max_rows;
+  a.table = (float *)t.d_data;
+  a.flags = t.d_flags;
+  a.imp = t.d_imp;
+  a.ver = t.d_ver;
+  a.acc = t.d_acc;
+  a.z = t.d_z;
+  a.zmax = t.d_zmax;
+  a.version_records = t.cfg.version_maintain;
+  a.step = t.ada_cfg.init_step_size;
+  a.S = t.ada_cfg.max_snapshots_per_row;
+  a.snap_ver = t.d_snap_ver;
+  a.snap_cnt = t.d_snap_cnt;
+  a.snap_acc = t.d_snap_acc;
+  a.words = t.d_ada_words;
+  a.new_keys = t.d_new_keys;
+  a.new_slots = t.d_new_slots;
+  return a;
+}
+
+psx_status enqueue_ada(psx_ctx *c, TableState &t, const psx::AdaArgs &a);
+
 bool has_sparse_serialized(const psx_ctx *c) {
   for (auto &t : c->tables)
     if (!t.cfg.oplog_dense_serialized) return true;
@@ -392,8 +448,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     HIP_TRY(c, hipEventRecord(c->ev_ready[slot], prep));
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_ready[slot], 0));
   }
-  // 2) a duplicate row in any fast table turns the whole call into a replay
-  if (fast.n && any_ordered) {
+  // 2) a duplicate row in any fast table turns the whole call into a replay (or, with an
+  //    AdaRevision table in the context, into an error: that logic has no ordered replay)
+  if (fast.n && (any_ordered || c->has_ada)) {
     st = timed(c, "dup_gate", [&] {
       return psx::launch_gate(segs, counters, fast, n, call_st, c->stream);
     });
@@ -441,6 +498,21 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   for (int i = 0; i < fast.n; ++i) {
     const int ti = fast.t[i];
     TableState &t = c->tables[ti];
+    if (t.ada) {
+      psx::AdaArgs aa = ada_args(t, ti);
+      aa.ss = ss;
+      aa.segs = segs;
+      aa.B = n;
+      aa.inv = t.d_inv[slot];
+      aa.inv_ss = layouts[ti].ss;
+      aa.inv_sb = layouts[ti].sb;
+      aa.counters = counters;
+      aa.sticky = sticky;
+      aa.call_status = call_st;
+      st = enqueue_ada(c, t, aa);
+      if (st) return st;
+      continue;
+    }
     psx::DenseArgs a{};
     a.ss = ss;
     a.segs = segs;
@@ -476,10 +548,65 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   return PSX_OK;
 }
 
+// AdaRevision stage of one call for table t: rows the call creates get their
+// ServerRowCreated initial deltas (drawn on the host from the table's generator, in
+// creation order), then every record goes through the logic.  Synchronous when the
+// table draws Gaussian initial rows.
+psx_status enqueue_ada(psx_ctx *c, TableState &t, const psx::AdaArgs &a) {
+  if (t.ada_cfg.gaussian_init) {
+    HIP_TRY(c, hipMemsetAsync(t.d_ada_words + 1, 0, sizeof(uint32_t), c->stream));
+    psx_status st = timed(c, "ada_new_rows", [&] { return psx::launch_ada_new_rows(a, c->stream); });
+    if (st) return st;
+    uint32_t nn = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nn, t.d_ada_words + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (nn) {
+      // CreateRow order = first touch (message, position); each new row takes row_capacity
+      // draws of the one generator (ServerRowCreated, adarevision_server_table_logic.cpp:43-46)
+      const int64_t R = t.cfg.max_rows;
+      size_t tb = t.new_tmp_bytes;
+      HIP_TRY(c, psx::launch_ada_sort(t.d_new_tmp, &tb, t.d_new_keys, t.d_new_keys + R, t.d_new_slots,
+                                      t.d_new_slots + R, (int)nn, c->stream));
+      const size_t need = (size_t)nn * (size_t)t.cfg.row_capacity;
+      std::vector<float> d(need);
+      for (float &x : d) x = (*t.ada_dist)(*t.ada_gen);
+      if (need > t.init_cap) {
+        if (t.d_init) hipFree(t.d_init);
+        t.d_init = nullptr;
+        t.init_cap = 0;
+        HIP_TRY(c, hipMalloc(&t.d_init, need * sizeof(float)));
+        t.init_cap = need;
+      }
+      HIP_TRY(c, hipMemcpyAsync(t.d_init, d.data(), need * sizeof(float), hipMemcpyHostToDevice, c->stream));
+      st = timed(c, "ada_init_rows", [&] {
+        return psx::launch_ada_init_rows(a, t.d_new_slots + R, t.d_init, (int32_t)nn, c->stream);
+      });
+      if (st) return st;
+      HIP_TRY(c, hipStreamSynchronize(c->stream));   // `d` is pageable host memory
+    }
+  }
+  return timed(c, "ada_apply", [&] { return psx::launch_ada_apply(a, c->stream); });
+}
+
+// ServerRowSent for the rows a push just emitted (sizes != 0) or for a list of slots.
+psx_status ada_rows_sent(psx_ctx *c, TableState &t, int ti, const int32_t *list, const int64_t *sizes, int64_t n,
+                         uint64_t clients) {
+  psx::AdaArgs a = ada_args(t, ti);
+  HIP_TRY(c, hipMemsetAsync(t.d_ada_words + 2, 0, sizeof(uint32_t), c->stream));
+  HIP_TRY(c, psx::launch_ada_sent(a, list, sizes, n, clients, c->stream));
+  uint32_t err = 0;
+  HIP_TRY(c, hipMemcpyAsync(&err, t.d_ada_words + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (err) return fail(c, PSX_ERR_CAPACITY, "AdaRevision: a row already holds max_snapshots_per_row live snapshots");
+  return PSX_OK;
+}
+
 psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
   if (sticky & psx::kStUnknownTable) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table id in a device stream");
   if (sticky & psx::kStMalformed) return fail(c, PSX_ERR_MALFORMED, "malformed device stream");
   if (sticky & psx::kStRowRange) return fail(c, PSX_ERR_ROW_RANGE, "row id outside this shard's range");
+  if (sticky & psx::kStState)
+    return fail(c, PSX_ERR_STATE, "AdaRevision: a record names a (row, version) without a snapshot");
   if (sticky & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "row capacity exceeded (column >= row_capacity or sorted/map row over max_entries)");
   if (sticky & psx::kStUnsupported) return fail(c, PSX_ERR_UNSUPPORTED, "table repeated within one message");
   return PSX_OK;
@@ -503,6 +630,14 @@ psx_status sync_impl(psx_ctx *c) {
   c->deferred = PSX_OK;
   if (d != PSX_OK) return d;
   uint32_t replay_sticky = 0;
+  if ((sticky & psx::kStDuplicateRow) && c->has_ada) {
+    // the call with the duplicate and every later one applied nothing, and the AdaRevision
+    // logic has no ordered replay
+    psx_status e = sticky_error(c, sticky & ~psx::kStDuplicateRow);
+    if (e) return e;
+    return fail(c, PSX_ERR_UNSUPPORTED,
+                "a row occurs twice in one message: contexts with an AdaRevision table have no ordered replay");
+  }
   if (sticky & psx::kStDuplicateRow) {
     // A message held a row twice: that call and every later one were skipped.  Replay
     // them, in order, on the ordered path (per-row record order preserved).
@@ -577,6 +712,7 @@ const char *psx_status_string(psx_status s) {
     case PSX_ERR_UNSUPPORTED: return "unsupported";
     case PSX_ERR_SENDER: return "unknown sender";
     case PSX_ERR_NO_DEVICE: return "no HIP device";
+    case PSX_ERR_STATE: return "server logic state missing";
   }
   return "?";
 }
@@ -698,6 +834,8 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     return fail(c, PSX_ERR_UNSUPPORTED, "version_maintain needs dense rows with dense-serialized kDenseRowOpLog records");
   if (f16 && cfg->dtype != PSX_F32)
     return fail(c, PSX_ERR_UNSUPPORTED, "float16 records need f32 rows (dense_row_oplog_float16.hpp:28)");
+  if (c->has_ada && !cfg->oplog_dense_serialized)
+    return fail(c, PSX_ERR_UNSUPPORTED, "contexts with an AdaRevision table take dense-serialized tables only");
   TableState t;
   t.cfg = *cfg;
   if (!f16) t.cfg.row_oplog_type = 0;   // kSparse*RowOpLog: no server-side difference for sparse records
@@ -1073,6 +1211,13 @@ psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, 
     HIP_TRY(c, psx::launch_serve_emit(args[i], c->stream));
   }
   HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
+  for (size_t i = 0; i < T && clear_dirty; ++i) {   // ServerRowSent (server_table.cpp:252-255)
+    TableState &t = c->tables[i];
+    if (!t.ada) continue;
+    psx_status st = ada_rows_sent(c, t, (int)i, nullptr, args[i].sizes, args[i].max_rows,
+                                  (uint64_t)t.ada_cfg.push_clients);
+    if (st) return st;
+  }
   if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return PSX_OK;
@@ -1125,6 +1270,11 @@ psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used
     a.keys = nullptr;
     a.sel = t.d_pvals[1];
     a.nsel = std::min<int64_t>((int64_t)nd, t.cfg.server_push_row_upper_bound);
+    if (t.ada) {   // !AllowSend(): too many live snapshots (adarevision_server_table_logic.cpp:192-197)
+      uint32_t live = 0;
+      HIP_TRY(c, hipMemcpy(&live, t.d_ada_words, sizeof(uint32_t), hipMemcpyDeviceToHost));
+      if ((uint64_t)live >= t.ada_cfg.old_grad_upper_bound) a.nsel = 0;
+    }
     a.lsizes = t.d_lsizes;
     a.loffs = t.d_loffs;
     if (a.nsel > 0) {
@@ -1168,8 +1318,127 @@ psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used
     HIP_TRY(c, psx::launch_serve_emit_list(args[i], c->stream));
   }
   HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
+  for (size_t i = 0; i < T && clear_dirty; ++i) {   // ServerRowSent (server_table.cpp:412-415)
+    TableState &t = c->tables[i];
+    if (!t.ada || args[i].nsel <= 0) continue;
+    psx_status st = ada_rows_sent(c, t, (int)i, args[i].sel, nullptr, args[i].nsel,
+                                  (uint64_t)t.ada_cfg.push_clients);
+    if (st) return st;
+  }
   if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_table_set_adarevision(psx_ctx *c, int32_t table_id, const psx_adarevision_config *cfg) {
+  if (!c || !cfg) return PSX_ERR_INVALID_ARG;
+  TableState *t = find_table(c, table_id);
+  if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
+  if (t->ada) return fail(c, PSX_ERR_INVALID_ARG, "AdaRevision already attached");
+  if (cfg->push_clients < 0 || cfg->max_snapshots_per_row < 0 || cfg->max_snapshots_per_row > psx::kAdaMaxS)
+    return fail(c, PSX_ERR_INVALID_ARG, "bad push_clients / max_snapshots_per_row (1..8, 0 -> 4)");
+  if (t->cfg.row_kind != PSX_ROW_DENSE || t->cfg.dtype != PSX_F32 || !t->cfg.oplog_dense_serialized ||
+      t->rec_f16() || t->cfg.dense_row_oplog_capacity != t->cfg.row_capacity)
+    return fail(c, PSX_ERR_UNSUPPORTED,
+                "AdaRevision needs f32 dense rows with row-wide dense records (adarevision_server_table_logic.cpp:65-68)");
+  for (auto &o : c->tables)
+    if (!o.cfg.oplog_dense_serialized)
+      return fail(c, PSX_ERR_UNSUPPORTED, "contexts with an AdaRevision table take dense-serialized tables only");
+  psx_adarevision_config k = *cfg;
+  if (k.push_clients == 0) k.push_clients = 1;
+  if (k.max_snapshots_per_row == 0) k.max_snapshots_per_row = 4;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const size_t R = (size_t)t->cfg.max_rows, cap = (size_t)t->cfg.row_capacity, S = (size_t)k.max_snapshots_per_row;
+  TableState &x = *t;
+  hipError_t e = hipMalloc(&x.d_acc, R * cap * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&x.d_z, R * cap * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&x.d_zmax, R * cap * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&x.d_snap_ver, R * S * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&x.d_snap_cnt, R * S * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&x.d_snap_acc, R * S * cap * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&x.d_ada_words, 4 * sizeof(uint32_t));
+  // AdaRevisionRow(row_size): accum 0, z 1, z_max 1 (adarevision_server_table_logic.hpp:12-16)
+  if (e == hipSuccess) e = hipMemsetAsync(x.d_acc, 0, R * cap * sizeof(float), c->stream);
+  if (e == hipSuccess) e = psx::launch_fill_f32(x.d_z, (int64_t)(R * cap), 1.0f, c->stream);
+  if (e == hipSuccess) e = psx::launch_fill_f32(x.d_zmax, (int64_t)(R * cap), 1.0f, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(x.d_snap_cnt, 0, R * S * sizeof(uint64_t), c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(x.d_ada_words, 0, 4 * sizeof(uint32_t), c->stream);
+  if (e == hipSuccess && k.gaussian_init) {
+    e = hipMalloc(&x.d_new_keys, 2 * R * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&x.d_new_slots, 2 * R * sizeof(int32_t));
+    size_t tb = 0;
+    if (e == hipSuccess)
+      e = psx::launch_ada_sort(nullptr, &tb, x.d_new_keys, x.d_new_keys + R, x.d_new_slots, x.d_new_slots + R,
+                               (int)R, c->stream);
+    if (e == hipSuccess) e = hipMalloc(&x.d_new_tmp, tb ? tb : 1);
+    x.new_tmp_bytes = tb;
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "AdaRevision state allocation");
+  x.ada_gen = std::make_shared<std::mt19937>(12345);                          // :32
+  x.ada_dist = std::make_shared<std::normal_distribution<float>>(0.0f, 0.1f);  // :33
+  x.ada_cfg = k;
+  x.ada = true;
+  c->has_ada = true;
+  return PSX_OK;
+}
+
+psx_status psx_row_sent(psx_ctx *c, int32_t table_id, const int32_t *row_ids, int32_t n, int32_t num_clients) {
+  if (!c || n < 0 || (n && !row_ids) || num_clients <= 0) return PSX_ERR_INVALID_ARG;
+  int ti = 0;
+  TableState *t = find_table(c, table_id, &ti);
+  if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
+  if (n == 0) return PSX_OK;
+  std::vector<int32_t> slots(n);
+  std::vector<int64_t> slots64(n);
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t s = slot_of(*t, row_ids[i]);
+    if (s < 0) return fail(c, PSX_ERR_ROW_RANGE, "row " + std::to_string(row_ids[i]) + " not owned by this shard");
+    slots[i] = (int32_t)s;
+    slots64[i] = s;
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // the replied rows exist (the request path creates them, server.cpp:107-118)
+  std::vector<uint8_t> flags(n);
+  for (int32_t i = 0; i < n; ++i)
+    HIP_TRY(c, hipMemcpyAsync(&flags[i], t->d_flags + slots64[i], 1, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int32_t i = 0; i < n; ++i)
+    if (!(flags[i] & 1)) return fail(c, PSX_ERR_INVALID_ARG, "row " + std::to_string(row_ids[i]) + " does not exist");
+  if (!t->ada) return PSX_OK;   // ServerTable::RowSent: only a logic reacts (server_table.cpp:191-195)
+  int32_t *d = nullptr;
+  HIP_TRY(c, hipMalloc(&d, sizeof(int32_t) * n));
+  hipError_t e = hipMemcpyAsync(d, slots.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
+  psx_status st = e == hipSuccess ? ada_rows_sent(c, *t, ti, d, nullptr, n, (uint64_t)num_clients)
+                                  : hip_fail(c, e, "row_sent upload");
+  hipStreamSynchronize(c->stream);
+  hipFree(d);
+  return st;
+}
+
+psx_status psx_adarevision_state(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows, float *accum,
+                                 float *z, float *z_max, uint64_t *live_snapshots) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  if (!t->ada) return fail(c, PSX_ERR_INVALID_ARG, "table has no AdaRevision logic");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->side));
+  const size_t cap = (size_t)t->cfg.row_capacity, nb = (size_t)num_rows * cap * sizeof(float);
+  const size_t off = (size_t)s * cap;
+  if (accum && nb) HIP_TRY(c, hipMemcpyAsync(accum, t->d_acc + off, nb, hipMemcpyDeviceToHost, c->stream));
+  if (z && nb) HIP_TRY(c, hipMemcpyAsync(z, t->d_z + off, nb, hipMemcpyDeviceToHost, c->stream));
+  if (z_max && nb) HIP_TRY(c, hipMemcpyAsync(z_max, t->d_zmax + off, nb, hipMemcpyDeviceToHost, c->stream));
+  uint32_t live = 0;
+  HIP_TRY(c, hipMemcpyAsync(&live, t->d_ada_words, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (live_snapshots) *live_snapshots = live;
   return PSX_OK;
 }
 

@@ -163,6 +163,31 @@ class Server:
             self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(out.ctypes.data)))
         return out
 
+    def set_adarevision(self, table_id, init_step_size=0.1, gaussian_init=True, old_grad_upper_bound=10000,
+                        push_clients=1, max_snapshots_per_row=4):
+        """Attach AdaRevisionServerTableLogic to a table (adarevision_server_table_logic.cpp:19-36;
+        defaults are its gflags, :8-10)."""
+        cfg = _abi.psx_adarevision_config(float(init_step_size), int(bool(gaussian_init)),
+                                          int(old_grad_upper_bound), int(push_clients),
+                                          int(max_snapshots_per_row))
+        _check(self._L, self._ctx, self._L.psx_table_set_adarevision(self._ctx, table_id, ctypes.byref(cfg)))
+
+    def row_sent(self, table_id, row_ids, num_clients):
+        """Server::RowSent -> ServerRowSent (server.cpp:436-441)."""
+        ids = np.ascontiguousarray(row_ids, dtype=np.int32)
+        _check(self._L, self._ctx, self._L.psx_row_sent(self._ctx, table_id, ctypes.c_void_p(ids.ctypes.data),
+                                                          int(ids.size), int(num_clients)))
+
+    def adarevision_state(self, table_id, first_row, num_rows):
+        """(accum_gradients, z, z_max) [num_rows, row_capacity] f32 and the live snapshot count."""
+        cap = self.tables[table_id].row_capacity
+        acc, z, zm = (np.zeros((num_rows, cap), np.float32) for _ in range(3))
+        live = ctypes.c_uint64(0)
+        _check(self._L, self._ctx, self._L.psx_adarevision_state(
+            self._ctx, table_id, first_row, num_rows, ctypes.c_void_p(acc.ctypes.data),
+            ctypes.c_void_p(z.ctypes.data), ctypes.c_void_p(zm.ctypes.data), ctypes.byref(live)))
+        return acc, z, zm, int(live.value)
+
     def clear_dirty(self, table_id):
         _check(self._L, self._ctx, self._L.psx_clear_dirty(self._ctx, table_id))
 

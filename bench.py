@@ -50,6 +50,9 @@ def parse():
                    help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows; "
                         "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange")
     p.add_argument("--c4-rows", type=int, default=10_000_000, help="C4 total rows (all shards)")
+    p.add_argument("--adarevision", action="store_true",
+                   help="C2 through the AdaRevision server-table logic (adarevision_server_table_logic.cpp): "
+                        "per element the adaptive step on accum/z/z_max state beside every row")
     p.add_argument("--importance", action="store_true",
                    help="C2 with importance accumulation (SSPAggr RelativeMagnitude tables)")
     p.add_argument("--pcie", action="store_true",
@@ -85,13 +88,15 @@ def cpu_baseline(args):
         for t in range(nthreads):
             o = OracleServer(bgs)
             o.create_table(1, DENSE, F32, cap)
+            if args.adarevision:
+                assert o.set_adarevision(1, init_step_size=0.1, gaussian_init=False) == 0
             o.load_dense_rows(1, t, init[t::nthreads], stride=nthreads)
             msgs = []
             for b in range(B):
                 m = (perms[b] % nthreads) == t
                 msgs.append(wire.dense_stream_np(1, perms[b][m], upds[b][m]))
             shards.append((o, msgs))
-        step_bytes = sum(m.size for _, ms in shards for m in ms) + 2 * rows * cap * 4
+        step_bytes = sum(m.size for _, ms in shards for m in ms) + (8 if args.adarevision else 2) * rows * cap * 4
 
         def one(t, ver):
             o, msgs = shards[t]
@@ -448,6 +453,8 @@ def main():
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
                                      row_offset=base, max_rows=rows, accum_importance=args.importance,
                                      row_oplog_type=3 if args.f16_records else 0))
+    if args.adarevision:
+        srv.set_adarevision(1, init_step_size=0.1, gaussian_init=False)
     srv.load_rows(1, base, None, on_device_ptr=table0.data_ptr(), num_rows=rows)
     del table0
     torch.cuda.empty_cache()
@@ -476,8 +483,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     srv.sync()
+    apply_kernel = "ada_apply" if args.adarevision else "dense_apply"
     kernels = {k: srv.timing_read(k) for k in ("decode_streams", "dense_index", "dense_verify",
-                                               "dense_apply", "finish_call")}
+                                               apply_kernel, "finish_call")}
     srv.timing(False)
 
     if world > 1:
@@ -486,15 +494,17 @@ def main():
         elapsed = float(t.item())
 
     stream_bytes = sum(s.numel() for s in streams)
-    step_bytes = stream_bytes + 2 * rows * cap * 4            # per GPU
+    # per GPU: streams + row read/write (+ accum, z, z_max read/write for AdaRevision)
+    step_bytes = stream_bytes + (8 if args.adarevision else 2) * rows * cap * 4
     total_bytes = step_bytes * args.steps * world
     value = total_bytes / elapsed / 1e9
 
-    apply_ms, apply_n = kernels["dense_apply"]
+    apply_ms, apply_n = kernels[apply_kernel]
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
     traffic = None
-    default_cfg = (rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
+    default_cfg = ((rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
+                   and not args.adarevision)
     if default_cfg and args.pmc_json and os.path.exists(args.pmc_json):
         traffic = json.load(open(args.pmc_json)).get("dense_apply_hbm_bytes_per_launch")
 
@@ -505,7 +515,8 @@ def main():
             cpu = cpu_baseline(args)
         line = {
             "metric": "row-update apply GB/s (device-resident), dense float rows"
-                      + (", float16 records" if args.f16_records else ""),
+                      + (", float16 records" if args.f16_records else "")
+                      + (", AdaRevision server logic" if args.adarevision else ""),
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -524,11 +535,12 @@ def main():
                 "algorithmic_bytes_per_step_per_gpu": step_bytes,
                 "parallelism": f"row-range shards x{world}, no collective",
                 "importance": bool(args.importance),
+                "server_table_logic": "AdaRevision" if args.adarevision else None,
                 "record_format": "float16 (row_oplog_type 3)" if args.f16_records else "V[cap] (DenseRowOpLog)",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "dense_apply",
+                "kernel": apply_kernel,
                 "achieved": round(achieved, 2) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -216,6 +216,147 @@ __global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
   }
 }
 
+// ApplyRowOpLog for every record of the call, with the row and its AdaRevisionRow state
+// held in registers across the call's records: per touched row, a scalar pre-pass
+// resolves each record (payload, snapshot, end_of_version release) in message order into
+// a per-wave LDS list; then per chunk of 64*EPL elements the row, accum, z, z_max are
+// loaded once, every listed record's step runs in message order, and the four arrays are
+// stored once.  VEC: EPL = 4 contiguous elements per lane through 16-B accesses
+// (row_capacity % 4 == 0; records are only byte-aligned behind version trailers: gfx950
+// runs with unaligned access enabled).
+template <bool IMP, bool VEC>
+__global__ void __launch_bounds__(256) ada_apply_v2_kernel(AdaArgs a) {
+  constexpr int EPL = VEC ? 4 : 1;
+  __shared__ int32_t s_idx[4][kMaxFused][64];   // the tile's inverse-index entries
+  __shared__ const uint8_t *s_rec[4][kMaxFused];
+  __shared__ const float *s_old[4][kMaxFused];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + w;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const bool skip = !ada_go(a);
+  const int S = a.S;
+  const float step = a.step;
+  const int64_t ntiles = (a.max_rows + 63) / 64;
+  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
+    const int64_t my = tile * 64 + lane;
+    const bool mine = my < a.max_rows;
+    bool touched = false;
+    uint64_t nrec = 0;
+    for (int b = 0; b < a.B; ++b) {
+      int32_t v = -1;
+      if (mine) {
+        int32_t *p = a.inv + my * a.inv_ss + b * a.inv_sb;
+        v = *p;
+        if (v >= 0) {
+          touched = true;
+          ++nrec;
+          *p = -1;
+        }
+      }
+      s_idx[w][b][lane] = v;
+    }
+    if (skip) continue;
+    if (touched) {
+      a.flags[my] = 3;
+      if (a.ver) a.ver[my] += nrec;
+    }
+    uint64_t live = __ballot(touched);
+    while (live) {
+      const int k = __builtin_ctzll(live);
+      live &= live - 1;
+      const int64_t s = tile * 64 + k;
+      bool snap_dirty = false;
+      // the row's snapshot slots, slot q in lane q
+      const bool qlane = lane < S;
+      const uint64_t sv = qlane ? a.snap_ver[s * S + lane] : 0;
+      uint64_t sc = qlane ? a.snap_cnt[s * S + lane] : 0;
+      int nb = 0;
+      for (int b = 0; b < a.B; ++b) {
+        const int32_t i = __builtin_amdgcn_readfirstlane(s_idx[w][b][k]);
+        if (i < 0) continue;
+        const Seg sg = a.segs[b * kMaxTables + a.t];
+        const uint8_t *rec = a.ss.data[b] + sg.rec0 + 4 + (int64_t)i * a.stride;
+        const float *old = nullptr;
+        if (a.version_records) {
+          const uint64_t rv = ld_u64(rec + a.cap * 4);
+          const bool eov = rec[a.cap * 4 + 8] != 0;
+          if (rv) {
+            const uint64_t hit = __ballot(qlane && sc != 0 && sv == rv);
+            if (!hit) {
+              if (lane == 0) atomicOr(a.call_status, kStState);
+              continue;
+            }
+            const int q0 = __builtin_ctzll(hit);
+            old = a.snap_acc + (s * S + q0) * a.cap;
+            if (eov) {
+              if (lane == q0) {
+                sc -= 1;
+                if (sc == 0) atomicSub(a.words, 1u);
+              }
+              snap_dirty = true;
+            }
+          }
+        }
+        s_rec[w][nb] = rec;   // every lane stores the same (wave-uniform) entry
+        s_old[w][nb] = old;
+        ++nb;
+      }
+      float *row = a.table + s * a.cap;
+      float *acc = a.acc + s * a.cap, *z = a.z + s * a.cap, *zmax = a.zmax + s * a.cap;
+      double impt = IMP ? a.imp[s] : 0.0;
+      for (int64_t e = (int64_t)lane * EPL; e < a.cap; e += 64 * EPL) {
+        float x[EPL], ac[EPL], zz[EPL], zm[EPL], eta[EPL];
+        __builtin_memcpy(x, row + e, 4 * EPL);
+        __builtin_memcpy(ac, acc + e, 4 * EPL);
+        __builtin_memcpy(zz, z + e, 4 * EPL);
+        __builtin_memcpy(zm, zmax + e, 4 * EPL);
+        // step/sqrt(z_max) of the current z_max: a record's eta_old is the previous
+        // record's eta (same operands, same correctly rounded result)
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) eta[j] = step / sqrtf(zm[j]);
+#pragma unroll 2
+        for (int r = 0; r < nb; ++r) {
+          const uint8_t *rec = s_rec[w][r];
+          const float *op = s_old[w][r];
+          float u[EPL], old[EPL];
+          __builtin_memcpy(u, rec + e * 4, 4 * EPL);
+          if (op) {
+            __builtin_memcpy(old, op + e, 4 * EPL);
+          } else {
+#pragma unroll
+            for (int j = 0; j < EPL; ++j) old[j] = 0.0f;
+          }
+          double p = 0.0;   // NSSumImpCalc terms of this record's chunk
+#pragma unroll
+          for (int j = 0; j < EPL; ++j) {
+            const float g_bck = ac[j] - old[j];
+            const float eta_old = eta[j];
+            zz[j] = zz[j] + u[j] * (u[j] + 2.0f * g_bck);
+            if (!(zz[j] < zm[j])) {   // z_max grows: a new step size
+              zm[j] = zz[j];
+              eta[j] = step / sqrtf(zm[j]);
+            }
+            const float d = -(eta[j] * u[j]) + (eta_old - eta[j]) * g_bck;
+            ac[j] = ac[j] + u[j];
+            if constexpr (IMP) p += imp_term<float>(x[j], d);
+            x[j] = x[j] + d;
+          }
+          if constexpr (IMP) impt += wave_sum_f64(p);
+        }
+        __builtin_memcpy(row + e, x, 4 * EPL);
+        __builtin_memcpy(acc + e, ac, 4 * EPL);
+        __builtin_memcpy(z + e, zz, 4 * EPL);
+        __builtin_memcpy(zmax + e, zm, 4 * EPL);
+      }
+      if (IMP && lane == 0) a.imp[s] = impt;
+      if (snap_dirty && qlane) a.snap_cnt[s * S + lane] = sc;
+    }
+  }
+}
+
+int g_ada_variant = 1;   // 0: per-record kernel, 1: register-resident state (default)
+
 // ServerRowSent (:177-190) for the rows in `list` (n entries) or, with list == nullptr,
 // for every slot s < n whose serve-back size is non-zero (the rows a push just sent).
 __global__ void __launch_bounds__(256) ada_sent_kernel(AdaArgs a, const int32_t *list, const int64_t *sizes,
@@ -294,6 +435,18 @@ hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st) {
   int64_t blocks = (tiles + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
+  if (g_ada_variant == 1) {
+    const bool vec = a.cap % 4 == 0;
+    if (a.imp && vec)
+      hipLaunchKernelGGL((ada_apply_v2_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else if (a.imp)
+      hipLaunchKernelGGL((ada_apply_v2_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else if (vec)
+      hipLaunchKernelGGL((ada_apply_v2_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((ada_apply_v2_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.imp)
     hipLaunchKernelGGL(ada_apply_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else

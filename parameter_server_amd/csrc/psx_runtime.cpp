@@ -1566,13 +1566,15 @@ namespace psx {
 extern int g_index_variant;
 extern int g_apply_variant;
 extern int g_inv_layout;
+extern int g_ada_variant;
 extern int g_imp_pair;
 }  // namespace psx
 
 extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
   int *v = which == PSX_VARIANT_DENSE_INDEX ? &psx::g_index_variant
            : which == PSX_VARIANT_DENSE_APPLY ? &psx::g_apply_variant
-           : which == PSX_VARIANT_INV_LAYOUT ? &psx::g_inv_layout : nullptr;
+           : which == PSX_VARIANT_INV_LAYOUT ? &psx::g_inv_layout
+           : which == PSX_VARIANT_ADA_APPLY ? &psx::g_ada_variant : nullptr;
   if (!v) return -1;
   int old = *v;
   *v = variant;
@@ -1583,6 +1585,7 @@ extern "C" int32_t psx_debug_get_variant(int32_t which) {
   if (which == PSX_VARIANT_DENSE_INDEX) return psx::g_index_variant;
   if (which == PSX_VARIANT_DENSE_APPLY) return psx::g_apply_variant;
   if (which == PSX_VARIANT_INV_LAYOUT) return psx::g_inv_layout;
+  if (which == PSX_VARIANT_ADA_APPLY) return psx::g_ada_variant;
   return -1;
 }
 
@@ -1594,6 +1597,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_INDEX_VARIANT")) psx::g_index_variant = atoi(v);
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_INV_LAYOUT")) psx::g_inv_layout = atoi(v);
+    if (const char *v = getenv("PSX_ADA_VARIANT")) psx::g_ada_variant = atoi(v);
     if (const char *v = getenv("PSX_IMP_PAIR")) psx::g_imp_pair = atoi(v);
   }
 } variant_env;

@@ -49,7 +49,18 @@ def _apply(srv, orc, streams, bgs, vers):
         assert orc.apply_stream(s, bg, v) == 0
 
 
-def _check(srv, orc, rows):
+@pytest.fixture(params=[1, 0], ids=["regstate", "perrecord"])
+def ada_variant(request):
+    """Both apply kernels: 1 = state held in registers across a call's records
+    (default), 0 = one pass over the row per record."""
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    old = L.psx_debug_set_variant(3, request.param)
+    yield request.param
+    L.psx_debug_set_variant(3, old)
+
+
+def _check(srv, orc, rows, importance=False):
     u32 = np.uint32
     flags = srv.row_flags(1, 0, rows)
     live = np.nonzero(flags & 1)[0]
@@ -63,6 +74,11 @@ def _check(srv, orc, rows):
         for got, w in zip((acc[r], z[r], zm[r]), want):
             assert np.array_equal(got.view(u32), w.view(u32)), r
     assert nsnap == orc.ada_num_snapshots(1)
+    if importance:
+        # f64 importance: lane-parallel partial sums, rel <= 1e-12 of the element-order sum
+        got_i = srv.row_importance(1, 0, rows)
+        want_i = np.array([orc.importance(1, r) if r in live else 0.0 for r in range(rows)])
+        assert np.allclose(got_i, want_i, rtol=1e-12, atol=0)
     got_v = srv.row_versions(1, 0, rows)
     assert np.array_equal(got_v, np.array([orc.row_version(1, r) for r in range(rows)], np.uint64))
     return got_v
@@ -94,11 +110,12 @@ class _Snapshots:
 
 
 @pytest.mark.parametrize("gaussian", [False, True])
-@pytest.mark.parametrize("B", [1, 4])
+@pytest.mark.parametrize("B", [1, 4, 16])
 @pytest.mark.parametrize("importance", [False, True])
-def test_adarevision_rounds_match_checker(gaussian, B, importance):
-    rng = np.random.RandomState(7 + 2 * B + gaussian + 4 * importance)
-    rows, cap = 300, 70                      # cap % 64 != 0: ragged element tail per wave
+@pytest.mark.parametrize("cap", [70, 260])   # scalar / 16-B paths, ragged element tails
+def test_adarevision_rounds_match_checker(gaussian, B, importance, cap, ada_variant):
+    rng = np.random.RandomState(7 + 2 * B + gaussian + 4 * importance + cap)
+    rows = 300
     bgs = list(range(10, 10 + B))
     srv, orc = _pair(rows, cap, bgs, step=0.05, gaussian=gaussian, clients=2, importance=importance)
     model = _Snapshots(2)
@@ -112,16 +129,16 @@ def test_adarevision_rounds_match_checker(gaussian, B, importance):
                 1, ids, rng.normal(0, 1, (n, cap)).astype(np.float32),
                 versions=np.array([v for v, _ in vv], np.uint64), end_of_version=[e for _, e in vv]))
         _apply(srv, orc, streams, bgs, [rnd] * B)
-        versions = _check(srv, orc, rows)
+        versions = _check(srv, orc, rows, importance)
         got = srv.serialize_dirty(clear=True)
         want = orc.serialize_dirty([1], clear=True)
         assert bytes(got) == bytes(want)
         model.pushed(got, versions)
-        _check(srv, orc, rows)
+        _check(srv, orc, rows, importance)
         assert srv.adarevision_state(1, 0, 1)[3] == len(model.live)
 
 
-def test_adarevision_plain_records():
+def test_adarevision_plain_records(ada_variant):
     """A table without version_maintain: records carry no version (every record is
     version 0, server_table.cpp:527-535) and the push snapshots under version 0."""
     rng = np.random.RandomState(5)
@@ -138,7 +155,7 @@ def test_adarevision_plain_records():
         _check(srv, orc, rows)
 
 
-def test_adarevision_allow_send_and_row_sent():
+def test_adarevision_allow_send_and_row_sent(ada_variant):
     rng = np.random.RandomState(9)
     rows, cap = 100, 33
     srv, orc = _pair(rows, cap, [1], upper=5, clients=1, gaussian=False)
@@ -162,7 +179,7 @@ def test_adarevision_allow_send_and_row_sent():
     _check(srv, orc, rows)
 
 
-def test_adarevision_missing_snapshot_is_state_error():
+def test_adarevision_missing_snapshot_is_state_error(ada_variant):
     srv, orc = _pair(50, 16, [1], gaussian=False)
     s = wire.dense_variant_stream_np(1, np.array([2], np.int32), np.ones((1, 16), np.float32),
                                      versions=np.array([7], np.uint64))

@@ -243,6 +243,10 @@ __device__ __forceinline__ uint32_t half_to_f32_bits(uint32_t h) {
   return nan ? (((h & 0x8000u) << 16) | 0x7f800000u | ((h & 0x3ffu) << 13)) : hw;
 }
 
+__device__ __forceinline__ uint32_t half_to_f32_bits_hw(uint32_t h) {
+  return __builtin_bit_cast(uint32_t, (float)__builtin_bit_cast(_Float16, (uint16_t)h));
+}
+
 // Butterfly sum over the 64 lanes of a wave; every lane receives the total.
 __device__ __forceinline__ double wave_sum_f64(double x) {
 #pragma unroll

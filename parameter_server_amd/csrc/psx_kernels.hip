@@ -462,7 +462,7 @@ __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { __builtin_memcpy(
 
 // Four binary16 record values (8 bytes, 2-byte aligned) -> four f32 bit patterns.
 typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
-template <bool NT>
+template <bool NT, bool HWNAN = false>
 __device__ __forceinline__ u32x4 load_h4(const uint8_t *p) {
   uint32_t w0, w1;
   if constexpr (NT) {
@@ -473,6 +473,9 @@ __device__ __forceinline__ u32x4 load_h4(const uint8_t *p) {
     __builtin_memcpy(&w0, p, 4);
     __builtin_memcpy(&w1, p + 4, 4);
   }
+  if constexpr (HWNAN)   // the hardware conversion alone: NaNs come out quieted
+    return u32x4{half_to_f32_bits_hw(w0 & 0xffffu), half_to_f32_bits_hw(w0 >> 16),
+                 half_to_f32_bits_hw(w1 & 0xffffu), half_to_f32_bits_hw(w1 >> 16)};
   return u32x4{half_to_f32_bits(w0 & 0xffffu), half_to_f32_bits(w0 >> 16), half_to_f32_bits(w1 & 0xffffu),
                half_to_f32_bits(w1 >> 16)};
 }
@@ -542,9 +545,10 @@ __device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
 // all of a row's terms of one call share one f64 accumulator (non-negative terms: within
 // (cap*B-1)*2^-53 relative of the reference's record-by-record sum).
 // H16 (f32 tables with kDenseRowOpLogFloat16 records): record payloads are binary16, so a
-// lane's 4 elements come from one 8-byte load and are decompressed before the add.
+// lane's 4 elements come from one 8-byte load and are decompressed before the add
+// (1: NaN payloads kept unquieted as the oracle restates it; 2: hardware conversion only).
 // STNT: the updated table row is written with non-temporal stores (rows 16-byte aligned).
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, bool H16 = false, bool STNT = false>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0, bool STNT = false>
 __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;        // elements per 16-byte lane vector
@@ -647,7 +651,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           for (int b = 0; b < BMAX; ++b) {
             if constexpr (H16) {
               const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * 2 : a.zero_chunk + lane * 8;
-              u[q][b] = full ? load_h4<NT>(src) : u32x4{0, 0, 0, 0};
+              u[q][b] = full ? load_h4<NT, H16 == 2>(src) : u32x4{0, 0, 0, 0};
             } else {
               const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * VS : a.zero_chunk + lane * 16;
               u[q][b] = full ? load16<NT>(src) : u32x4{0, 0, 0, 0};
@@ -688,7 +692,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
                 if constexpr (H16) {
                   uint16_t h;
                   __builtin_memcpy(&h, rp[q][b] + e * 2, 2);
-                  u = __builtin_bit_cast(V, half_to_f32_bits(h));
+                  u = __builtin_bit_cast(V, H16 == 2 ? half_to_f32_bits_hw(h) : half_to_f32_bits(h));
                 } else {
                   u = Elem<V>::load_rec(rp[q][b] + e * VS);
                 }
@@ -701,6 +705,206 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
       }
       if constexpr (IMP) {
         // ServerRow::AccumImportance (server_row.hpp:56-62,124-126)
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          const double tot = imp0[q] + wave_sum_f64(ib[q]);
+          if (has[q] && lane == 0) a.imp[s0 + ks[q]] = tot;
+        }
+      }
+    }
+  }
+}
+
+// dense_apply_v3: dense_apply_v2 with the record addresses kept as one wave-uniform
+// SGPR base per message (its first record's payload) plus a 32-bit per-lane VGPR offset,
+// so the loads are global_load_dwordx4 v, v_off, s[base] (saddr form).  v2 keeps
+// PAIR x BMAX uniform 64-bit record pointers, which overflow the SGPR file and spill to
+// VGPR lanes (~500 v_readlane/v_writelane per row pair).  Streams must be < 4 GiB.
+typedef const uint8_t __attribute__((address_space(1))) *gbyte_p;
+typedef const u32x4_a4 __attribute__((address_space(1))) *gu32x4_p;
+typedef uint32_t u32x2_a2g __attribute__((ext_vector_type(2), aligned(2)));
+typedef const u32x2_a2g __attribute__((address_space(1))) *gu32x2_p;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 gload16(const uint8_t *base, uint32_t off) {
+  const gu32x4_p p = (gu32x4_p)((gbyte_p)base + off);
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <bool NT, bool HWNAN>
+__device__ __forceinline__ u32x4 gload_h4(const uint8_t *base, uint32_t off) {
+  const gu32x2_p p = (gu32x2_p)((gbyte_p)base + off);
+  u32x2_a2g v;
+  if constexpr (NT) v = __builtin_nontemporal_load(p);
+  else v = *p;
+  const uint32_t w0 = v[0], w1 = v[1];
+  if constexpr (HWNAN)
+    return u32x4{half_to_f32_bits_hw(w0 & 0xffffu), half_to_f32_bits_hw(w0 >> 16),
+                 half_to_f32_bits_hw(w1 & 0xffffu), half_to_f32_bits_hw(w1 >> 16)};
+  return u32x4{half_to_f32_bits(w0 & 0xffffu), half_to_f32_bits(w0 >> 16), half_to_f32_bits(w1 & 0xffffu),
+               half_to_f32_bits(w1 >> 16)};
+}
+
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0>
+__global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
+  static_assert(PAIR * BMAX <= 32, "presence mask is 32 bits");
+  constexpr int VS = (int)sizeof(V);
+  constexpr int EPV = 16 / VS;
+  constexpr int CHUNK = 64 * EPV;
+  constexpr int RB = H16 ? 2 : VS;    // record bytes per element
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int B = a.B;
+
+  bool skip = (*a.call_status & kStFatal) != 0 || (*a.sticky & kStDuplicateRow) != 0;
+  bool dup = false;
+  const uint8_t *pay0[BMAX];
+  uint32_t real = 0;   // bit b: message b holds this table
+#pragma unroll
+  for (int b = 0; b < BMAX; ++b) {
+    pay0[b] = a.zero_chunk;
+    if (b < B) {
+      const Seg sg = a.segs[b * kMaxTables + a.t];
+      if (sg.rec0 >= 0 && !sg.sparse) {
+        pay0[b] = a.ss.data[b] + sg.rec0 + 4;
+        real |= 1u << b;
+        if (a.counters[a.t * kMaxFused + b] != (uint32_t)sg.num_rows) dup = true;
+      }
+    }
+  }
+  if (dup && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.call_status, kStDuplicateRow);
+  skip = skip || dup;
+
+  const int64_t vec_elems = (a.cap / EPV) * EPV;
+  const int64_t row_bytes = a.row_cap * VS;
+  const uint32_t stride = (uint32_t)a.stride;
+  const uint32_t lane_off = (uint32_t)(lane * EPV * RB);
+  uint8_t *table = reinterpret_cast<uint8_t *>(a.table);
+  const int64_t ntiles = (a.max_rows + TILE - 1) / TILE;
+
+  for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
+    const int64_t s0 = tile * TILE;
+    const int64_t my_slot = s0 + lane;
+    const bool mine = lane < TILE && my_slot < a.max_rows;
+    int32_t idx[BMAX];
+    bool touched = false;
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) {
+      idx[b] = -1;
+      if (b < B && mine) {
+        idx[b] = a.inv[my_slot * a.inv_ss + b * a.inv_sb];
+        if (idx[b] >= 0) {
+          touched = true;
+          a.inv[my_slot * a.inv_ss + b * a.inv_sb] = -1;
+        }
+      }
+    }
+    if (skip) continue;
+    if (touched) {
+      a.flags[my_slot] = 3;
+      if (a.ver) {
+        uint64_t n = 0;
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) n += idx[b] >= 0 ? 1u : 0u;
+        a.ver[my_slot] += n;
+      }
+    }
+    uint64_t live = __ballot(touched);
+
+    while (live) {
+      int ks[PAIR];
+      bool has[PAIR];
+#pragma unroll
+      for (int q = 0; q < PAIR; ++q) {
+        has[q] = live != 0;
+        ks[q] = has[q] ? __builtin_ctzll(live) : 0;
+        if (has[q]) live &= live - 1;
+      }
+      uint32_t presm = 0;
+      uint32_t voff[PAIR][BMAX];   // per-lane byte offset of the lane's first element
+      uint8_t *trow[PAIR];
+#pragma unroll
+      for (int q = 0; q < PAIR; ++q) {
+        trow[q] = table + (s0 + ks[q]) * row_bytes;
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) {
+          const int32_t i = __builtin_amdgcn_readlane(idx[b], ks[q]);
+          if (has[q] && ((real >> b) & 1u) && i >= 0) presm |= 1u << (q * BMAX + b);
+          voff[q][b] = (uint32_t)i * stride + lane_off;
+        }
+      }
+      double ib[IMP ? PAIR : 1], imp0[IMP ? PAIR : 1];
+#pragma unroll
+      for (int q = 0; q < (IMP ? PAIR : 1); ++q) {
+        ib[q] = 0.0;
+        if constexpr (IMP) imp0[q] = has[q] ? a.imp[s0 + ks[q]] : 0.0;
+      }
+      for (int64_t c0 = 0; c0 < vec_elems; c0 += CHUNK) {
+        const int64_t e0 = c0 + (int64_t)lane * EPV;
+        const bool full = e0 < vec_elems;
+        const uint32_t coff = (uint32_t)(c0 * RB);
+        // Branch-free loads (no exec-mask saves): every address is in bounds — a lane
+        // past the row's vector part reads element 0, an absent record reads the
+        // message's first record (or the zero chunk) — and absent values are never added.
+        const int64_t te = full ? e0 : 0;
+        u32x4 t[PAIR];
+        u32x4 u[PAIR][BMAX];
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          t[q] = load16<false>(trow[q] + te * VS);
+#pragma unroll
+          for (int b = 0; b < BMAX; ++b) {
+            const bool pr = (presm >> (q * BMAX + b)) & 1u;
+            const uint32_t off = full ? (pr ? voff[q][b] : lane_off) + coff : 0u;
+            if constexpr (H16)
+              u[q][b] = gload_h4<NT, H16 == 2>(pay0[b], off);
+            else
+              u[q][b] = gload16<NT>(pay0[b], off);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          u32x4 acc = t[q];
+#pragma unroll
+          for (int b = 0; b < BMAX; ++b)
+            if ((presm >> (q * BMAX + b)) & 1u) {
+              if constexpr (IMP) {
+                if (full) ib[q] += vec_imp<V>(acc, u[q][b]);
+              }
+              acc = Vec<V>::add(acc, u[q][b]);
+            }
+          if (full && has[q]) store16(trow[q] + e0 * VS, acc);
+        }
+      }
+      const int64_t tail = a.cap - vec_elems;
+      if (tail) {
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          if (has[q] && lane < tail) {
+            const int64_t e = vec_elems + lane;
+            V acc = *reinterpret_cast<const V *>(trow[q] + e * VS);
+#pragma unroll
+            for (int b = 0; b < BMAX; ++b)
+              if ((presm >> (q * BMAX + b)) & 1u) {
+                const uint8_t *rec = pay0[b] + (int64_t)__builtin_amdgcn_readlane(idx[b], ks[q]) * a.stride;
+                V u;
+                if constexpr (H16) {
+                  uint16_t h;
+                  __builtin_memcpy(&h, rec + e * 2, 2);
+                  u = __builtin_bit_cast(V, H16 == 2 ? half_to_f32_bits_hw(h) : half_to_f32_bits(h));
+                } else {
+                  u = Elem<V>::load_rec(rec + e * VS);
+                }
+                if constexpr (IMP) ib[q] += imp_term<V>(acc, u);
+                acc = Elem<V>::add(acc, u);
+              }
+            *reinterpret_cast<V *>(trow[q] + e * VS) = acc;
+          }
+        }
+      }
+      if constexpr (IMP) {
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
           const double tot = imp0[q] + wave_sum_f64(ib[q]);
@@ -859,7 +1063,8 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
 }
 
 int g_index_variant = 2;
-int g_apply_variant = 6;
+int g_apply_variant = 10;   // v3 (saddr record loads; v2 when a stream is >= 4 GiB): 1% over v2 (6)
+int g_h16_variant = 2;     // v3 + hardware conversion
 int g_inv_layout = 1;
 
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
@@ -918,12 +1123,36 @@ static unsigned resident_blocks(K kernel, int64_t want) {
   return (unsigned)(cap < 1 ? 1 : cap);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, bool H16 = false, bool STNT = false>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0, bool STNT = false>
 static void launch_v2(const DenseArgs &a, hipStream_t st) {
   auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16, STNT>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>
+static void launch_v3(const DenseArgs &a, hipStream_t st) {
+  auto k = dense_apply_v3_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
+  const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
+  const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <typename V, bool IMP, int H16>
+static void launch_adaptive_v3(const DenseArgs &a, hipStream_t st) {
+  if (a.B <= 1) launch_v3<V, 1, 16, true, 8, IMP, H16>(a, st);
+  else if (a.B <= 2) launch_v3<V, 2, 16, true, 4, IMP, H16>(a, st);
+  else if (a.B <= 4) launch_v3<V, 4, 16, true, 3, IMP, H16>(a, st);
+  else if (a.B <= 8) launch_v3<V, 8, 16, true, 2, IMP, H16>(a, st);
+  else launch_v3<V, 16, 16, true, 1, IMP, H16>(a, st);
+}
+
+// v3 addresses records by 32-bit offsets from each message's first record.
+static bool v3_ok(const DenseArgs &a) {
+  for (int b = 0; b < a.B; ++b)
+    if ((uint64_t)a.ss.size[b] >= 0xffff0000ull) return false;
+  return true;
 }
 
 template <typename V, int BMAX>
@@ -984,11 +1213,28 @@ static void launch_adaptive_imp(const DenseArgs &a, hipStream_t st) {
 // element, so more rows in flight per wave at the same load count.
 template <bool IMP>
 static void launch_adaptive_h16(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 1) launch_v2<float, 1, 16, true, 8, IMP, true>(a, st);
-  else if (a.B <= 2) launch_v2<float, 2, 16, true, 4, IMP, true>(a, st);
-  else if (a.B <= 4) launch_v2<float, 4, 16, true, 3, IMP, true>(a, st);
-  else if (a.B <= 8) launch_v2<float, 8, 16, true, 2, IMP, true>(a, st);
-  else launch_v2<float, 16, 16, true, 1, IMP, true>(a, st);
+  // Decompression by the hardware conversion alone (H16 = 2): it keeps NaN payloads and
+  // quiets them, and every decompressed value goes through `row += u`, which quiets
+  // anyway, so rows are bit-identical to the payload-exact decompression (H16 = 1,
+  // g_h16_variant 1) at 23% less time on C2 (VALU-bound: 2.02 -> 1.57 ms, A/B in
+  // profiles/r01/exp_f16_variants.txt).
+  if (g_h16_variant == 2 && v3_ok(a)) {   // default
+    launch_adaptive_v3<float, IMP, 2>(a, st);
+    return;
+  }
+  if (g_h16_variant == 1) {   // payload-exact NaN decompression (v2)
+    if (a.B <= 1) launch_v2<float, 1, 16, true, 8, IMP, 1>(a, st);
+    else if (a.B <= 2) launch_v2<float, 2, 16, true, 4, IMP, 1>(a, st);
+    else if (a.B <= 4) launch_v2<float, 4, 16, true, 3, IMP, 1>(a, st);
+    else if (a.B <= 8) launch_v2<float, 8, 16, true, 2, IMP, 1>(a, st);
+    else launch_v2<float, 16, 16, true, 1, IMP, 1>(a, st);
+    return;
+  }
+  if (a.B <= 1) launch_v2<float, 1, 16, true, 8, IMP, 2>(a, st);
+  else if (a.B <= 2) launch_v2<float, 2, 16, true, 4, IMP, 2>(a, st);
+  else if (a.B <= 4) launch_v2<float, 4, 16, true, 3, IMP, 2>(a, st);
+  else if (a.B <= 8) launch_v2<float, 8, 16, true, 2, IMP, 2>(a, st);
+  else launch_v2<float, 16, 16, true, 1, IMP, 2>(a, st);
 }
 
 template <typename V>
@@ -1004,7 +1250,9 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
     } else {
       launch_adaptive_imp<V>(a, st);
     }
-  } else if (g_apply_variant == 6)
+  } else if (g_apply_variant == 10 && v3_ok(a))
+    launch_adaptive_v3<V, false, 0>(a, st);
+  else if (g_apply_variant == 6 || g_apply_variant == 10)
     launch_adaptive<V>(a, st);
   else if (a.B <= 8)
     launch_apply_bmax<V, 8>(a, st);

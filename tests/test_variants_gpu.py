@@ -254,3 +254,41 @@ def test_float16_records_large_against_torch():
     from parameter_server_amd import _abi
     assert _abi.load().psx_table_read_rows(srv.handle, 1, 0, rows, got.data_ptr(), 1) == 0
     assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_float16_apply_variants(variant):
+    """The fused-apply kernels for binary16 records: 0 = hardware conversion (v2 kernel),
+    1 = payload-exact NaNs (v2), 2 = hardware conversion in the saddr-addressed v3 kernel
+    (default); same
+    rows as the checker (NaN as NaN), and bit-identical to variant 1, NaN payloads
+    included."""
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    old = L.psx_debug_set_variant(4, variant)
+    try:
+        rng = np.random.RandomState(40 + variant)
+        rows, cap, B = 700, 256, 8
+        bgs = list(range(100, 100 + B))
+        srv, orc = _pair(F32, rows, cap, bgs, row_oplog_type=3)
+        init = rng.normal(0, 1, size=(rows, cap)).astype(np.float32)
+        srv.load_rows(1, 0, init)
+        orc.load_dense_rows(1, 0, init)
+        streams = []
+        for _ in range(B):
+            n = rng.randint(1, rows + 1)
+            streams.append(wire.dense_variant_stream_np(1, rng.permutation(rows)[:n].astype(np.int32),
+                                                        _halves(rng, (n, cap)), f16=True))
+        _apply_dev(srv, orc, streams, bgs)
+        got = srv.read_rows(1, 0, rows)
+        assert _same_f32(got, orc.read_dense_rows(1, 0, rows))
+        L.psx_debug_set_variant(4, 0 if variant == 1 else 1)
+        srv2, _ = _pair(F32, rows, cap, bgs, row_oplog_type=3)
+        srv2.load_rows(1, 0, init)
+        dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+        torch.cuda.synchronize()
+        srv2.apply_device([(d.data_ptr(), d.numel(), bg, 0) for d, bg in zip(dev, bgs)])
+        srv2.sync()
+        assert np.array_equal(_bits(srv2.read_rows(1, 0, rows)), _bits(got))
+    finally:
+        L.psx_debug_set_variant(4, old)

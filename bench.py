@@ -503,10 +503,12 @@ def main():
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
     traffic = None
-    default_cfg = ((rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
-                   and not args.adarevision)
-    if default_cfg and args.pmc_json and os.path.exists(args.pmc_json):
-        traffic = json.load(open(args.pmc_json)).get("dense_apply_hbm_bytes_per_launch")
+    c2_dims = (rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
+    pmc_json = args.pmc_json
+    if args.adarevision:   # the AdaRevision kernel's own PMC passes (tools/gpu_session5.sh)
+        pmc_json = os.path.join(ROOT, "profiles", "r01", "pmc_ada_apply.json")
+    if c2_dims and pmc_json and os.path.exists(pmc_json):
+        traffic = json.load(open(pmc_json)).get("dense_apply_hbm_bytes_per_launch")
 
     pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie else None
     if rank == 0:
@@ -546,7 +548,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
-                "traffic_source": os.path.relpath(args.pmc_json, ROOT) if traffic else None,
+                "traffic_source": os.path.relpath(pmc_json, ROOT) if traffic else None,
                 "dram_GBps": round(traffic / apply_avg_s / 1e9, 1) if traffic and apply_avg_s > 0 else None,
                 "avg_launch_ms": round(apply_avg_s * 1e3, 4),
             },

@@ -8,7 +8,7 @@ request counts times their sizes, as MI355X_MICROARCH.md "HBM" prescribes for gf
 (FETCH_SIZE tallies a 128-B request at 64 B, so it is reported only as a cross-check,
 doubled).
 
-usage: python tools/pmc_summary.py gpurun_out/pmc [out.json]"""
+usage: python tools/pmc_summary.py gpurun_out/pmc [out.json] [kernel-substring]"""
 import collections
 import csv
 import glob
@@ -29,9 +29,13 @@ def load(root):
     return {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in per.items()}
 
 
-def dense_apply_traffic(kernels):
-    for name, c in kernels.items():
-        if "dense_apply_v2_kernel<float, 8, 16, true, 2" not in name:
+KERNEL_KEYS = ("dense_apply_v3_kernel<float, 8, 16, true, 2", "dense_apply_v2_kernel<float, 8, 16, true, 2")
+
+
+def dense_apply_traffic(kernels, keys=KERNEL_KEYS):
+    for name, c in sorted(kernels.items(), key=lambda kv: [k in kv[0] for k in keys].index(True)
+                          if any(k in kv[0] for k in keys) else len(keys)):
+        if not any(k in name for k in keys):
             continue
         rd128 = c.get("TCC_EA0_RDREQ_128B_sum")
         rd64 = c.get("TCC_EA0_RDREQ_64B_sum")
@@ -42,7 +46,7 @@ def dense_apply_traffic(kernels):
         read = rd128 * 128 + rd64 * 64
         write = wr64 * 64 + (wr - wr64) * 32
         return {"kernel": name, "read_bytes": read, "write_bytes": write,
-                "dense_apply_hbm_bytes_per_launch": read + write,
+                "dense_apply_hbm_bytes_per_launch": read + write, "hbm_bytes_per_launch": read + write,
                 "fetch_size_x2_bytes": 2 * 1024 * c["FETCH_SIZE"] if "FETCH_SIZE" in c else None,
                 "write_size_bytes": 1024 * c["WRITE_SIZE"] if "WRITE_SIZE" in c else None}, name
     return None, None
@@ -51,7 +55,8 @@ def dense_apply_traffic(kernels):
 if __name__ == "__main__":
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     kernels = load(root)
-    traffic, name = dense_apply_traffic(kernels)
+    keys = (sys.argv[3],) if len(sys.argv) > 3 else KERNEL_KEYS
+    traffic, name = dense_apply_traffic(kernels, keys)
     out = {"kernels": kernels}
     if traffic:
         out.update(traffic)

@@ -128,6 +128,25 @@ class Server {
     return out;
   }
 
+  // TableInfo.server_table_logic = AdaRevision: AdaRevisionServerTableLogic::Init
+  // (adarevision_server_table_logic.cpp:19-36), before the table's first apply.
+  void SetAdaRevision(int32_t table_id, const psx_adarevision_config &cfg) {
+    Check(psx_table_set_adarevision(ctx_, table_id, &cfg));
+  }
+
+  // Server::RowSent (server.cpp:436-441), called by ServerThread after a row request
+  // reply (server_thread.cpp:221).
+  void RowSent(int32_t table_id, const std::vector<int32_t> &row_ids, int32_t num_clients) {
+    Check(psx_row_sent(ctx_, table_id, row_ids.data(), (int32_t)row_ids.size(), num_clients));
+  }
+
+  // VersionServerRow::get_version for a row range (version_server_row.hpp:66).
+  std::vector<uint64_t> RowVersions(int32_t table_id, int64_t first_row, int64_t num_rows) {
+    std::vector<uint64_t> v((size_t)num_rows);
+    Check(psx_row_versions(ctx_, table_id, first_row, num_rows, v.data()));
+    return v;
+  }
+
   psx_ctx *handle() const { return ctx_; }
 
  private:

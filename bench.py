@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--adarevision", action="store_true",
                    help="C2 through the AdaRevision server-table logic (adarevision_server_table_logic.cpp): "
                         "per element the adaptive step on accum/z/z_max state beside every row")
+    p.add_argument("--indexed", action="store_true",
+                   help="C3 through psx_apply_indexed: producer record indexes replace the sequential sparse walk")
     p.add_argument("--importance", action="store_true",
                    help="C2 with importance accumulation (SSPAggr RelativeMagnitude tables)")
     p.add_argument("--pcie", action="store_true",
@@ -161,9 +163,17 @@ def run_c3(args):
     srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
                                      oplog_dense_serialized=False, max_rows=rows, max_entries=K))
     ver = [0]
+    idx = None
+    if args.indexed:   # the producer's record index (psx_pack_stream emits the same), built before timing
+        from parameter_server_amd import wire as _w
+        idx = [torch.from_numpy(_w.stream_record_offsets(s, {3: None}).view(np.int64)).cuda() for s in streams]
 
     def step():
-        srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
+        msgs = [(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)]
+        if idx is not None:
+            srv.apply_indexed(msgs, [o.data_ptr() for o in idx])
+        else:
+            srv.apply_device(msgs)
         ver[0] += 1
 
     for _ in range(args.warmup):
@@ -202,7 +212,8 @@ def run_c3(args):
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
         "dtype": "int32", "data": "synthetic (Zipf rows, uniform nnz 1..32, values +-1..3)",
-        "config": {"workload": f"C3: {rows} rows x K={K}, {B} batches x 10000 rows/step",
+        "config": {"workload": f"C3: {rows} rows x K={K}, {B} batches x 10000 rows/step"
+                               + (", producer record index (psx_apply_indexed)" if args.indexed else ""),
                    "updates_per_step": nupd, "stream_bytes_per_step": stream_bytes},
         "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
         "cpu_baseline": cpu}), flush=True)

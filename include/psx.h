@@ -202,6 +202,16 @@ psx_status psx_apply_stream(psx_ctx *ctx, const void *oplog, size_t oplog_size,
  * array order (per-row update order preserved => bit-exact float sums).  Asynchronous
  * on the context stream; device buffers must stay valid until psx_sync(). */
 psx_status psx_apply_streams_device(psx_ctx *ctx, const psx_stream *streams, int32_t n);
+/* psx_apply_streams_device with producer-supplied record indexes (SURVEY §8(b)
+ * psx_apply_indexed): record_offsets[i] (device, 8-byte aligned; NULL = none) holds, for
+ * every record of message i, all tables in stream order, the byte offset of its row id —
+ * exactly psx_pack_stream's record_offsets.  Sparse tables then skip the sequential
+ * record walk (SerializedOpLogReader::Next's size chain, serialized_oplog_reader.hpp:
+ * 57-84): the offsets are copied and the chain checked in parallel; a sparse table's
+ * entries that do not describe its records are PSX_ERR_MALFORMED at psx_sync, nothing
+ * applied.  Dense tables' entries are counted but not read (fixed stride). */
+psx_status psx_apply_indexed(psx_ctx *ctx, const psx_stream *streams, const uint64_t *const *record_offsets,
+                             int32_t n);
 /* Wait for all queued work and report any device-detected error. */
 psx_status psx_sync(psx_ctx *ctx);
 

@@ -120,6 +120,7 @@ def load():
         "psx_clear_dirty": ([vp, i32], ctypes.c_int),
         "psx_apply_stream": ([vp, vp, sz, i32, u32], ctypes.c_int),
         "psx_apply_streams_device": ([vp, P(psx_stream), i32], ctypes.c_int),
+        "psx_apply_indexed": ([vp, P(psx_stream), P(vp), i32], ctypes.c_int),
         "psx_sync": ([vp], ctypes.c_int),
         "psx_serialize_rows": ([vp, i32, vp, i32, vp, sz, P(sz)], ctypes.c_int),
         "psx_serialize_dirty": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),

@@ -114,6 +114,13 @@ struct AdaArgs {
   int32_t *new_slots;
 };
 
+// Producer-supplied record indexes of one call (psx_apply_indexed): for message b, the
+// byte offset of every record's row id, all tables in stream order (psx_pack_stream's
+// record_offsets); nullptr: walk that message.
+struct IdxSet {
+  const uint64_t *p[kMaxFused];
+};
+
 // Fast-path dense tables of one call (for the duplicate-row gate).
 struct TableMask {
   int32_t n;

@@ -40,17 +40,22 @@ constexpr int kDecodeThreads = 1024;
 constexpr int kDecodeWindowWords = 8192;    // 32 KiB window
 constexpr uint32_t kUnk = 0xFFFFFFFFu;      // chain position unknown (header outside window / bad)
 
+// Indexed messages (ix.p[b] set, psx_apply_indexed): a sparse table's record offsets come
+// from the producer's index; all threads copy them and check the chain in parallel
+// (first offset = the table's first byte, each record ends where the next begins, all
+// inside the message) instead of hopping it.
 __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSet ss, TableDir dir, Seg *segs,
                                                                         uint64_t *recoff, uint32_t *call_status,
-                                                                        uint32_t *counters, uint32_t *ntouched) {
+                                                                        uint32_t *counters, uint32_t *ntouched,
+                                                                        IdxSet ix) {
   __shared__ uint32_t win[kDecodeWindowWords];
   __shared__ uint32_t j1[kDecodeWindowWords], j2[kDecodeWindowWords], j4[kDecodeWindowWords];
   __shared__ uint32_t qlist[kDecodeWindowWords / 8];   // chain positions starting 4-record hops
   __shared__ uint32_t slist[kDecodeWindowWords / 2];   // single-record positions (window tail)
   __shared__ uint32_t sh_nq, sh_ns;
   __shared__ int32_t sh_bad;
-  __shared__ uint64_t sh_off, sh_rk, sh_left;
-  __shared__ int32_t sh_state;   // 0 walking headers, 1 sparse walk needs a window, 2 done
+  __shared__ uint64_t sh_off, sh_rk, sh_left, sh_kk, sh_end;
+  __shared__ int32_t sh_state;   // 0 walking headers, 1 sparse walk needs a window, 2 done, 3 indexed sparse table
   __shared__ int32_t sh_t, sh_ntab, sh_k;
   const int b = blockIdx.x;
   for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
@@ -69,6 +74,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
     sh_off = 4;
     sh_k = 0;
     sh_rk = ss.recoff_base[b];
+    sh_kk = 0;
     if (size == 0) {
       // empty message (server.cpp:128)
     } else if (size < 4 || ld32(p) < 0) {
@@ -107,6 +113,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
           sg->sparse = 0;
           sh_off = off + need;
           sh_k = sh_k + 1;
+          sh_kk = sh_kk + (uint64_t)nrows;
         } else if (off & 3) {
           // the sparse walk stages 4-byte words: a sparse table behind a version table's
           // odd-sized records (9-byte trailers) is not supported
@@ -118,13 +125,49 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
           sh_t = t;
           sh_off = off;
           sh_left = (uint64_t)nrows;
-          if (nrows) sh_state = 1;
+          sh_bad = 0;
+          if (nrows) sh_state = ix.p[b] ? 3 : 1;
           else sh_k = sh_k + 1;
         }
       }
     }
     __syncthreads();
     if (sh_state == 2) break;
+    if (sh_state == 3) {
+      // A') indexed sparse table: copy + verify the producer's offsets (all threads)
+      const uint64_t *ofs = ix.p[b] + sh_kk;
+      const uint64_t nrec = sh_left, start = sh_off, rk = sh_rk;
+      const uint64_t pair = 4 + (uint64_t)dir.vsize[sh_t];
+      for (uint64_t i = threadIdx.x; i < nrec; i += blockDim.x) {
+        const uint64_t o = ofs[i];
+        bool ok = (o & 3) == 0 && o >= start && o + 8 <= size && (i > 0 || o == start);
+        uint64_t end = 0;
+        if (ok) {
+          const int32_t n = ld32(p + o + 4);
+          end = o + 8 + (uint64_t)(n < 0 ? 0 : n) * pair;
+          ok = n >= 0 && end <= size;
+        }
+        if (ok && i + 1 < nrec) ok = ofs[i + 1] == end;
+        if (!ok) sh_bad = 1;
+        recoff[rk + i] = o;
+        if (i + 1 == nrec) sh_end = end;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        if (sh_bad) {
+          atomicOr(call_status, kStMalformed);
+          sh_state = 2;
+        } else {
+          sh_off = sh_end;
+          sh_rk = rk + nrec;
+          sh_kk = sh_kk + nrec;
+          sh_k = sh_k + 1;
+          sh_state = 0;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     // B) stage a window starting at the current record (4-byte aligned by construction)
     const uint64_t w0 = sh_off;
     uint64_t wbytes = size - w0;
@@ -211,6 +254,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
         if (!sh_left) {
           sh_state = 0;
           sh_k = sh_k + 1;
+          sh_kk = sh_kk + (uint64_t)segs[b * kMaxTables + sh_t].num_rows;
         } else if (sh_off + 8 > size) {
           atomicOr(call_status, kStMalformed);
           sh_state = 2;
@@ -1056,9 +1100,10 @@ __global__ void gather_flags_kernel(const uint8_t *flags, const int64_t *slots, 
 // ---------------------------------------------------------------------------
 // Host-side launchers (internal to libpsx).
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
-                         uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, hipStream_t st) {
+                         uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
+                         hipStream_t st) {
   hipLaunchKernelGGL(decode_streams_kernel, dim3(ss.n), dim3(kDecodeThreads), 0, st, ss, dir, segs, recoff,
-                     call_status, counters, ntouched);
+                     call_status, counters, ntouched, ix);
   return hipGetLastError();
 }
 

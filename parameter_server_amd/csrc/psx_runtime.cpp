@@ -21,7 +21,8 @@
 
 namespace psx {
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
-                         uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, hipStream_t st);
+                         uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
+                         hipStream_t st);
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
                               InvLayout L, uint32_t *call_status, hipStream_t st);
@@ -361,7 +362,8 @@ bool has_sparse_serialized(const psx_ctx *c) {
 
 // Enqueue the device pipeline for n messages already resident in HBM (versions checked).
 // force_ordered: every table goes through the ordered path (duplicate-row replay).
-psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_ordered) {
+psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_ordered,
+                         const uint64_t *const *record_offsets = nullptr) {
   const int slot = (int)(c->call_seq & 1);
   // Stage 1 (decode, index, verify) runs on the side stream once the slot's previous
   // user (call k-2) has finished applying; stage 2 runs on the main stream after it.
@@ -396,6 +398,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       c->list_cap = list_need;
     }
   }
+  psx::IdxSet ix{};
+  for (int i = 0; i < n && record_offsets; ++i) ix.p[i] = record_offsets[i];
   psx::TableDir dir{};
   dir.n = (int32_t)c->tables.size();
   for (size_t i = 0; i < c->tables.size(); ++i) {
@@ -414,7 +418,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   psx_status st = timed(
       c, "decode_streams",
       [&] {
-        return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], prep);
+        return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
   if (st) return st;
@@ -1002,8 +1006,24 @@ psx_status psx_row_versions(psx_ctx *c, int32_t table_id, int64_t first_row, int
   return PSX_OK;
 }
 
+static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
+                                    const uint64_t *const *record_offsets);
+
+psx_status psx_apply_indexed(psx_ctx *c, const psx_stream *s, const uint64_t *const *record_offsets, int32_t n) {
+  if (!c || !s || !record_offsets || n <= 0 || n > PSX_MAX_FUSED_STREAMS) return PSX_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i)
+    if (record_offsets[i] && ((uintptr_t)record_offsets[i] & 7))
+      return fail(c, PSX_ERR_INVALID_ARG, "record_offsets must be 8-byte aligned device arrays");
+  return apply_device_impl(c, s, n, record_offsets);
+}
+
 psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) {
   if (!c || !s || n <= 0 || n > PSX_MAX_FUSED_STREAMS) return PSX_ERR_INVALID_ARG;
+  return apply_device_impl(c, s, n, nullptr);
+}
+
+static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
+                                    const uint64_t *const *record_offsets) {
   // Version rule of Server::ApplyOpLogUpdateVersion (server.cpp:124-126), checked for
   // the whole batch before anything is enqueued.
   std::map<int32_t, int64_t> v = c->versions;
@@ -1022,7 +1042,7 @@ psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) 
     psx_status d = sync_impl(c);
     if (d != PSX_OK) c->deferred = d;
   }
-  psx_status st = enqueue_apply(c, s, n, false);
+  psx_status st = enqueue_apply(c, s, n, false, record_offsets);
   if (st) return st;
   c->versions = v;
   return PSX_OK;

@@ -119,6 +119,19 @@ class Server:
             arr[i].version = ver
         _check(self._L, self._ctx, self._L.psx_apply_streams_device(self._ctx, arr, n))
 
+    def apply_indexed(self, streams, record_offsets):
+        """apply_device with producer record indexes: record_offsets[i] is the device
+        pointer of message i's uint64 row-id offsets (psx_pack_stream's), or None."""
+        n = len(streams)
+        arr = (psx_stream * n)()
+        for i, (ptr, nbytes, bg, ver) in enumerate(streams):
+            arr[i].data = ptr
+            arr[i].size = nbytes
+            arr[i].bg_id = bg
+            arr[i].version = ver
+        offs = (ctypes.c_void_p * n)(*[o or None for o in record_offsets])
+        _check(self._L, self._ctx, self._L.psx_apply_indexed(self._ctx, arr, offs, n))
+
     def sync(self):
         _check(self._L, self._ctx, self._L.psx_sync(self._ctx))
 

@@ -81,6 +81,28 @@ def sparse_stream_np(table_id, vsize, rows):
     return np.concatenate(parts)
 
 
+def stream_record_offsets(stream, tables):
+    """tables: {table_id: body_bytes or None}; body_bytes for dense-serialized tables
+    (cap * update_size, + 9 for version records), None for sparse tables."""
+    b = bytes(np.asarray(stream, dtype=np.uint8))
+    ntab = int(np.frombuffer(b[:4], "<i4")[0]) if len(b) >= 4 else 0
+    off, out = 4, []
+    for _ in range(ntab):
+        tid, = np.frombuffer(b[off:off + 4], "<i4")
+        usz, = np.frombuffer(b[off + 4:off + 12], "<u8")
+        nrows, = np.frombuffer(b[off + 12:off + 16], "<i4")
+        off += 16
+        body = tables[int(tid)]
+        for _ in range(int(nrows)):
+            out.append(off)
+            if body is None:
+                n, = np.frombuffer(b[off + 4:off + 8], "<i4")
+                off += 8 + int(n) * (4 + int(usz))
+            else:
+                off += 4 + body
+    return np.array(out, dtype=np.uint64)
+
+
 def pack_np(tables):
     """One multi-table message, as CreateOpLogMsgs + OpLogSerializer lay it out
     (abstract_bg_worker.cpp:590-649, oplog_serializer.hpp:12-37): tables in ascending id,

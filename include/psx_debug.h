@@ -11,7 +11,8 @@ extern "C" {
 #endif
 
 enum { PSX_VARIANT_DENSE_INDEX = 0, PSX_VARIANT_DENSE_APPLY = 1, PSX_VARIANT_INV_LAYOUT = 2,
-       PSX_VARIANT_ADA_APPLY = 3, PSX_VARIANT_H16_APPLY = 4 };
+       PSX_VARIANT_ADA_APPLY = 3, PSX_VARIANT_H16_APPLY = 4,
+       PSX_VARIANT_ORD_GRID = 5 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */
 int32_t psx_debug_set_variant(int32_t which, int32_t variant);

@@ -668,6 +668,8 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 }
 
 // ---------------------------------------------------------------------------
+int g_ord_grid = 1;   // reg-kernel grid: 0 by 64-row tiles, 1 by rows (<= 4096 blocks), 2 by rows (<= 8192)
+
 hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
   const int64_t n = a.max_rows;
   hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
@@ -675,8 +677,12 @@ hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
   const int64_t tiles = (n + 63) / 64;
   if (a.kind != 0 && a.max_entries <= 1024) {
-    int64_t blocks = (tiles + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
+    // one touched row per wave at a time: size the grid by rows (the touched count is on
+    // the device), not by 64-row tiles — 100K rows as tiles gave 1,564 waves for ~35K
+    // touched rows, 1.5 waves per SIMD (g_ord_grid 0 keeps that for A/B)
+    int64_t blocks = g_ord_grid == 0 ? (tiles + 3) / 4 : (n + 3) / 4;
+    const int64_t cap = g_ord_grid == 2 ? 8192 : 4096;
+    if (blocks > cap) blocks = cap;
 #define PSX_REG(V, KIND)                                                                           \
   do {                                                                                             \
     if (a.max_entries <= 64)                                                                       \
@@ -703,7 +709,7 @@ hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
   int wpb = 4;
   while (wpb > 1 && per_wave * wpb > 150 * 1024) --wpb;
   const size_t lds = (size_t)per_wave * wpb;
-  int64_t blocks = (tiles + wpb - 1) / wpb;
+  int64_t blocks = g_ord_grid == 0 ? (tiles + wpb - 1) / wpb : (n + wpb - 1) / wpb;   // one row per wave
   if (blocks > 4096) blocks = 4096;
 #define PSX_ORD(V)                                                                                 \
   do {                                                                                             \

@@ -1588,6 +1588,7 @@ extern int g_apply_variant;
 extern int g_inv_layout;
 extern int g_ada_variant;
 extern int g_h16_variant;
+extern int g_ord_grid;
 extern int g_imp_pair;
 }  // namespace psx
 
@@ -1596,7 +1597,8 @@ extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
            : which == PSX_VARIANT_DENSE_APPLY ? &psx::g_apply_variant
            : which == PSX_VARIANT_INV_LAYOUT ? &psx::g_inv_layout
            : which == PSX_VARIANT_ADA_APPLY ? &psx::g_ada_variant
-           : which == PSX_VARIANT_H16_APPLY ? &psx::g_h16_variant : nullptr;
+           : which == PSX_VARIANT_H16_APPLY ? &psx::g_h16_variant
+           : which == PSX_VARIANT_ORD_GRID ? &psx::g_ord_grid : nullptr;
   if (!v) return -1;
   int old = *v;
   *v = variant;
@@ -1609,6 +1611,7 @@ extern "C" int32_t psx_debug_get_variant(int32_t which) {
   if (which == PSX_VARIANT_INV_LAYOUT) return psx::g_inv_layout;
   if (which == PSX_VARIANT_ADA_APPLY) return psx::g_ada_variant;
   if (which == PSX_VARIANT_H16_APPLY) return psx::g_h16_variant;
+  if (which == PSX_VARIANT_ORD_GRID) return psx::g_ord_grid;
   return -1;
 }
 
@@ -1622,6 +1625,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_INV_LAYOUT")) psx::g_inv_layout = atoi(v);
     if (const char *v = getenv("PSX_ADA_VARIANT")) psx::g_ada_variant = atoi(v);
     if (const char *v = getenv("PSX_H16_VARIANT")) psx::g_h16_variant = atoi(v);
+    if (const char *v = getenv("PSX_ORD_GRID")) psx::g_ord_grid = atoi(v);
     if (const char *v = getenv("PSX_IMP_PAIR")) psx::g_imp_pair = atoi(v);
   }
 } variant_env;

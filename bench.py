@@ -6,7 +6,8 @@ batches, each a full Appendix-A stream (ClientSendOpLogMsg payload) holding one 
 record per row in a per-batch random row order, updates N(0, 0.01).  Streams and table
 are resident in HBM before the timed region.  Synthetic data, generated on the GPU.
 
-Algorithmic bytes per step: sum_b (20 + N*(4 + 4R)) + 2 * N * 4R.
+Algorithmic bytes per step: sum_b (20 + N_b*(4 + 4R)) + 2 * N_touched * 4R
+(N_b = N at full density; --density 0.125 gives the §8(d) partial-coverage variant).
 value = bytes of all ranks / max-over-ranks wall time.  Multi-GPU: each rank owns a
 2^20-row shard (row range) and receives its own already-split batches, as the reference
 client splits oplogs by owning server (abstract_bg_worker.cpp:590-649): no collective,
@@ -53,6 +54,8 @@ def parse():
     p.add_argument("--adarevision", action="store_true",
                    help="C2 through the AdaRevision server-table logic (adarevision_server_table_logic.cpp): "
                         "per element the adaptive step on accum/z/z_max state beside every row")
+    p.add_argument("--density", type=float, default=1.0,
+                   help="C2 fraction of rows each batch covers (SURVEY §8(d) C2 variant: 0.125)")
     p.add_argument("--indexed", action="store_true",
                    help="C3 through psx_apply_indexed: producer record indexes replace the sequential sparse walk")
     p.add_argument("--importance", action="store_true",
@@ -119,7 +122,13 @@ def cpu_baseline(args):
 
     v1, n1, e1 = timed_run(1, args.cpu_seconds / 3)
     vt, nt, et = timed_run(T, args.cpu_seconds * 2 / 3) if T > 1 else (v1, n1, e1)
-    return {"value": round(vt, 3), "unit": "GB/s", "cores": T, "kind": "port",
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
+    return {"value": round(vt, 3), "unit": "GB/s", "cores": T, "kind": "port", "cpu_model": model,
             "single_thread_GBps": round(v1, 3),
             "sample": f"{rows} rows x {cap} f32, {B} batches/step; {T} threads (rows % {T} shards): {nt} steps in "
                       f"{et:.1f} s; 1 thread: {n1} steps in {e1:.1f} s (oracle/psx_oracle.c restatement of "
@@ -448,14 +457,20 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(1234 + 7919 * rank)
     table0 = torch.randn(rows, cap, device="cuda", generator=g) * 0.1
     streams = []
+    nb = max(1, int(round(rows * args.density)))   # records per batch
+    touched = torch.zeros(rows, dtype=torch.bool, device="cuda")
     for b in range(B):
-        perm = torch.randperm(rows, device="cuda", generator=g).to(torch.int32) + base
-        upd = torch.randn(rows, cap, device="cuda", generator=g) * 0.01
+        perm = torch.randperm(rows, device="cuda", generator=g)[:nb].to(torch.int32)
+        touched[perm.long()] = True
+        perm += base
+        upd = torch.randn(nb, cap, device="cuda", generator=g) * 0.01
         if args.f16_records:
             streams.append(wire.dense_stream_torch_f16(1, perm, upd.half()))
         else:
             streams.append(wire.dense_stream_torch(1, perm, upd))
         del upd, perm
+    n_touched = int(touched.sum().item())
+    del touched
     torch.cuda.synchronize()
 
     bgs = [100 + b for b in range(B)]
@@ -506,7 +521,7 @@ def main():
 
     stream_bytes = sum(s.numel() for s in streams)
     # per GPU: streams + row read/write (+ accum, z, z_max read/write for AdaRevision)
-    step_bytes = stream_bytes + (8 if args.adarevision else 2) * rows * cap * 4
+    step_bytes = stream_bytes + (8 if args.adarevision else 2) * n_touched * cap * 4
     total_bytes = step_bytes * args.steps * world
     value = total_bytes / elapsed / 1e9
 
@@ -514,7 +529,8 @@ def main():
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
     traffic = None
-    c2_dims = (rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
+    c2_dims = ((rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
+               and args.density == 1.0)
     pmc_json = args.pmc_json
     if args.adarevision:   # the AdaRevision kernel's own PMC passes (tools/gpu_session5.sh)
         pmc_json = os.path.join(ROOT, "profiles", "r01", "pmc_ada_apply.json")
@@ -543,8 +559,10 @@ def main():
             "data": "synthetic (GPU-generated N(0,0.1) table, N(0,0.01) updates, random row order per batch)",
             "config": {
                 "workload": f"C2: DenseRow<float> table {rows} rows x {cap} cols per GPU, "
-                            f"{B} worker batches (Appendix-A streams) applied per step",
+                            f"{B} worker batches (Appendix-A streams) applied per step"
+                            + (f", each covering {args.density:g} of the rows" if args.density != 1.0 else ""),
                 "rows_per_gpu": rows, "cols": cap, "batches_per_step": B,
+                "density": args.density, "rows_touched_per_step": n_touched,
                 "algorithmic_bytes_per_step_per_gpu": step_bytes,
                 "parallelism": f"row-range shards x{world}, no collective",
                 "importance": bool(args.importance),

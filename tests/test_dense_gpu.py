@@ -239,7 +239,7 @@ def test_smoke_entry():
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("index_variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_every_kernel_variant_bit_exact(apply_variant, index_variant, layout):

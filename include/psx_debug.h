@@ -12,7 +12,7 @@ extern "C" {
 
 enum { PSX_VARIANT_DENSE_INDEX = 0, PSX_VARIANT_DENSE_APPLY = 1, PSX_VARIANT_INV_LAYOUT = 2,
        PSX_VARIANT_ADA_APPLY = 3, PSX_VARIANT_H16_APPLY = 4,
-       PSX_VARIANT_ORD_GRID = 5 };
+       PSX_VARIANT_ORD_GRID = 5, PSX_VARIANT_ORD_SPLIT = 6 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */
 int32_t psx_debug_set_variant(int32_t which, int32_t variant);

@@ -455,7 +455,11 @@ __device__ __forceinline__ T bcast(T x, int src) {
   }
 }
 
-template <typename V, int KIND, int J>
+// CLS splits a call's rows between two launches by the size their image can reach
+// (entries now + this call's record entries): 1 = rows that fit 64*J entries (the others
+// are marked with flags bit 2), 2 = the marked rows, 0 = every row.  Small rows then run
+// at the small image's occupancy.
+template <typename V, int KIND, int J, int CLS = 0>
 __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
   __shared__ int32_t sort_scratch[4][64];
@@ -473,6 +477,9 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   const int64_t nt = go ? (int64_t)*a.ntouched : 0;
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
     const int64_t slot = a.touched[ti];
+    if constexpr (CLS == 2) {   // only the rows the CLS = 1 launch marked (flags bit 2)
+      if (!(a.flags[slot] & 4)) continue;
+    }
     if (lane == 0) a.flags[slot] = 3;
     {
       const int32_t beg = a.off[slot];
@@ -493,8 +500,26 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
       }
-      // load the row image
       int32_t n = a.nent[slot];
+      if constexpr (CLS == 1) {
+        // classify on the row as it is before this call; a row too big for the J-image
+        // is marked (flags bit 2) for the CLS = 2 launch, which clears the mark
+        int32_t grow = 0;   // this lane's records' entry counts
+        for (int32_t q = lane; q < L; q += 64) {
+          const int32_t r = L <= 64 ? mine : lst[q];
+          int b;
+          uint64_t roff;
+          locate(a, rs, r, b, roff);
+          grow += o_ld32(a.ss.data[b] + roff + 4);
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) grow += __shfl_xor(grow, m, 64);
+        if ((int64_t)n + grow > 64 * (int64_t)J) {
+          if (lane == 0) a.flags[slot] = 3 | 4;
+          continue;
+        }
+      }
+      // load the row image
       const uint8_t *row = a.entries + slot * a.max_entries * ES;
       int32_t key[J];
       V val[J];
@@ -668,6 +693,7 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 }
 
 // ---------------------------------------------------------------------------
+int g_ord_split = 1;  // rows of > 256-entry tables split into a 256-entry and a 1,024-entry image launch
 int g_ord_grid = 1;   // reg-kernel grid: 0 by 64-row tiles, 1 by rows (<= 4096 blocks), 2 by rows (<= 8192)
 
 hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
@@ -689,7 +715,10 @@ hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
     else if (a.max_entries <= 256)                                                                 \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
-    else                                                                                           \
+    else if (g_ord_split) {                                                                        \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, 2>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+    } else                                                                                         \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
   } while (0)
 #define PSX_REGK(V) do { if (a.kind == 1) PSX_REG(V, 1); else PSX_REG(V, 2); } while (0)

@@ -1589,6 +1589,7 @@ extern int g_inv_layout;
 extern int g_ada_variant;
 extern int g_h16_variant;
 extern int g_ord_grid;
+extern int g_ord_split;
 extern int g_imp_pair;
 }  // namespace psx
 
@@ -1598,7 +1599,8 @@ extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
            : which == PSX_VARIANT_INV_LAYOUT ? &psx::g_inv_layout
            : which == PSX_VARIANT_ADA_APPLY ? &psx::g_ada_variant
            : which == PSX_VARIANT_H16_APPLY ? &psx::g_h16_variant
-           : which == PSX_VARIANT_ORD_GRID ? &psx::g_ord_grid : nullptr;
+           : which == PSX_VARIANT_ORD_GRID ? &psx::g_ord_grid
+           : which == PSX_VARIANT_ORD_SPLIT ? &psx::g_ord_split : nullptr;
   if (!v) return -1;
   int old = *v;
   *v = variant;
@@ -1612,6 +1614,7 @@ extern "C" int32_t psx_debug_get_variant(int32_t which) {
   if (which == PSX_VARIANT_ADA_APPLY) return psx::g_ada_variant;
   if (which == PSX_VARIANT_H16_APPLY) return psx::g_h16_variant;
   if (which == PSX_VARIANT_ORD_GRID) return psx::g_ord_grid;
+  if (which == PSX_VARIANT_ORD_SPLIT) return psx::g_ord_split;
   return -1;
 }
 
@@ -1626,6 +1629,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_ADA_VARIANT")) psx::g_ada_variant = atoi(v);
     if (const char *v = getenv("PSX_H16_VARIANT")) psx::g_h16_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_GRID")) psx::g_ord_grid = atoi(v);
+    if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_IMP_PAIR")) psx::g_imp_pair = atoi(v);
   }
 } variant_env;

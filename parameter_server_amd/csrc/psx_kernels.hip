@@ -173,8 +173,23 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
     uint64_t wbytes = size - w0;
     if (wbytes > (uint64_t)kDecodeWindowWords * 4) wbytes = (uint64_t)kDecodeWindowWords * 4;
     const uint32_t nw = (uint32_t)(wbytes / 4);
-    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x)
-      win[i] = reinterpret_cast<const uint32_t *>(p + w0)[i];
+    {
+      // all of a thread's loads in flight before any LDS store (one DRAM round trip per
+      // window instead of one per word)
+      constexpr int PER = kDecodeWindowWords / kDecodeThreads;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(p + w0);
+      uint32_t tmp[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kDecodeThreads;
+        tmp[k] = i < nw ? src[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kDecodeThreads;
+        if (i < nw) win[i] = tmp[k];
+      }
+    }
     // C) jump tables over the window (all threads): j1[q] = word index of the record
     //    after a record starting at word q, j2 = j1 o j1, j4 = j2 o j2; kUnk where a
     //    header lies outside the window or the record is malformed.

@@ -224,8 +224,9 @@ __global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
 // stored once.  VEC: EPL = 4 contiguous elements per lane through 16-B accesses
 // (row_capacity % 4 == 0; records are only byte-aligned behind version trailers: gfx950
 // runs with unaligned access enabled).
-template <bool IMP, bool VEC>
-__global__ void __launch_bounds__(256) ada_apply_v2_kernel(AdaArgs a) {
+template <bool IMP, bool VEC, int OCC = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) ada_apply_v2_kernel(AdaArgs a) {
+  constexpr int UNR = OCC > 5 ? 1 : 2;   // records in flight per element chunk
   constexpr int EPL = VEC ? 4 : 1;
   __shared__ int32_t s_idx[4][kMaxFused][64];   // the tile's inverse-index entries
   __shared__ const uint8_t *s_rec[4][kMaxFused];
@@ -315,7 +316,7 @@ __global__ void __launch_bounds__(256) ada_apply_v2_kernel(AdaArgs a) {
         // record's eta (same operands, same correctly rounded result)
 #pragma unroll
         for (int j = 0; j < EPL; ++j) eta[j] = step / sqrtf(zm[j]);
-#pragma unroll 2
+#pragma unroll UNR
         for (int r = 0; r < nb; ++r) {
           const uint8_t *rec = s_rec[w][r];
           const float *op = s_old[w][r];
@@ -355,7 +356,10 @@ __global__ void __launch_bounds__(256) ada_apply_v2_kernel(AdaArgs a) {
   }
 }
 
-int g_ada_variant = 1;   // 0: per-record kernel, 1: register-resident state (default)
+// 0: per-record kernel, 1: register-resident state, 2 (default): 1 held to 6 waves/SIMD
+// with one record in flight for f32 rows of row_capacity % 4 == 0 without importance
+// (4.25-4.34 -> 3.93 ms on C2, profiles/r01/exp_ada_variants.txt)
+int g_ada_variant = 2;
 
 // ServerRowSent (:177-190) for the rows in `list` (n entries) or, with list == nullptr,
 // for every slot s < n whose serve-back size is non-zero (the rows a push just sent).
@@ -435,7 +439,11 @@ hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st) {
   int64_t blocks = (tiles + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  if (g_ada_variant == 1) {
+  if (g_ada_variant == 2 && a.cap % 4 == 0 && !a.imp) {   // 6 waves/SIMD, one record in flight
+    hipLaunchKernelGGL((ada_apply_v2_kernel<false, true, 6>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  if (g_ada_variant >= 1) {
     const bool vec = a.cap % 4 == 0;
     if (a.imp && vec)
       hipLaunchKernelGGL((ada_apply_v2_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);

@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
 // runs with unaligned access enabled).
 template <bool IMP, bool VEC, int OCC = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) ada_apply_v2_kernel(AdaArgs a) {
-  constexpr int UNR = OCC > 5 ? 1 : 2;   // records in flight per element chunk
+  constexpr int UNR = (OCC > 5 || !VEC || IMP) ? 1 : 2;   // records in flight per element chunk
   constexpr int EPL = VEC ? 4 : 1;
   __shared__ int32_t s_idx[4][kMaxFused][64];   // the tile's inverse-index entries
   __shared__ const uint8_t *s_rec[4][kMaxFused];

@@ -805,8 +805,8 @@ __device__ __forceinline__ u32x4 gload_h4(const uint8_t *base, uint32_t off) {
                half_to_f32_bits(w1 >> 16)};
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0>
-__global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0, int OCC = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) dense_apply_v3_kernel(DenseArgs a) {
   static_assert(PAIR * BMAX <= 32, "presence mask is 32 bits");
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;
@@ -1324,9 +1324,9 @@ static void launch_v2(const DenseArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0, int OCC = 1>
 static void launch_v3(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v3_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
+  auto k = dense_apply_v3_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16, OCC>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
@@ -1438,7 +1438,11 @@ static void launch_adaptive_h16(const DenseArgs &a, hipStream_t st) {
   // anyway, so rows are bit-identical to the payload-exact decompression (H16 = 1,
   // g_h16_variant 1) at 23% less time on C2 (VALU-bound: 2.02 -> 1.57 ms, A/B in
   // profiles/r01/exp_f16_variants.txt).
-  if (g_h16_variant == 2 && v3_ok(a)) {   // default
+  if (g_h16_variant == 3 && v3_ok(a) && a.B > 4 && a.B <= 8) {   // 5 waves/SIMD
+    launch_v3<float, 8, 16, true, 2, IMP, 2, 5>(a, st);
+    return;
+  }
+  if (g_h16_variant >= 2 && v3_ok(a)) {   // default
     launch_adaptive_v3<float, IMP, 2>(a, st);
     return;
   }
@@ -1476,6 +1480,8 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
     launch_adaptive_v3<V, false, 0>(a, st);
   else if (g_apply_variant >= 11 && g_apply_variant <= 13)
     launch_compact<V>(a, st);
+  else if (g_apply_variant == 14 && v3_ok(a) && a.B > 4 && a.B <= 8)
+    launch_v3<V, 8, 16, true, 2, false, 0, 5>(a, st);   // 5 waves/SIMD
   else if (g_apply_variant == 6 || g_apply_variant == 10)
     launch_adaptive<V>(a, st);
   else if (a.B <= 8)

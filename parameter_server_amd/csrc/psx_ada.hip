@@ -224,10 +224,9 @@ __global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
 // stored once.  VEC: EPL = 4 contiguous elements per lane through 16-B accesses
 // (row_capacity % 4 == 0; records are only byte-aligned behind version trailers: gfx950
 // runs with unaligned access enabled).
-template <bool IMP, bool VEC, int OCC = 1>
+template <bool IMP, int EPL, int OCC = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) ada_apply_v2_kernel(AdaArgs a) {
-  constexpr int UNR = (OCC > 5 || !VEC || IMP) ? 1 : 2;   // records in flight per element chunk
-  constexpr int EPL = VEC ? 4 : 1;
+  constexpr int UNR = (OCC > 5 || EPL != 4 || IMP) ? 1 : 2;   // records in flight per element chunk
   __shared__ int32_t s_idx[4][kMaxFused][64];   // the tile's inverse-index entries
   __shared__ const uint8_t *s_rec[4][kMaxFused];
   __shared__ const float *s_old[4][kMaxFused];
@@ -439,20 +438,28 @@ hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st) {
   int64_t blocks = (tiles + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
+  if (g_ada_variant == 3 && a.cap % 2 == 0 && !a.imp) {   // 8-B accesses, 8 waves/SIMD
+    hipLaunchKernelGGL((ada_apply_v2_kernel<false, 2, 8>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  if (g_ada_variant == 4 && a.cap % 2 == 0 && !a.imp) {   // 8-B accesses, 6 waves/SIMD
+    hipLaunchKernelGGL((ada_apply_v2_kernel<false, 2, 6>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   if (g_ada_variant == 2 && a.cap % 4 == 0 && !a.imp) {   // 6 waves/SIMD, one record in flight
-    hipLaunchKernelGGL((ada_apply_v2_kernel<false, true, 6>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ada_apply_v2_kernel<false, 4, 6>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   if (g_ada_variant >= 1) {
     const bool vec = a.cap % 4 == 0;
     if (a.imp && vec)
-      hipLaunchKernelGGL((ada_apply_v2_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((ada_apply_v2_kernel<true, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     else if (a.imp)
-      hipLaunchKernelGGL((ada_apply_v2_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((ada_apply_v2_kernel<true, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     else if (vec)
-      hipLaunchKernelGGL((ada_apply_v2_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((ada_apply_v2_kernel<false, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((ada_apply_v2_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((ada_apply_v2_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   if (a.imp)

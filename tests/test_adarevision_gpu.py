@@ -49,7 +49,7 @@ def _apply(srv, orc, streams, bgs, vers):
         assert orc.apply_stream(s, bg, v) == 0
 
 
-@pytest.fixture(params=[1, 2, 0], ids=["regstate", "regstate_occ6", "perrecord"])
+@pytest.fixture(params=[1, 2, 3, 4, 0], ids=["regstate", "regstate_occ6", "regstate8B_occ8", "regstate8B_occ6", "perrecord"])
 def ada_variant(request):
     """Both apply kernels: 1 = state held in registers across a call's records
     (default), 0 = one pass over the row per record."""

@@ -1,7 +1,9 @@
 /*
- * psx_debug.h — experiment hooks of libpsx (not part of the reference boundary).
- * Selects kernel variants at run time so A/B measurements run interleaved in one
- * process (cdna_hip_programming.md §5.4 rule 24).
+ * psx_debug.h — kernel selectors of libpsx (not part of the reference boundary).
+ * The defaults are the measured winners; the alternatives are the kernels the product
+ * itself falls back to (v2 for >= 4 GiB streams, v4 for partially covered calls) plus
+ * two load-form knobs, selectable so the parity suite covers every kernel and A/B runs
+ * stay interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
  */
 #ifndef PSX_DEBUG_H_
 #define PSX_DEBUG_H_
@@ -10,9 +12,13 @@
 extern "C" {
 #endif
 
-enum { PSX_VARIANT_DENSE_INDEX = 0, PSX_VARIANT_DENSE_APPLY = 1, PSX_VARIANT_INV_LAYOUT = 2,
-       PSX_VARIANT_ADA_APPLY = 3, PSX_VARIANT_H16_APPLY = 4,
-       PSX_VARIANT_ORD_GRID = 5, PSX_VARIANT_ORD_SPLIT = 6 };
+enum {
+  PSX_VARIANT_DENSE_INDEX = 0,  /* 0: non-temporal row-id loads (default), 1: plain loads */
+  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact,
+                                   3: v3 with plain record loads */
+  PSX_VARIANT_ORD_SPLIT = 6     /* 1: sorted/map rows of > 256 entries split into a 256- and a
+                                   1,024-entry image launch (default), 0: one launch */
+};
 
 /* Returns the previous variant, or -1 for an unknown selector. */
 int32_t psx_debug_set_variant(int32_t which, int32_t variant);

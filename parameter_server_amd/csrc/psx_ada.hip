@@ -7,6 +7,8 @@
 // row; old_accum_gradients_ ((row, version) -> (accum_gradients_ when that version was
 // sent, clients left), :64-67) is S slots per row: {version, count} + an f32 row image.
 //
+//   ada_check      (version records) every record's snapshot exists, in message order,
+//                  before anything of the call is applied — kStState, all or nothing.
 //   ada_new_rows   rows this call creates (touched, not present before), keyed by their
 //                  first record (message, position): the order CreateRow runs in
 //                  (server.cpp:154-178).  The host sorts the keys and draws each new row's
@@ -98,22 +100,17 @@ __device__ __forceinline__ uint64_t ld_u64(const uint8_t *p) {
   return v;
 }
 
-// ApplyRowOpLog (:52-175) for every record of the call, per row in message order.
-template <bool IMP>
-__global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
+// State check (all-or-nothing error contract): before anything of the call is applied,
+// replay every touched row's snapshot bookkeeping in message order — each versioned
+// record must name a live (row, version) snapshot (old_accum_gradients_.find, :114-116),
+// and an end_of_version record releases one client of it (:165-170), which can retire the
+// snapshot for the records after it.  A miss sets kStState; ada_apply then skips the call.
+// Reads the inverse index without restoring it (ada_apply does that).
+__global__ void __launch_bounds__(256) ada_check_kernel(AdaArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
-  const bool skip = !ada_go(a);
-  const uint8_t *pay0[kMaxFused];   // payload of record 0 of message b
-#pragma unroll
-  for (int b = 0; b < kMaxFused; ++b) {
-    pay0[b] = nullptr;
-    if (b < a.B) {
-      const Seg sg = a.segs[b * kMaxTables + a.t];
-      if (sg.rec0 >= 0 && !sg.sparse) pay0[b] = a.ss.data[b] + sg.rec0 + 4;
-    }
-  }
+  if (!ada_go(a)) return;
   const int S = a.S;
   const int64_t ntiles = (a.max_rows + 63) / 64;
   for (int64_t tile = wave_g; tile < ntiles; tile += nwaves) {
@@ -121,97 +118,34 @@ __global__ void __launch_bounds__(256) ada_apply_kernel(AdaArgs a) {
     const bool mine = my < a.max_rows;
     int32_t idx[kMaxFused];
     bool touched = false;
-    uint64_t nrec = 0;
 #pragma unroll
     for (int b = 0; b < kMaxFused; ++b) {
-      idx[b] = -1;
-      if (b < a.B && mine) {
-        int32_t *p = a.inv + my * a.inv_ss + b * a.inv_sb;
-        idx[b] = *p;
-        if (idx[b] >= 0) {
-          touched = true;
-          ++nrec;
-          *p = -1;   // restore the index for the next call
-        }
-      }
-    }
-    if (skip) continue;
-    if (touched) {
-      a.flags[my] = 3;
-      if (a.ver) a.ver[my] += nrec;   // VersionServerRow: version_++ per RowBatchInc_
+      idx[b] = (b < a.B && mine) ? a.inv[my * a.inv_ss + b * a.inv_sb] : -1;
+      touched = touched || idx[b] >= 0;
     }
     uint64_t live = __ballot(touched);
     while (live) {
       const int k = __builtin_ctzll(live);
       live &= live - 1;
       const int64_t s = tile * 64 + k;
-      float *row = a.table + s * a.cap;
-      float *acc = a.acc + s * a.cap, *z = a.z + s * a.cap, *zmax = a.zmax + s * a.cap;
-      uint64_t sv[kAdaMaxS], sc[kAdaMaxS];   // the row's snapshot slots, wave-uniform
+      const bool qlane = lane < S;
+      const uint64_t sv = qlane ? a.snap_ver[s * S + lane] : 0;
+      uint64_t sc = qlane ? a.snap_cnt[s * S + lane] : 0;
 #pragma unroll
-      for (int q = 0; q < kAdaMaxS; ++q) {
-        sv[q] = q < S ? a.snap_ver[s * S + q] : 0;
-        sc[q] = q < S ? a.snap_cnt[s * S + q] : 0;
-      }
-      bool snap_dirty = false;
-      double impt = IMP ? a.imp[s] : 0.0;
-      for (int b = 0; b < a.B; ++b) {
+      for (int b = 0; b < kMaxFused; ++b) {
         const int32_t i = __builtin_amdgcn_readlane(idx[b], k);
-        if (i < 0) continue;
-        const uint8_t *rec = pay0[b] + (int64_t)i * a.stride;
-        uint64_t rv = 0;
-        bool eov = false;
-        if (a.version_records) {   // ExtractOpLogVersion (server_table.cpp:527-535)
-          rv = ld_u64(rec + a.cap * 4);
-          eov = rec[a.cap * 4 + 8] != 0;
+        if (b >= a.B || i < 0) continue;
+        const Seg sg = a.segs[b * kMaxTables + a.t];
+        const uint8_t *rec = a.ss.data[b] + sg.rec0 + 4 + (int64_t)i * a.stride;
+        const uint64_t rv = ld_u64(rec + a.cap * 4);
+        if (!rv) continue;
+        const uint64_t hit = __ballot(qlane && sc != 0 && sv == rv);
+        if (!hit) {
+          if (lane == 0) atomicOr(a.call_status, kStState);
+          break;
         }
-        int q0 = -1;
-        if (rv) {   // old_accum_gradients_.find((row, version)) (:114-116)
-#pragma unroll
-          for (int q = 0; q < kAdaMaxS; ++q)
-            if (q0 < 0 && q < S && sc[q] && sv[q] == rv) q0 = q;
-          if (q0 < 0) {
-            if (lane == 0) atomicOr(a.call_status, kStState);
-            continue;
-          }
-        }
-        const float *old = q0 >= 0 ? a.snap_acc + (s * S + q0) * a.cap : nullptr;
-        double p = 0.0;
-        for (int64_t e = lane; e < a.cap; e += 64) {
-          float u;
-          __builtin_memcpy(&u, rec + e * 4, 4);
-          const float ac = acc[e];
-          const float g_bck = ac - (old ? old[e] : 0.0f);
-          const float zm0 = zmax[e];
-          const float eta_old = a.step / sqrtf(zm0);
-          const float zz = z[e] + u * (u + 2.0f * g_bck);
-          const float zm = zz < zm0 ? zm0 : zz;   // std::max(z_, z_max_)
-          const float eta = a.step / sqrtf(zm);
-          const float d = -(eta * u) + (eta_old - eta) * g_bck;
-          z[e] = zz;
-          zmax[e] = zm;
-          acc[e] = ac + u;
-          const float x = row[e];   // RowBatchInc_(deltas) (:173-174)
-          if constexpr (IMP) p += imp_term<float>(x, d);
-          row[e] = x + d;
-        }
-        if constexpr (IMP) impt += wave_sum_f64(p);
-        if (q0 >= 0 && eov) {   // the client is done with this version (:165-170)
-#pragma unroll
-          for (int q = 0; q < kAdaMaxS; ++q)
-            if (q == q0) {
-              sc[q] -= 1;
-              if (sc[q] == 0 && lane == 0) atomicSub(a.words, 1u);
-            }
-          snap_dirty = true;
-        }
+        if (rec[a.cap * 4 + 8] != 0 && lane == (int)__builtin_ctzll(hit)) sc -= 1;
       }
-      if (snap_dirty) {
-#pragma unroll
-        for (int q = 0; q < kAdaMaxS; ++q)
-          if (q < S && lane == q) a.snap_cnt[s * S + q] = sc[q];
-      }
-      if (IMP && lane == 0) a.imp[s] = impt;
     }
   }
 }
@@ -355,15 +289,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
   }
 }
 
-// 0: per-record kernel, 1: register-resident state, 2 (default): 1 held to 6 waves/SIMD
-// with one record in flight for f32 rows of row_capacity % 4 == 0 without importance
-// (4.25-4.34 -> 3.93 ms on C2, profiles/r01/exp_ada_variants.txt)
-int g_ada_variant = 2;
-
 // ServerRowSent (:177-190) for the rows in `list` (n entries) or, with list == nullptr,
 // for every slot s < n whose serve-back size is non-zero (the rows a push just sent).
+// check_only: report (words[2] |= kStCapacity) a row that would need a snapshot slot and
+// has none, writing nothing — the push runs this before it clears any dirty bit.
+// subs (optional): ServerRowSent's num_clients is the row's subscriber count
+// (server_table.cpp:252-255 via CallBackSubs::AppendRowToBuffs).
 __global__ void __launch_bounds__(256) ada_sent_kernel(AdaArgs a, const int32_t *list, const int64_t *sizes,
-                                                      int64_t n, uint64_t clients) {
+                                                      int64_t n, uint64_t clients, const uint64_t *subs,
+                                                      int check_only) {
   const int lane = threadIdx.x & 63;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -389,12 +323,14 @@ __global__ void __launch_bounds__(256) ada_sent_kernel(AdaArgs a, const int32_t 
         if (lane == 0) atomicOr(a.words + 2, kStCapacity);
         continue;
       }
+      if (check_only) continue;
+      const uint64_t nc = subs ? (uint64_t)__builtin_popcountll(subs[s]) : clients;
       float *dst = a.snap_acc + (s * S + fr) * a.cap;
       const float *src = a.acc + s * a.cap;
       for (int64_t e = lane; e < a.cap; e += 64) dst[e] = src[e];
       if (lane == 0) {
         a.snap_ver[s * S + fr] = v;
-        a.snap_cnt[s * S + fr] = clients;
+        a.snap_cnt[s * S + fr] = nc;
         atomicAdd(a.words, 1u);
       }
     }
@@ -433,48 +369,42 @@ hipError_t launch_ada_init_rows(const AdaArgs &a, const int32_t *slots, const fl
   return hipGetLastError();
 }
 
+// Register-resident state kernel: held to 6 waves/SIMD with one record in flight for f32
+// rows of row_capacity % 4 == 0 without importance (4.25-4.34 -> 3.93 ms on C2,
+// profiles/r01/exp_ada_variants.txt).
 hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st) {
   const int64_t tiles = (a.max_rows + 63) / 64;
   int64_t blocks = (tiles + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  if (g_ada_variant == 3 && a.cap % 2 == 0 && !a.imp) {   // 8-B accesses, 8 waves/SIMD
-    hipLaunchKernelGGL((ada_apply_v2_kernel<false, 2, 8>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  if (g_ada_variant == 4 && a.cap % 2 == 0 && !a.imp) {   // 8-B accesses, 6 waves/SIMD
-    hipLaunchKernelGGL((ada_apply_v2_kernel<false, 2, 6>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  if (g_ada_variant == 2 && a.cap % 4 == 0 && !a.imp) {   // 6 waves/SIMD, one record in flight
+  const bool vec = a.cap % 4 == 0;
+  if (vec && !a.imp)
     hipLaunchKernelGGL((ada_apply_v2_kernel<false, 4, 6>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  if (g_ada_variant >= 1) {
-    const bool vec = a.cap % 4 == 0;
-    if (a.imp && vec)
-      hipLaunchKernelGGL((ada_apply_v2_kernel<true, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    else if (a.imp)
-      hipLaunchKernelGGL((ada_apply_v2_kernel<true, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    else if (vec)
-      hipLaunchKernelGGL((ada_apply_v2_kernel<false, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((ada_apply_v2_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  if (a.imp)
-    hipLaunchKernelGGL(ada_apply_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (a.imp && vec)
+    hipLaunchKernelGGL((ada_apply_v2_kernel<true, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (a.imp)
+    hipLaunchKernelGGL((ada_apply_v2_kernel<true, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(ada_apply_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ada_apply_v2_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st) {
+  const int64_t tiles = (a.max_rows + 63) / 64;
+  int64_t blocks = (tiles + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(ada_check_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t *sizes, int64_t n,
-                           uint64_t clients, hipStream_t st) {
+                           uint64_t clients, const uint64_t *subs, int check_only, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(ada_sent_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, list, sizes, n, clients);
+  hipLaunchKernelGGL(ada_sent_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, list, sizes, n, clients, subs,
+                     check_only);
   return hipGetLastError();
 }
 

@@ -3,7 +3,7 @@
 // Device layout (one context = one server shard, see DESIGN.md "Data layout in HBM"):
 //   dense table   : V rows[max_rows][row_capacity]            (slot-major, row_capacity*sizeof(V) B/row)
 //   row flags     : uint8 flags[max_rows]  bit0 exists, bit1 dirty  (ServerRow::dirty_, server_row.hpp:133)
-//   inverse index : int32 inv[max_rows][B]  record number of slot s in message b, -1 = absent.
+//   inverse index : int32 inv[B][max_rows]  record number of slot s in message b, -1 = absent.
 //                   All -1 between calls: the apply kernel restores every entry it reads.
 //   segments      : Seg segs[kMaxFused][kMaxTables]  (stream b, table t) decoded by decode_streams
 #pragma once
@@ -54,7 +54,8 @@ struct Seg {
   int32_t sparse;     // 1: record offsets live in recoff[recoff_base[b] + k]
 };
 
-// Inverse-index addressing: entry (slot s, message b) lives at inv[s*ss + b*sb].
+// Inverse-index addressing: entry (slot s, message b) lives at inv[s*ss + b*sb]; the
+// runtime uses the batch-major layout.
 // Batch-major ([b][s]: ss = 1, sb = max_rows) keeps one message's scattered writes
 // inside a max_rows*4-byte window so the XCD L2s can merge them.
 struct InvLayout {
@@ -157,6 +158,8 @@ struct OrdArgs {
   double *imp;            // non-null: accumulate NSSumImpCalc importance per slot
   uint64_t *ver;          // non-null: VersionServerRow::version_ per slot (+1 per record)
   int rec_f16;            // dense records are binary16 (kDenseRowOpLogFloat16)
+  uint32_t *keyflag;      // sorted/map tables: set once a key outside [0, max_entries) is seen
+                          // (from then on every call runs the capacity dry run)
 };
 
 // Arguments of the serve-back kernels (psx_serve.hip).

@@ -298,25 +298,6 @@ __device__ __forceinline__ int64_t slot_of(int32_t rid, const Geo &g) {
   return d < g.max_rows ? d : -1;
 }
 
-// dense_index: grid-stride over every record of every message containing table t.
-__global__ void __launch_bounds__(256) dense_index_kernel(StreamSet ss, const Seg *segs, int t, int B,
-                                                         int64_t stride, Geo g, int32_t *inv, InvLayout L,
-                                                         uint32_t *call_status) {
-  const int64_t gsz = (int64_t)gridDim.x * blockDim.x;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int b = 0; b < B; ++b) {
-    const Seg sg = segs[b * kMaxTables + t];
-    if (sg.rec0 < 0 || sg.sparse) continue;
-    const uint8_t *base = ss.data[b] + sg.rec0;
-    for (int64_t i = gid; i < sg.num_rows; i += gsz) {
-      const int32_t rid = ld32(base + i * stride);
-      const int64_t s = slot_of(rid, g);
-      if (s < 0) { atomicOr(call_status, kStRowRange); continue; }
-      inv[s * L.ss + b * L.sb] = (int32_t)i;
-    }
-  }
-}
-
 // dense_verify: counters[t][b] = number of slots claimed by message b.
 __global__ void __launch_bounds__(256) dense_verify_kernel(const int32_t *inv, InvLayout L, int t, int B,
                                                           int64_t max_rows, uint32_t *counters) {
@@ -374,129 +355,6 @@ template <> struct Elem<int64_t> {
   __device__ static int64_t add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 };
 
-
-// dense_apply: each wave owns a tile of 64 consecutive slots.  Lane k reads the B
-// inverse-index entries of slot k (and restores them to -1), writes the slot's flags,
-// then the wave walks the touched slots; for each, 4 elements per lane per 256-element
-// chunk: 1 table load + B record loads issued back to back, then the in-order sum.
-// IMP: also accumulate each record's NSSumImpCalc importance, sum_i |u_i / v_i| with v_i
-// the value before that record's add (ns_sum_imp_calc.hpp:79-98), into imp[slot] in
-// message order (ServerRow::AccumImportance, server_row.hpp:56-62,124-126).  Within a
-// record the f64 terms are summed lane-parallel (non-negative terms: the result is
-// within (cap-1)*2^-53 relative of the reference's element-order sum).
-template <typename V, int BMAX, bool IMP>
-__global__ void __launch_bounds__(256) dense_apply_kernel(DenseArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int B = a.B;
-
-  // Per-call gate: fatal errors, a duplicate row in any message, or a duplicate still
-  // pending from an earlier call (ordering) => apply nothing, just restore the index.
-  bool skip = (*a.call_status & kStFatal) != 0 || (*a.sticky & kStDuplicateRow) != 0;
-  bool dup = false;
-  int64_t rec0[BMAX];
-#pragma unroll
-  for (int b = 0; b < BMAX; ++b) {
-    rec0[b] = -1;
-    if (b < B) {
-      const Seg sg = a.segs[b * kMaxTables + a.t];
-      if (sg.rec0 >= 0 && !sg.sparse) {
-        rec0[b] = sg.rec0;
-        if (a.counters[a.t * kMaxFused + b] != (uint32_t)sg.num_rows) dup = true;
-      }
-    }
-  }
-  if (dup && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.call_status, kStDuplicateRow);
-  skip = skip || dup;
-
-  const int64_t s0 = tile * 64;
-  if (s0 >= a.max_rows) return;
-  const int64_t my_slot = s0 + lane;
-  const bool in_range = my_slot < a.max_rows;
-  int32_t idx[BMAX];
-  bool touched = false;
-#pragma unroll
-  for (int b = 0; b < BMAX; ++b) {
-    idx[b] = -1;
-    if (b < B && in_range) {
-      idx[b] = a.inv[my_slot * a.inv_ss + b * a.inv_sb];
-      if (idx[b] >= 0) {
-        touched = true;
-        a.inv[my_slot * a.inv_ss + b * a.inv_sb] = -1;
-      }
-    }
-  }
-  if (skip) return;
-  if (touched) {
-    a.flags[my_slot] = 3;   // exists | dirty
-    if (a.ver) {            // VersionServerRow: version_++ per applied record (version_server_row.hpp:44-53)
-      uint64_t n = 0;
-#pragma unroll
-      for (int b = 0; b < BMAX; ++b) n += idx[b] >= 0 ? 1u : 0u;
-      a.ver[my_slot] += n;
-    }
-  }
-
-  uint64_t live = __ballot(touched);
-  V *table = reinterpret_cast<V *>(a.table);
-  while (live) {
-    const int k = __builtin_ctzll(live);
-    live &= live - 1;
-    const int64_t slot = s0 + k;
-    V *trow = table + slot * a.row_cap;
-    const uint8_t *rb[BMAX];
-    bool present[BMAX];
-#pragma unroll
-    for (int b = 0; b < BMAX; ++b) {
-      const int32_t i = __builtin_amdgcn_readlane(idx[b], k);
-      present[b] = (b < B) && i >= 0;
-      rb[b] = present[b] ? a.ss.data[b] + rec0[b] + (int64_t)i * a.stride + 4 : a.zero_chunk;
-    }
-    double ib[IMP ? BMAX : 1];
-#pragma unroll
-    for (int b = 0; b < (IMP ? BMAX : 1); ++b) ib[b] = 0.0;
-    for (int64_t c0 = 0; c0 < a.cap; c0 += 256) {
-      V t[4];
-      V u[BMAX][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t e = c0 + lane + 64 * j;
-        t[j] = e < a.cap ? trow[e] : V(0);
-      }
-#pragma unroll
-      for (int b = 0; b < BMAX; ++b) {
-        const uint8_t *base = present[b] ? rb[b] + c0 * (int64_t)sizeof(V) : a.zero_chunk;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t e = c0 + lane + 64 * j;
-          u[b][j] = e < a.cap ? Elem<V>::load_rec(base + (lane + 64 * j) * sizeof(V)) : V(0);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        V acc = t[j];
-        const int64_t e = c0 + lane + 64 * j;
-#pragma unroll
-        for (int b = 0; b < BMAX; ++b)
-          if (present[b]) {
-            if constexpr (IMP) {
-              if (e < a.cap) ib[b] += imp_term<V>(acc, u[b][j]);
-            }
-            acc = Elem<V>::add(acc, u[b][j]);
-          }
-        if (e < a.cap) trow[e] = acc;
-      }
-    }
-    if constexpr (IMP) {
-      double tot = a.imp[slot];
-#pragma unroll
-      for (int b = 0; b < BMAX; ++b)
-        if (present[b]) tot += wave_sum_f64(ib[b]);
-      if (lane == 0) a.imp[slot] = tot;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // dense_apply_v2: 16 bytes per lane per load.  Record payloads start 4 bytes after a
 // row id, so they are only 4-byte aligned: the loads are unaligned global_load_dwordx4
@@ -519,9 +377,11 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p) {
 }
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
 
-// Four binary16 record values (8 bytes, 2-byte aligned) -> four f32 bit patterns.
+// Four binary16 record values (8 bytes, 2-byte aligned) -> four f32 bit patterns, by the
+// hardware conversion (NaN payloads kept and quieted; every value then goes through
+// `row += u`, which quiets anyway).
 typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
-template <bool NT, bool HWNAN = false>
+template <bool NT>
 __device__ __forceinline__ u32x4 load_h4(const uint8_t *p) {
   uint32_t w0, w1;
   if constexpr (NT) {
@@ -532,11 +392,8 @@ __device__ __forceinline__ u32x4 load_h4(const uint8_t *p) {
     __builtin_memcpy(&w0, p, 4);
     __builtin_memcpy(&w1, p + 4, 4);
   }
-  if constexpr (HWNAN)   // the hardware conversion alone: NaNs come out quieted
-    return u32x4{half_to_f32_bits_hw(w0 & 0xffffu), half_to_f32_bits_hw(w0 >> 16),
-                 half_to_f32_bits_hw(w1 & 0xffffu), half_to_f32_bits_hw(w1 >> 16)};
-  return u32x4{half_to_f32_bits(w0 & 0xffffu), half_to_f32_bits(w0 >> 16), half_to_f32_bits(w1 & 0xffffu),
-               half_to_f32_bits(w1 >> 16)};
+  return u32x4{half_to_f32_bits_hw(w0 & 0xffffu), half_to_f32_bits_hw(w0 >> 16), half_to_f32_bits_hw(w1 & 0xffffu),
+               half_to_f32_bits_hw(w1 >> 16)};
 }
 
 template <typename V> struct Vec;
@@ -600,14 +457,14 @@ __device__ __forceinline__ double vec_imp(u32x4 a, u32x4 b) {
   return r;
 }
 
-// IMP: also accumulate the rows' importance (see dense_apply_kernel) into imp[slot]; here
+// IMP: also accumulate each record's NSSumImpCalc importance, sum_i |u_i / v_i| with v_i
+// the value before that record's add (ns_sum_imp_calc.hpp:79-98), into imp[slot]; here
 // all of a row's terms of one call share one f64 accumulator (non-negative terms: within
 // (cap*B-1)*2^-53 relative of the reference's record-by-record sum).
 // H16 (f32 tables with kDenseRowOpLogFloat16 records): record payloads are binary16, so a
 // lane's 4 elements come from one 8-byte load and are decompressed before the add
-// (1: NaN payloads kept unquieted as the oracle restates it; 2: hardware conversion only).
-// STNT: the updated table row is written with non-temporal stores (rows 16-byte aligned).
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0, bool STNT = false>
+// (2: the hardware conversion).
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0>
 __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;        // elements per 16-byte lane vector
@@ -617,7 +474,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int B = a.B;
 
-  bool skip = (*a.call_status & kStFatal) != 0 || (*a.sticky & kStDuplicateRow) != 0;
+  bool skip = (*a.call_status & (kStFatal | kStDuplicateRow)) != 0 || (*a.sticky & kStDuplicateRow) != 0;
   bool dup = false;
   const uint8_t *pay0[BMAX];   // payload of record 0 of message b (nullptr: table absent)
 #pragma unroll
@@ -710,7 +567,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
           for (int b = 0; b < BMAX; ++b) {
             if constexpr (H16) {
               const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * 2 : a.zero_chunk + lane * 8;
-              u[q][b] = full ? load_h4<NT, H16 == 2>(src) : u32x4{0, 0, 0, 0};
+              u[q][b] = full ? load_h4<NT>(src) : u32x4{0, 0, 0, 0};
             } else {
               const uint8_t *src = pres[q][b] ? rp[q][b] + e0 * VS : a.zero_chunk + lane * 16;
               u[q][b] = full ? load16<NT>(src) : u32x4{0, 0, 0, 0};
@@ -728,12 +585,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
               }
               acc = Vec<V>::add(acc, u[q][b]);
             }
-          if (full && has[q]) {
-            if constexpr (STNT)
-              __builtin_nontemporal_store(acc, reinterpret_cast<u32x4 *>(trow[q] + e0 * VS));
-            else
-              store16(trow[q] + e0 * VS, acc);
-          }
+          if (full && has[q]) store16(trow[q] + e0 * VS, acc);
         }
       }
       // ragged tail (cap % EPV elements): element-wise on the first lanes
@@ -751,7 +603,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
                 if constexpr (H16) {
                   uint16_t h;
                   __builtin_memcpy(&h, rp[q][b] + e * 2, 2);
-                  u = __builtin_bit_cast(V, H16 == 2 ? half_to_f32_bits_hw(h) : half_to_f32_bits(h));
+                  u = __builtin_bit_cast(V, half_to_f32_bits_hw(h));
                 } else {
                   u = Elem<V>::load_rec(rp[q][b] + e * VS);
                 }
@@ -791,22 +643,19 @@ __device__ __forceinline__ u32x4 gload16(const uint8_t *base, uint32_t off) {
   else return *p;
 }
 
-template <bool NT, bool HWNAN>
+template <bool NT>
 __device__ __forceinline__ u32x4 gload_h4(const uint8_t *base, uint32_t off) {
   const gu32x2_p p = (gu32x2_p)((gbyte_p)base + off);
   u32x2_a2g v;
   if constexpr (NT) v = __builtin_nontemporal_load(p);
   else v = *p;
   const uint32_t w0 = v[0], w1 = v[1];
-  if constexpr (HWNAN)
-    return u32x4{half_to_f32_bits_hw(w0 & 0xffffu), half_to_f32_bits_hw(w0 >> 16),
-                 half_to_f32_bits_hw(w1 & 0xffffu), half_to_f32_bits_hw(w1 >> 16)};
-  return u32x4{half_to_f32_bits(w0 & 0xffffu), half_to_f32_bits(w0 >> 16), half_to_f32_bits(w1 & 0xffffu),
-               half_to_f32_bits(w1 >> 16)};
+  return u32x4{half_to_f32_bits_hw(w0 & 0xffffu), half_to_f32_bits_hw(w0 >> 16), half_to_f32_bits_hw(w1 & 0xffffu),
+               half_to_f32_bits_hw(w1 >> 16)};
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0, int OCC = 1>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) dense_apply_v3_kernel(DenseArgs a) {
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP, int H16 = 0>
+__global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
   static_assert(PAIR * BMAX <= 32, "presence mask is 32 bits");
   constexpr int VS = (int)sizeof(V);
   constexpr int EPV = 16 / VS;
@@ -817,7 +666,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int B = a.B;
 
-  bool skip = (*a.call_status & kStFatal) != 0 || (*a.sticky & kStDuplicateRow) != 0;
+  bool skip = (*a.call_status & (kStFatal | kStDuplicateRow)) != 0 || (*a.sticky & kStDuplicateRow) != 0;
   bool dup = false;
   const uint8_t *pay0[BMAX];
   uint32_t real = 0;   // bit b: message b holds this table
@@ -918,7 +767,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
             const bool pr = (presm >> (q * BMAX + b)) & 1u;
             const uint32_t off = full ? (pr ? voff[q][b] : lane_off) + coff : 0u;
             if constexpr (H16)
-              u[q][b] = gload_h4<NT, H16 == 2>(pay0[b], off);
+              u[q][b] = gload_h4<NT>(pay0[b], off);
             else
               u[q][b] = gload16<NT>(pay0[b], off);
           }
@@ -952,7 +801,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
                 if constexpr (H16) {
                   uint16_t h;
                   __builtin_memcpy(&h, rec + e * 2, 2);
-                  u = __builtin_bit_cast(V, H16 == 2 ? half_to_f32_bits_hw(h) : half_to_f32_bits(h));
+                  u = __builtin_bit_cast(V, half_to_f32_bits_hw(h));
                 } else {
                   u = Elem<V>::load_rec(rec + e * VS);
                 }
@@ -992,7 +841,7 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int B = a.B;
 
-  bool skip = (*a.call_status & kStFatal) != 0 || (*a.sticky & kStDuplicateRow) != 0;
+  bool skip = (*a.call_status & (kStFatal | kStDuplicateRow)) != 0 || (*a.sticky & kStDuplicateRow) != 0;
   bool dup = false;
   const uint8_t *pay0[BMAX];
 #pragma unroll
@@ -1162,43 +1011,6 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
   }
 }
 
-// dense_index_xcd: message b's records go to the blocks of XCD group b % 8 (blocks are
-// dealt round-robin over the 8 XCDs, MI355X_MICROARCH.md "Workgroup dispatch"), so one
-// message's scattered 4-byte stores land in one XCD's L2 (its max_rows*4-byte window of
-// the batch-major index) and can merge there before they are written back, instead of
-// leaving as one 64-byte write request each.  Used when B is a multiple of 8.
-template <int UNROLL>
-__global__ void __launch_bounds__(256) dense_index_xcd_kernel(StreamSet ss, const Seg *segs, int t, int B,
-                                                             int64_t stride, Geo g, int32_t *inv, InvLayout L,
-                                                             uint32_t *call_status) {
-  const int grp = blockIdx.x & 7;
-  const int64_t G = (int64_t)(gridDim.x >> 3) * blockDim.x;   // threads per XCD group
-  const int64_t tid = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x;
-  for (int b = grp; b < B; b += 8) {
-    const Seg sg = segs[b * kMaxTables + t];
-    if (sg.rec0 < 0 || sg.sparse) continue;
-    const uint8_t *base = ss.data[b] + sg.rec0;
-    const int64_t n = sg.num_rows;
-    int32_t *invb = inv + b * L.sb;
-    for (int64_t r0 = tid; r0 < n; r0 += G * UNROLL) {
-      int32_t rid[UNROLL];
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const int64_t r = r0 + u * G;
-        rid[u] = r < n ? __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(base + r * stride)) : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const int64_t r = r0 + u * G;
-        if (r >= n) continue;
-        const int64_t sl = slot_of(rid[u], g);
-        if (sl < 0) { atomicOr(call_status, kStRowRange); continue; }
-        invb[sl * L.ss] = (int32_t)r;
-      }
-    }
-  }
-}
-
 // finish_call: fold the per-call status into the sticky word and free the ring slot.
 __global__ void finish_call_kernel(uint32_t *sticky, uint32_t *call_status, uint32_t *call_log) {
   if (threadIdx.x == 0) {
@@ -1255,36 +1067,22 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
   return hipGetLastError();
 }
 
-int g_index_variant = 2;
-int g_apply_variant = 10;   // v3 (saddr record loads; v2 when a stream is >= 4 GiB): 1% over v2 (6)
-int g_h16_variant = 2;     // v3 + hardware conversion
-int g_inv_layout = 1;
+// Run-time selectors (include/psx_debug.h): the defaults are the measured winners; the
+// alternatives stay selectable so the parity suite runs every kernel the product can
+// launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
+int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads
+int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact), 3: v3 with plain record loads
 
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows,
                               int32_t *inv, InvLayout L, uint32_t *call_status, hipStream_t st) {
   Geo g{row_offset, row_stride, max_rows};
-  switch (g_index_variant) {
-    case 0:
-      hipLaunchKernelGGL(dense_index_kernel, dim3(4096), dim3(256), 0, st, ss, segs, t, B, stride, g,
-                         inv, L, call_status);
-      break;
-    case 1:
-      hipLaunchKernelGGL((dense_index_v2_kernel<8, false>), dim3(2048), dim3(256), 0, st, ss, segs, t, B,
-                         stride, g, inv, L, call_status);
-      break;
-    case 3:
-      if (B % 8 == 0) {
-        hipLaunchKernelGGL((dense_index_xcd_kernel<8>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g,
-                           inv, L, call_status);
-        break;
-      }
-      [[fallthrough]];
-    default:
-      hipLaunchKernelGGL((dense_index_v2_kernel<8, true>), dim3(2048), dim3(256), 0, st, ss, segs, t, B,
-                         stride, g, inv, L, call_status);
-      break;
-  }
+  if (g_index_variant == 1)
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, false>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g,
+                       inv, L, call_status);
+  else
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, true>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g,
+                       inv, L, call_status);
   return hipGetLastError();
 }
 
@@ -1316,46 +1114,63 @@ static unsigned resident_blocks(K kernel, int64_t want) {
   return (unsigned)(cap < 1 ? 1 : cap);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0, bool STNT = false>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>
 static void launch_v2(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16, STNT>;
+  auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
 }
 
-template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0, int OCC = 1>
+template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>
 static void launch_v3(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v3_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16, OCC>;
+  auto k = dense_apply_v3_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
 }
 
-template <typename V, bool IMP, int H16>
+// BMAX is the next power of two >= B and the rows in flight per wave grow as B shrinks,
+// so every wave keeps ~8-18 16-byte loads in flight whatever the batch width.
+template <typename V, bool IMP, int H16, bool NT = true>
 static void launch_adaptive_v3(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 1) launch_v3<V, 1, 16, true, 8, IMP, H16>(a, st);
-  else if (a.B <= 2) launch_v3<V, 2, 16, true, 4, IMP, H16>(a, st);
-  else if (a.B <= 4) launch_v3<V, 4, 16, true, 3, IMP, H16>(a, st);
-  else if (a.B <= 8) launch_v3<V, 8, 16, true, 2, IMP, H16>(a, st);
-  else launch_v3<V, 16, 16, true, 1, IMP, H16>(a, st);
+  if (a.B <= 1) launch_v3<V, 1, 16, NT, 8, IMP, H16>(a, st);
+  else if (a.B <= 2) launch_v3<V, 2, 16, NT, 4, IMP, H16>(a, st);
+  else if (a.B <= 4) launch_v3<V, 4, 16, NT, 3, IMP, H16>(a, st);
+  else if (a.B <= 8) launch_v3<V, 8, 16, NT, 2, IMP, H16>(a, st);
+  else launch_v3<V, 16, 16, NT, 1, IMP, H16>(a, st);
 }
 
-template <typename V, int BMAX, int PAIR, int M>
-static void launch_v4(const DenseArgs &a, hipStream_t st) {
-  auto k = dense_apply_v4_kernel<V, BMAX, 16, true, PAIR, M>;
-  const int64_t tiles = (a.max_rows + 15) / 16;
-  const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
+// v2 (64-bit record pointers): streams of >= 4 GiB, which v3's 32-bit offsets cannot reach.
+template <typename V, int H16>
+static void launch_adaptive_v2(const DenseArgs &a, hipStream_t st) {
+  if (a.B <= 1) launch_v2<V, 1, 16, true, 8, false, H16>(a, st);
+  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4, false, H16>(a, st);
+  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3, false, H16>(a, st);
+  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2, false, H16>(a, st);
+  else launch_v2<V, 16, 16, true, 1, false, H16>(a, st);
+}
+
+// Importance tables: the f64 terms cost registers, so fewer rows in flight per wave buys
+// back occupancy.
+template <typename V, int H16>
+static void launch_adaptive_imp(const DenseArgs &a, hipStream_t st) {
+  if (a.B <= 1) launch_v2<V, 1, 16, true, 4, true, H16>(a, st);
+  else if (a.B <= 2) launch_v2<V, 2, 16, true, 2, true, H16>(a, st);
+  else if (a.B <= 4) launch_v2<V, 4, 16, true, 2, true, H16>(a, st);
+  else if (a.B <= 8) launch_v2<V, 8, 16, true, 1, true, H16>(a, st);
+  else launch_v2<V, 16, 16, true, 1, true, H16>(a, st);
 }
 
 template <typename V>
-static void launch_compact(const DenseArgs &a, hipStream_t st) {
-  // g_apply_variant 11: 8 rows / 16 slots, 12: 4 rows / 8 slots, 13: 4 rows / 12 slots
-  if (a.B > 8) launch_v4<V, 16, 8, 16>(a, st);
-  else if (g_apply_variant == 12) launch_v4<V, 8, 4, 8>(a, st);
-  else if (g_apply_variant == 13) launch_v4<V, 8, 4, 12>(a, st);
-  else launch_v4<V, 8, 8, 16>(a, st);
+static void launch_v4(const DenseArgs &a, hipStream_t st) {
+  if (a.B > 8) {
+    auto k = dense_apply_v4_kernel<V, 16, 16, true, 8, 16>;
+    hipLaunchKernelGGL(k, dim3(resident_blocks(k, ((a.max_rows + 15) / 16 + 3) / 4)), dim3(256), 0, st, a);
+  } else {
+    auto k = dense_apply_v4_kernel<V, 8, 16, true, 4, 12>;
+    hipLaunchKernelGGL(k, dim3(resident_blocks(k, ((a.max_rows + 15) / 16 + 3) / 4)), dim3(256), 0, st, a);
+  }
 }
 
 // v3 addresses records by 32-bit offsets from each message's first record.
@@ -1375,126 +1190,25 @@ static bool sparse_coverage(const DenseArgs &a) {
   return a.B <= 8 && bytes / (uint64_t)a.stride <= 2 * (uint64_t)a.max_rows;
 }
 
-template <typename V, int BMAX>
-static void launch_apply_bmax(const DenseArgs &a, hipStream_t st) {
-  switch (g_apply_variant) {
-    case 0: {
-      const int64_t tiles = (a.max_rows + 63) / 64;
-      hipLaunchKernelGGL((dense_apply_kernel<V, BMAX, false>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, a);
-      break;
-    }
-    case 1: launch_v2<V, BMAX, 64, false, 1>(a, st); break;
-    case 2: launch_v2<V, BMAX, 64, true, 1>(a, st); break;
-    case 3: launch_v2<V, BMAX, 16, true, 1>(a, st); break;
-    case 4: launch_v2<V, BMAX, 16, true, 2>(a, st); break;
-    case 7:   // non-temporal table stores (16-byte aligned rows only)
-      if ((a.row_cap * (int64_t)sizeof(V)) % 16 == 0) launch_v2<V, BMAX, 16, true, 2, false, false, true>(a, st);
-      else launch_v2<V, BMAX, 16, true, 2>(a, st);
-      break;
-    case 8: launch_v2<V, BMAX, 16, true, 3>(a, st); break;
-    case 9: launch_v2<V, BMAX, 32, true, 2>(a, st); break;
-    default: launch_v2<V, BMAX, 64, true, 2>(a, st); break;
-  }
-}
-
-// Variant 6 (default): the message-count template BMAX is the next power of two >= B
-// and the number of rows in flight per wave grows as B shrinks, so every wave keeps
-// ~8-18 16-byte loads in flight whatever the batch width (B = 1 for a single message).
-template <typename V>
-static void launch_adaptive(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 1) launch_v2<V, 1, 16, true, 8>(a, st);
-  else if (a.B <= 2) launch_v2<V, 2, 16, true, 4>(a, st);
-  else if (a.B <= 4) launch_v2<V, 4, 16, true, 3>(a, st);
-  else if (a.B <= 8) launch_v2<V, 8, 16, true, 2>(a, st);
-  else launch_v2<V, 16, 16, true, 1>(a, st);
-}
-
-// Importance tables: the f64 terms cost registers, so fewer rows in flight per wave
-// buys back occupancy (PSX_IMP_PAIR=2 selects the plain table's pairing for A/B).
-int g_imp_pair = 1;
-template <typename V>
-static void launch_adaptive_imp(const DenseArgs &a, hipStream_t st) {
-  if (g_imp_pair >= 2) {
-    if (a.B <= 1) launch_v2<V, 1, 16, true, 8, true>(a, st);
-    else if (a.B <= 2) launch_v2<V, 2, 16, true, 4, true>(a, st);
-    else if (a.B <= 4) launch_v2<V, 4, 16, true, 3, true>(a, st);
-    else if (a.B <= 8) launch_v2<V, 8, 16, true, 2, true>(a, st);
-    else launch_v2<V, 16, 16, true, 1, true>(a, st);
-  } else {
-    if (a.B <= 1) launch_v2<V, 1, 16, true, 4, true>(a, st);
-    else if (a.B <= 2) launch_v2<V, 2, 16, true, 2, true>(a, st);
-    else if (a.B <= 4) launch_v2<V, 4, 16, true, 2, true>(a, st);
-    else if (a.B <= 8) launch_v2<V, 8, 16, true, 1, true>(a, st);
-    else launch_v2<V, 16, 16, true, 1, true>(a, st);
-  }
-}
-
-// f32 tables with binary16 records (kDenseRowOpLogFloat16): half the record bytes per
-// element, so more rows in flight per wave at the same load count.
-template <bool IMP>
-static void launch_adaptive_h16(const DenseArgs &a, hipStream_t st) {
-  // Decompression by the hardware conversion alone (H16 = 2): it keeps NaN payloads and
-  // quiets them, and every decompressed value goes through `row += u`, which quiets
-  // anyway, so rows are bit-identical to the payload-exact decompression (H16 = 1,
-  // g_h16_variant 1) at 23% less time on C2 (VALU-bound: 2.02 -> 1.57 ms, A/B in
-  // profiles/r01/exp_f16_variants.txt).
-  if (g_h16_variant == 3 && v3_ok(a) && a.B > 4 && a.B <= 8) {   // 5 waves/SIMD
-    launch_v3<float, 8, 16, true, 2, IMP, 2, 5>(a, st);
-    return;
-  }
-  if (g_h16_variant >= 2 && v3_ok(a)) {   // default
-    launch_adaptive_v3<float, IMP, 2>(a, st);
-    return;
-  }
-  if (g_h16_variant == 1) {   // payload-exact NaN decompression (v2)
-    if (a.B <= 1) launch_v2<float, 1, 16, true, 8, IMP, 1>(a, st);
-    else if (a.B <= 2) launch_v2<float, 2, 16, true, 4, IMP, 1>(a, st);
-    else if (a.B <= 4) launch_v2<float, 4, 16, true, 3, IMP, 1>(a, st);
-    else if (a.B <= 8) launch_v2<float, 8, 16, true, 2, IMP, 1>(a, st);
-    else launch_v2<float, 16, 16, true, 1, IMP, 1>(a, st);
-    return;
-  }
-  if (a.B <= 1) launch_v2<float, 1, 16, true, 8, IMP, 2>(a, st);
-  else if (a.B <= 2) launch_v2<float, 2, 16, true, 4, IMP, 2>(a, st);
-  else if (a.B <= 4) launch_v2<float, 4, 16, true, 3, IMP, 2>(a, st);
-  else if (a.B <= 8) launch_v2<float, 8, 16, true, 2, IMP, 2>(a, st);
-  else launch_v2<float, 16, 16, true, 1, IMP, 2>(a, st);
-}
-
 template <typename V>
 static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
-  const int64_t tiles = (a.max_rows + 63) / 64;
-  const dim3 grid((unsigned)((tiles + 3) / 4));
-  if (a.imp) {   // importance tables (SSPAggr): same kernels plus the f64 importance sums
-    if (g_apply_variant == 0) {
-      if (a.B <= 8)
-        hipLaunchKernelGGL((dense_apply_kernel<V, 8, true>), grid, dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((dense_apply_kernel<V, 16, true>), grid, dim3(256), 0, st, a);
-    } else {
-      launch_adaptive_imp<V>(a, st);
-    }
-  } else if (g_apply_variant == 10 && v3_ok(a) && sparse_coverage(a))
-    launch_v4<V, 8, 4, 12>(a, st);
-  else if (g_apply_variant == 10 && v3_ok(a))
-    launch_adaptive_v3<V, false, 0>(a, st);
-  else if (g_apply_variant >= 11 && g_apply_variant <= 13)
-    launch_compact<V>(a, st);
-  else if (g_apply_variant == 14 && v3_ok(a) && a.B > 4 && a.B <= 8)
-    launch_v3<V, 8, 16, true, 2, false, 0, 5>(a, st);   // 5 waves/SIMD
-  else if (g_apply_variant == 6 || g_apply_variant == 10)
-    launch_adaptive<V>(a, st);
-  else if (a.B <= 8)
-    launch_apply_bmax<V, 8>(a, st);
-  else
-    launch_apply_bmax<V, 16>(a, st);
+  if (a.imp) launch_adaptive_imp<V, 0>(a, st);
+  else if (g_apply_variant == 1 || !v3_ok(a)) launch_adaptive_v2<V, 0>(a, st);
+  else if (g_apply_variant == 2 || (g_apply_variant == 0 && sparse_coverage(a))) launch_v4<V>(a, st);
+  else if (g_apply_variant == 3) launch_adaptive_v3<V, false, 0, false>(a, st);
+  else launch_adaptive_v3<V, false, 0>(a, st);
   return hipGetLastError();
 }
 
 hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st, bool rec_f16) {
   if (rec_f16) {   // f32 tables only (checked at table creation)
-    if (a.imp) launch_adaptive_h16<true>(a, st);
-    else launch_adaptive_h16<false>(a, st);
+    // binary16 records decompressed by the hardware conversion (H16 = 2): it keeps NaN
+    // payloads and quiets them, and every decompressed value goes through `row += u`,
+    // which quiets anyway, so rows are bit-identical to the payload-exact decompression
+    // at 23% less time on C2 (VALU-bound, profiles/r01/exp_f16_variants.txt).
+    if (a.imp) launch_adaptive_imp<float, 2>(a, st);
+    else if (g_apply_variant == 1 || !v3_ok(a)) launch_adaptive_v2<float, 2>(a, st);
+    else launch_adaptive_v3<float, false, 2>(a, st);
     return hipGetLastError();
   }
   switch (dtype) {

@@ -9,6 +9,10 @@
 //   ordered_fill   list[off[slot] + --cnt[slot]] = flattened record number r
 //                  (r orders records by (message, position) = reference apply order;
 //                  cnt returns to zero, the invariant between calls)
+//   capacity check (sorted/map tables whose keys ever left [0, max_entries)): a dry run of
+//                  the apply on the rows whose entries + the call's record entries exceed
+//                  max_entries; a row that would overflow fails the whole call
+//                  (kStCapacity) before anything is applied
 //   ordered_apply  one wave per touched slot: sort the slot's r-list, then apply the
 //                  records in order with the reference store semantics:
 //                    DenseRow     VectorStore::Inc          vector_store.hpp:100-102
@@ -107,6 +111,13 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
           const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
           for (int32_t i = 0; i < n; ++i)
             if (cols[i] < 0 || cols[i] >= a.row_cap) { atomicOr(a.call_status, kStCapacity); break; }
+        } else if (a.kind != 0 && a.keyflag && !*a.keyflag) {
+          // sorted/map rows: while every key stays in [0, max_entries) no row can hold
+          // more than max_entries entries and the capacity dry run is skipped
+          const int32_t n = o_ld32(p + 4);
+          const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
+          for (int32_t i = 0; i < n; ++i)
+            if (cols[i] < 0 || cols[i] >= a.max_entries) { atomicOr(a.keyflag, 1u); break; }
         }
         first = atomicAdd(&a.cnt[s], 1) == 0;
       }
@@ -149,6 +160,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int32_t wave_sum_i32(int32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
 }
 
 template <typename V> struct OV;
@@ -221,7 +238,9 @@ __device__ __forceinline__ double sparse_importance(const uint8_t *vals, int32_t
   return wave_sum_f64(p);
 }
 
-template <typename V, int KIND>
+// DRY: the capacity dry run — same walk on the LDS image, nothing written back; only rows
+// whose entries plus the call's record entries exceed max_entries are simulated.
+template <typename V, int KIND, bool DRY = false>
 __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ int32_t sort_scratch[4][64];
@@ -231,7 +250,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   if (wib >= wpb) return;
-  const bool go = o_gate(a);
+  const bool go = o_gate(a) && (!DRY || *a.keyflag);
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
   uint8_t *E = dyn + (size_t)wib * (size_t)a.max_entries * ES;   // this wave's row image
   const int64_t wave_g = (int64_t)blockIdx.x * wpb + wib;
@@ -241,11 +260,22 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
   const int64_t nt = go ? (int64_t)*a.ntouched : 0;
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
     const int64_t slot = a.touched[ti];
-    if (lane == 0) a.flags[slot] = 3;
+    if (!DRY && lane == 0) a.flags[slot] = 3;
     {
       const int32_t beg = a.off[slot];
       const int32_t L = a.off[slot + 1] - beg;
       int32_t *lst = a.list + beg;
+      if constexpr (DRY) {
+        int32_t grow = 0;
+        for (int32_t q = lane; q < L; q += 64) {
+          int b;
+          uint64_t roff;
+          locate(a, rs, lst[q], b, roff);
+          grow += o_ld32(a.ss.data[b] + roff + 4);
+        }
+        grow = wave_sum_i32(grow);
+        if ((int64_t)a.nent[slot] + grow <= a.max_entries) continue;
+      }
       // order the slot's records by r = (message, position)
       int32_t mine = 0;
       if (L <= 64) {
@@ -275,7 +305,8 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
       uint8_t *drow = reinterpret_cast<uint8_t *>(a.dense) + slot * a.row_cap * (int64_t)sizeof(V);
       double impt = a.imp ? a.imp[slot] : 0.0;
 
-      for (int32_t q = 0; q < L; ++q) {
+      bool over = false;   // DRY: this row would exceed max_entries
+      for (int32_t q = 0; q < L && !over; ++q) {
         const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
         int b;
         uint64_t roff;
@@ -327,7 +358,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
           continue;
         }
         // sorted-map / map rows: each Inc(col, delta) in order, wave-parallel over entries
-        for (int32_t i = 0; i < nn; ++i) {
+        for (int32_t i = 0; i < nn && !over; ++i) {
           const int32_t key = o_ld32(cols + i * 4);
           const V delta = ldv<V>(vals + (int64_t)i * sizeof(V));
           if (delta == V(0)) continue;                         // :306
@@ -341,6 +372,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
           if (idx < 0) {
             if (n >= a.max_entries) {
               if (lane == 0) atomicOr(a.call_status, kStCapacity);
+              over = DRY;
               continue;
             }
             int32_t p = n;
@@ -405,6 +437,10 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
           }
         }
       }
+      if (DRY) {
+        wave_sync();
+        continue;
+      }
       if (KIND != 0) {
         uint32_t *dst = reinterpret_cast<uint32_t *>(a.entries + slot * a.max_entries * ES);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(E);
@@ -459,7 +495,8 @@ __device__ __forceinline__ T bcast(T x, int src) {
 // (entries now + this call's record entries): 1 = rows that fit 64*J entries (the others
 // are marked with flags bit 2), 2 = the marked rows, 0 = every row.  Small rows then run
 // at the small image's occupancy.
-template <typename V, int KIND, int J, int CLS = 0>
+// DRY: the capacity dry run (see ordered_apply_kernel); J must hold max_entries.
+template <typename V, int KIND, int J, int CLS = 0, bool DRY = false>
 __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
   __shared__ int32_t sort_scratch[4][64];
@@ -467,7 +504,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
-  const bool go = o_gate(a);
+  const bool go = o_gate(a) && (!DRY || *a.keyflag);
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + wib;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -480,7 +517,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
     if constexpr (CLS == 2) {   // only the rows the CLS = 1 launch marked (flags bit 2)
       if (!(a.flags[slot] & 4)) continue;
     }
-    if (lane == 0) a.flags[slot] = 3;
+    if (!DRY && lane == 0) a.flags[slot] = 3;
     {
       const int32_t beg = a.off[slot];
       const int32_t L = a.off[slot + 1] - beg;
@@ -501,6 +538,16 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         __builtin_amdgcn_wave_barrier();
       }
       int32_t n = a.nent[slot];
+      if constexpr (DRY) {
+        int32_t grow = 0;
+        for (int32_t q = lane; q < L; q += 64) {
+          int b;
+          uint64_t roff;
+          locate(a, rs, L <= 64 ? mine : lst[q], b, roff);
+          grow += o_ld32(a.ss.data[b] + roff + 4);
+        }
+        if ((int64_t)n + wave_sum_i32(grow) <= (int64_t)cap) continue;
+      }
       if constexpr (CLS == 1) {
         // classify on the row as it is before this call; a row too big for the J-image
         // is marked (flags bit 2) for the CLS = 2 launch, which clears the mark
@@ -530,7 +577,8 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         val[j] = i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
       }
       double impt = a.imp ? a.imp[slot] : 0.0;
-      for (int32_t q = 0; q < L; ++q) {
+      bool over = false;   // DRY: this row would exceed max_entries
+      for (int32_t q = 0; q < L && !over; ++q) {
         const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
         int b;
         uint64_t roff;
@@ -540,12 +588,12 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         const uint8_t *cols = rec + 8;
         const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
         if (a.imp) impt += sparse_importance<V>(vals, nn, lane);
-        for (int32_t c0 = 0; c0 < nn; c0 += 64) {
+        for (int32_t c0 = 0; c0 < nn && !over; c0 += 64) {
           const int32_t pi = c0 + lane;
           const int32_t my_col = pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0;
           const V my_d = pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0);
           const int32_t cnt = nn - c0 < 64 ? nn - c0 : 64;
-          for (int32_t t = 0; t < cnt; ++t) {
+          for (int32_t t = 0; t < cnt && !over; ++t) {
             const int32_t c = __builtin_amdgcn_readlane(my_col, t);
             const V d = bcast(my_d, t);
             if (d == V(0)) continue;                                  // :306
@@ -560,6 +608,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
             if (idx < 0) {
               if (n >= cap) {
                 if (lane == 0) atomicOr(a.call_status, kStCapacity);
+                over = DRY;
                 continue;
               }
               int32_t p = n;
@@ -659,6 +708,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
           }
         }
       }
+      if (DRY) continue;
       // write the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)
       uint8_t *wrow = a.entries + slot * a.max_entries * ES;
 #pragma unroll
@@ -694,32 +744,77 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 
 // ---------------------------------------------------------------------------
 int g_ord_split = 1;  // rows of > 256-entry tables split into a 256-entry and a 1,024-entry image launch
-int g_ord_grid = 1;   // reg-kernel grid: 0 by 64-row tiles, 1 by rows (<= 4096 blocks), 2 by rows (<= 8192)
 
-hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
-  const int64_t n = a.max_rows;
+// One touched row per wave at a time: the grid is sized by rows (the touched count is on
+// the device), not by 64-row tiles — 100K rows as tiles gave 1,564 waves for ~35K touched
+// rows, 1.5 waves per SIMD (profiles/r01/exp_c3_grid.txt).
+static unsigned row_blocks(int64_t n, int wpb) {
+  int64_t blocks = (n + wpb - 1) / wpb;
+  if (blocks > 4096) blocks = 4096;
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
+static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
+  const int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
+  const int64_t per_wave = a.kind == 0 ? 0 : a.max_entries * esz;
+  int w = 4;
+  while (w > 1 && per_wave * w > 150 * 1024) --w;
+  *wpb = w;
+  *lds = (size_t)per_wave * w;
+}
+
+template <typename V, int KIND>
+static void launch_dry(const OrdArgs &a, int dtype, hipStream_t st) {
+  const unsigned blocks = row_blocks(a.max_rows, 4);
+  if (a.max_entries <= 64)
+    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+  else if (a.max_entries <= 256)
+    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+  else if (a.max_entries <= 1024)
+    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+  else {
+    int wpb;
+    size_t lds;
+    lds_geometry(dtype, a, &wpb, &lds);
+    hipLaunchKernelGGL((ordered_apply_kernel<V, KIND, true>), dim3(row_blocks(a.max_rows, wpb)), dim3(256), lds, st,
+                       a, wpb);
+  }
+}
+
+// Stage 1 of the ordered path (before any table of the call is applied): record lists by
+// slot, every validation, and the capacity dry run of sorted/map tables.
+hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
-  launch_exclusive_scan<int32_t>(a.cnt, n, a.off, a.tsum, st);
+  launch_exclusive_scan<int32_t>(a.cnt, a.max_rows, a.off, a.tsum, st);
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
-  const int64_t tiles = (n + 63) / 64;
+  if (a.kind != 0 && !a.dense_records && a.keyflag) {
+#define PSX_DRY(V) do { if (a.kind == 1) launch_dry<V, 1>(a, dtype, st); else launch_dry<V, 2>(a, dtype, st); } while (0)
+    switch (dtype) {
+      case 0: PSX_DRY(float); break;
+      case 1: PSX_DRY(double); break;
+      case 2: PSX_DRY(int32_t); break;
+      default: PSX_DRY(int64_t); break;
+    }
+#undef PSX_DRY
+  }
+  return hipGetLastError();
+}
+
+// Stage 2: the apply (after every table's stage 1 and the duplicate-row gate).
+hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st) {
   if (a.kind != 0 && a.max_entries <= 1024) {
-    // one touched row per wave at a time: size the grid by rows (the touched count is on
-    // the device), not by 64-row tiles — 100K rows as tiles gave 1,564 waves for ~35K
-    // touched rows, 1.5 waves per SIMD (g_ord_grid 0 keeps that for A/B)
-    int64_t blocks = g_ord_grid == 0 ? (tiles + 3) / 4 : (n + 3) / 4;
-    const int64_t cap = g_ord_grid == 2 ? 8192 : 4096;
-    if (blocks > cap) blocks = cap;
+    const unsigned blocks = row_blocks(a.max_rows, 4);
 #define PSX_REG(V, KIND)                                                                           \
   do {                                                                                             \
     if (a.max_entries <= 64)                                                                       \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3(blocks), dim3(256), 0, st, a);   \
     else if (a.max_entries <= 256)                                                                 \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, a);   \
     else if (g_ord_split) {                                                                        \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, 2>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, 1>), dim3(blocks), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, 2>), dim3(blocks), dim3(256), 0, st, a); \
     } else                                                                                         \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3((unsigned)blocks), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, st, a);  \
   } while (0)
 #define PSX_REGK(V) do { if (a.kind == 1) PSX_REG(V, 1); else PSX_REG(V, 2); } while (0)
     switch (dtype) {
@@ -733,21 +828,18 @@ hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st) {
     return hipGetLastError();
   }
   // LDS row images (max_entries > 1024) or dense rows
-  int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
-  int64_t per_wave = a.kind == 0 ? 0 : a.max_entries * esz;
-  int wpb = 4;
-  while (wpb > 1 && per_wave * wpb > 150 * 1024) --wpb;
-  const size_t lds = (size_t)per_wave * wpb;
-  int64_t blocks = g_ord_grid == 0 ? (tiles + wpb - 1) / wpb : (n + wpb - 1) / wpb;   // one row per wave
-  if (blocks > 4096) blocks = 4096;
+  int wpb;
+  size_t lds;
+  lds_geometry(dtype, a, &wpb, &lds);
+  const unsigned blocks = row_blocks(a.max_rows, wpb);
 #define PSX_ORD(V)                                                                                 \
   do {                                                                                             \
     if (a.kind == 0)                                                                               \
-      hipLaunchKernelGGL((ordered_apply_kernel<V, 0>), dim3((unsigned)blocks), dim3(256), lds, st, a, wpb); \
+      hipLaunchKernelGGL((ordered_apply_kernel<V, 0>), dim3(blocks), dim3(256), lds, st, a, wpb);  \
     else if (a.kind == 1)                                                                          \
-      hipLaunchKernelGGL((ordered_apply_kernel<V, 1>), dim3((unsigned)blocks), dim3(256), lds, st, a, wpb); \
+      hipLaunchKernelGGL((ordered_apply_kernel<V, 1>), dim3(blocks), dim3(256), lds, st, a, wpb);  \
     else                                                                                           \
-      hipLaunchKernelGGL((ordered_apply_kernel<V, 2>), dim3((unsigned)blocks), dim3(256), lds, st, a, wpb); \
+      hipLaunchKernelGGL((ordered_apply_kernel<V, 2>), dim3(blocks), dim3(256), lds, st, a, wpb);  \
   } while (0)
   switch (dtype) {
     case 0: PSX_ORD(float); break;

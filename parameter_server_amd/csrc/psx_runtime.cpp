@@ -28,7 +28,6 @@ hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64
                               InvLayout L, uint32_t *call_status, hipStream_t st);
 hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, int64_t max_rows,
                                uint32_t *counters, hipStream_t st);
-extern int g_inv_layout;
 hipError_t launch_finish(uint32_t *sticky, uint32_t *call_status, uint32_t *log, hipStream_t st);
 hipError_t launch_flags_or(uint8_t *flags, int64_t first, int64_t num, uint8_t bits, hipStream_t st);
 hipError_t launch_flags_and(uint8_t *flags, int64_t num, uint8_t bits, hipStream_t st);
@@ -47,9 +46,11 @@ hipError_t launch_ada_init_rows(const AdaArgs &a, const int32_t *slots, const fl
                                 hipStream_t st);
 hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st);
 hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t *sizes, int64_t n,
-                           uint64_t clients, hipStream_t st);
+                           uint64_t clients, const uint64_t *subs, int check_only, hipStream_t st);
 hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
-hipError_t launch_ordered(int dtype, const OrdArgs &a, hipStream_t st);
+hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st);
+hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st);
+hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st);
 hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
                        uint32_t *call_status, hipStream_t st);
 hipError_t launch_serve_sizes(const ServeArgs &a, hipStream_t st);
@@ -87,6 +88,7 @@ struct TableState {
   int32_t *d_off = nullptr;        // ordered path: exclusive prefix (max_rows + 1)
   int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
+  uint32_t *d_keyflag = nullptr;   // sorted/map: a key outside [0, max_entries) was seen
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
   double *d_imp = nullptr;         // accum_importance: ServerRow::importance_ per slot
@@ -127,7 +129,7 @@ struct TableState {
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_srv_sizes, t.d_srv_offs,
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_srv_sizes, t.d_srv_offs,
                   t.d_imp, t.d_ver, t.d_acc, t.d_z, t.d_zmax, t.d_snap_ver, t.d_snap_cnt, t.d_snap_acc,
                   t.d_ada_words, t.d_new_keys, t.d_new_slots, t.d_new_tmp, t.d_init, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
@@ -360,8 +362,23 @@ bool has_sparse_serialized(const psx_ctx *c) {
   return false;
 }
 
+// Smallest record of any table in the context: bounds the records a message can hold
+// (ordered-path record lists are sized by it).  Sparse records are >= 8 bytes
+// ({int32 row_id; int32 n}); dense ones 4 + dense_body.
+size_t min_record_bytes(const psx_ctx *c) {
+  int64_t m = 8;
+  for (auto &t : c->tables)
+    if (t.cfg.oplog_dense_serialized && 4 + t.dense_body() < m) m = 4 + t.dense_body();
+  return (size_t)m;
+}
+
 // Enqueue the device pipeline for n messages already resident in HBM (versions checked).
 // force_ordered: every table goes through the ordered path (duplicate-row replay).
+//
+// Error contract: every check runs before any table is touched — decode (framing,
+// unknown tables), the dense index (row range), the ordered prep (row range, columns,
+// the sorted/map capacity dry run), the AdaRevision state check, and the duplicate-row
+// gate — so a call that fails applies nothing.
 psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_ordered,
                          const uint64_t *const *record_offsets = nullptr) {
   const int slot = (int)(c->call_seq & 1);
@@ -373,12 +390,13 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   size_t rec_need = 0, list_need = 0;
   const bool sparse = has_sparse_serialized(c);
   bool any_ordered = sparse || force_ordered;
+  const size_t min_rec = min_record_bytes(c);
   for (int i = 0; i < n; ++i) {
     ss.data[i] = (const uint8_t *)s[i].data;
     ss.size[i] = s[i].size;
     ss.recoff_base[i] = rec_need;
     if (sparse) rec_need += s[i].size / 8 + 1;
-    list_need += s[i].size / 8 + 1;       // every record is >= 8 bytes
+    list_need += s[i].size / min_rec + 1;
   }
   if (rec_need > c->recoff_cap[slot] || (any_ordered && list_need > c->list_cap)) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -423,17 +441,15 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       prep);
   if (st) return st;
 
-  // 1) fast dense tables: inverse index + per-message claim counts
+  // 1) fast dense tables: inverse index (batch-major [b][slot]) + per-message claim counts
   psx::TableMask fast{};
-  std::vector<psx::InvLayout> layouts(c->tables.size());
+  const psx::InvLayout L0{1, 0};
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
     if (!t.fast() || force_ordered) continue;
     fast.t[fast.n++] = (int32_t)ti;
     const int64_t stride = t.dense_stride();
-    // 0: slot-major [s][b]; 1: batch-major [b][s] (default)
-    const psx::InvLayout L = psx::g_inv_layout ? psx::InvLayout{1, t.cfg.max_rows} : psx::InvLayout{n, 1};
-    layouts[ti] = L;
+    const psx::InvLayout L{L0.ss, t.cfg.max_rows};
     st = timed(
         c, "dense_index",
         [&] {
@@ -452,19 +468,13 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     HIP_TRY(c, hipEventRecord(c->ev_ready[slot], prep));
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_ready[slot], 0));
   }
-  // 2) a duplicate row in any fast table turns the whole call into a replay (or, with an
-  //    AdaRevision table in the context, into an error: that logic has no ordered replay)
-  if (fast.n && (any_ordered || c->has_ada)) {
-    st = timed(c, "dup_gate", [&] {
-      return psx::launch_gate(segs, counters, fast, n, call_st, c->stream);
-    });
-    if (st) return st;
-  }
-  // 3) ordered tables
+  // 2) ordered tables, stage 1: record lists, validation, capacity dry run
+  std::vector<psx::OrdArgs> ord(c->tables.size());
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
     if (t.fast() && !force_ordered) continue;
-    psx::OrdArgs a{};
+    psx::OrdArgs &a = ord[ti];
+    a = psx::OrdArgs{};
     a.ss = ss;
     a.segs = segs;
     a.t = (int)ti;
@@ -495,25 +505,53 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.sticky = sticky;
     a.force = force_ordered ? 1 : 0;
     a.imp = t.d_imp;
-    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered(t.cfg.dtype, a, c->stream); });
+    a.keyflag = t.d_keyflag;
+    st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
     if (st) return st;
   }
-  // 4) fast dense apply
+  // 3) AdaRevision tables with version records: every record's snapshot must exist
+  std::vector<psx::AdaArgs> ada(c->tables.size());
+  for (int i = 0; i < fast.n; ++i) {
+    const int ti = fast.t[i];
+    TableState &t = c->tables[ti];
+    if (!t.ada) continue;
+    psx::AdaArgs &aa = ada[ti];
+    aa = ada_args(t, ti);
+    aa.ss = ss;
+    aa.segs = segs;
+    aa.B = n;
+    aa.inv = t.d_inv[slot];
+    aa.inv_ss = L0.ss;
+    aa.inv_sb = t.cfg.max_rows;
+    aa.counters = counters;
+    aa.sticky = sticky;
+    aa.call_status = call_st;
+    if (t.cfg.version_maintain) {
+      st = timed(c, "ada_check", [&] { return psx::launch_ada_check(aa, c->stream); });
+      if (st) return st;
+    }
+  }
+  // 4) a duplicate row in any fast table turns the whole call into a replay (or, with an
+  //    AdaRevision table in the context, into an error: that logic has no ordered replay).
+  //    A single fast table with nothing else in the call checks its own counts.
+  if (fast.n > 1 || (fast.n && (any_ordered || c->has_ada))) {
+    st = timed(c, "dup_gate", [&] {
+      return psx::launch_gate(segs, counters, fast, n, call_st, c->stream);
+    });
+    if (st) return st;
+  }
+  // 5) applies: ordered tables, then fast dense tables
+  for (size_t ti = 0; ti < c->tables.size(); ++ti) {
+    TableState &t = c->tables[ti];
+    if (t.fast() && !force_ordered) continue;
+    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered_apply(t.cfg.dtype, ord[ti], c->stream); });
+    if (st) return st;
+  }
   for (int i = 0; i < fast.n; ++i) {
     const int ti = fast.t[i];
     TableState &t = c->tables[ti];
     if (t.ada) {
-      psx::AdaArgs aa = ada_args(t, ti);
-      aa.ss = ss;
-      aa.segs = segs;
-      aa.B = n;
-      aa.inv = t.d_inv[slot];
-      aa.inv_ss = layouts[ti].ss;
-      aa.inv_sb = layouts[ti].sb;
-      aa.counters = counters;
-      aa.sticky = sticky;
-      aa.call_status = call_st;
-      st = enqueue_ada(c, t, aa);
+      st = enqueue_ada(c, t, ada[ti]);
       if (st) return st;
       continue;
     }
@@ -530,8 +568,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.ver = t.d_ver;
     a.flags = t.d_flags;
     a.inv = t.d_inv[slot];
-    a.inv_ss = layouts[ti].ss;
-    a.inv_sb = layouts[ti].sb;
+    a.inv_ss = L0.ss;
+    a.inv_sb = t.cfg.max_rows;
     a.counters = counters;
     a.sticky = sticky;
     a.call_status = call_st;
@@ -592,16 +630,21 @@ psx_status enqueue_ada(psx_ctx *c, TableState &t, const psx::AdaArgs &a) {
   return timed(c, "ada_apply", [&] { return psx::launch_ada_apply(a, c->stream); });
 }
 
-// ServerRowSent for the rows a push just emitted (sizes != 0) or for a list of slots.
+// ServerRowSent for the rows a push emits (sizes != 0) or for a list of slots; num_clients
+// is `clients`, or each row's subscriber count when subs is given.  check_only: verify
+// that every such row can take its snapshot (a free slot or a live one for its version),
+// writing nothing — pushes run it before they clear any dirty bit.
 psx_status ada_rows_sent(psx_ctx *c, TableState &t, int ti, const int32_t *list, const int64_t *sizes, int64_t n,
-                         uint64_t clients) {
+                         uint64_t clients, const uint64_t *subs, bool check_only) {
   psx::AdaArgs a = ada_args(t, ti);
   HIP_TRY(c, hipMemsetAsync(t.d_ada_words + 2, 0, sizeof(uint32_t), c->stream));
-  HIP_TRY(c, psx::launch_ada_sent(a, list, sizes, n, clients, c->stream));
+  HIP_TRY(c, psx::launch_ada_sent(a, list, sizes, n, clients, subs, check_only ? 1 : 0, c->stream));
   uint32_t err = 0;
   HIP_TRY(c, hipMemcpyAsync(&err, t.d_ada_words + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  if (err) return fail(c, PSX_ERR_CAPACITY, "AdaRevision: a row already holds max_snapshots_per_row live snapshots");
+  if (err)
+    return fail(c, PSX_ERR_CAPACITY,
+                "AdaRevision: a sent row already holds max_snapshots_per_row live snapshots (nothing was sent)");
   return PSX_OK;
 }
 
@@ -630,17 +673,26 @@ psx_status sync_impl(psx_ctx *c) {
     uint32_t zero = 0;
     HIP_TRY(c, hipMemcpy(c->d_status, &zero, sizeof(uint32_t), hipMemcpyHostToDevice));
   }
-  psx_status d = c->deferred;
+  // An error stored by an earlier automatic sync is reported after this sync has done
+  // its own work (the replay below), so no accepted call is ever dropped.
+  const psx_status deferred = c->deferred;
+  const std::string deferred_msg = c->err;
   c->deferred = PSX_OK;
-  if (d != PSX_OK) return d;
+  auto finish = [&](psx_status s) {
+    if (deferred != PSX_OK) {
+      c->err = deferred_msg;
+      return deferred;
+    }
+    return s;
+  };
   uint32_t replay_sticky = 0;
   if ((sticky & psx::kStDuplicateRow) && c->has_ada) {
     // the call with the duplicate and every later one applied nothing, and the AdaRevision
     // logic has no ordered replay
     psx_status e = sticky_error(c, sticky & ~psx::kStDuplicateRow);
-    if (e) return e;
-    return fail(c, PSX_ERR_UNSUPPORTED,
-                "a row occurs twice in one message: contexts with an AdaRevision table have no ordered replay");
+    if (e) return finish(e);
+    return finish(fail(c, PSX_ERR_UNSUPPORTED,
+                       "a row occurs twice in one message: contexts with an AdaRevision table have no ordered replay"));
   }
   if (sticky & psx::kStDuplicateRow) {
     // A message held a row twice: that call and every later one were skipped.  Replay
@@ -652,7 +704,7 @@ psx_status sync_impl(psx_ctx *c) {
       if (log[pending[i].ring] & psx::kStDuplicateRow) { first = i; break; }
     for (size_t i = first; i < pending.size(); ++i) {
       psx_status st = enqueue_apply(c, pending[i].streams.data(), (int32_t)pending[i].streams.size(), true);
-      if (st) return st;
+      if (st) return finish(st);
     }
     c->pending.clear();
     c->pending_calls = 0;
@@ -665,8 +717,8 @@ psx_status sync_impl(psx_ctx *c) {
     }
   }
   psx_status e = sticky_error(c, sticky & ~psx::kStDuplicateRow);
-  if (e) return e;
-  return sticky_error(c, replay_sticky);
+  if (e) return finish(e);
+  return finish(sticky_error(c, replay_sticky));
 }
 
 // Serve-back kernel arguments for table t (allocates its size/offset scratch once).
@@ -896,6 +948,10 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (e == hipSuccess) e = hipMalloc(&t.d_off, (R + 1) * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&t.d_tsum, ntiles * sizeof(int32_t));
   if (e == hipSuccess) e = hipMalloc(&t.d_touched, R * sizeof(int32_t));
+  if (e == hipSuccess && cfg->row_kind != PSX_ROW_DENSE) {
+    e = hipMalloc(&t.d_keyflag, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_keyflag, 0, sizeof(uint32_t), c->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     free_table(t);
@@ -905,6 +961,9 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   return PSX_OK;
 }
 
+// Row-range addressing of the row accessors.  Every accessor first settles the calls
+// still in flight (their replays included), so it observes every accepted message —
+// and reports a device-detected error of those calls, as psx_sync would.
 static psx_status row_range(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows,
                             TableState **out, int64_t *first_slot) {
   TableState *t = find_table(c, table_id);
@@ -912,6 +971,8 @@ static psx_status row_range(psx_ctx *c, int32_t table_id, int64_t first_row, int
   if (num_rows < 0) return fail(c, PSX_ERR_INVALID_ARG, "num_rows < 0");
   int64_t s = slot_of(*t, first_row);
   if (s < 0 || s + num_rows > t->cfg.max_rows) return fail(c, PSX_ERR_ROW_RANGE, "row range outside shard");
+  psx_status st = sync_impl(c);
+  if (st) return st;
   *out = t;
   *first_slot = s;
   return PSX_OK;
@@ -967,7 +1028,8 @@ psx_status psx_clear_dirty(psx_ctx *c, int32_t table_id) {
   if (!c) return PSX_ERR_INVALID_ARG;
   TableState *t = find_table(c, table_id);
   if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
-  HIP_TRY(c, hipSetDevice(c->device));
+  psx_status sst = sync_impl(c);
+  if (sst) return sst;
   HIP_TRY(c, psx::launch_flags_and(t->d_flags, t->cfg.max_rows, (uint8_t)~2u, c->stream));
   return PSX_OK;
 }
@@ -1100,8 +1162,8 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
   TableState *t = find_table(c, table_id);
   if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
   if (n == 0) return PSX_OK;
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  psx_status sst = sync_impl(c);
+  if (sst) return sst;
   std::vector<int64_t> slots(n);
   for (int32_t i = 0; i < n; ++i) slots[i] = slot_of(*t, row_ids[i]);
   const bool dense = t->cfg.row_kind == PSX_ROW_DENSE;
@@ -1181,9 +1243,9 @@ psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, 
   if (!c || !used) return PSX_ERR_INVALID_ARG;
   *used = 0;
   if (out_on_device && ((uintptr_t)out & 3)) return fail(c, PSX_ERR_INVALID_ARG, "device output must be 4-byte aligned");
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->side));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // every accepted message is applied before the push is built (server_thread.cpp:241-288)
+  psx_status sst = sync_impl(c);
+  if (sst) return sst;
   const size_t T = c->tables.size();
   std::vector<psx::ServeArgs> args(T);
   for (size_t i = 0; i < T; ++i) {
@@ -1213,6 +1275,16 @@ psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, 
   *used = (size_t)pos;
   if ((size_t)pos > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize_dirty: *used bytes needed");
   if (pos == 0) return PSX_OK;
+  for (size_t i = 0; i < T && clear_dirty; ++i) {   // ServerRowSent must not fail after the clear
+    TableState &t = c->tables[i];
+    if (!t.ada) continue;
+    psx_status st = ada_rows_sent(c, t, (int)i, nullptr, args[i].sizes, args[i].max_rows,
+                                  (uint64_t)t.ada_cfg.push_clients, nullptr, true);
+    if (st) {
+      *used = 0;
+      return st;
+    }
+  }
   uint8_t *dst = (uint8_t *)out;
   if (!out_on_device) {
     if ((size_t)pos > c->staging_cap) {
@@ -1235,7 +1307,7 @@ psx_status psx_serialize_dirty(psx_ctx *c, void *out, size_t cap, size_t *used, 
     TableState &t = c->tables[i];
     if (!t.ada) continue;
     psx_status st = ada_rows_sent(c, t, (int)i, nullptr, args[i].sizes, args[i].max_rows,
-                                  (uint64_t)t.ada_cfg.push_clients);
+                                  (uint64_t)t.ada_cfg.push_clients, nullptr, false);
     if (st) return st;
   }
   if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
@@ -1248,9 +1320,8 @@ psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used
   if (!c || !used) return PSX_ERR_INVALID_ARG;
   *used = 0;
   if (out_on_device && ((uintptr_t)out & 3)) return fail(c, PSX_ERR_INVALID_ARG, "device output must be 4-byte aligned");
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->side));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  psx_status sst = sync_impl(c);
+  if (sst) return sst;
   if (!c->d_ndirty) HIP_TRY(c, hipMalloc(&c->d_ndirty, sizeof(uint32_t)));
   const size_t T = c->tables.size();
   std::vector<psx::ServeArgs> args(T);
@@ -1320,6 +1391,16 @@ psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used
   }
   *used = (size_t)pos;
   if ((size_t)pos > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize_partial: *used bytes needed");
+  for (size_t i = 0; i < T && clear_dirty; ++i) {
+    TableState &t = c->tables[i];
+    if (!t.ada || args[i].nsel <= 0) continue;
+    psx_status st = ada_rows_sent(c, t, (int)i, args[i].sel, nullptr, args[i].nsel,
+                                  (uint64_t)t.ada_cfg.push_clients, nullptr, true);
+    if (st) {
+      *used = 0;
+      return st;
+    }
+  }
   uint8_t *dst = (uint8_t *)out;
   if (!out_on_device) {
     if ((size_t)pos > c->staging_cap) {
@@ -1342,7 +1423,7 @@ psx_status psx_serialize_partial(psx_ctx *c, void *out, size_t cap, size_t *used
     TableState &t = c->tables[i];
     if (!t.ada || args[i].nsel <= 0) continue;
     psx_status st = ada_rows_sent(c, t, (int)i, args[i].sel, nullptr, args[i].nsel,
-                                  (uint64_t)t.ada_cfg.push_clients);
+                                  (uint64_t)t.ada_cfg.push_clients, nullptr, false);
     if (st) return st;
   }
   if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out, dst, (size_t)pos, hipMemcpyDeviceToHost, c->stream));
@@ -1419,9 +1500,8 @@ psx_status psx_row_sent(psx_ctx *c, int32_t table_id, const int32_t *row_ids, in
     slots[i] = (int32_t)s;
     slots64[i] = s;
   }
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->side));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  psx_status sst = sync_impl(c);
+  if (sst) return sst;
   // the replied rows exist (the request path creates them, server.cpp:107-118)
   std::vector<uint8_t> flags(n);
   for (int32_t i = 0; i < n; ++i)
@@ -1433,7 +1513,7 @@ psx_status psx_row_sent(psx_ctx *c, int32_t table_id, const int32_t *row_ids, in
   int32_t *d = nullptr;
   HIP_TRY(c, hipMalloc(&d, sizeof(int32_t) * n));
   hipError_t e = hipMemcpyAsync(d, slots.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
-  psx_status st = e == hipSuccess ? ada_rows_sent(c, *t, ti, d, nullptr, n, (uint64_t)num_clients)
+  psx_status st = e == hipSuccess ? ada_rows_sent(c, *t, ti, d, nullptr, n, (uint64_t)num_clients, nullptr, false)
                                   : hip_fail(c, e, "row_sent upload");
   hipStreamSynchronize(c->stream);
   hipFree(d);
@@ -1580,27 +1660,25 @@ psx_status psx_timing_reset(psx_ctx *c) {
 
 }  // extern "C"
 
-// ---- experiment hooks (include/psx_debug.h) ----------------------------------
+// ---- kernel selectors (include/psx_debug.h) ------------------------------------
 #include "../../include/psx_debug.h"
 namespace psx {
 extern int g_index_variant;
 extern int g_apply_variant;
-extern int g_inv_layout;
-extern int g_ada_variant;
-extern int g_h16_variant;
-extern int g_ord_grid;
 extern int g_ord_split;
-extern int g_imp_pair;
 }  // namespace psx
 
+static int *variant_slot(int32_t which) {
+  switch (which) {
+    case PSX_VARIANT_DENSE_INDEX: return &psx::g_index_variant;
+    case PSX_VARIANT_DENSE_APPLY: return &psx::g_apply_variant;
+    case PSX_VARIANT_ORD_SPLIT: return &psx::g_ord_split;
+    default: return nullptr;
+  }
+}
+
 extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
-  int *v = which == PSX_VARIANT_DENSE_INDEX ? &psx::g_index_variant
-           : which == PSX_VARIANT_DENSE_APPLY ? &psx::g_apply_variant
-           : which == PSX_VARIANT_INV_LAYOUT ? &psx::g_inv_layout
-           : which == PSX_VARIANT_ADA_APPLY ? &psx::g_ada_variant
-           : which == PSX_VARIANT_H16_APPLY ? &psx::g_h16_variant
-           : which == PSX_VARIANT_ORD_GRID ? &psx::g_ord_grid
-           : which == PSX_VARIANT_ORD_SPLIT ? &psx::g_ord_split : nullptr;
+  int *v = variant_slot(which);
   if (!v) return -1;
   int old = *v;
   *v = variant;
@@ -1608,29 +1686,18 @@ extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
 }
 
 extern "C" int32_t psx_debug_get_variant(int32_t which) {
-  if (which == PSX_VARIANT_DENSE_INDEX) return psx::g_index_variant;
-  if (which == PSX_VARIANT_DENSE_APPLY) return psx::g_apply_variant;
-  if (which == PSX_VARIANT_INV_LAYOUT) return psx::g_inv_layout;
-  if (which == PSX_VARIANT_ADA_APPLY) return psx::g_ada_variant;
-  if (which == PSX_VARIANT_H16_APPLY) return psx::g_h16_variant;
-  if (which == PSX_VARIANT_ORD_GRID) return psx::g_ord_grid;
-  if (which == PSX_VARIANT_ORD_SPLIT) return psx::g_ord_split;
-  return -1;
+  int *v = variant_slot(which);
+  return v ? *v : -1;
 }
 
 namespace {
-// PSX_INDEX_VARIANT / PSX_APPLY_VARIANT override the default kernels at load time
-// (used to run the parity suite against every variant).
+// PSX_INDEX_VARIANT / PSX_APPLY_VARIANT / PSX_ORD_SPLIT override the defaults at load time
+// (A/B runs of bench.py and the parity suite).
 struct VariantEnv {
   VariantEnv() {
     if (const char *v = getenv("PSX_INDEX_VARIANT")) psx::g_index_variant = atoi(v);
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
-    if (const char *v = getenv("PSX_INV_LAYOUT")) psx::g_inv_layout = atoi(v);
-    if (const char *v = getenv("PSX_ADA_VARIANT")) psx::g_ada_variant = atoi(v);
-    if (const char *v = getenv("PSX_H16_VARIANT")) psx::g_h16_variant = atoi(v);
-    if (const char *v = getenv("PSX_ORD_GRID")) psx::g_ord_grid = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
-    if (const char *v = getenv("PSX_IMP_PAIR")) psx::g_imp_pair = atoi(v);
   }
 } variant_env;
 }  // namespace

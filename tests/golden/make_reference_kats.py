@@ -6,8 +6,10 @@ expected values its EXPECT_EQ lines state); no reference code is copied or run.
   store_test.cpp = tests/petuum_ps/storage/store_test.cpp
   row_test.cpp   = apps/lda/src/row_test.cpp
 
-row_test.cpp holds inputs only (it LOGs its output); its expected entry order is
-the one SURVEY.md §4 recorded from running that test, and is marked as such.
+row_test.cpp holds inputs only (it LOGs its output and asserts nothing), so it is NOT a
+reference-held vector: its inputs and the entry order SURVEY.md §4 recorded from running
+it go to survey_recorded.json, a cross-check with that provenance, separate from the
+reference's EXPECT_EQ values in reference_kats.json.
 Run:  python tests/golden/make_reference_kats.py
 """
 import json
@@ -45,6 +47,10 @@ kats = {
         # empty, so entries 151..299 are not asserted by the reference.
         "expect": [[i, 0] for i in range(151)],
     },
+}
+
+# Not reference-held (row_test.cpp asserts nothing): SURVEY.md §4's recorded run.
+survey_recorded = {
     "RowTestSortedVectorMapRow": {   # row_test.cpp:11-46 (SortedVectorMapRow<int32_t>, Init(0))
         "store": "SortedVectorMapRow<int32_t>", "init_capacity": 0,
         "ops": [[1, 10], [13, 2], [112, 2], [22, 2], [13, 2], [1, -10]],
@@ -57,5 +63,7 @@ kats = {
 
 if __name__ == "__main__":
     with open(os.path.join(HERE, "reference_kats.json"), "w") as f:
-        json.dump(kats, f, indent=1)
+        json.dump(kats, f, separators=(",", ":"))
+    with open(os.path.join(HERE, "survey_recorded.json"), "w") as f:
+        json.dump(survey_recorded, f, separators=(",", ":"))
     print("wrote", len(kats), "cases")

@@ -239,17 +239,16 @@ def test_smoke_entry():
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
-@pytest.mark.parametrize("index_variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("layout", [0, 1])
-def test_every_kernel_variant_bit_exact(apply_variant, index_variant, layout):
-    """Every selectable index/apply kernel variant (include/psx_debug.h) matches the oracle,
-    including a ragged row tail (cap 301) and 8-byte values."""
+@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3], ids=["auto", "v2", "v4", "v3plain"])
+@pytest.mark.parametrize("index_variant", [0, 1], ids=["nt", "plain"])
+def test_every_kernel_variant_bit_exact(apply_variant, index_variant):
+    """Every dense kernel the product can launch (include/psx_debug.h: v3 default, v2 the
+    >= 4 GiB fallback, v4 the partial-coverage kernel, plain-load forms) matches the
+    oracle, including a ragged row tail (cap 301) and 8-byte values."""
     from parameter_server_amd import _abi
     L = _abi.load()
     old_a = L.psx_debug_set_variant(1, apply_variant)
     old_i = L.psx_debug_set_variant(0, index_variant)
-    old_l = L.psx_debug_set_variant(2, layout)
     try:
         for dt, cap, B in [(F32, 301, 9), (F64, 130, 8), (I32, 64, 3)]:
             rng = np.random.RandomState(apply_variant * 10 + index_variant + cap)
@@ -269,4 +268,3 @@ def test_every_kernel_variant_bit_exact(apply_variant, index_variant, layout):
     finally:
         L.psx_debug_set_variant(1, old_a)
         L.psx_debug_set_variant(0, old_i)
-        L.psx_debug_set_variant(2, old_l)

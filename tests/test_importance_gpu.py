@@ -70,17 +70,11 @@ def _check_importance(srv, orc, tid, rows):
     return got
 
 
-@pytest.mark.parametrize("variant", [6, 0])
 @pytest.mark.parametrize("dt", [F32, F64, I32, I64])
 @pytest.mark.parametrize("B", [1, 2, 3, 5, 9])
-def test_dense_importance_matches_oracle(dt, B, variant, built_lib):
-    """Both importance kernels: the vectorised adaptive one (default, variant 6) and the
-    one-row-per-wave one (variant 0)."""
-    old = built_lib.psx_debug_set_variant(1, variant)
-    try:
-        _dense_importance_case(dt, B)
-    finally:
-        built_lib.psx_debug_set_variant(1, old)
+def test_dense_importance_matches_oracle(dt, B, built_lib):
+    """The vectorised importance kernel (dense_apply_v2 with IMP)."""
+    _dense_importance_case(dt, B)
 
 
 def _dense_importance_case(dt, B):

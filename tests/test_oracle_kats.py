@@ -1,5 +1,7 @@
 """Pins the CPU oracle against the reference's own known-answer tests
-(tests/golden/reference_kats.json, transcribed from store_test.cpp and row_test.cpp)."""
+(tests/golden/reference_kats.json: the EXPECT_EQ values of store_test.cpp), and
+cross-checks it against SURVEY.md §4's recorded run of row_test.cpp
+(tests/golden/survey_recorded.json; that test asserts nothing, so it pins nothing)."""
 import json
 import os
 
@@ -8,7 +10,9 @@ import pytest
 
 from oracle.oracle import OracleServer, DENSE, SORTED_MAP, MAP, I32
 
-KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+KATS = json.load(open(os.path.join(GOLDEN, "reference_kats.json")))
+SURVEY = json.load(open(os.path.join(GOLDEN, "survey_recorded.json")))
 
 
 def _server_for(case):
@@ -20,9 +24,9 @@ def _server_for(case):
     return s
 
 
-@pytest.mark.parametrize("name", sorted(KATS))
+@pytest.mark.parametrize("name", sorted(KATS) + sorted(SURVEY))
 def test_reference_kat(oracle_lib, name):
-    case = KATS[name]
+    case = KATS.get(name) or SURVEY[name]
     s = _server_for(case)
     for col, delta in case["ops"]:
         s.row_inc(0, 0, col, delta)

@@ -39,12 +39,27 @@
  *                                                        src/petuum_ps/server/server.cpp:311-420,
  *                           ServerTable::GetPartialTableToSendRegular / AppendRowsToBuffsPartial
  *                                                        src/petuum_ps/server/server_table.cpp:301-346,381-420
+ *   psx_clock_until         Server::ClockUntil -> VectorClock::TickUntil
+ *                                                        src/petuum_ps/server/server.cpp:62-79,
+ *                                                        src/petuum_ps_common/util/vector_clock.cpp:28-79
+ *   psx_min_clock           Server::GetMinClock          src/petuum_ps/server/server.cpp:181-184
+ *   psx_row_subscribe       Server::FindCreateRow + SSPPushServerThread::RowSubscribe
+ *                                                        src/petuum_ps/server/server.cpp:46-60,
+ *                                                        src/petuum_ps/server/ssp_push_server_thread.cpp:51-54,
+ *                                                        src/petuum_ps/server/callback_subs.hpp:21-28
+ *   psx_serialize_push      Server::CreateSendServerPushRowMsgs with subscriptions (one body per client)
+ *                                                        src/petuum_ps/server/server.cpp:189-309,
+ *                                                        src/petuum_ps/server/server_table.cpp:197-261,
+ *                                                        src/petuum_ps/server/callback_subs.hpp:39-59
  *
  * Error behaviour: the reference aborts via glog CHECK on a version gap
  * (server.cpp:124-126) or an unknown table id (serialized_oplog_reader.hpp:112-120).
- * Here every call returns a psx_status instead; a failed call applies nothing.
- * Errors discovered by device kernels (malformed records, out-of-range rows) are
- * reported by the next psx_sync() on the same context.
+ * Here every call returns a psx_status instead; a failed call applies nothing: every
+ * check of an apply call (framing, tables, row range, columns, the sorted/map capacity
+ * dry run, AdaRevision snapshots, duplicate rows) runs on the device before any table is
+ * touched.  Errors discovered by device kernels are reported by the next psx_sync() —
+ * or by the next call that reads or serves rows, which first settles the calls in
+ * flight (so it sees every accepted message, as the reference server thread does).
  *
  * Threading: one host thread per context (one context = one server shard = one
  * reference ServerThread, server_thread.hpp:90).  Buffers are borrowed for the call
@@ -60,12 +75,15 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 3
+#define PSX_ABI_VERSION 4
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
 /* Maximum number of tables per context. */
 #define PSX_MAX_TABLES 64
+/* Clients of the per-client push: PETUUM_MAX_NUM_CLIENTS as the reference builds it
+ * (defns.mk: -DPETUUM_MAX_NUM_CLIENTS=64; CallBackSubs' bitset, callback_subs.hpp:96). */
+#define PSX_MAX_CLIENTS 64
 
 typedef enum psx_status {
   PSX_OK = 0,
@@ -74,7 +92,9 @@ typedef enum psx_status {
   PSX_ERR_UNKNOWN_TABLE = 3,  /* CHECK(table_iter != end) serialized_oplog_reader.hpp:112 */
   PSX_ERR_MALFORMED = 4,      /* stream shorter than its headers say, negative counts */
   PSX_ERR_ROW_RANGE = 5,      /* row id not owned by this shard's row range */
-  PSX_ERR_CAPACITY = 6,       /* sparse row exceeded max_entries / column >= capacity */
+  PSX_ERR_CAPACITY = 6,       /* a sorted/map row would exceed max_entries, a column >= row_capacity
+                                 of a dense row, or no AdaRevision snapshot slot; nothing applied
+                                 or sent */
   PSX_ERR_DEVICE = 7,         /* HIP runtime error */
   PSX_ERR_OOM = 8,            /* device allocation failed */
   PSX_ERR_BUFFER_TOO_SMALL = 9,
@@ -83,8 +103,7 @@ typedef enum psx_status {
   PSX_ERR_NO_DEVICE = 12,     /* no HIP device visible */
   PSX_ERR_STATE = 13          /* server-logic state missing: an AdaRevision record names a
                                  (row, version) with no accum_gradients_ snapshot (CHECK,
-                                 adarevision_server_table_logic.cpp:114-116); the call is
-                                 partially applied */
+                                 adarevision_server_table_logic.cpp:114-116); nothing applied */
 } psx_status;
 
 /* Row storage kinds (TableInfo.row_type -> registered AbstractRow). */
@@ -247,6 +266,41 @@ psx_status psx_serialize_dirty(psx_ctx *ctx, void *out, size_t cap, size_t *used
  * On PSX_ERR_BUFFER_TOO_SMALL *used holds the bytes needed and nothing is cleared. */
 psx_status psx_serialize_partial(psx_ctx *ctx, void *out, size_t cap, size_t *used,
                                  int32_t out_on_device, int32_t clear_dirty);
+
+/* ---- clocks (SSP) ------------------------------------------------------------------- */
+/* bg_clock_: every registered sender starts at clock 0 (Server::Init, server.cpp:21-24).
+ * psx_clock_until advances bg_id's clock to `clock` one tick at a time
+ * (VectorClock::TickUntil); *new_min_clock receives the new minimum clock over all
+ * senders if it advanced, 0 otherwise — ClockUntil's "clock changed", after which the
+ * reference server fulfils waiting row requests and pushes (server_thread.cpp:262-288). */
+psx_status psx_clock_until(psx_ctx *ctx, int32_t bg_id, int32_t clock, int32_t *new_min_clock);
+psx_status psx_min_clock(psx_ctx *ctx, int32_t *min_clock);
+psx_status psx_sender_clock(psx_ctx *ctx, int32_t bg_id, int32_t *clock);
+
+/* ---- subscriptions and the per-client push (SSPPush) --------------------------------- */
+/* GlobalContext::get_num_clients(): the clients psx_serialize_push writes bodies for
+ * (1..PSX_MAX_CLIENTS, default 1). */
+psx_status psx_set_num_clients(psx_ctx *ctx, int32_t num_clients);
+/* Row request path (ServerThread::HandleRowRequest, server_thread.cpp:185-200): create each
+ * listed row if it does not exist (ServerTable::CreateRow; an AdaRevision table draws its
+ * ServerRowCreated initial values, in list order) and subscribe client_id to it. */
+psx_status psx_row_subscribe(psx_ctx *ctx, int32_t table_id, const int32_t *row_ids, int32_t n,
+                             int32_t client_id);
+/* CallBackSubs bitsets of num_rows rows (psx_row_flags addressing), bit c = client c. */
+psx_status psx_row_subscriptions(psx_ctx *ctx, int32_t table_id, int64_t first_row, int64_t num_rows,
+                                 uint64_t *dst);
+/* Server::CreateSendServerPushRowMsgs as SSPPush runs it: one body per client c in
+ * [0, num_clients), written to out[c] (cap[c] bytes; used[c] receives its size): per
+ * table (creation order) int32 table_id, the dirty rows client c subscribes to as
+ * RecordBuff records in ascending row id, int32 -1 between tables, -2 at the end.  Every
+ * client gets a body, even one without rows.  With clear_dirty, a dirty row some client
+ * subscribes to has dirty and importance reset and ServerRowSent(its subscriber count)
+ * runs; a dirty row nobody subscribes to stays dirty (server_table.cpp:222-225).
+ * PSX_ERR_BUFFER_TOO_SMALL (out == NULL or some cap too small): used[] holds the sizes,
+ * nothing is cleared.  psx_serialize_dirty is the single-body form in which one client
+ * subscribes to every row.  out_on_device: out[c] are 4-byte-aligned device buffers. */
+psx_status psx_serialize_push(psx_ctx *ctx, void *const *out, const size_t *cap, size_t *used,
+                              int32_t out_on_device, int32_t clear_dirty);
 
 /* ---- AdaRevision server-table logic ------------------------------------------------ */
 /* AdaRevisionServerTableLogic (src/petuum_ps/server/adarevision_server_table_logic.cpp),

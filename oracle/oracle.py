@@ -73,6 +73,15 @@ def lib():
         L.orc_serialize_partial.restype = i64
         L.orc_partition_server.argtypes = [i32, i32, i32, i32]
         L.orc_partition_server.restype = i32
+        L.orc_clock_until.argtypes = [vp, i32, i32]
+        L.orc_clock_until.restype = i32
+        L.orc_min_clock.argtypes = [vp]
+        L.orc_min_clock.restype = i32
+        L.orc_subscribe.argtypes = [vp, i32, i32, i32]
+        L.orc_row_subs.argtypes = [vp, i32, i32]
+        L.orc_row_subs.restype = ctypes.c_uint64
+        L.orc_serialize_push.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_int]
+        L.orc_serialize_push.restype = i64
         _lib = L
     return _lib
 
@@ -232,6 +241,41 @@ class OracleServer:
                 continue
             assert r >= 0, r
             return out[:r].tobytes()
+
+    def clock_until(self, bg, clock):
+        """Server::ClockUntil (server.cpp:62-79): the new min clock if it advanced, else 0."""
+        r = self._L.orc_clock_until(self._s, bg, clock)
+        assert r >= 0, "unknown sender"
+        return r
+
+    def min_clock(self):
+        return self._L.orc_min_clock(self._s)
+
+    def subscribe(self, table_id, row_id, client_id):
+        """FindCreateRow + RowSubscribe (server_thread.cpp:185-200)."""
+        assert self._L.orc_subscribe(self._s, table_id, row_id, client_id) == ST_OK
+
+    def row_subs(self, table_id, row_id):
+        return self._L.orc_row_subs(self._s, table_id, row_id)
+
+    def serialize_push(self, table_ids, num_clients, clear=True):
+        """Server::CreateSendServerPushRowMsgs with per-client subscriptions
+        (server.cpp:189-309, server_table.cpp:197-261): one body per client."""
+        tids = np.ascontiguousarray(table_ids, dtype=np.int32)
+        nb = 1 << 16
+        while True:
+            bufs = [np.zeros(nb, dtype=np.uint8) for _ in range(num_clients)]
+            ptrs = (ctypes.c_void_p * num_clients)(*[b.ctypes.data for b in bufs])
+            caps = np.full(num_clients, nb, dtype=np.uint64)
+            used = np.zeros(num_clients, dtype=np.int64)
+            r = self._L.orc_serialize_push(self._s, _ptr(tids), tids.size, num_clients,
+                                           ctypes.cast(ptrs, ctypes.c_void_p), _ptr(caps), _ptr(used),
+                                           1 if clear else 0)
+            if r == -2:
+                nb = int(max(used.max(), nb)) * 2
+                continue
+            assert r == 0, r
+            return [b[:u].tobytes() for b, u in zip(bufs, used)]
 
     def get(self, table_id, row_id, col):
         kind, dt, cap = self.tables[table_id]

@@ -222,6 +222,7 @@ typedef struct {
   uint64_t version;      /* VersionServerRow::version_ (version_server_row.hpp:13-19,69): 1 at
                             creation, +1 per applied record; read only for version tables */
   float *ada_acc, *ada_z, *ada_zmax;   /* AdaRevisionRow (adarevision_server_table_logic.hpp:11-22) */
+  uint64_t subs;         /* CallBackSubs::subscriptions_ (callback_subs.hpp:96), client c = bit c */
 } orc_row;
 
 typedef struct {
@@ -251,6 +252,8 @@ typedef struct {
   int ntables;
   int32_t bg_ids[1024];
   int64_t bg_versions[1024];
+  int32_t bg_clocks[1024];   /* bg_clock_ (server.hpp; VectorClock, vector_clock.cpp) */
+  int32_t min_clock;         /* VectorClock::min_clock_: -1 until the first AddClock */
   int nbg;
 } orc_server;
 
@@ -258,7 +261,11 @@ typedef struct {
 static size_t entry_size(int dt) { return dt_size(dt) == 4 ? 8 : 16; }
 static size_t entry_val_off(int dt) { return dt_size(dt) == 4 ? 4 : 8; }
 
-orc_server *orc_server_create(void) { return (orc_server *)calloc(1, sizeof(orc_server)); }
+orc_server *orc_server_create(void) {
+  orc_server *s = (orc_server *)calloc(1, sizeof(orc_server));
+  if (s) s->min_clock = -1;   /* VectorClock() : min_clock_(-1) (vector_clock.cpp:5-6) */
+  return s;
+}
 
 static void row_free(orc_table *t, orc_row *r) {
   free(r->dense); free(r->entries);
@@ -280,12 +287,47 @@ void orc_server_destroy(orc_server *s) {
 }
 
 /* Server::Init: bg_version_map_[bg] = -1 (server.cpp:21-24). */
+/* Server::Init (server.cpp:18-31): bg_clock_.AddClock(bg, 0), bg_version_map_[bg] = -1.
+ * AddClock (vector_clock.cpp:19-26) lowers min_clock_ to the new clock, or sets it when
+ * it is still -1. */
 int orc_register_sender(orc_server *s, int32_t bg) {
   for (int i = 0; i < s->nbg; ++i) if (s->bg_ids[i] == bg) return ORC_OK;
   if (s->nbg >= 1024) return ORC_ERR_INVALID_ARG;
-  s->bg_ids[s->nbg] = bg; s->bg_versions[s->nbg] = -1; s->nbg++;
+  s->bg_ids[s->nbg] = bg; s->bg_versions[s->nbg] = -1; s->bg_clocks[s->nbg] = 0; s->nbg++;
+  if (s->min_clock == -1 || 0 < s->min_clock) s->min_clock = 0;
   return ORC_OK;
 }
+
+/* VectorClock::IsUniqueMin (vector_clock.cpp:66-79) */
+static int clock_is_unique_min(const orc_server *s, int i) {
+  if (s->bg_clocks[i] != s->min_clock) return 0;
+  int n = 0;
+  for (int k = 0; k < s->nbg; ++k)
+    if (s->bg_clocks[k] == s->min_clock && ++n > 1) return 0;
+  return 1;
+}
+
+/* Server::ClockUntil -> VectorClock::TickUntil (server.cpp:62-79, vector_clock.cpp:38-51):
+ * tick the sender's clock up to `clock`, one Tick (:28-36) at a time; returns the new
+ * min clock if it advanced, 0 otherwise; -1 for an unknown sender.  (No snapshots: the
+ * snapshot_clock branch is out of scope.) */
+int32_t orc_clock_until(orc_server *s, int32_t bg, int32_t clock) {
+  int i = 0;
+  while (i < s->nbg && s->bg_ids[i] != bg) ++i;
+  if (i == s->nbg) return -1;
+  int32_t changed = 0;
+  for (int32_t n = clock - s->bg_clocks[i]; n > 0; --n) {
+    if (clock_is_unique_min(s, i)) {
+      ++s->bg_clocks[i];
+      changed = ++s->min_clock;
+    } else {
+      ++s->bg_clocks[i];
+    }
+  }
+  return changed;
+}
+
+int32_t orc_min_clock(orc_server *s) { return s->min_clock; }   /* Server::GetMinClock (:181-184) */
 
 static orc_table *find_table(orc_server *s, int32_t table_id) {
   for (int i = 0; i < s->ntables; ++i) if (s->tables[i]->table_id == table_id) return s->tables[i];
@@ -1209,4 +1251,109 @@ int64_t orc_serialize_partial(orc_server *s, const int32_t *table_ids, int ntabl
   }
   for (int ti = 0; ti < ntables; ++ti) free(sel[ti]);
   return ret;
+}
+
+/* ---- subscriptions and the per-client push (SSPPush) ----------------------------- */
+/* ServerThread::HandleRowRequest -> Server::FindCreateRow + SSPPushServerThread::RowSubscribe
+ * (server_thread.cpp:185-200, server.cpp:46-60, ssp_push_server_thread.cpp:51-54,
+ * CallBackSubs::Subscribe callback_subs.hpp:21-28): create the row if missing (its
+ * AdaRevision ServerRowCreated included), then set the client's bit. */
+int orc_subscribe(orc_server *s, int32_t table_id, int32_t row_id, int32_t client_id) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_UNKNOWN_TABLE;
+  if (client_id < 0 || client_id >= 64) return ORC_ERR_INVALID_ARG;
+  orc_row *r = find_row(t, row_id);
+  if (!r) {
+    r = create_row(t, row_id);
+    if (t->ada) ada_row_created(t, r);
+  }
+  r->subs |= (uint64_t)1 << client_id;
+  return ORC_OK;
+}
+
+uint64_t orc_row_subs(orc_server *s, int32_t table_id, int32_t row_id) {
+  orc_table *t = find_table(s, table_id);
+  orc_row *r = t ? find_row(t, row_id) : NULL;
+  return r ? r->subs : 0;
+}
+
+/* Server::CreateSendServerPushRowMsgs (server.cpp:189-309) for num_clients clients, one
+ * unsplit message body each: per table (in the order given) int32 table_id, then
+ * ServerTable::AppendTableToBuffs (server_table.cpp:197-261): a row no client subscribes
+ * to is skipped and stays dirty (:222-225); a clean row is skipped; a dirty subscribed row
+ * has dirty_ and importance_ reset (:233-235), is serialized once and appended to every
+ * subscribed client's buffer (CallBackSubs::AppendRowToBuffs, callback_subs.hpp:39-59),
+ * then ServerRowSent(row, version, subscriber count) (:250-255); tables are separated by
+ * int32 -1 and every body ends with -2.  Rows go in ascending row id (the reference
+ * iterates a boost::unordered_map, whose order is unspecified).  outs[c]/caps[c]: client
+ * c's buffer; used[c] receives its size.  Returns 0, -2 if a buffer is too small (nothing
+ * is cleared then), -3 for an unknown table. */
+int64_t orc_serialize_push(orc_server *s, const int32_t *table_ids, int ntables, int nclients, void **outs,
+                           const size_t *caps, int64_t *used, int clear) {
+  if (nclients <= 0 || nclients > 64) return -3;
+  for (int c = 0; c < nclients; ++c) used[c] = 0;
+  /* size pass: one RecordBuff record per (row, subscribed client) */
+  size_t scap = 1 << 16;
+  uint8_t *scratch = (uint8_t *)malloc(scap);
+  for (int ti = 0; ti < ntables; ++ti) {
+    orc_table *t = find_table(s, table_ids[ti]);
+    if (!t) { free(scratch); return -3; }
+    for (int c = 0; c < nclients; ++c) used[c] += 8;   /* table id + separator */
+    for (int64_t i = 0; i < t->index.cap; ++i) {
+      if (t->index.used[i] != 1) continue;
+      orc_row *r = t->rows[t->index.vals[i]];
+      if (!r->subs || !r->dirty) continue;
+      int64_t w;
+      while ((w = orc_serialize_records(s, t->table_id, &t->index.keys[i], 1, scratch, scap)) == -2) {
+        scap *= 4;
+        free(scratch);
+        scratch = (uint8_t *)malloc(scap);
+      }
+      for (int c = 0; c < nclients; ++c)
+        if ((r->subs >> c) & 1) used[c] += w;
+    }
+  }
+  free(scratch);
+  for (int c = 0; c < nclients; ++c)
+    if ((size_t)used[c] > caps[c]) return -2;
+  int64_t pos[64];
+  for (int c = 0; c < nclients; ++c) pos[c] = 0;
+  for (int ti = 0; ti < ntables; ++ti) {
+    orc_table *t = find_table(s, table_ids[ti]);
+    for (int c = 0; c < nclients; ++c) {
+      memcpy((uint8_t *)outs[c] + pos[c], &table_ids[ti], 4);
+      pos[c] += 4;
+    }
+    int32_t *ids = (int32_t *)malloc((size_t)(t->nrows + 1) * 4);
+    int64_t nd = 0;
+    for (int64_t i = 0; i < t->index.cap; ++i)
+      if (t->index.used[i] == 1) {
+        orc_row *r = t->rows[t->index.vals[i]];
+        if (r->subs && r->dirty) ids[nd++] = t->index.keys[i];
+      }
+    qsort(ids, (size_t)nd, 4, cmp_i32);
+    for (int64_t k = 0; k < nd; ++k) {
+      orc_row *r = find_row(t, ids[k]);
+      size_t nc = 0;
+      for (int c = 0; c < nclients; ++c) {
+        if (!((r->subs >> c) & 1)) continue;
+        int64_t w = orc_serialize_records(s, t->table_id, &ids[k], 1, (uint8_t *)outs[c] + pos[c], caps[c] - pos[c]);
+        if (w < 0) { free(ids); return w; }
+        pos[c] += w;
+        ++nc;
+      }
+      if (clear) {
+        r->dirty = 0;
+        r->importance = 0;
+        if (t->ada) ada_row_sent(t, ids[k], r, nc);
+      }
+    }
+    free(ids);
+    for (int c = 0; c < nclients; ++c) {
+      int32_t sep = ti + 1 < ntables ? -1 : -2;
+      memcpy((uint8_t *)outs[c] + pos[c], &sep, 4);
+      pos[c] += 4;
+    }
+  }
+  return 0;
 }

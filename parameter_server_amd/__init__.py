@@ -6,8 +6,8 @@ reference's server apply interface (src/petuum_ps/server/server.hpp).
 """
 from . import _abi
 from ._abi import PsxError, F32, F64, I32, I64, ROW_DENSE, ROW_SORTED_MAP, ROW_MAP
-from .server import Server, TableInfo
+from .server import Server, ServerThread, TableInfo
 from . import wire
 
-__all__ = ["Server", "TableInfo", "PsxError", "F32", "F64", "I32", "I64",
+__all__ = ["Server", "ServerThread", "TableInfo", "PsxError", "F32", "F64", "I32", "I64",
            "ROW_DENSE", "ROW_SORTED_MAP", "ROW_MAP", "wire"]

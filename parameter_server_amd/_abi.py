@@ -21,6 +21,7 @@ STATUS_NAMES = {
 ROW_DENSE, ROW_SORTED_MAP, ROW_MAP = 0, 1, 2
 F32, F64, I32, I64 = 0, 1, 2, 3
 MAX_FUSED_STREAMS = 16
+MAX_CLIENTS = 64
 # TableInfo.row_oplog_type (configs.hpp:35-40)
 DENSE_ROW_OPLOG, SPARSE_ROW_OPLOG, SPARSE_VECTOR_ROW_OPLOG, DENSE_ROW_OPLOG_FLOAT16 = 0, 1, 2, 3
 
@@ -131,6 +132,13 @@ def load():
         "psx_row_sent": ([vp, i32, vp, i32, i32], ctypes.c_int),
         "psx_adarevision_state": ([vp, i32, i64, i64, vp, vp, vp, P(ctypes.c_uint64)], ctypes.c_int),
         "psx_pack_stream": ([vp, P(psx_pack_table), i32, vp, sz, P(sz), vp], ctypes.c_int),
+        "psx_clock_until": ([vp, i32, i32, P(i32)], ctypes.c_int),
+        "psx_min_clock": ([vp, P(i32)], ctypes.c_int),
+        "psx_sender_clock": ([vp, i32, P(i32)], ctypes.c_int),
+        "psx_set_num_clients": ([vp, i32], ctypes.c_int),
+        "psx_row_subscribe": ([vp, i32, vp, i32, i32], ctypes.c_int),
+        "psx_row_subscriptions": ([vp, i32, i64, i64, vp], ctypes.c_int),
+        "psx_serialize_push": ([vp, vp, vp, vp, i32, i32], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),
         "psx_timing_enable": ([vp, i32], ctypes.c_int),

@@ -179,6 +179,8 @@ struct ServeArgs {
   uint8_t *flags_rw;         // non-null: clear bit1 (dirty) of every emitted row
   double *imp_rw;            // non-null (with flags_rw): reset importance of every emitted row
   const uint64_t *ver;       // non-null: version table, append uint64 version to every row body
+  const uint64_t *subs;      // non-null: only rows with (subs[s] & cmask) != 0 (per-client push)
+  uint64_t cmask;
   // partial push (psx_serialize_partial)
   const double *imp;         // importance per slot (null: no importance ordering)
   double *keys;              // sort keys per slot: importance (or 0) if dirty, -1 otherwise

@@ -958,7 +958,10 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
 
 // dense_index_v2: flattened (message, record) space, UNROLL row-id loads in flight per
 // thread before any store.
-template <int UNROLL, bool NT>
+// MODE 0: non-temporal row-id loads; 1: plain loads; 2: plain loads issued one lane at a
+// time (a wave instruction touching 64 lines leaves L2 as 128-B requests; the A/B of the
+// request size a single-lane load produces is profiles/r02).
+template <int UNROLL, int MODE>
 __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const Seg *segs, int t, int B,
                                                             int64_t stride, Geo g, int32_t *inv, InvLayout L,
                                                             uint32_t *call_status) {
@@ -986,20 +989,38 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
     int32_t rid[UNROLL];
     int32_t bi[UNROLL];
     int64_t ii[UNROLL];
+    const int32_t *ptr[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int64_t r = r0 + u * G;
       bi[u] = -1;
       ii[u] = 0;
       rid[u] = 0;
+      ptr[u] = nullptr;
       if (r < total) {
         int b = 0;
         while (b + 1 < B && pre[b + 1] <= r) ++b;
         bi[u] = b;
         ii[u] = r - pre[b];
-        const int32_t *p = reinterpret_cast<const int32_t *>(base[b] + ii[u] * stride);
-        rid[u] = NT ? __builtin_nontemporal_load(p) : *p;
+        ptr[u] = reinterpret_cast<const int32_t *>(base[b] + ii[u] * stride);
       }
+    }
+    if constexpr (MODE == 2) {
+      typedef const int32_t __attribute__((address_space(1))) *gint_p;
+      const int lane = threadIdx.x & 63;
+      gint_p gp[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) gp[u] = (gint_p)(ptr[u] ? ptr[u] : reinterpret_cast<const int32_t *>(base[0]));
+      for (int l = 0; l < 64; ++l) {
+        if (lane == l) {
+#pragma unroll
+          for (int u = 0; u < UNROLL; ++u) rid[u] = *gp[u];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u)
+        if (ptr[u]) rid[u] = MODE == 0 ? __builtin_nontemporal_load(ptr[u]) : *ptr[u];
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -1070,7 +1091,7 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
 // Run-time selectors (include/psx_debug.h): the defaults are the measured winners; the
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
-int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads
+int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads, 2: plain, one lane at a time
 int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact), 3: v3 with plain record loads
 
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
@@ -1078,11 +1099,14 @@ hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64
                               int32_t *inv, InvLayout L, uint32_t *call_status, hipStream_t st) {
   Geo g{row_offset, row_stride, max_rows};
   if (g_index_variant == 1)
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, false>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g,
-                       inv, L, call_status);
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, 1>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
+                       call_status);
+  else if (g_index_variant == 2)
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, 2>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
+                       call_status);
   else
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, true>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g,
-                       inv, L, call_status);
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, 0>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
+                       call_status);
   return hipGetLastError();
 }
 

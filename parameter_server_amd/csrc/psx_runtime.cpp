@@ -56,6 +56,9 @@ hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMas
 hipError_t launch_serve_sizes(const ServeArgs &a, hipStream_t st);
 hipError_t launch_serve_emit(const ServeArgs &a, hipStream_t st);
 hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st);
+hipError_t launch_serve_clear(uint8_t *flags, double *imp, const uint64_t *subs, int64_t n, hipStream_t st);
+hipError_t launch_subscribe(uint8_t *flags, uint64_t *subs, const int64_t *slots, int32_t n, uint64_t bit,
+                            hipStream_t st);
 hipError_t launch_serve_list_sizes(const ServeArgs &a, hipStream_t st);
 hipError_t launch_serve_emit_list(const ServeArgs &a, hipStream_t st);
 hipError_t launch_pack_count(int dtype, PackTab t, hipStream_t st);
@@ -89,6 +92,7 @@ struct TableState {
   int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
   uint32_t *d_keyflag = nullptr;   // sorted/map: a key outside [0, max_entries) was seen
+  uint64_t *d_subs = nullptr;      // CallBackSubs::subscriptions_ per slot (bit c = client c), lazily
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
   double *d_imp = nullptr;         // accum_importance: ServerRow::importance_ per slot
@@ -129,7 +133,7 @@ struct TableState {
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_srv_sizes, t.d_srv_offs,
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_subs, t.d_srv_sizes, t.d_srv_offs,
                   t.d_imp, t.d_ver, t.d_acc, t.d_z, t.d_zmax, t.d_snap_ver, t.d_snap_cnt, t.d_snap_acc,
                   t.d_ada_words, t.d_new_keys, t.d_new_slots, t.d_new_tmp, t.d_init, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
@@ -155,6 +159,9 @@ struct psx_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   std::map<int32_t, int64_t> versions;   // bg_version_map_
+  std::map<int32_t, int32_t> clocks;     // bg_clock_ (VectorClock::vec_clock_)
+  int32_t min_clock = -1;                // VectorClock::min_clock_
+  int32_t num_clients = 1;               // GlobalContext::get_num_clients (per-client push)
   std::vector<TableState> tables;
   bool has_ada = false;                  // some table runs the AdaRevision logic
   // Per-call state lives in two slots (call k uses slot k & 1) so that the decode/index
@@ -398,6 +405,13 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (sparse) rec_need += s[i].size / 8 + 1;
     list_need += s[i].size / min_rec + 1;
   }
+  // every ordered table keeps its record lists from its stage 1 to its apply: one
+  // list_need-sized region each
+  size_t n_ord = 0;
+  for (auto &t : c->tables)
+    if (!t.fast() || force_ordered) ++n_ord;
+  const size_t list_region = list_need;
+  list_need *= n_ord ? n_ord : 1;
   if (rec_need > c->recoff_cap[slot] || (any_ordered && list_need > c->list_cap)) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->side));
@@ -470,6 +484,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   }
   // 2) ordered tables, stage 1: record lists, validation, capacity dry run
   std::vector<psx::OrdArgs> ord(c->tables.size());
+  size_t ord_k = 0;
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
     if (t.fast() && !force_ordered) continue;
@@ -493,7 +508,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.cnt = t.d_cnt;
     a.off = t.d_off;
     a.tsum = t.d_tsum;
-    a.list = c->d_list;
+    a.list = c->d_list + list_region * ord_k++;
     a.touched = t.d_touched;
     a.ntouched = c->d_ntouched[slot] + ti;
     a.dense = t.d_data;
@@ -856,7 +871,52 @@ void *psx_ctx_get_stream(psx_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 psx_status psx_register_sender(psx_ctx *c, int32_t bg_id) {
   if (!c) return PSX_ERR_INVALID_ARG;
-  if (!c->versions.count(bg_id)) c->versions[bg_id] = -1;
+  if (!c->versions.count(bg_id)) {
+    c->versions[bg_id] = -1;
+    // bg_clock_.AddClock(bg, 0) (server.cpp:21-24, vector_clock.cpp:19-26)
+    c->clocks[bg_id] = 0;
+    if (c->min_clock == -1 || 0 < c->min_clock) c->min_clock = 0;
+  }
+  return PSX_OK;
+}
+
+psx_status psx_clock_until(psx_ctx *c, int32_t bg_id, int32_t clock, int32_t *new_min_clock) {
+  if (!c || !new_min_clock) return PSX_ERR_INVALID_ARG;
+  *new_min_clock = 0;
+  auto it = c->clocks.find(bg_id);
+  if (it == c->clocks.end()) return fail(c, PSX_ERR_SENDER, "bg_id " + std::to_string(bg_id) + " not registered");
+  // VectorClock::TickUntil (vector_clock.cpp:38-51): one Tick (:28-36) per clock; a tick by
+  // the unique slowest sender advances the min clock (IsUniqueMin, :66-79)
+  for (int32_t k = clock - it->second; k > 0; --k) {
+    bool unique_min = it->second == c->min_clock;
+    if (unique_min) {
+      int num_min = 0;
+      for (auto &kv : c->clocks)
+        if (kv.second == c->min_clock && ++num_min > 1) { unique_min = false; break; }
+    }
+    ++it->second;
+    if (unique_min) *new_min_clock = ++c->min_clock;
+  }
+  return PSX_OK;
+}
+
+psx_status psx_min_clock(psx_ctx *c, int32_t *min_clock) {
+  if (!c || !min_clock) return PSX_ERR_INVALID_ARG;
+  *min_clock = c->min_clock;
+  return PSX_OK;
+}
+
+psx_status psx_sender_clock(psx_ctx *c, int32_t bg_id, int32_t *clock) {
+  if (!c || !clock) return PSX_ERR_INVALID_ARG;
+  auto it = c->clocks.find(bg_id);
+  if (it == c->clocks.end()) return fail(c, PSX_ERR_SENDER, "unknown sender");
+  *clock = it->second;
+  return PSX_OK;
+}
+
+psx_status psx_set_num_clients(psx_ctx *c, int32_t num_clients) {
+  if (!c || num_clients < 1 || num_clients > PSX_MAX_CLIENTS) return PSX_ERR_INVALID_ARG;
+  c->num_clients = num_clients;
   return PSX_OK;
 }
 
@@ -1626,6 +1686,185 @@ psx_status psx_pack_stream(psx_ctx *c, const psx_pack_table *tables, int32_t n, 
   for (size_t k = 0; k < live.size(); ++k)
     HIP_TRY(c, psx::launch_pack_emit(live[k]->dtype, pt[k], (uint8_t *)out, record_offsets, c->stream));
   HIP_TRY(c, psx::launch_pack_header((uint8_t *)out, h, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+// ---- subscriptions and the per-client push (SSPPush) ---------------------------------
+
+static psx_status ensure_subs(psx_ctx *c, TableState &t) {
+  if (t.d_subs) return PSX_OK;
+  const size_t R = (size_t)t.cfg.max_rows;
+  HIP_TRY(c, hipMalloc(&t.d_subs, R * sizeof(uint64_t)));
+  HIP_TRY(c, hipMemsetAsync(t.d_subs, 0, R * sizeof(uint64_t), c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_row_subscribe(psx_ctx *c, int32_t table_id, const int32_t *row_ids, int32_t n, int32_t client_id) {
+  if (!c || n < 0 || (n && !row_ids) || client_id < 0 || client_id >= PSX_MAX_CLIENTS) return PSX_ERR_INVALID_ARG;
+  int ti = 0;
+  TableState *t = find_table(c, table_id, &ti);
+  if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table");
+  if (n == 0) return PSX_OK;
+  std::vector<int64_t> slots(n);
+  for (int32_t i = 0; i < n; ++i) {
+    slots[i] = slot_of(*t, row_ids[i]);
+    if (slots[i] < 0) return fail(c, PSX_ERR_ROW_RANGE, "row " + std::to_string(row_ids[i]) + " not owned by this shard");
+  }
+  psx_status st = sync_impl(c);
+  if (st) return st;
+  st = ensure_subs(c, *t);
+  if (st) return st;
+  int64_t *d_slots = nullptr;
+  HIP_TRY(c, hipMalloc(&d_slots, sizeof(int64_t) * n));
+  std::unique_ptr<int64_t, decltype(&hipFree)> hold(d_slots, &hipFree);
+  HIP_TRY(c, hipMemcpyAsync(d_slots, slots.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c->stream));
+  if (t->ada && t->ada_cfg.gaussian_init) {
+    // ServerTable::CreateRow -> ServerRowCreated for the rows that do not exist yet, in
+    // request order (adarevision_server_table_logic.cpp:38-50): N(0, 0.1) draws of the
+    // table's generator added to the zero row
+    std::vector<uint8_t> flags(n);
+    uint8_t *d_flags = nullptr;
+    HIP_TRY(c, hipMalloc(&d_flags, n));
+    std::unique_ptr<uint8_t, decltype(&hipFree)> hold_f(d_flags, &hipFree);
+    HIP_TRY(c, psx::launch_gather_flags(t->d_flags, d_slots, n, d_flags, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(flags.data(), d_flags, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int32_t> fresh;
+    for (int32_t i = 0; i < n; ++i)
+      if (!(flags[i] & 1) && std::find(fresh.begin(), fresh.end(), (int32_t)slots[i]) == fresh.end())
+        fresh.push_back((int32_t)slots[i]);
+    if (!fresh.empty()) {
+      const size_t cap = (size_t)t->cfg.row_capacity;
+      std::vector<float> d(fresh.size() * cap);
+      for (float &x : d) x = (*t->ada_dist)(*t->ada_gen);
+      int32_t *d_fresh = nullptr;
+      float *d_vals = nullptr;
+      HIP_TRY(c, hipMalloc(&d_fresh, sizeof(int32_t) * fresh.size()));
+      std::unique_ptr<int32_t, decltype(&hipFree)> hold_s(d_fresh, &hipFree);
+      HIP_TRY(c, hipMalloc(&d_vals, sizeof(float) * d.size()));
+      std::unique_ptr<float, decltype(&hipFree)> hold_v(d_vals, &hipFree);
+      HIP_TRY(c, hipMemcpyAsync(d_fresh, fresh.data(), sizeof(int32_t) * fresh.size(), hipMemcpyHostToDevice,
+                                c->stream));
+      HIP_TRY(c, hipMemcpyAsync(d_vals, d.data(), sizeof(float) * d.size(), hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(c, psx::launch_ada_init_rows(ada_args(*t, ti), d_fresh, d_vals, (int32_t)fresh.size(), c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+  }
+  HIP_TRY(c, psx::launch_subscribe(t->d_flags, t->d_subs, d_slots, n, (uint64_t)1 << client_id, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_row_subscriptions(psx_ctx *c, int32_t table_id, int64_t first_row, int64_t num_rows, uint64_t *dst) {
+  if (!c || (!dst && num_rows)) return PSX_ERR_INVALID_ARG;
+  TableState *t;
+  int64_t s;
+  psx_status st = row_range(c, table_id, first_row, num_rows, &t, &s);
+  if (st) return st;
+  if (!t->d_subs) {
+    for (int64_t i = 0; i < num_rows; ++i) dst[i] = 0;
+    return PSX_OK;
+  }
+  HIP_TRY(c, hipMemcpyAsync(dst, t->d_subs + s, sizeof(uint64_t) * (size_t)num_rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+psx_status psx_serialize_push(psx_ctx *c, void *const *out, const size_t *cap, size_t *used, int32_t out_on_device,
+                              int32_t clear_dirty) {
+  if (!c || !used || !cap) return PSX_ERR_INVALID_ARG;
+  const int C = c->num_clients;
+  for (int k = 0; k < C; ++k) {
+    used[k] = 0;
+    if (out && out[k] && out_on_device && ((uintptr_t)out[k] & 3))
+      return fail(c, PSX_ERR_INVALID_ARG, "device outputs must be 4-byte aligned");
+  }
+  psx_status st = sync_impl(c);
+  if (st) return st;
+  const size_t T = c->tables.size();
+  std::vector<psx::ServeArgs> args(T);
+  for (size_t i = 0; i < T; ++i) {
+    st = serve_args(c, c->tables[i], &args[i]);
+    if (st) return st;
+    st = ensure_subs(c, c->tables[i]);
+    if (st) return st;
+    args[i].subs = c->tables[i].d_subs;
+  }
+  // sizes: per client, per table {table_id, records, -1 | -2}
+  std::vector<std::vector<int64_t>> tot(C, std::vector<int64_t>(T, 0));
+  bool small = false;
+  for (int k = 0; k < C; ++k) {
+    int64_t pos = 0;
+    for (size_t i = 0; i < T; ++i) {
+      args[i].cmask = (uint64_t)1 << k;
+      HIP_TRY(c, psx::launch_serve_sizes(args[i], c->stream));
+      HIP_TRY(c, hipMemcpyAsync(&tot[k][i], args[i].offs + args[i].max_rows, sizeof(int64_t), hipMemcpyDeviceToHost,
+                                c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      pos += 8 + tot[k][i];
+    }
+    used[k] = (size_t)pos;
+    if (used[k] > cap[k] || !out || !out[k]) small = true;
+  }
+  if (small) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "serialize_push: used[] bytes needed");
+  // ServerRowSent must not fail after a row was cleared: check every AdaRevision table first
+  for (size_t i = 0; i < T && clear_dirty; ++i) {
+    TableState &t = c->tables[i];
+    if (!t.ada) continue;
+    args[i].cmask = ~(uint64_t)0;
+    HIP_TRY(c, psx::launch_serve_sizes(args[i], c->stream));
+    st = ada_rows_sent(c, t, (int)i, nullptr, args[i].sizes, args[i].max_rows, 0, t.d_subs, true);
+    if (st) {
+      for (int k = 0; k < C; ++k) used[k] = 0;
+      return st;
+    }
+  }
+  size_t stage = 0;
+  for (int k = 0; k < C; ++k) stage = std::max(stage, used[k]);
+  if (!out_on_device && stage > c->staging_cap) {
+    if (c->d_staging) hipFree(c->d_staging);
+    c->d_staging = nullptr;
+    c->staging_cap = 0;
+    HIP_TRY(c, hipMalloc(&c->d_staging, stage));
+    c->staging_cap = stage;
+  }
+  for (int k = 0; k < C; ++k) {
+    uint8_t *dst = out_on_device ? (uint8_t *)out[k] : c->d_staging;
+    psx::Words w{};
+    int64_t pos = 0;
+    for (size_t i = 0; i < T; ++i) {
+      w.pos[w.n] = pos;
+      w.val[w.n++] = c->tables[i].cfg.table_id;
+      pos += 4;
+      args[i].cmask = (uint64_t)1 << k;
+      args[i].out = dst + pos;
+      args[i].flags_rw = nullptr;   // cleared once, after every client's body
+      args[i].imp_rw = nullptr;
+      if (tot[k][i]) {
+        HIP_TRY(c, psx::launch_serve_sizes(args[i], c->stream));
+        HIP_TRY(c, psx::launch_serve_emit(args[i], c->stream));
+      }
+      pos += tot[k][i];
+      w.pos[w.n] = pos;
+      w.val[w.n++] = i + 1 < T ? -1 : -2;
+      pos += 4;
+    }
+    HIP_TRY(c, psx::launch_put_words(dst, w, c->stream));
+    if (!out_on_device) HIP_TRY(c, hipMemcpyAsync(out[k], dst, used[k], hipMemcpyDeviceToHost, c->stream));
+  }
+  if (clear_dirty) {
+    for (size_t i = 0; i < T; ++i) {
+      TableState &t = c->tables[i];
+      if (t.ada) {   // ServerRowSent(row, version, subscriber count) (server_table.cpp:250-255)
+        args[i].cmask = ~(uint64_t)0;
+        HIP_TRY(c, psx::launch_serve_sizes(args[i], c->stream));
+        st = ada_rows_sent(c, t, (int)i, nullptr, args[i].sizes, args[i].max_rows, 0, t.d_subs, false);
+        if (st) return st;
+      }
+      HIP_TRY(c, psx::launch_serve_clear(t.d_flags, t.d_imp, t.d_subs, t.cfg.max_rows, c->stream));
+    }
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return PSX_OK;
 }

@@ -41,7 +41,7 @@ __device__ __forceinline__ int64_t body_bytes(const ServeArgs &a, int64_t s) {
 __global__ void __launch_bounds__(256) serve_sizes_kernel(ServeArgs a) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = s < a.max_rows;
-  const bool dirty = in && (a.flags[s] & 3) == 3;
+  const bool dirty = in && (a.flags[s] & 3) == 3 && (!a.subs || (a.subs[s] & a.cmask) != 0);
   if (in) a.sizes[s] = dirty ? 12 + body_bytes(a, s) : 0;
   if (a.keys) {
     if (in) {
@@ -125,6 +125,43 @@ __global__ void __launch_bounds__(256) serve_emit_list_kernel(ServeArgs a) {
   const int64_t wave_g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t i = wave_g; i < a.nsel; i += nwaves) emit_row(a, a.sel[i], a.out + a.loffs[i], lane);
+}
+
+// After a per-client push: every dirty row some client subscribes to was sent — ResetDirty
+// + ResetImportance_ (server_table.cpp:233-235); unsubscribed dirty rows stay dirty (:222-225).
+__global__ void __launch_bounds__(256) serve_clear_kernel(uint8_t *flags, double *imp, const uint64_t *subs,
+                                                         int64_t n) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n && (flags[s] & 3) == 3 && subs[s] != 0) {
+    flags[s] &= (uint8_t)~2u;
+    if (imp) imp[s] = 0.0;
+  }
+}
+
+// FindCreateRow + CallBackSubs::Subscribe for a list of slots (server.cpp:46-60,
+// callback_subs.hpp:21-28): the row exists from now on; the client's bit is set.
+__global__ void __launch_bounds__(256) subscribe_kernel(uint8_t *flags, uint64_t *subs, const int64_t *slots,
+                                                       int32_t n, uint64_t bit) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int64_t s = slots[i];
+    flags[s] |= 1;
+    subs[s] |= bit;
+  }
+}
+
+hipError_t launch_serve_clear(uint8_t *flags, double *imp, const uint64_t *subs, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(serve_clear_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, flags, imp, subs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_subscribe(uint8_t *flags, uint64_t *subs, const int64_t *slots, int32_t n, uint64_t bit,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(subscribe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, flags, subs, slots, n,
+                     bit);
+  return hipGetLastError();
 }
 
 __global__ void put_words_kernel(uint8_t *out, Words w) {

@@ -250,6 +250,56 @@ class Server:
                                       ctypes.byref(used), 0, 1 if clear else 0))
         return out[:used.value]
 
+    # -- clocks and subscriptions (SSP / SSPPush) -------------------------------------
+    def ClockUntil(self, bg_thread_id, clock):
+        """Server::ClockUntil (server.cpp:62-79): advance the sender's clock; returns the new
+        min clock if it advanced, else 0 (the reference's "clock changed")."""
+        out = ctypes.c_int32()
+        _check(self._L, self._ctx, self._L.psx_clock_until(self._ctx, bg_thread_id, clock, ctypes.byref(out)))
+        return out.value
+
+    def GetMinClock(self):
+        out = ctypes.c_int32()
+        _check(self._L, self._ctx, self._L.psx_min_clock(self._ctx, ctypes.byref(out)))
+        return out.value
+
+    def sender_clock(self, bg_thread_id):
+        out = ctypes.c_int32()
+        _check(self._L, self._ctx, self._L.psx_sender_clock(self._ctx, bg_thread_id, ctypes.byref(out)))
+        return out.value
+
+    def set_num_clients(self, n):
+        _check(self._L, self._ctx, self._L.psx_set_num_clients(self._ctx, n))
+        self.num_clients = n
+
+    def subscribe(self, table_id, row_ids, client_id):
+        """FindCreateRow + RowSubscribe for the listed rows (server_thread.cpp:185-200)."""
+        ids = np.ascontiguousarray(row_ids, dtype=np.int32)
+        _check(self._L, self._ctx, self._L.psx_row_subscribe(self._ctx, table_id, ctypes.c_void_p(ids.ctypes.data),
+                                                               int(ids.size), client_id))
+
+    def row_subscriptions(self, table_id, first_row, num_rows):
+        out = np.zeros(num_rows, dtype=np.uint64)
+        _check(self._L, self._ctx, self._L.psx_row_subscriptions(self._ctx, table_id, first_row, num_rows,
+                                                                   ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+    def serialize_push(self, clear=True):
+        """Server::CreateSendServerPushRowMsgs with subscriptions (server.cpp:189-309): a list
+        of num_clients push bodies (bytes), one per client."""
+        C = getattr(self, "num_clients", 1)
+        caps = (ctypes.c_size_t * C)()
+        used = (ctypes.c_size_t * C)()
+        st = self._L.psx_serialize_push(self._ctx, None, caps, used, 0, 0)
+        if st not in (_abi.PSX_OK, 9):
+            _check(self._L, self._ctx, st)
+        bufs = [np.zeros(max(used[k], 1), np.uint8) for k in range(C)]
+        ptrs = (ctypes.c_void_p * C)(*[b.ctypes.data for b in bufs])
+        for k in range(C):
+            caps[k] = bufs[k].size
+        _check(self._L, self._ctx, self._L.psx_serialize_push(self._ctx, ptrs, caps, used, 0, 1 if clear else 0))
+        return [bufs[k][:used[k]].tobytes() for k in range(C)]
+
     # -- client-side pack -------------------------------------------------------------
     def pack_stream(self, tables, with_index=False):
         """Pack per-table oplog rows into one message on the device (psx_pack_stream).
@@ -303,3 +353,56 @@ class Server:
 
     def timing_reset(self):
         _check(self._L, self._ctx, self._L.psx_timing_reset(self._ctx))
+
+
+class ServerThread:
+    """The caller of the apply path: ServerThread::HandleOpLogMsg and HandleRowRequest
+    (server_thread.cpp:185-299) with SSPPush's push-on-clock-change, over any server
+    backend exposing the Server methods below (psx Server; the oracle adapter in tests).
+
+    push(bodies, min_clock): receives one push body per client whenever the server's min
+    clock advances (ServerPushRow -> CreateSendServerPushRowMsgs, ssp_push_server_thread.cpp:39-49).
+    reply(bg_id, table_id, row_id, server_clock, record): the row-request reply
+    (ReplyRowRequest, server_thread.cpp:205-222) with the row as one RecordBuff record.
+    """
+
+    def __init__(self, server, push, reply=None):
+        self.server = server
+        self.push = push
+        self.reply = reply
+        self.requests = {}   # clock -> [(bg_id, table_id, row_id)] (Server::AddRowRequest, server.cpp:81-98)
+
+    @staticmethod
+    def client_of(bg_id):
+        """GlobalContext::thread_id_to_client_id: thread ids are client * 1000 + k (context.hpp:410-414)."""
+        return bg_id // 1000
+
+    def _reply(self, bg_id, table_id, row_id):
+        s = self.server
+        s.subscribe(table_id, [row_id], self.client_of(bg_id))           # RowSubscribe
+        rec = s.serialize_rows(table_id, [row_id])
+        if self.reply:
+            self.reply(bg_id, table_id, row_id, s.GetMinClock(), rec)
+        s.row_sent(table_id, [row_id], 1)                                # Server::RowSent(.., 1)
+
+    def HandleRowRequest(self, bg_id, table_id, row_id, clock):
+        """server_thread.cpp:185-200: answer now, or once the min clock reaches `clock`."""
+        if self.server.GetMinClock() < clock:
+            self.requests.setdefault(clock, []).append((bg_id, table_id, row_id))
+            return False
+        self._reply(bg_id, table_id, row_id)
+        return True
+
+    def HandleOpLogMsg(self, bg_id, payload, is_clock, bg_clock, version):
+        """server_thread.cpp:224-299: apply, advance the sender's clock, and on a new min
+        clock fulfil the waiting row requests and push the dirty rows to every client."""
+        self.server.ApplyOpLogUpdateVersion(payload, len(payload), bg_id, version)
+        changed = False
+        if is_clock:
+            changed = self.server.ClockUntil(bg_id, bg_clock) != 0
+            if changed:   # Server::GetFulfilledRowRequests: the requests of exactly the new min clock
+                for req in self.requests.pop(self.server.GetMinClock(), []):
+                    self._reply(*req)
+        if changed:
+            self.push(self.server.serialize_push(clear=True), self.server.GetMinClock())
+        return changed

@@ -1,0 +1,190 @@
+"""Server clocks, subscriptions and the per-client push (SSPPush) on the GPU, against the
+oracle's restatement, and SURVEY §8(d) C5: a clocked mixed dense + sparse stream under
+SSP staleness 4, every push body of every client compared byte for byte.
+
+The caller is parameter_server_amd.ServerThread (server_thread.cpp:185-299), run once
+over libpsx and once over the oracle on the identical message/request sequence.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import parameter_server_amd as psa
+from parameter_server_amd import wire, ServerThread
+from oracle.oracle import OracleServer, DENSE, SORTED_MAP, F32, I32
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built_lib, oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+class OracleBackend:
+    """The Server methods ServerThread calls, over the oracle."""
+
+    def __init__(self, bgs, num_clients):
+        self.o = OracleServer(bgs)
+        self.num_clients = num_clients
+        self.tables = []
+
+    def create(self, tid, kind, dt, cap, dense_serialized=True):
+        self.o.create_table(tid, kind, dt, cap if kind == DENSE else 0, oplog_dense_serialized=dense_serialized)
+        self.tables.append(tid)
+
+    def ApplyOpLogUpdateVersion(self, payload, size, bg, version):
+        assert self.o.apply_stream(payload, bg, version) == 0
+
+    def ClockUntil(self, bg, clock):
+        return self.o.clock_until(bg, clock)
+
+    def GetMinClock(self):
+        return self.o.min_clock()
+
+    def subscribe(self, tid, rows, client):
+        for r in rows:
+            self.o.subscribe(tid, int(r), client)
+
+    def serialize_rows(self, tid, rows):
+        return self.o.serialize_records(tid, rows)
+
+    def row_sent(self, tid, rows, n):
+        for r in rows:
+            assert self.o.row_sent(tid, int(r), n) == 0
+
+    def serialize_push(self, clear=True):
+        return self.o.serialize_push(self.tables, self.num_clients, clear=clear)
+
+
+def test_clock_until_matches_vector_clock():
+    rng = np.random.RandomState(5)
+    bgs = [1100, 2100, 3100, 4100, 5100]
+    srv = psa.Server(0, 1, bgs)
+    orc = OracleServer(bgs)
+    assert srv.GetMinClock() == orc.min_clock() == 0
+    clocks = {b: 0 for b in bgs}
+    for _ in range(300):
+        b = bgs[rng.randint(len(bgs))]
+        target = clocks[b] + rng.randint(0, 3)
+        clocks[b] = target
+        assert srv.ClockUntil(b, target) == orc.clock_until(b, target)
+        assert srv.GetMinClock() == orc.min_clock() == min(clocks.values())
+        assert srv.sender_clock(b) == target
+
+
+def _backends(bgs, C, tables):
+    srv = psa.Server(0, 1, bgs)
+    srv.set_num_clients(C)
+    orc = OracleBackend(bgs, C)
+    for tid, kind, dt, cap, rows in tables:
+        dense_ser = kind == psa.ROW_DENSE
+        srv.CreateTable(tid, psa.TableInfo(row_kind=kind, dtype=dt, row_capacity=cap, oplog_dense_serialized=dense_ser,
+                                           max_rows=rows, max_entries=cap if kind != psa.ROW_DENSE else 0))
+        orc.create(tid, kind, dt, cap, dense_ser)
+    return srv, orc
+
+
+def test_per_client_push_follows_subscriptions():
+    """Three clients subscribe to different rows; a push sends each client its subscribed
+    dirty rows, leaves unsubscribed dirty rows dirty (server_table.cpp:222-225), and a row
+    subscribed later goes out with the next push."""
+    rng = np.random.RandomState(6)
+    C, rows, cap, K = 3, 200, 16, 32
+    bgs = [c * 1000 + 100 for c in range(C)]
+    srv, orc = _backends(bgs, C, [(1, psa.ROW_DENSE, F32, cap, rows), (3, psa.ROW_SORTED_MAP, I32, K, rows)])
+    for c in range(C):
+        for tid in (1, 3):
+            sub = rng.choice(rows, size=40, replace=False).astype(np.int32)
+            srv.subscribe(tid, sub, c)
+            orc.subscribe(tid, sub, c)
+    for t in (1, 3):
+        got = srv.row_subscriptions(t, 0, rows)
+        assert [int(x) for x in got] == [orc.o.row_subs(t, r) for r in range(rows)]
+    for rnd in range(3):
+        for b, bg in enumerate(bgs):
+            ids1 = rng.permutation(rows)[:120].astype(np.int32)
+            ids3 = rng.permutation(rows)[:60].astype(np.int32)
+            cnt = np.zeros((60, K), np.int32)
+            for r in range(60):
+                cc = rng.choice(K, size=rng.randint(1, 6), replace=False)
+                cnt[r, cc] = rng.choice([-1, 1, 2], size=cc.size)
+            msg = wire.pack_np([dict(table_id=1, dense_serialized=True, row_ids=ids1,
+                                     oplogs=rng.normal(size=(120, cap)).astype(np.float32)),
+                                dict(table_id=3, dense_serialized=False, row_ids=ids3, oplogs=cnt)])
+            srv.ApplyOpLogUpdateVersion(msg, msg.size, bg, rnd)
+            orc.ApplyOpLogUpdateVersion(msg, msg.size, bg, rnd)
+        got, want = srv.serialize_push(), orc.serialize_push()
+        assert got == want, f"round {rnd}"
+        assert all(len(g) > 16 for g in got)
+        # dirty rows nobody subscribes to stay dirty
+        flags = srv.row_flags(1, 0, rows)
+        for r in range(rows):
+            assert bool(flags[r] & 2) == orc.o.row_dirty(1, r)
+        late = int(rng.randint(rows))
+        srv.subscribe(1, [late], 2)
+        orc.subscribe(1, [late], 2)
+
+
+def _c5_workload(rng, C, rows_d, cap, rows_s, K, per_client_d, per_client_s):
+    ids_d = rng.permutation(rows_d)[:per_client_d].astype(np.int32)
+    ids_s = rng.choice(rows_s, size=per_client_s, replace=False).astype(np.int32)
+    cnt = np.zeros((per_client_s, K), np.int32)
+    for r in range(per_client_s):
+        cc = rng.choice(K, size=rng.randint(1, 17), replace=False)
+        cnt[r, cc] = rng.choice([-1, 1, 2], size=cc.size)
+    return wire.pack_np([dict(table_id=1, dense_serialized=True, row_ids=ids_d,
+                              oplogs=rng.normal(0, 0.01, size=(per_client_d, cap)).astype(np.float32)),
+                         dict(table_id=3, dense_serialized=False, row_ids=ids_s, oplogs=cnt)])
+
+
+def test_c5_ssp_staleness4_clocked_stream():
+    """C5 (reduced): 8 clients (one bg thread each), a dense f32 table and a sorted-map
+    int32 table, 14 clocks.  Clients send one is_clock message per clock in a random
+    arrival order bounded by SSP staleness 4 (a client at clock c blocks in Get until the
+    server's pushed min clock reaches c - 4, ssp_push_consistency_controller.cpp:70-88);
+    row requests arrive along the way (some wait for their clock, server.cpp:81-118).
+    Every push body of every client and every row-request reply must match the oracle."""
+    rng = np.random.RandomState(55)
+    C, staleness, clocks = 8, 4, 14
+    rows_d, cap, rows_s, K = 4096, 64, 3000, 128
+    bgs = [c * 1000 + 100 for c in range(C)]
+    srv, orc = _backends(bgs, C, [(1, psa.ROW_DENSE, F32, cap, rows_d), (3, psa.ROW_SORTED_MAP, I32, K, rows_s)])
+    log = {"gpu": [], "orc": []}
+    threads = {
+        "gpu": ServerThread(srv, lambda bodies, clk: log["gpu"].append(("push", clk, bodies)),
+                            lambda bg, t, r, clk, rec: log["gpu"].append(("reply", bg, t, r, clk, rec))),
+        "orc": ServerThread(orc, lambda bodies, clk: log["orc"].append(("push", clk, bodies)),
+                            lambda bg, t, r, clk, rec: log["orc"].append(("reply", bg, t, r, clk, rec))),
+    }
+    for c in range(C):   # initial reads: every client subscribes to its working set
+        for tid, n in ((1, rows_d), (3, rows_s)):
+            sub = rng.choice(n, size=n // 4, replace=False)
+            for th in threads.values():
+                th.server.subscribe(tid, sub.astype(np.int32), c)
+    client_clock = [0] * C
+    min_pushed = 0
+    events = 0
+    while min(client_clock) < clocks:
+        ready = [c for c in range(C) if client_clock[c] < clocks and client_clock[c] - min_pushed <= staleness]
+        c = int(rng.choice(ready))
+        msg = _c5_workload(rng, C, rows_d, cap, rows_s, K, rows_d // 4, 200)
+        req = None
+        if rng.rand() < 0.3:   # a Get that misses the cache: row request at the client's clock
+            req = (bgs[c], 3, int(rng.randint(rows_s)), client_clock[c] + int(rng.randint(0, 3)))
+        for th in threads.values():
+            if req:
+                th.HandleRowRequest(*req)
+            th.HandleOpLogMsg(bgs[c], msg, True, client_clock[c] + 1, client_clock[c])
+        client_clock[c] += 1
+        min_pushed = srv.GetMinClock()
+        events += 1
+    assert srv.GetMinClock() == orc.GetMinClock() == clocks
+    assert len(log["gpu"]) == len(log["orc"]) and len(log["gpu"]) >= clocks
+    for k, (g, o) in enumerate(zip(log["gpu"], log["orc"])):
+        assert g == o, f"event {k}: {g[0]}"
+    np.testing.assert_array_equal(srv.read_rows(1, 0, rows_d).view(np.uint32),
+                                  orc.o.read_dense_rows(1, 0, rows_d).view(np.uint32))
+    assert srv.serialize_rows(3, list(range(rows_s))) == orc.o.serialize_records(3, list(range(rows_s)))

@@ -1,0 +1,84 @@
+"""Interleaved A/B of C2 kernel selectors in one process (cdna_hip_programming.md §5.4
+rule 24): the headline workload of bench.py, then R rounds; each round runs every
+configuration for K steps and records the per-kernel HIP-event times.  Prints JSON with
+the median ms of every kernel per configuration.
+Usage: python tools/ab_c2.py --configs 0:0,1:0,2:0 [--rounds 5 --steps 5]
+       (index_variant:apply_variant, include/psx_debug.h)"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="0:0,1:0")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=1 << 20)
+    ap.add_argument("--cols", type=int, default=256)
+    ap.add_argument("--batches", type=int, default=8)
+    args = ap.parse_args()
+    import torch
+    import parameter_server_amd as psa
+    from parameter_server_amd import wire, _abi
+    L = _abi.load()
+    rows, cap, B = args.rows, args.cols, args.batches
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    table0 = torch.randn(rows, cap, device="cuda", generator=g) * 0.1
+    streams = []
+    for b in range(B):
+        perm = torch.randperm(rows, device="cuda", generator=g).to(torch.int32)
+        upd = torch.randn(rows, cap, device="cuda", generator=g) * 0.01
+        streams.append(wire.dense_stream_torch(1, perm, upd))
+        del upd, perm
+    bgs = [100 + b for b in range(B)]
+    srv = psa.Server(device=0, server_id=1, bg_ids=bgs)
+    srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows))
+    srv.load_rows(1, 0, None, on_device_ptr=table0.data_ptr(), num_rows=rows)
+    del table0
+    ver = [0]
+    kernels = ("decode_streams", "dense_index", "dense_verify", "dense_apply", "finish_call")
+    configs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
+    res = {c: {k: [] for k in kernels + ("step",)} for c in configs}
+
+    def run(c, steps):
+        L.psx_debug_set_variant(0, c[0])
+        L.psx_debug_set_variant(1, c[1])
+        srv.timing(True)
+        srv.timing_reset()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record()
+        for _ in range(steps):
+            srv.apply_device([(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)])
+            ver[0] += 1
+        ev1.record()
+        srv.sync()
+        torch.cuda.synchronize()
+        out = {k: srv.timing_read(k) for k in kernels}
+        srv.timing(False)
+        return out, ev0.elapsed_time(ev1) / steps
+
+    for c in configs:   # warm-up of every configuration
+        run(c, 2)
+    for _ in range(args.rounds):
+        for c in configs:
+            kt, step_ms = run(c, args.steps)
+            for k in kernels:
+                ms, n = kt[k]
+                res[c][k].append(ms / max(n, 1))
+            res[c]["step"].append(step_ms)
+    out = {f"index{c[0]}_apply{c[1]}": {k: round(statistics.median(v), 4) for k, v in res[c].items()}
+           for c in configs}
+    print(json.dumps(out, indent=1))
+    srv.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -7,9 +7,11 @@ mkdir -p gpurun_out/s1
 export TMPDIR=/tmp
 step() { echo "== $(date +%T) $*"; }
 step pytest
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-  > gpurun_out/s1/pytest.log 2>&1 || { tail -30 gpurun_out/s1/pytest.log; exit 1; }
-tail -3 gpurun_out/s1/pytest.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+  > gpurun_out/s1/pytest.log 2>&1
+rc=$?
+grep -E "^FAILED|^ERROR|passed|failed" gpurun_out/s1/pytest.log | tail -30
+case $rc in 0|1) ;; *) echo "pytest rc=$rc: stopping"; exit 1;; esac
 step bench
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/s1/bench.log 2>&1 || { tail -20 gpurun_out/s1/bench.log; exit 1; }
 tail -1 gpurun_out/s1/bench.log | cut -c1-600

@@ -63,7 +63,56 @@ def parse():
     p.add_argument("--pcie", action="store_true",
                    help="also time the host-buffer form: pinned H2D of the 8 messages + apply + D2H of "
                         "every (dirty) row, i.e. the rate including PCIe (reported, never `value`)")
+    p.add_argument("--master-port", type=int, default=29531,
+                   help="rendezvous port when bench.py launches its own ranks (--gpus N, WORLD_SIZE unset)")
+    p.add_argument("--selftest-launch", action="store_true",
+                   help="exercise only the multi-rank harness (rank launch, barriers, max-over-ranks timing, "
+                        "the JSON line) over gloo with a no-op step: the CPU test of --gpus N")
     return p.parse_args()
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` without a launcher: start N ranks, one per GPU, through
+    torch.distributed.run as a CHILD process (this process has touched no GPU) and exit
+    with its status.  Rank 0 prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={args.master_port}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def selftest_launch(args):
+    """The harness of the N-rank bench with a no-op step (gloo, CPU): barrier + max-over-
+    ranks timing around K steps, rank 0 prints one JSON line with n_gpus = world."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    for _ in range(args.warmup):
+        pass
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (1 + rank))
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "selftest-launch", "value": round(args.steps / el, 3), "unit": "steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 4)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(args):
@@ -434,6 +483,10 @@ def run_c5(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.selftest_launch:
+        return selftest_launch(args)
     if args.workload == "c5":
         return run_c5(args)
     if args.workload == "c3":

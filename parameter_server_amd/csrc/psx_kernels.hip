@@ -958,9 +958,9 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
 
 // dense_index_v2: flattened (message, record) space, UNROLL row-id loads in flight per
 // thread before any store.
-// MODE 0: non-temporal row-id loads; 1: plain loads; 2: plain loads issued one lane at a
-// time (a wave instruction touching 64 lines leaves L2 as 128-B requests; the A/B of the
-// request size a single-lane load produces is profiles/r02).
+// MODE 0: non-temporal row-id loads; 1: plain loads.  Either way every 4-byte row id costs
+// one 128-B L2->DRAM request (PMC, profiles/r02/pmc_request_sizes_index_apply.json); loads
+// issued one lane at a time were no faster (profiles/r02/ab_index_loads.json).
 template <int UNROLL, int MODE>
 __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const Seg *segs, int t, int B,
                                                             int64_t stride, Geo g, int32_t *inv, InvLayout L,
@@ -1005,23 +1005,9 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
         ptr[u] = reinterpret_cast<const int32_t *>(base[b] + ii[u] * stride);
       }
     }
-    if constexpr (MODE == 2) {
-      typedef const int32_t __attribute__((address_space(1))) *gint_p;
-      const int lane = threadIdx.x & 63;
-      gint_p gp[UNROLL];
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) gp[u] = (gint_p)(ptr[u] ? ptr[u] : reinterpret_cast<const int32_t *>(base[0]));
-      for (int l = 0; l < 64; ++l) {
-        if (lane == l) {
-#pragma unroll
-          for (int u = 0; u < UNROLL; ++u) rid[u] = *gp[u];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u)
-        if (ptr[u]) rid[u] = MODE == 0 ? __builtin_nontemporal_load(ptr[u]) : *ptr[u];
-    }
+    for (int u = 0; u < UNROLL; ++u)
+      if (ptr[u]) rid[u] = MODE == 0 ? __builtin_nontemporal_load(ptr[u]) : *ptr[u];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       if (bi[u] < 0) continue;
@@ -1091,7 +1077,7 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
 // Run-time selectors (include/psx_debug.h): the defaults are the measured winners; the
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
-int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads, 2: plain, one lane at a time
+int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads
 int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact), 3: v3 with plain record loads
 
 hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
@@ -1100,9 +1086,6 @@ hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64
   Geo g{row_offset, row_stride, max_rows};
   if (g_index_variant == 1)
     hipLaunchKernelGGL((dense_index_v2_kernel<8, 1>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
-                       call_status);
-  else if (g_index_variant == 2)
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, 2>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
                        call_status);
   else
     hipLaunchKernelGGL((dense_index_v2_kernel<8, 0>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,

@@ -9,6 +9,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -52,18 +53,17 @@ def main():
         L.psx_debug_set_variant(1, c[1])
         srv.timing(True)
         srv.timing_reset()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
-        ev0.record()
+        t0 = time.perf_counter()
         for _ in range(steps):
             srv.apply_device([(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)])
             ver[0] += 1
-        ev1.record()
         srv.sync()
         torch.cuda.synchronize()
+        el = time.perf_counter() - t0
         out = {k: srv.timing_read(k) for k in kernels}
         srv.timing(False)
-        return out, ev0.elapsed_time(ev1) / steps
+        return out, el / steps * 1e3
 
     for c in configs:   # warm-up of every configuration
         run(c, 2)

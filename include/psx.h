@@ -39,6 +39,13 @@
  *                                                        src/petuum_ps/server/server.cpp:311-420,
  *                           ServerTable::GetPartialTableToSendRegular / AppendRowsToBuffsPartial
  *                                                        src/petuum_ps/server/server_table.cpp:301-346,381-420
+ *   psx_encode/decode_oplog_header  ClientSendOpLogMsg  src/petuum_ps/thread/ps_msgs.hpp:1003-1055,
+ *                                                        src/petuum_ps_common/thread/msg_base.hpp:81-188
+ *   psx_encode/decode_push_header   ServerPushRowMsg    src/petuum_ps/thread/ps_msgs.hpp:1057-1103
+ *   psx_handle_oplog_msg    ServerThread::HandleOpLogMsg (apply + ClockUntil)
+ *                                                        src/petuum_ps/server/server_thread.cpp:224-266
+ *   psx_ctx_set_compat      SerializedOpLogReader's int32 offset_
+ *                                                        src/petuum_ps/server/serialized_oplog_reader.hpp:137
  *   psx_clock_until         Server::ClockUntil -> VectorClock::TickUntil
  *                                                        src/petuum_ps/server/server.cpp:62-79,
  *                                                        src/petuum_ps_common/util/vector_clock.cpp:28-79
@@ -47,6 +54,10 @@
  *                                                        src/petuum_ps/server/server.cpp:46-60,
  *                                                        src/petuum_ps/server/ssp_push_server_thread.cpp:51-54,
  *                                                        src/petuum_ps/server/callback_subs.hpp:21-28
+ *   psx_apply_push_body     SSPPushBgWorker::ApplyServerPushedRow -> SerializedRowReader -> ResetRowData
+ *                                                        src/petuum_ps/thread/ssp_push_bg_worker.cpp:70-122,
+ *                                                        src/petuum_ps/client/serialized_row_reader.hpp:30-100,
+ *                                                        src/petuum_ps_common/storage/numeric_store_row.hpp:142-145
  *   psx_serialize_push      Server::CreateSendServerPushRowMsgs with subscriptions (one body per client)
  *                                                        src/petuum_ps/server/server.cpp:189-309,
  *                                                        src/petuum_ps/server/server_table.cpp:197-261,
@@ -267,6 +278,56 @@ psx_status psx_serialize_dirty(psx_ctx *ctx, void *out, size_t cap, size_t *used
 psx_status psx_serialize_partial(psx_ctx *ctx, void *out, size_t cap, size_t *used,
                                  int32_t out_on_device, int32_t clear_dirty);
 
+/* ---- message headers --------------------------------------------------------------- */
+/* MsgType values (msg_base.hpp:14-40) of the two messages on the path. */
+#define PSX_MSG_CLIENT_SEND_OPLOG 12
+#define PSX_MSG_SERVER_PUSH_ROW 18
+/* ClientSendOpLogMsg (ps_msgs.hpp:1003-1055): the ArbitrarySizedMsg prefix MsgType(4)
+ * seq(8) ack(8) avai_size(8) (msg_base.hpp:81-188), then is_clock(1) client_id(4)
+ * version(4) bg_clock(4): 41 bytes, packed, little endian; the oplog stream follows. */
+#define PSX_OPLOG_MSG_HEADER_BYTES 41
+typedef struct psx_oplog_msg_header {
+  uint64_t seq_num;     /* NumberedMsg::get_seq_num (flow control, msg_tracker.cpp) */
+  uint64_t ack_num;
+  uint64_t avai_size;   /* payload bytes */
+  int32_t is_clock;     /* bool */
+  int32_t client_id;
+  uint32_t version;     /* the sender's message version (server.cpp:124-126) */
+  int32_t bg_clock;     /* the sender's clock when is_clock (server_thread.cpp:262-263) */
+} psx_oplog_msg_header;
+/* ServerPushRowMsg (ps_msgs.hpp:1057-1103): the same prefix, then clock(4) version(4)
+ * is_clock(1): 37 bytes; the push body follows. */
+#define PSX_PUSH_MSG_HEADER_BYTES 37
+typedef struct psx_push_msg_header {
+  uint64_t seq_num;
+  uint64_t ack_num;
+  uint64_t avai_size;
+  int32_t clock;        /* the server's min clock (ssp_push_server_thread.cpp:28-31) */
+  uint32_t version;     /* the receiver's last applied message version */
+  int32_t is_clock;
+} psx_push_msg_header;
+/* out: PSX_OPLOG_MSG_HEADER_BYTES / PSX_PUSH_MSG_HEADER_BYTES bytes.  Decode checks the
+ * message type and that avai_size payload bytes follow within msg_size. */
+psx_status psx_encode_oplog_header(const psx_oplog_msg_header *h, void *out);
+psx_status psx_decode_oplog_header(const void *msg, size_t msg_size, psx_oplog_msg_header *h);
+psx_status psx_encode_push_header(const psx_push_msg_header *h, void *out);
+psx_status psx_decode_push_header(const void *msg, size_t msg_size, psx_push_msg_header *h);
+
+/* Reference-compatibility mode.  PSX_COMPAT_INT32_STREAM_OFFSETS: reject (PSX_ERR_UNSUPPORTED,
+ * nothing applied) any message of 2 GiB or more — the reference's SerializedOpLogReader
+ * keeps its cursor in an int32 offset_ (serialized_oplog_reader.hpp:137); producers split
+ * larger batches (wire.split_stream).  Default 0: 64-bit offsets, any size. */
+#define PSX_COMPAT_INT32_STREAM_OFFSETS 1
+psx_status psx_ctx_set_compat(psx_ctx *ctx, int32_t flags);
+
+/* ServerThread::HandleOpLogMsg's server part (server_thread.cpp:224-266) on a whole
+ * ClientSendOpLogMsg in host memory: decode the header, apply the payload
+ * (psx_apply_stream) and, for a clock message, psx_clock_until(sender, bg_clock);
+ * *clock_changed receives the new min clock if it advanced, else 0 (then the caller pushes,
+ * psx_serialize_push, and acks). */
+psx_status psx_handle_oplog_msg(psx_ctx *ctx, const void *msg, size_t msg_size, int32_t sender,
+                                int32_t *clock_changed);
+
 /* ---- clocks (SSP) ------------------------------------------------------------------- */
 /* bg_clock_: every registered sender starts at clock 0 (Server::Init, server.cpp:21-24).
  * psx_clock_until advances bg_id's clock to `clock` one tick at a time
@@ -301,6 +362,24 @@ psx_status psx_row_subscriptions(psx_ctx *ctx, int32_t table_id, int64_t first_r
  * subscribes to every row.  out_on_device: out[c] are 4-byte-aligned device buffers. */
 psx_status psx_serialize_push(psx_ctx *ctx, void *const *out, const size_t *cap, size_t *used,
                               int32_t out_on_device, int32_t clear_dirty);
+
+/* ---- client side of serve-back ------------------------------------------------------ */
+/* A push body (or row-request reply) applied to this context used as a client process
+ * cache: SSPPushBgWorker::ApplyServerPushedRow (ssp_push_bg_worker.cpp:70-122) walks it
+ * with SerializedRowReader (serialized_row_reader.hpp:30-100) and, for every record of a
+ * row the cache holds (flags bit0; with insert_missing also rows it does not hold —
+ * InsertNonexistentRow, abstract_bg_worker.cpp:853-870), replaces the row with the bytes:
+ * ResetRowData (numeric_store_row.hpp:142-145) — dense rows are overwritten
+ * (VectorStore::ResetData), sorted/map rows are rebuilt from the entries (Deserialize).
+ * Version tables take the trailing uint64 as the row's version (ExtractRowVersion,
+ * abstract_bg_worker.cpp:1032-1040).  A row twice in one body ends with its last record.
+ * Oplog replay onto the reset row (no_oplog_replay = false) is the caller's.  Records of
+ * rows outside the context's shard are skipped; an unknown table, a malformed body or a
+ * sorted/map row over max_entries fails the call with nothing applied.  body_on_device: a
+ * 4-byte-aligned device buffer (walked on the device); otherwise host bytes, borrowed for
+ * the call.  Synchronous. */
+psx_status psx_apply_push_body(psx_ctx *ctx, const void *body, size_t size, int32_t body_on_device,
+                               int32_t insert_missing);
 
 /* ---- AdaRevision server-table logic ------------------------------------------------ */
 /* AdaRevisionServerTableLogic (src/petuum_ps/server/adarevision_server_table_logic.cpp),

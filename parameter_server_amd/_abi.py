@@ -78,6 +78,34 @@ class psx_adarevision_config(ctypes.Structure):
     ]
 
 
+class psx_oplog_msg_header(ctypes.Structure):
+    _fields_ = [
+        ("seq_num", ctypes.c_uint64),
+        ("ack_num", ctypes.c_uint64),
+        ("avai_size", ctypes.c_uint64),
+        ("is_clock", ctypes.c_int32),
+        ("client_id", ctypes.c_int32),
+        ("version", ctypes.c_uint32),
+        ("bg_clock", ctypes.c_int32),
+    ]
+
+
+class psx_push_msg_header(ctypes.Structure):
+    _fields_ = [
+        ("seq_num", ctypes.c_uint64),
+        ("ack_num", ctypes.c_uint64),
+        ("avai_size", ctypes.c_uint64),
+        ("clock", ctypes.c_int32),
+        ("version", ctypes.c_uint32),
+        ("is_clock", ctypes.c_int32),
+    ]
+
+
+OPLOG_MSG_HEADER_BYTES = 41
+PUSH_MSG_HEADER_BYTES = 37
+COMPAT_INT32_STREAM_OFFSETS = 1
+
+
 class PsxError(RuntimeError):
     def __init__(self, status, msg):
         self.status = status
@@ -139,6 +167,13 @@ def load():
         "psx_row_subscribe": ([vp, i32, vp, i32, i32], ctypes.c_int),
         "psx_row_subscriptions": ([vp, i32, i64, i64, vp], ctypes.c_int),
         "psx_serialize_push": ([vp, vp, vp, vp, i32, i32], ctypes.c_int),
+        "psx_apply_push_body": ([vp, vp, sz, i32, i32], ctypes.c_int),
+        "psx_encode_oplog_header": ([P(psx_oplog_msg_header), vp], ctypes.c_int),
+        "psx_decode_oplog_header": ([vp, sz, P(psx_oplog_msg_header)], ctypes.c_int),
+        "psx_encode_push_header": ([P(psx_push_msg_header), vp], ctypes.c_int),
+        "psx_decode_push_header": ([vp, sz, P(psx_push_msg_header)], ctypes.c_int),
+        "psx_ctx_set_compat": ([vp, i32], ctypes.c_int),
+        "psx_handle_oplog_msg": ([vp, vp, sz, i32, P(i32)], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),
         "psx_timing_enable": ([vp, i32], ctypes.c_int),

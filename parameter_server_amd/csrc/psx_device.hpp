@@ -266,6 +266,31 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
   return x;
 }
 
+// One record of a push body (psx_client.hip): its table, row, and payload bytes.
+struct PushEntry {
+  int32_t table_id;
+  int32_t row_id;
+  uint64_t offset;   // byte offset of the row bytes in the body
+  uint64_t size;     // size_t size of the record (row bytes + version trailer)
+};
+
+// A client-cache table as the push apply sees it (device array, one per table).
+struct ClientTable {
+  int32_t table_id;
+  int32_t kind;      // psx_row_kind
+  int32_t vsize;
+  int32_t es;        // sizeof(Entry<V>)
+  int64_t row_cap;
+  int64_t max_entries;
+  int64_t row_offset, row_stride, max_rows;
+  uint8_t *flags;
+  uint8_t *dense;
+  uint8_t *entries;
+  int32_t *nent;
+  uint64_t *ver;     // version tables: the pushed row version
+  int32_t *claim;    // per slot, zero between calls
+};
+
 // Write a few 4-byte words (table ids and separators) into the body.
 struct Words {
   int32_t n;

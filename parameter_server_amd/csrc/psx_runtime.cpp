@@ -59,6 +59,10 @@ hipError_t launch_put_words(uint8_t *out, const Words &w, hipStream_t st);
 hipError_t launch_serve_clear(uint8_t *flags, double *imp, const uint64_t *subs, int64_t n, hipStream_t st);
 hipError_t launch_subscribe(uint8_t *flags, uint64_t *subs, const int64_t *slots, int32_t n, uint64_t bit,
                             hipStream_t st);
+hipError_t launch_push_walk(const uint8_t *body, uint64_t size, PushEntry *ent, uint32_t *nent, uint32_t max_ent,
+                            uint32_t *status, hipStream_t st);
+hipError_t launch_push_apply(const uint8_t *body, const PushEntry *ent, const uint32_t *nent, uint32_t max_ent,
+                             const ClientTable *ct, int nt, int insert, uint32_t *status, hipStream_t st);
 hipError_t launch_serve_list_sizes(const ServeArgs &a, hipStream_t st);
 hipError_t launch_serve_emit_list(const ServeArgs &a, hipStream_t st);
 hipError_t launch_pack_count(int dtype, PackTab t, hipStream_t st);
@@ -162,6 +166,7 @@ struct psx_ctx {
   std::map<int32_t, int32_t> clocks;     // bg_clock_ (VectorClock::vec_clock_)
   int32_t min_clock = -1;                // VectorClock::min_clock_
   int32_t num_clients = 1;               // GlobalContext::get_num_clients (per-client push)
+  int32_t compat = 0;                    // psx_ctx_set_compat flags
   std::vector<TableState> tables;
   bool has_ada = false;                  // some table runs the AdaRevision logic
   // Per-call state lives in two slots (call k uses slot k & 1) so that the decode/index
@@ -176,6 +181,12 @@ struct psx_ctx {
   hipEvent_t ev_free[2] = {nullptr, nullptr};     // slot's apply stage done (main -> side)
   bool pipeline = false;                          // PSX_PIPELINE=1: overlap (no gain measured, DRAM-bound)
   uint32_t *d_ndirty = nullptr;          // partial push: dirty-row count
+  uint8_t *d_push_body = nullptr;        // psx_apply_push_body: host body staged in HBM
+  size_t push_body_cap = 0;
+  psx::PushEntry *d_push_ent = nullptr;  // the body's records
+  size_t push_ent_cap = 0;
+  uint32_t *d_push_words = nullptr;      // [0] records, [1] status
+  psx::ClientTable *d_client_tabs = nullptr;
   int64_t *d_pack = nullptr;             // psx_pack_stream: sparse record sizes + offsets
   size_t pack_cap = 0;                   // entries
   uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
@@ -851,6 +862,10 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->d_status) hipFree(c->d_status);
   if (c->d_zero) hipFree(c->d_zero);
   if (c->d_ndirty) hipFree(c->d_ndirty);
+  if (c->d_push_body) hipFree(c->d_push_body);
+  if (c->d_push_ent) hipFree(c->d_push_ent);
+  if (c->d_push_words) hipFree(c->d_push_words);
+  if (c->d_client_tabs) hipFree(c->d_client_tabs);
   if (c->d_pack) hipFree(c->d_pack);
   if (c->d_staging) hipFree(c->d_staging);
   if (c->own) hipStreamDestroy(c->own);
@@ -1150,6 +1165,9 @@ static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
   // the whole batch before anything is enqueued.
   std::map<int32_t, int64_t> v = c->versions;
   for (int i = 0; i < n; ++i) {
+    if ((c->compat & PSX_COMPAT_INT32_STREAM_OFFSETS) && s[i].size > (size_t)INT32_MAX)
+      return fail(c, PSX_ERR_UNSUPPORTED, "stream of " + std::to_string(s[i].size) +
+                                              " bytes: the reference reader's int32 offset_ caps messages below 2 GiB");
     if (s[i].size && (!s[i].data || ((uintptr_t)s[i].data & 3)))
       return fail(c, PSX_ERR_INVALID_ARG, "device stream must be non-null and 4-byte aligned");
     auto it = v.find(s[i].bg_id);
@@ -1173,6 +1191,9 @@ static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
 psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, int32_t bg_id,
                             uint32_t version) {
   if (!c || (oplog_size && !oplog)) return PSX_ERR_INVALID_ARG;
+  if ((c->compat & PSX_COMPAT_INT32_STREAM_OFFSETS) && oplog_size > (size_t)INT32_MAX)
+    return fail(c, PSX_ERR_UNSUPPORTED, "stream of " + std::to_string(oplog_size) +
+                                            " bytes: the reference reader's int32 offset_ caps messages below 2 GiB");
   auto it = c->versions.find(bg_id);
   if (it == c->versions.end()) return fail(c, PSX_ERR_SENDER, "bg_id " + std::to_string(bg_id) + " not registered");
   if (it->second + 1 != (int64_t)version)
@@ -1866,6 +1887,171 @@ psx_status psx_serialize_push(psx_ctx *c, void *const *out, const size_t *cap, s
     }
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return PSX_OK;
+}
+
+// ---- client side of serve-back ----------------------------------------------------------
+
+psx_status psx_apply_push_body(psx_ctx *c, const void *body, size_t size, int32_t body_on_device,
+                               int32_t insert_missing) {
+  if (!c || (size && !body)) return PSX_ERR_INVALID_ARG;
+  if (body_on_device && ((uintptr_t)body & 3)) return fail(c, PSX_ERR_INVALID_ARG, "device body must be 4-byte aligned");
+  if (size == 0) return PSX_OK;
+  psx_status st = sync_impl(c);
+  if (st) return st;
+  const size_t max_ent = size / 12 + 1;
+  if (!body_on_device && size > c->push_body_cap) {
+    if (c->d_push_body) hipFree(c->d_push_body);
+    c->d_push_body = nullptr;
+    c->push_body_cap = 0;
+    HIP_TRY(c, hipMalloc(&c->d_push_body, size));
+    c->push_body_cap = size;
+  }
+  if (max_ent > c->push_ent_cap) {
+    if (c->d_push_ent) hipFree(c->d_push_ent);
+    c->d_push_ent = nullptr;
+    c->push_ent_cap = 0;
+    HIP_TRY(c, hipMalloc(&c->d_push_ent, max_ent * sizeof(psx::PushEntry)));
+    c->push_ent_cap = max_ent;
+  }
+  if (!c->d_push_words) HIP_TRY(c, hipMalloc(&c->d_push_words, 2 * sizeof(uint32_t)));
+  if (!c->d_client_tabs) HIP_TRY(c, hipMalloc(&c->d_client_tabs, psx::kMaxTables * sizeof(psx::ClientTable)));
+  std::vector<psx::ClientTable> ct(c->tables.size());
+  for (size_t i = 0; i < c->tables.size(); ++i) {
+    TableState &t = c->tables[i];
+    psx::ClientTable &x = ct[i];
+    x = psx::ClientTable{};
+    x.table_id = t.cfg.table_id;
+    x.kind = t.cfg.row_kind;
+    x.vsize = t.vsize;
+    x.es = t.es;
+    x.row_cap = t.cfg.row_capacity;
+    x.max_entries = t.max_entries;
+    x.row_offset = t.cfg.row_offset;
+    x.row_stride = t.cfg.row_stride;
+    x.max_rows = t.cfg.max_rows;
+    x.flags = t.d_flags;
+    x.dense = (uint8_t *)t.d_data;
+    x.entries = t.d_entries;
+    x.nent = t.d_nent;
+    x.ver = t.d_ver;
+    x.claim = t.d_cnt;   // the ordered path's per-slot counts: zero between calls
+  }
+  const uint8_t *dbody = (const uint8_t *)body;
+  if (!body_on_device) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_push_body, body, size, hipMemcpyHostToDevice, c->stream));
+    dbody = c->d_push_body;
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->d_client_tabs, ct.data(), ct.size() * sizeof(psx::ClientTable), hipMemcpyHostToDevice,
+                            c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_push_words, 0, 2 * sizeof(uint32_t), c->stream));
+  uint32_t *nent = c->d_push_words, *status = c->d_push_words + 1;
+  st = timed(c, "push_walk", [&] {
+    return psx::launch_push_walk(dbody, size, c->d_push_ent, nent, (uint32_t)max_ent, status, c->stream);
+  });
+  if (st) return st;
+  st = timed(c, "push_apply", [&] {
+    return psx::launch_push_apply(dbody, c->d_push_ent, nent, (uint32_t)max_ent, c->d_client_tabs, (int)ct.size(),
+                                  insert_missing ? 1 : 0, status, c->stream);
+  });
+  if (st) return st;
+  uint32_t words[2] = {0, 0};
+  HIP_TRY(c, hipMemcpyAsync(words, c->d_push_words, sizeof(words), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (words[1] & psx::kStUnknownTable) return fail(c, PSX_ERR_UNKNOWN_TABLE, "push body names a table this context lacks");
+  if (words[1] & psx::kStMalformed) return fail(c, PSX_ERR_MALFORMED, "malformed push body");
+  if (words[1] & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "pushed row exceeds max_entries");
+  return PSX_OK;
+}
+
+// ---- message headers (ps_msgs.hpp / msg_base.hpp) ---------------------------------------
+
+namespace {
+void put32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+void put64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+}  // namespace
+
+// ArbitrarySizedMsg prefix: MsgType(4) seq(8) ack(8) avai_size(8) (msg_base.hpp:81-188)
+psx_status psx_encode_oplog_header(const psx_oplog_msg_header *h, void *out) {
+  if (!h || !out) return PSX_ERR_INVALID_ARG;
+  uint8_t *p = (uint8_t *)out;
+  put32(p + 0, (uint32_t)PSX_MSG_CLIENT_SEND_OPLOG);
+  put64(p + 4, h->seq_num);
+  put64(p + 12, h->ack_num);
+  put64(p + 20, h->avai_size);
+  p[28] = h->is_clock ? 1 : 0;                 // bool is_clock (ps_msgs.hpp:1018-1021)
+  put32(p + 29, (uint32_t)h->client_id);       // :1023-1026
+  put32(p + 33, h->version);                   // :1028-1032
+  put32(p + 37, (uint32_t)h->bg_clock);        // :1034-1038
+  return PSX_OK;
+}
+
+psx_status psx_decode_oplog_header(const void *msg, size_t msg_size, psx_oplog_msg_header *h) {
+  if (!msg || !h) return PSX_ERR_INVALID_ARG;
+  if (msg_size < PSX_OPLOG_MSG_HEADER_BYTES) return PSX_ERR_MALFORMED;
+  const uint8_t *p = (const uint8_t *)msg;
+  if ((int32_t)rd32h(p) != PSX_MSG_CLIENT_SEND_OPLOG) return PSX_ERR_MALFORMED;
+  h->seq_num = rd64h(p + 4);
+  h->ack_num = rd64h(p + 12);
+  h->avai_size = rd64h(p + 20);
+  h->is_clock = p[28] ? 1 : 0;
+  h->client_id = (int32_t)rd32h(p + 29);
+  h->version = rd32h(p + 33);
+  h->bg_clock = (int32_t)rd32h(p + 37);
+  // get_size() = header + avai_size (:1045-1048): the payload must be all there
+  if (h->avai_size > msg_size - PSX_OPLOG_MSG_HEADER_BYTES) return PSX_ERR_MALFORMED;
+  return PSX_OK;
+}
+
+psx_status psx_encode_push_header(const psx_push_msg_header *h, void *out) {
+  if (!h || !out) return PSX_ERR_INVALID_ARG;
+  uint8_t *p = (uint8_t *)out;
+  put32(p + 0, (uint32_t)PSX_MSG_SERVER_PUSH_ROW);
+  put64(p + 4, h->seq_num);
+  put64(p + 12, h->ack_num);
+  put64(p + 20, h->avai_size);
+  put32(p + 28, (uint32_t)h->clock);           // ServerPushRowMsg::get_clock (ps_msgs.hpp:1072-1075)
+  put32(p + 32, h->version);                   // :1077-1080
+  p[36] = h->is_clock ? 1 : 0;                 // :1082-1086
+  return PSX_OK;
+}
+
+psx_status psx_decode_push_header(const void *msg, size_t msg_size, psx_push_msg_header *h) {
+  if (!msg || !h) return PSX_ERR_INVALID_ARG;
+  if (msg_size < PSX_PUSH_MSG_HEADER_BYTES) return PSX_ERR_MALFORMED;
+  const uint8_t *p = (const uint8_t *)msg;
+  if ((int32_t)rd32h(p) != PSX_MSG_SERVER_PUSH_ROW) return PSX_ERR_MALFORMED;
+  h->seq_num = rd64h(p + 4);
+  h->ack_num = rd64h(p + 12);
+  h->avai_size = rd64h(p + 20);
+  h->clock = (int32_t)rd32h(p + 28);
+  h->version = rd32h(p + 32);
+  h->is_clock = p[36] ? 1 : 0;
+  if (h->avai_size > msg_size - PSX_PUSH_MSG_HEADER_BYTES) return PSX_ERR_MALFORMED;
+  return PSX_OK;
+}
+
+psx_status psx_ctx_set_compat(psx_ctx *c, int32_t flags) {
+  if (!c || (flags & ~PSX_COMPAT_INT32_STREAM_OFFSETS)) return PSX_ERR_INVALID_ARG;
+  c->compat = flags;
+  return PSX_OK;
+}
+
+psx_status psx_handle_oplog_msg(psx_ctx *c, const void *msg, size_t msg_size, int32_t sender,
+                                int32_t *clock_changed) {
+  if (!c || !msg || !clock_changed) return PSX_ERR_INVALID_ARG;
+  *clock_changed = 0;
+  psx_oplog_msg_header h;
+  psx_status st = psx_decode_oplog_header(msg, msg_size, &h);
+  if (st) return fail(c, st, "not a ClientSendOpLogMsg (41-byte header + avai_size payload bytes)");
+  st = psx_apply_stream(c, (const uint8_t *)msg + PSX_OPLOG_MSG_HEADER_BYTES, (size_t)h.avai_size, sender, h.version);
+  if (st) return st;
+  if (h.is_clock) {
+    int32_t changed = 0;
+    st = psx_clock_until(c, sender, h.bg_clock, &changed);
+    if (st) return st;
+    *clock_changed = changed;
+  }
   return PSX_OK;
 }
 

@@ -300,6 +300,19 @@ class Server:
         _check(self._L, self._ctx, self._L.psx_serialize_push(self._ctx, ptrs, caps, used, 0, 1 if clear else 0))
         return [bufs[k][:used[k]].tobytes() for k in range(C)]
 
+    # -- client side of serve-back ------------------------------------------------------
+    def apply_push_body(self, body, insert_missing=False, device_ptr=None, size=None):
+        """SSPPushBgWorker::ApplyServerPushedRow on this context as a client cache
+        (ssp_push_bg_worker.cpp:70-122): host bytes, or a device buffer (device_ptr, size)."""
+        if device_ptr is not None:
+            _check(self._L, self._ctx, self._L.psx_apply_push_body(self._ctx, device_ptr, size, 1,
+                                                                     1 if insert_missing else 0))
+            return
+        buf = np.ascontiguousarray(np.frombuffer(bytes(body), dtype=np.uint8))
+        _check(self._L, self._ctx, self._L.psx_apply_push_body(
+            self._ctx, ctypes.c_void_p(buf.ctypes.data) if buf.size else None, buf.size, 0,
+            1 if insert_missing else 0))
+
     # -- client-side pack -------------------------------------------------------------
     def pack_stream(self, tables, with_index=False):
         """Pack per-table oplog rows into one message on the device (psx_pack_stream).

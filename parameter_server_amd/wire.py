@@ -185,3 +185,114 @@ def parse_push_body(body):
             rows[rid] = bytes(body[off:off + size])
             off += size
     return out
+
+
+# ---- message headers (ClientSendOpLogMsg / ServerPushRowMsg) through libpsx -----------------
+
+def encode_oplog_msg(payload, version, client_id=0, is_clock=False, bg_clock=0, seq_num=0, ack_num=0):
+    """A whole ClientSendOpLogMsg: the 41-byte header (psx_encode_oplog_header,
+    ps_msgs.hpp:1003-1055) followed by the payload stream."""
+    import ctypes
+    from . import _abi
+    payload = np.ascontiguousarray(np.asarray(payload, dtype=np.uint8))
+    h = _abi.psx_oplog_msg_header(seq_num, ack_num, payload.size, 1 if is_clock else 0, client_id, version, bg_clock)
+    out = np.zeros(_abi.OPLOG_MSG_HEADER_BYTES + payload.size, dtype=np.uint8)
+    assert _abi.load().psx_encode_oplog_header(ctypes.byref(h), ctypes.c_void_p(out.ctypes.data)) == 0
+    out[_abi.OPLOG_MSG_HEADER_BYTES:] = payload
+    return out
+
+
+def decode_oplog_msg(msg):
+    """(header dict, payload view) of a ClientSendOpLogMsg; raises PsxError if malformed."""
+    import ctypes
+    from . import _abi
+    msg = np.ascontiguousarray(np.asarray(msg, dtype=np.uint8))
+    h = _abi.psx_oplog_msg_header()
+    st = _abi.load().psx_decode_oplog_header(ctypes.c_void_p(msg.ctypes.data), msg.size, ctypes.byref(h))
+    if st:
+        raise _abi.PsxError(st, "decode_oplog_msg")
+    d = {k: getattr(h, k) for k, _ in h._fields_}
+    return d, msg[_abi.OPLOG_MSG_HEADER_BYTES:_abi.OPLOG_MSG_HEADER_BYTES + h.avai_size]
+
+
+def encode_push_msg(body, clock, version, is_clock=True, seq_num=0, ack_num=0):
+    import ctypes
+    from . import _abi
+    body = np.ascontiguousarray(np.frombuffer(bytes(body), dtype=np.uint8))
+    h = _abi.psx_push_msg_header(seq_num, ack_num, body.size, clock, version, 1 if is_clock else 0)
+    out = np.zeros(_abi.PUSH_MSG_HEADER_BYTES + body.size, dtype=np.uint8)
+    assert _abi.load().psx_encode_push_header(ctypes.byref(h), ctypes.c_void_p(out.ctypes.data)) == 0
+    out[_abi.PUSH_MSG_HEADER_BYTES:] = body
+    return out
+
+
+def decode_push_msg(msg):
+    import ctypes
+    from . import _abi
+    msg = np.ascontiguousarray(np.asarray(msg, dtype=np.uint8))
+    h = _abi.psx_push_msg_header()
+    st = _abi.load().psx_decode_push_header(ctypes.c_void_p(msg.ctypes.data), msg.size, ctypes.byref(h))
+    if st:
+        raise _abi.PsxError(st, "decode_push_msg")
+    d = {k: getattr(h, k) for k, _ in h._fields_}
+    return d, msg[_abi.PUSH_MSG_HEADER_BYTES:_abi.PUSH_MSG_HEADER_BYTES + h.avai_size]
+
+
+def split_stream(stream, tables, max_bytes=(1 << 31) - 1):
+    """Split one Appendix-A message into messages of at most max_bytes each, at record
+    boundaries, keeping table and record order (what a producer must do for the
+    reference reader's int32 offset_, serialized_oplog_reader.hpp:137).  tables:
+    {table_id: dense body bytes or None for sparse}, as stream_record_offsets takes.
+    Returns a list of numpy uint8 messages; applying them in order equals applying
+    `stream` (per-row update order is unchanged)."""
+    b = np.asarray(stream, dtype=np.uint8)
+    if b.size <= max_bytes:
+        return [b]
+    ntab = int(b[:4].view(np.int32)[0])
+    # every record: (table index, start, end)
+    recs, off = [], 4
+    heads = []
+    for k in range(ntab):
+        tid, = np.frombuffer(b[off:off + 4].tobytes(), "<i4")
+        usz, = np.frombuffer(b[off + 4:off + 12].tobytes(), "<u8")
+        nrows, = np.frombuffer(b[off + 12:off + 16].tobytes(), "<i4")
+        heads.append((int(tid), int(usz)))
+        off += 16
+        body = tables[int(tid)]
+        for _ in range(int(nrows)):
+            if body is None:
+                n, = np.frombuffer(b[off + 4:off + 8].tobytes(), "<i4")
+                end = off + 8 + int(n) * (4 + int(usz))
+            else:
+                end = off + 4 + body
+            recs.append((k, off, end))
+            off = end
+    out, cur, size = [], [], 4
+    for k, s0, e0 in recs:
+        extra = (e0 - s0) + (16 if not cur or cur[-1][0] != k else 0)
+        if cur and size + extra > max_bytes:
+            out.append(cur)
+            cur, size = [], 4
+            extra = (e0 - s0) + 16
+        if size + extra > max_bytes:
+            raise ValueError("a single record exceeds max_bytes")
+        cur.append((k, s0, e0))
+        size += extra
+    if cur:
+        out.append(cur)
+    msgs = []
+    for piece in out:
+        groups = []
+        for k, s0, e0 in piece:
+            if groups and groups[-1][0] == k and groups[-1][2] == s0:
+                groups[-1][2] = e0
+                groups[-1][3] += 1
+            else:
+                groups.append([k, s0, e0, 1])
+        parts = [np.array([len(groups)], np.int32).view(np.uint8)]
+        for k, s0, e0, n in groups:
+            tid, usz = heads[k]
+            parts += [np.array([tid], np.int32).view(np.uint8), np.array([usz], np.uint64).view(np.uint8),
+                      np.array([n], np.int32).view(np.uint8), b[s0:e0]]
+        msgs.append(np.concatenate(parts))
+    return msgs

@@ -188,3 +188,48 @@ def test_c5_ssp_staleness4_clocked_stream():
     np.testing.assert_array_equal(srv.read_rows(1, 0, rows_d).view(np.uint32),
                                   orc.o.read_dense_rows(1, 0, rows_d).view(np.uint32))
     assert srv.serialize_rows(3, list(range(rows_s))) == orc.o.serialize_records(3, list(range(rows_s)))
+
+
+def test_handle_oplog_msg_whole_messages():
+    """psx_handle_oplog_msg on whole ClientSendOpLogMsgs (41-byte header + stream): apply,
+    then ClockUntil(sender, bg_clock) for clock messages; same rows and clocks as the oracle."""
+    import ctypes
+    from parameter_server_amd import _abi
+    rng = np.random.RandomState(31)
+    bgs, cap, rows = [1100, 2100], 8, 50
+    srv = psa.Server(0, 1, bgs)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=F32, row_capacity=cap, max_rows=rows))
+    orc = OracleServer(bgs)
+    orc.create_table(1, DENSE, F32, cap)
+    L = _abi.load()
+    ver = {b: 0 for b in bgs}
+    clk = {b: 0 for b in bgs}
+    for step in range(12):
+        bg = bgs[step % 2] if step < 8 else bgs[0]
+        s = wire.dense_stream_np(1, rng.permutation(rows)[:20].astype(np.int32),
+                                 rng.normal(size=(20, cap)).astype(np.float32))
+        is_clock = step % 3 != 2
+        if is_clock:
+            clk[bg] += 1
+        msg = wire.encode_oplog_msg(s, version=ver[bg], client_id=bg // 1000, is_clock=is_clock, bg_clock=clk[bg])
+        changed = ctypes.c_int32()
+        assert L.psx_handle_oplog_msg(srv.handle, ctypes.c_void_p(msg.ctypes.data), msg.size, bg,
+                                      ctypes.byref(changed)) == 0
+        assert orc.apply_stream(s, bg, ver[bg]) == 0
+        want = orc.clock_until(bg, clk[bg]) if is_clock else 0
+        assert changed.value == want
+        ver[bg] += 1
+    assert srv.GetMinClock() == orc.min_clock()
+    assert np.array_equal(srv.read_rows(1, 0, rows).view(np.uint32), orc.read_dense_rows(1, 0, rows).view(np.uint32))
+
+
+def test_compat_mode_rejects_2gib_messages():
+    from parameter_server_amd import _abi
+    srv = psa.Server(0, 1, [100])
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=F32, row_capacity=4, max_rows=8))
+    assert _abi.load().psx_ctx_set_compat(srv.handle, _abi.COMPAT_INT32_STREAM_OFFSETS) == 0
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(psa.PsxError) as e:
+        srv.apply_device([(d.data_ptr(), 1 << 31, 100, 0)])   # rejected on its size alone
+    assert e.value.status == 10
+    assert srv.GetBgVersion(100) == -1                        # nothing accepted

@@ -18,6 +18,7 @@ def built_lib():
     """libpsx.so built in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
     subprocess.run(["make", "-s", "-j4", "-C", os.path.join(ROOT, "parameter_server_amd", "csrc")],
                    check=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], check=True)
     from parameter_server_amd import _abi
     return _abi.load()
 

@@ -13,6 +13,7 @@ torch = pytest.importorskip("torch")
 import parameter_server_amd as psa
 from parameter_server_amd import wire, ServerThread
 from oracle.oracle import OracleServer, DENSE, SORTED_MAP, F32, I32
+from oracle_backend import OracleBackend
 
 pytestmark = pytest.mark.gpu
 
@@ -21,42 +22,6 @@ pytestmark = pytest.mark.gpu
 def _gpu(built_lib, oracle_lib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-
-
-class OracleBackend:
-    """The Server methods ServerThread calls, over the oracle."""
-
-    def __init__(self, bgs, num_clients):
-        self.o = OracleServer(bgs)
-        self.num_clients = num_clients
-        self.tables = []
-
-    def create(self, tid, kind, dt, cap, dense_serialized=True):
-        self.o.create_table(tid, kind, dt, cap if kind == DENSE else 0, oplog_dense_serialized=dense_serialized)
-        self.tables.append(tid)
-
-    def ApplyOpLogUpdateVersion(self, payload, size, bg, version):
-        assert self.o.apply_stream(payload, bg, version) == 0
-
-    def ClockUntil(self, bg, clock):
-        return self.o.clock_until(bg, clock)
-
-    def GetMinClock(self):
-        return self.o.min_clock()
-
-    def subscribe(self, tid, rows, client):
-        for r in rows:
-            self.o.subscribe(tid, int(r), client)
-
-    def serialize_rows(self, tid, rows):
-        return self.o.serialize_records(tid, rows)
-
-    def row_sent(self, tid, rows, n):
-        for r in rows:
-            assert self.o.row_sent(tid, int(r), n) == 0
-
-    def serialize_push(self, clear=True):
-        return self.o.serialize_push(self.tables, self.num_clients, clear=clear)
 
 
 def test_clock_until_matches_vector_clock():

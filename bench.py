@@ -26,6 +26,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PMC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_dense_apply.json")
+
+
+def kernel_signature():
+    """Identity of the measured dense-apply code: a hash of the sources that define the
+    kernels and their launch policy and of the compile flags.  A PMC JSON carries the
+    signature it was measured on; traffic from another signature is not reported."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "parameter_server_amd", "csrc")
+    for f in ("psx_kernels.hip", "psx_device.hpp"):
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    for line in open(os.path.join(csrc, "Makefile")):
+        if line.startswith("HIPFLAGS") or line.startswith("           -"):
+            h.update(line.encode())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -42,7 +58,7 @@ def parse():
                    help="rows of the cpu_baseline sample (a quarter of C2: table and streams far larger than the caches)")
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="server threads of the cpu_baseline (capped at the visible CPUs; the GPU box's share is 16)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_dense_apply.json"),
+    p.add_argument("--pmc-json", default=PMC_JSON,
                    help="per-launch HBM bytes of dense_apply from the rocprofv3 --pmc passes "
                         "(tools/pmc_summary.py); used for roofline.traffic on the default C2 configuration")
     p.add_argument("--f16-records", action="store_true",
@@ -581,14 +597,21 @@ def main():
     apply_ms, apply_n = kernels[apply_kernel]
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
-    traffic = None
+    traffic, traffic_note = None, None
     c2_dims = ((rows, cap, B) == (1 << 20, 256, 8) and not args.importance and not args.f16_records
                and args.density == 1.0)
     pmc_json = args.pmc_json
     if args.adarevision:   # the AdaRevision kernel's own PMC passes (tools/gpu_session5.sh)
         pmc_json = os.path.join(ROOT, "profiles", "r01", "pmc_ada_apply.json")
     if c2_dims and pmc_json and os.path.exists(pmc_json):
-        traffic = json.load(open(pmc_json)).get("dense_apply_hbm_bytes_per_launch")
+        pmc = json.load(open(pmc_json))
+        if pmc.get("kernel_signature") == kernel_signature():
+            traffic = pmc.get("dense_apply_hbm_bytes_per_launch")
+        else:
+            traffic_note = (f"{os.path.relpath(pmc_json, ROOT)} was measured on kernel signature "
+                            f"{pmc.get('kernel_signature')}, this tree is {kernel_signature()}: not reported")
+    elif c2_dims:
+        traffic_note = "no PMC JSON for this tree"
 
     pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie else None
     if rank == 0:
@@ -631,6 +654,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "traffic_source": os.path.relpath(pmc_json, ROOT) if traffic else None,
+                "traffic_note": traffic_note,
+                "kernel_signature": kernel_signature(),
                 "dram_GBps": round(traffic / apply_avg_s / 1e9, 1) if traffic and apply_avg_s > 0 else None,
                 "avg_launch_ms": round(apply_avg_s * 1e3, 4),
             },

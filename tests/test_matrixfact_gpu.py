@@ -69,13 +69,13 @@ def run_driver(tmp_path, channels, staleness, iters=4, K=16, threads=2, extra=()
     return trace, losses
 
 
-def replay(trace, channels, K):
+def replay(trace, channels, K, r_dense_serialized=True):
     """Drive one oracle ServerThread per shard with the recorded events, comparing outputs."""
     events = [ln.split() for ln in open(trace / "index.txt").read().splitlines()]
     threads, got_push, want_push, got_reply, want_reply = [], [], [], [], []
     for ch in range(channels):
         be = OracleBackend([100 + ch], num_clients=1)
-        be.create(1, DENSE, F32, K)
+        be.create(1, DENSE, F32, K, dense_serialized=r_dense_serialized)
         be.create(2, DENSE, F32, 6)
         want_push.append([])
         want_reply.append([])
@@ -129,5 +129,5 @@ def test_c1_sparse_oplog_sparse_serialized(tmp_path):
     the shards receive {n, cols, vals} records for dense rows (zeros dropped)."""
     trace, losses = run_driver(tmp_path, 1, 1, iters=3, extra=("--row_oplog_type", "1", "--oplog_dense_serialized",
                                                                "false", "--no_oplog_replay", "true"))
-    replay(trace, 1, 16)
+    replay(trace, 1, 16, r_dense_serialized=False)
     assert len(losses) == 3

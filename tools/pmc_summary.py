@@ -8,13 +8,20 @@ request counts times their sizes, as MI355X_MICROARCH.md "HBM" prescribes for gf
 (FETCH_SIZE tallies a 128-B request at 64 B, so it is reported only as a cross-check,
 doubled).
 
+The output carries bench.kernel_signature() of the sources it was measured on; bench.py
+refuses (traffic null) a JSON whose signature differs from the tree it runs from.
+
 usage: python tools/pmc_summary.py gpurun_out/pmc [out.json] [kernel-substring]"""
 import collections
 import csv
 import glob
 import json
 import os
+import sqlite3
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_signature  # noqa: E402
 
 
 def load(root):
@@ -26,6 +33,12 @@ def load(root):
                 d = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 c = row["Counter_Name"]
                 per[k][c][d] = per[k][c].get(d, 0.0) + float(row["Counter_Value"])
+    # rocprofv3 on this image writes SQLite (pmc_results.db) instead of CSV
+    for f in glob.glob(os.path.join(root, "**", "*.db"), recursive=True):
+        con = sqlite3.connect(f)
+        for k, c, v, d in con.execute("select name, counter_name, counter_value, dispatch_id from pmc_events"):
+            per[k][c][(f, d)] = per[k][c].get((f, d), 0.0) + float(v)
+        con.close()
     return {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in per.items()}
 
 
@@ -57,7 +70,7 @@ if __name__ == "__main__":
     kernels = load(root)
     keys = (sys.argv[3],) if len(sys.argv) > 3 else KERNEL_KEYS
     traffic, name = dense_apply_traffic(kernels, keys)
-    out = {"kernels": kernels}
+    out = {"kernels": kernels, "kernel_signature": kernel_signature()}
     if traffic:
         out.update(traffic)
     text = json.dumps(out, indent=1)

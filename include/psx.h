@@ -449,7 +449,9 @@ psx_status psx_pack_stream(psx_ctx *ctx, const psx_pack_table *tables, int32_t n
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);
 const char *psx_status_string(psx_status s);
-/* Per-kernel HIP-event timing on the context stream (off by default). */
+/* Per-kernel HIP-event timing on the context stream (off by default).  on: 0 off,
+ * 1 every pipeline kernel, 2 only the apply kernels (dense_apply / ada_apply /
+ * ordered_apply: one event pair per launch, the least perturbation of a timed loop). */
 psx_status psx_timing_enable(psx_ctx *ctx, int32_t on);
 psx_status psx_timing_read(psx_ctx *ctx, const char *kernel, double *total_ms,
                            int64_t *launches);

@@ -959,8 +959,10 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
 // dense_index_v2: flattened (message, record) space, UNROLL row-id loads in flight per
 // thread before any store.
 // MODE 0: non-temporal row-id loads; 1: plain loads.  Either way every 4-byte row id costs
-// one 128-B L2->DRAM request (PMC, profiles/r02/pmc_request_sizes_index_apply.json); loads
-// issued one lane at a time were no faster (profiles/r02/ab_index_loads.json).
+// one 128-B L2->DRAM request (PMC, profiles/r02/pmc_request_sizes_index_apply.json).  Loads
+// issued one lane at a time, with sc0/sc1/nt scope hints (still 128-B requests), or as
+// scalar s_load_dword (64-B requests, but 0.51 vs 0.26 ms) were no faster
+// (profiles/r02/ab_index_loads.json, ab_index_policy.json).
 template <int UNROLL, int MODE>
 __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const Seg *segs, int t, int B,
                                                             int64_t stride, Geo g, int32_t *inv, InvLayout L,
@@ -1074,6 +1076,24 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
   return hipGetLastError();
 }
 
+// Resident-capacity grid for a persistent-style kernel (blocks per CU x CUs).
+template <typename K>
+static unsigned resident_blocks(K kernel, int64_t want) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  int64_t cap = (int64_t)per_cu * cus;
+  if (want < cap) cap = want;
+  return (unsigned)(cap < 1 ? 1 : cap);
+}
+
 // Run-time selectors (include/psx_debug.h): the defaults are the measured winners; the
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
@@ -1101,24 +1121,6 @@ hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, in
   hipLaunchKernelGGL(dense_verify_kernel, dim3((unsigned)blocks), dim3(256), 0, st, inv, L, t, B, max_rows,
                      counters);
   return hipGetLastError();
-}
-
-// Resident-capacity grid for a persistent-style kernel (blocks per CU x CUs).
-template <typename K>
-static unsigned resident_blocks(K kernel, int64_t want) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
-    per_cu = 2;
-  int64_t cap = (int64_t)per_cu * cus;
-  if (want < cap) cap = want;
-  return (unsigned)(cap < 1 ? 1 : cap);
 }
 
 template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>

@@ -200,7 +200,7 @@ struct psx_ctx {
   int64_t pending_calls = 0;
   psx_status deferred = PSX_OK;
   std::string err;
-  bool timing = false;
+  int timing = 0;                        // 0 off, 1 every kernel, 2 the apply kernels only
   std::vector<EventPair> pending_ev;
   std::vector<hipEvent_t> ev_pool;
   std::map<std::string, std::pair<double, int64_t>> times;
@@ -235,18 +235,25 @@ hipEvent_t get_event(psx_ctx *c) {
   return e;
 }
 
+// The kernels timing mode 2 brackets: the applies, whose launch durations the roofline
+// divides by (one event pair per launch instead of one per pipeline kernel).
+static bool is_apply_kernel(const char *name) {
+  return !strcmp(name, "dense_apply") || !strcmp(name, "ada_apply") || !strcmp(name, "ordered_apply");
+}
+
 // Run `launch` (which enqueues on `st`), bracketed by HIP events on `st` when timing is on.
 template <typename F>
 psx_status timed(psx_ctx *c, const char *name, F launch, hipStream_t st) {
   hipEvent_t a = nullptr, b = nullptr;
-  if (c->timing) {
+  const bool on = c->timing == 1 || (c->timing == 2 && is_apply_kernel(name));
+  if (on) {
     a = get_event(c);
     b = get_event(c);
     if (a) hipEventRecord(a, st);
   }
   hipError_t e = launch();
   if (e != hipSuccess) return hip_fail(c, e, name);
-  if (c->timing && a && b) {
+  if (on && a && b) {
     hipEventRecord(b, st);
     c->pending_ev.push_back({name, a, b});
   }
@@ -2059,7 +2066,8 @@ const char *psx_last_error(psx_ctx *c) { return c ? c->err.c_str() : "null conte
 
 psx_status psx_timing_enable(psx_ctx *c, int32_t on) {
   if (!c) return PSX_ERR_INVALID_ARG;
-  c->timing = on != 0;
+  if (on < 0 || on > 2) return fail(c, PSX_ERR_INVALID_ARG, "timing mode is 0, 1 or 2");
+  c->timing = on;
   return PSX_OK;
 }
 

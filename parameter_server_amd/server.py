@@ -355,7 +355,8 @@ class Server:
 
     # -- timing ------------------------------------------------------------------------
     def timing(self, on=True):
-        _check(self._L, self._ctx, self._L.psx_timing_enable(self._ctx, 1 if on else 0))
+        """on: False/0 off, True/1 every pipeline kernel, 2 the apply kernels only."""
+        _check(self._L, self._ctx, self._L.psx_timing_enable(self._ctx, int(on)))
 
     def timing_read(self, kernel):
         ms = ctypes.c_double()

@@ -168,7 +168,18 @@ def test_version_gap_applies_nothing():
     assert srv.GetBgVersion(100) == -1
 
 
-def test_device_stream_errors_reported_at_sync():
+@pytest.mark.parametrize("index_variant", [0, 1], ids=["nt", "plain"])
+def test_device_stream_errors_reported_at_sync(index_variant):
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    old = L.psx_debug_set_variant(0, index_variant)
+    try:
+        _device_stream_errors()
+    finally:
+        L.psx_debug_set_variant(0, old)
+
+
+def _device_stream_errors():
     srv, _ = _pair(F32, 10, 8, bgs=[100, 101, 102])
     good = wire.dense_stream_np(1, np.array([1, 2], np.int32), np.ones((2, 8), np.float32))
     unknown = good.copy()

@@ -88,6 +88,39 @@ __global__ void __launch_bounds__(256) gather_kernel(uint8_t *table, const uint8
   }
 }
 
+// Rows in message 0's record order: message 0 is read sequentially (its row ids inline),
+// the table rows and the other messages' records are gathered.
+template <int B, int PAIR>
+__global__ void __launch_bounds__(256) seq0_kernel(uint8_t *table, const uint8_t *stream, const int32_t *pos,
+                                                   const int32_t *perm0, int64_t R, int64_t stride, int64_t msg_bytes) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t i0 = wave * PAIR; i0 < R; i0 += nw * PAIR) {
+    u32x4 t[PAIR], u[PAIR][B];
+    int64_t rr[PAIR];
+#pragma unroll
+    for (int q = 0; q < PAIR; ++q) {
+      const int64_t i = i0 + q < R ? i0 + q : R - 1;
+      rr[q] = perm0[i];
+      t[q] = *(const u32x4 *)(table + rr[q] * 1024 + lane * 16);
+      u[q][0] = ld_nt(stream, i * stride + 4 + lane * 16);
+#pragma unroll
+      for (int b = 1; b < B; ++b) {
+        const int64_t p = pos[b * R + rr[q]];
+        u[q][b] = ld_nt(stream, b * msg_bytes + p * stride + 4 + lane * 16);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PAIR; ++q) {
+      u32x4 acc = t[q];
+#pragma unroll
+      for (int b = 0; b < B; ++b) acc = addf(acc, u[q][b]);
+      if (i0 + q < R) *(u32x4 *)(table + rr[q] * 1024 + lane * 16) = acc;
+    }
+  }
+}
+
 template <typename K>
 static unsigned resident(K k) {
   int per = 0, cus = 0;
@@ -128,15 +161,19 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&sink, 4));
   CK(hipMemset(table, 0, R * row));
   CK(hipMemset(stream, 0, B * msg_bytes));
-  std::vector<int32_t> h(B * R);
+  std::vector<int32_t> h(B * R), p0(R);
   std::mt19937 g(1234);
   for (int64_t b = 0; b < B; ++b) {
     std::vector<int32_t> perm(R);
     for (int64_t i = 0; i < R; ++i) perm[i] = (int32_t)i;
     std::shuffle(perm.begin(), perm.end(), g);
     for (int64_t i = 0; i < R; ++i) h[b * R + perm[i]] = (int32_t)i;   // row perm[i] is record i
+    if (b == 0) p0 = perm;
   }
   CK(hipMemcpy(pos, h.data(), h.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  int32_t *perm0;
+  CK(hipMalloc(&perm0, R * sizeof(int32_t)));
+  CK(hipMemcpy(perm0, p0.data(), R * sizeof(int32_t), hipMemcpyHostToDevice));
 
   const double tab_bytes = 2.0 * R * row;
   const double rec_bytes_w = (double)B * R * stride_w, rec_bytes_a = (double)B * R * stride_a;
@@ -163,5 +200,16 @@ int main(int argc, char **argv) {
   GATHER("gather_al", 2, true, stride_a, rec_bytes_a + tab_bytes + idx_bytes)
   GATHER("gather_al", 4, true, stride_a, rec_bytes_a + tab_bytes + idx_bytes)
   GATHER("norec_tab", 4, false, stride_w, tab_bytes)
+#define SEQ0(PAIR)                                                                                  \
+  {                                                                                                 \
+    auto k = seq0_kernel<8, PAIR>;                                                                  \
+    const unsigned blocks = resident(k);                                                            \
+    const double alg = rec_bytes_w + tab_bytes + idx_bytes;                                         \
+    ms = time_ms([&] { k<<<blocks, 256>>>(table, stream, pos, perm0, R, stride_w, msg_bytes); }, reps); \
+    printf("{\"probe\": \"seq0\", \"pair\": %d, \"ms\": %.4f, \"GBps_alg\": %.1f, \"blocks\": %u}\n", PAIR, ms, \
+           alg / ms / 1e6, blocks);                                                                 \
+  }
+  SEQ0(2)
+  SEQ0(4)
   return 0;
 }

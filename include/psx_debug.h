@@ -16,8 +16,9 @@ enum {
   PSX_VARIANT_DENSE_INDEX = 0,  /* 0: non-temporal row-id loads (default), 1: plain loads */
   PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact,
                                    3: v3 with plain record loads */
-  PSX_VARIANT_ORD_SPLIT = 6     /* 1: sorted/map rows of > 256 entries split into a 256- and a
-                                   1,024-entry image launch (default), 0: one launch */
+  PSX_VARIANT_ORD_SPLIT = 6     /* 1: rows of sorted/map tables with 256 < max_entries <= 1024
+                                   classified into a 256- and a 1,024-entry image launch that
+                                   run concurrently (default), 0: one 1,024-entry launch */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -7,6 +7,7 @@
 //                   All -1 between calls: the apply kernel restores every entry it reads.
 //   segments      : Seg segs[kMaxFused][kMaxTables]  (stream b, table t) decoded by decode_streams
 #pragma once
+#include <hip/hip_runtime.h>
 #include <cstdint>
 
 namespace psx {
@@ -160,6 +161,16 @@ struct OrdArgs {
   int rec_f16;            // dense records are binary16 (kDenseRowOpLogFloat16)
   uint32_t *keyflag;      // sorted/map tables: set once a key outside [0, max_entries) is seen
                           // (from then on every call runs the capacity dry run)
+  int32_t *grow;          // split tables (256 < max_entries <= 1024): entries the call's records
+                          // can add per slot (zero between calls); null otherwise
+  int32_t *split;         // [2][max_rows]: touched slots whose image fits 256 entries, the rest
+  uint32_t *nsplit;       // the two lists' lengths
+};
+
+// A side stream and two events for launches that run beside the context stream.
+struct Fork {
+  hipStream_t aux;
+  hipEvent_t fork, join;
 };
 
 // Arguments of the serve-back kernels (psx_serve.hip).

@@ -119,6 +119,7 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
           for (int32_t i = 0; i < n; ++i)
             if (cols[i] < 0 || cols[i] >= a.max_entries) { atomicOr(a.keyflag, 1u); break; }
         }
+        if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
         first = atomicAdd(&a.cnt[s], 1) == 0;
       }
     }
@@ -143,6 +144,7 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  if (a.nsplit && blockIdx.x == 0 && threadIdx.x < 2) a.nsplit[threadIdx.x] = 0;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
     int b;
     uint64_t off;
@@ -151,6 +153,38 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
     if (s < 0) continue;
     const int32_t p = atomicSub(&a.cnt[s], 1) - 1;
     a.list[a.off[s] + p] = (int32_t)r;
+  }
+}
+
+// ordered_classify (split tables): a touched row whose image can outgrow 256 entries in
+// this call (entries now + its records' entries) goes to the 1,024-entry list, the rest
+// to the 256-entry list; the two apply launches then run concurrently.  grow returns to 0.
+__global__ void __launch_bounds__(256) ordered_classify_kernel(OrdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nt = (int64_t)*a.ntouched;
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+  for (int64_t i0 = base0; i0 < nt; i0 += G) {
+    const int64_t i = i0 + lane;
+    int32_t s = 0;
+    bool big = false;
+    const bool have = i < nt;
+    if (have) {
+      s = a.touched[i];
+      big = (int64_t)a.nent[s] + a.grow[s] > 256;
+      a.grow[s] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint64_t m = __ballot(have && big == (k == 1));
+      if (!m) continue;
+      const int leader = __builtin_ctzll(m);
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&a.nsplit[k], (uint32_t)__builtin_popcountll(m));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if (have && big == (k == 1))
+        a.split[k * a.max_rows + base + __builtin_popcountll(m & ((1ull << lane) - 1))] = s;
+    }
   }
 }
 
@@ -259,11 +293,13 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
   // one touched row per wave at a time (rows are independent; hot rows spread out)
   const int64_t nt = go ? (int64_t)*a.ntouched : 0;
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
-    const int64_t slot = a.touched[ti];
+    // per-row scalars are wave-uniform: readfirstlane keeps them in SGPRs so the row's
+    // loops branch on SCC instead of running under exec masks
+    const int64_t slot = __builtin_amdgcn_readfirstlane(a.touched[ti]);
     if (!DRY && lane == 0) a.flags[slot] = 3;
     {
-      const int32_t beg = a.off[slot];
-      const int32_t L = a.off[slot + 1] - beg;
+      const int32_t beg = __builtin_amdgcn_readfirstlane(a.off[slot]);
+      const int32_t L = __builtin_amdgcn_readfirstlane(a.off[slot + 1]) - beg;
       int32_t *lst = a.list + beg;
       if constexpr (DRY) {
         int32_t grow = 0;
@@ -491,12 +527,11 @@ __device__ __forceinline__ T bcast(T x, int src) {
   }
 }
 
-// CLS splits a call's rows between two launches by the size their image can reach
-// (entries now + this call's record entries): 1 = rows that fit 64*J entries (the others
-// are marked with flags bit 2), 2 = the marked rows, 0 = every row.  Small rows then run
-// at the small image's occupancy.
+// Split tables run two launches of this kernel concurrently, over the touched rows
+// ordered_classify put in the 256- and the 1,024-entry list (a.touched / a.ntouched point
+// at one list each).
 // DRY: the capacity dry run (see ordered_apply_kernel); J must hold max_entries.
-template <typename V, int KIND, int J, int CLS = 0, bool DRY = false>
+template <typename V, int KIND, int J, bool DRY = false>
 __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
   __shared__ int32_t sort_scratch[4][64];
@@ -513,14 +548,13 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   // one touched row per wave at a time (rows are independent; hot rows spread out)
   const int64_t nt = go ? (int64_t)*a.ntouched : 0;
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
-    const int64_t slot = a.touched[ti];
-    if constexpr (CLS == 2) {   // only the rows the CLS = 1 launch marked (flags bit 2)
-      if (!(a.flags[slot] & 4)) continue;
-    }
+    // per-row scalars are wave-uniform: readfirstlane keeps them in SGPRs so the row's
+    // loops branch on SCC instead of running under exec masks
+    const int64_t slot = __builtin_amdgcn_readfirstlane(a.touched[ti]);
     if (!DRY && lane == 0) a.flags[slot] = 3;
     {
-      const int32_t beg = a.off[slot];
-      const int32_t L = a.off[slot + 1] - beg;
+      const int32_t beg = __builtin_amdgcn_readfirstlane(a.off[slot]);
+      const int32_t L = __builtin_amdgcn_readfirstlane(a.off[slot + 1]) - beg;
       int32_t *lst = a.list + beg;
       int32_t mine = 0;
       if (L <= 64) {
@@ -537,7 +571,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
       }
-      int32_t n = a.nent[slot];
+      int32_t n = __builtin_amdgcn_readfirstlane(a.nent[slot]);
       if constexpr (DRY) {
         int32_t grow = 0;
         for (int32_t q = lane; q < L; q += 64) {
@@ -547,24 +581,6 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
           grow += o_ld32(a.ss.data[b] + roff + 4);
         }
         if ((int64_t)n + wave_sum_i32(grow) <= (int64_t)cap) continue;
-      }
-      if constexpr (CLS == 1) {
-        // classify on the row as it is before this call; a row too big for the J-image
-        // is marked (flags bit 2) for the CLS = 2 launch, which clears the mark
-        int32_t grow = 0;   // this lane's records' entry counts
-        for (int32_t q = lane; q < L; q += 64) {
-          const int32_t r = L <= 64 ? mine : lst[q];
-          int b;
-          uint64_t roff;
-          locate(a, rs, r, b, roff);
-          grow += o_ld32(a.ss.data[b] + roff + 4);
-        }
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) grow += __shfl_xor(grow, m, 64);
-        if ((int64_t)n + grow > 64 * (int64_t)J) {
-          if (lane == 0) a.flags[slot] = 3 | 4;
-          continue;
-        }
       }
       // load the row image
       const uint8_t *row = a.entries + slot * a.max_entries * ES;
@@ -578,20 +594,59 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
       }
       double impt = a.imp ? a.imp[slot] : 0.0;
       bool over = false;   // DRY: this row would exceed max_entries
-      for (int32_t q = 0; q < L && !over; ++q) {
-        const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
+      // Record headers fetched for all of the row's records at once (lane q: record q in
+      // message order; rows with <= 64 records in the call), and each record's first 64
+      // (column, value) pairs loaded one record ahead, so the Inc chain does not wait on
+      // a dependent global load per record.
+      int hb = 0;
+      uint64_t hoff = 0;
+      int32_t hn = 0;
+      if (L <= 64 && lane < L) {
+        locate(a, rs, mine, hb, hoff);
+        hn = o_ld32(a.ss.data[hb] + hoff + 4);
+      }
+      auto rec_at = [&](int32_t q, const uint8_t *&rec, int32_t &nn) {
         int b;
-        uint64_t roff;
-        locate(a, rs, r, b, roff);
-        const uint8_t *rec = a.ss.data[b] + roff;
-        const int32_t nn = o_ld32(rec + 4);
+        uint64_t off;
+        if (L <= 64) {
+          b = __builtin_amdgcn_readlane(hb, q);
+          off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(hoff >> 32), q) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)hoff, q);
+          nn = __builtin_amdgcn_readlane(hn, q);
+        } else {
+          locate(a, rs, __builtin_amdgcn_readfirstlane(lst[q]), b, off);
+          b = __builtin_amdgcn_readfirstlane(b);
+          off = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(off >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)off);
+          nn = __builtin_amdgcn_readfirstlane(o_ld32(a.ss.data[b] + off + 4));
+        }
+        rec = a.ss.data[b] + off;
+      };
+      const uint8_t *rec_n = nullptr;
+      int32_t nn_n = 0, col_n = 0;
+      V d_n = V(0);
+      if (L > 0) {
+        rec_at(0, rec_n, nn_n);
+        col_n = lane < nn_n ? o_ld32(rec_n + 8 + (int64_t)lane * 4) : 0;
+        d_n = lane < nn_n ? ldv<V>(rec_n + 8 + (int64_t)nn_n * 4 + (int64_t)lane * sizeof(V)) : V(0);
+      }
+      for (int32_t q = 0; q < L && !over; ++q) {
+        const uint8_t *rec = rec_n;
+        const int32_t nn = nn_n;
+        int32_t col0 = col_n;
+        V d0 = d_n;
+        if (q + 1 < L) {
+          rec_at(q + 1, rec_n, nn_n);
+          col_n = lane < nn_n ? o_ld32(rec_n + 8 + (int64_t)lane * 4) : 0;
+          d_n = lane < nn_n ? ldv<V>(rec_n + 8 + (int64_t)nn_n * 4 + (int64_t)lane * sizeof(V)) : V(0);
+        }
         const uint8_t *cols = rec + 8;
         const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
         if (a.imp) impt += sparse_importance<V>(vals, nn, lane);
         for (int32_t c0 = 0; c0 < nn && !over; c0 += 64) {
           const int32_t pi = c0 + lane;
-          const int32_t my_col = pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0;
-          const V my_d = pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0);
+          const int32_t my_col = c0 == 0 ? col0 : (pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0);
+          const V my_d = c0 == 0 ? d0 : (pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0));
           const int32_t cnt = nn - c0 < 64 ? nn - c0 : 64;
           for (int32_t t = 0; t < cnt && !over; ++t) {
             const int32_t c = __builtin_amdgcn_readlane(my_col, t);
@@ -743,7 +798,7 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 }
 
 // ---------------------------------------------------------------------------
-int g_ord_split = 1;  // rows of > 256-entry tables split into a 256-entry and a 1,024-entry image launch
+int g_ord_split = 1;  // rows of > 256-entry tables classified into a 256- and a 1,024-entry image launch
 
 // One touched row per wave at a time: the grid is sized by rows (the touched count is on
 // the device), not by 64-row tiles — 100K rows as tiles gave 1,564 waves for ~35K touched
@@ -767,11 +822,11 @@ template <typename V, int KIND>
 static void launch_dry(const OrdArgs &a, int dtype, hipStream_t st) {
   const unsigned blocks = row_blocks(a.max_rows, 4);
   if (a.max_entries <= 64)
-    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.max_entries <= 256)
-    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.max_entries <= 1024)
-    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, 0, true>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, true>), dim3(blocks), dim3(256), 0, st, a);
   else {
     int wpb;
     size_t lds;
@@ -800,19 +855,32 @@ hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Stage 2: the apply (after every table's stage 1 and the duplicate-row gate).
-hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st) {
+// Stage 2: the apply (after every table's stage 1 and the duplicate-row gate).  Split
+// tables (a.grow set): ordered_classify, then the 1,024-entry launch on `aux` (its long
+// per-row chains start first) beside the 256-entry launch on `st`; `st` joins `aux`.
+hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk) {
   if (a.kind != 0 && a.max_entries <= 1024) {
     const unsigned blocks = row_blocks(a.max_rows, 4);
+    OrdArgs small = a, big = a;
+    if (a.grow) {
+      hipLaunchKernelGGL(ordered_classify_kernel, dim3(row_blocks(a.max_rows, 4)), dim3(256), 0, st, a);
+      small.touched = a.split;
+      small.ntouched = a.nsplit;
+      big.touched = a.split + a.max_rows;
+      big.ntouched = a.nsplit + 1;
+      hipError_t e = hipEventRecord(fk.fork, st);
+      if (e == hipSuccess) e = hipStreamWaitEvent(fk.aux, fk.fork, 0);
+      if (e != hipSuccess) return e;
+    }
 #define PSX_REG(V, KIND)                                                                           \
   do {                                                                                             \
     if (a.max_entries <= 64)                                                                       \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3(blocks), dim3(256), 0, st, a);   \
     else if (a.max_entries <= 256)                                                                 \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, a);   \
-    else if (g_ord_split) {                                                                        \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, 1>), dim3(blocks), dim3(256), 0, st, a); \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, 2>), dim3(blocks), dim3(256), 0, st, a); \
+    else if (a.grow) {                                                                             \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, fk.aux, big); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
     } else                                                                                         \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, st, a);  \
   } while (0)
@@ -825,6 +893,11 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st) {
     }
 #undef PSX_REGK
 #undef PSX_REG
+    if (a.grow) {
+      hipError_t e = hipEventRecord(fk.join, fk.aux);
+      if (e == hipSuccess) e = hipStreamWaitEvent(st, fk.join, 0);
+      if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
   }
   // LDS row images (max_entries > 1024) or dense rows

@@ -49,7 +49,8 @@ hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t 
                            uint64_t clients, const uint64_t *subs, int check_only, hipStream_t st);
 hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
 hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st);
-hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st);
+hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk);
+extern int g_ord_split;
 hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st);
 hipError_t launch_gate(const Seg *segs, const uint32_t *counters, const TableMask &m, int B,
                        uint32_t *call_status, hipStream_t st);
@@ -96,6 +97,9 @@ struct TableState {
   int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
   uint32_t *d_keyflag = nullptr;   // sorted/map: a key outside [0, max_entries) was seen
+  int32_t *d_grow = nullptr;       // split sorted/map tables: per-slot entry growth of a call
+  int32_t *d_split = nullptr;      // split sorted/map tables: [2][max_rows] row lists
+  uint32_t *d_nsplit = nullptr;    // their lengths
   uint64_t *d_subs = nullptr;      // CallBackSubs::subscriptions_ per slot (bit c = client c), lazily
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
@@ -124,6 +128,9 @@ struct TableState {
   void *d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   bool fast() const { return cfg.row_kind == PSX_ROW_DENSE && cfg.oplog_dense_serialized; }
+  // sorted/map rows that need the 1,024-entry register image: applied by two concurrent
+  // launches (rows that stay within 256 entries, the rest)
+  bool split() const { return cfg.row_kind != PSX_ROW_DENSE && max_entries > 256 && max_entries <= 1024; }
   bool rec_f16() const { return cfg.row_oplog_type == 3; }
   // Bytes of a dense record after its row id: V[cap] (dense_row_oplog.hpp:138-144), plus
   // {uint64 version; bool end_of_version} for version tables (version_dense_row_oplog.hpp:173-180),
@@ -137,7 +144,7 @@ struct TableState {
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_subs, t.d_srv_sizes, t.d_srv_offs,
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_grow, t.d_split, t.d_nsplit, t.d_subs, t.d_srv_sizes, t.d_srv_offs,
                   t.d_imp, t.d_ver, t.d_acc, t.d_z, t.d_zmax, t.d_snap_ver, t.d_snap_cnt, t.d_snap_acc,
                   t.d_ada_words, t.d_new_keys, t.d_new_slots, t.d_new_tmp, t.d_init, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
@@ -177,6 +184,8 @@ struct psx_ctx {
   uint64_t *d_recoff[2] = {nullptr, nullptr};
   size_t recoff_cap[2] = {0, 0};                  // entries
   hipStream_t side = nullptr;                     // decode/index/verify stage
+  hipStream_t aux = nullptr;                      // launches beside the context stream
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_ready[2] = {nullptr, nullptr};    // slot's index stage done (side -> main)
   hipEvent_t ev_free[2] = {nullptr, nullptr};     // slot's apply stage done (main -> side)
   bool pipeline = false;                          // PSX_PIPELINE=1: overlap (no gain measured, DRAM-bound)
@@ -539,6 +548,11 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.force = force_ordered ? 1 : 0;
     a.imp = t.d_imp;
     a.keyflag = t.d_keyflag;
+    if (t.split() && psx::g_ord_split) {
+      a.grow = t.d_grow;
+      a.split = t.d_split;
+      a.nsplit = t.d_nsplit;
+    }
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
     if (st) return st;
   }
@@ -577,7 +591,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
     if (t.fast() && !force_ordered) continue;
-    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered_apply(t.cfg.dtype, ord[ti], c->stream); });
+    const psx::Fork fk{c->aux, c->ev_fork, c->ev_join};
+    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered_apply(t.cfg.dtype, ord[ti], c->stream, fk); });
     if (st) return st;
   }
   for (int i = 0; i < fast.n; ++i) {
@@ -822,7 +837,11 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
   c->stream = c->own;
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+    return cleanup(PSX_ERR_DEVICE);
   for (int k = 0; k < 2; ++k) {
     if (hipEventCreateWithFlags(&c->ev_ready[k], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming) != hipSuccess)
@@ -849,6 +868,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (!c) return PSX_ERR_INVALID_ARG;
   hipSetDevice(c->device);
   if (c->side) hipStreamSynchronize(c->side);
+  if (c->aux) hipStreamSynchronize(c->aux);
   if (c->stream) hipStreamSynchronize(c->stream);
   for (auto &t : c->tables) free_table(t);
   if (c->d_list) hipFree(c->d_list);
@@ -866,6 +886,9 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
     if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
   }
   if (c->side) hipStreamDestroy(c->side);
+  if (c->aux) hipStreamDestroy(c->aux);
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  if (c->ev_join) hipEventDestroy(c->ev_join);
   if (c->d_status) hipFree(c->d_status);
   if (c->d_zero) hipFree(c->d_zero);
   if (c->d_ndirty) hipFree(c->d_ndirty);
@@ -1033,6 +1056,12 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (e == hipSuccess && cfg->row_kind != PSX_ROW_DENSE) {
     e = hipMalloc(&t.d_keyflag, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_keyflag, 0, sizeof(uint32_t), c->stream);
+  }
+  if (e == hipSuccess && t.split()) {
+    e = hipMalloc(&t.d_grow, R * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, R * sizeof(int32_t), c->stream);
+    if (e == hipSuccess) e = hipMalloc(&t.d_split, 2 * R * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * sizeof(uint32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {

@@ -34,11 +34,15 @@ __device__ __forceinline__ uint64_t ld64_a4(const uint8_t *p) {
 // ---------------------------------------------------------------------------
 // decode_streams: grid = B workgroups of 1024 threads; thread 0 walks one message's
 // headers.  Sparse tables' variable-length records form a dependency chain (each size
-// comes from its n), so the walk is sequential: the block stages the stream through
-// LDS in 64 KiB windows and thread 0 hops record to record at LDS latency.
+// comes from its n), so the walk is sequential: the block stages the table's records
+// through LDS in 32 KiB windows of a fixed grid (the next one prefetched into registers
+// while the current one is walked), builds 1/2/4/8/16-record jump tables in parallel, and
+// thread 0 hops the chain 16 records per dependent LDS read.
 constexpr int kDecodeThreads = 1024;
 constexpr int kDecodeWindowWords = 8192;    // 32 KiB window
-constexpr uint32_t kUnk = 0xFFFFFFFFu;      // chain position unknown (header outside window / bad)
+constexpr uint64_t kWinBytes = (uint64_t)kDecodeWindowWords * 4;
+constexpr int kJumpLevels = 5;              // 1, 2, 4, 8, 16 records
+constexpr uint16_t kU16 = 0xFFFFu;          // chain leaves the window / bad header
 
 // Indexed messages (ix.p[b] set, psx_apply_indexed): a sparse table's record offsets come
 // from the producer's index; all threads copy them and check the chain in parallel
@@ -48,13 +52,15 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
                                                                         uint64_t *recoff, uint32_t *call_status,
                                                                         uint32_t *counters, uint32_t *ntouched,
                                                                         IdxSet ix) {
-  __shared__ uint32_t win[kDecodeWindowWords];
-  __shared__ uint32_t j1[kDecodeWindowWords], j2[kDecodeWindowWords], j4[kDecodeWindowWords];
-  __shared__ uint32_t qlist[kDecodeWindowWords / 8];   // chain positions starting 4-record hops
-  __shared__ uint32_t slist[kDecodeWindowWords / 2];   // single-record positions (window tail)
-  __shared__ uint32_t sh_nq, sh_ns;
+  __shared__ uint32_t win[kDecodeWindowWords + 1];                 // + 1 halo word
+  __shared__ uint16_t jt[kJumpLevels][kDecodeWindowWords];          // jt[l]: 2^l records on
+  __shared__ uint16_t a16[kDecodeWindowWords / 32];                 // starts of 16-record hops
+  __shared__ uint16_t a4[8], a1s[16];                               // 4-record hops (<= 3), single records (<= 4)
+  __shared__ uint32_t sh_n16, sh_n4, sh_ns;
   __shared__ int32_t sh_bad;
-  __shared__ uint64_t sh_off, sh_rk, sh_left, sh_kk, sh_end;
+  __shared__ uint64_t sh_off, sh_rk, sh_left, sh_kk, sh_end, sh_t0;
+  uint32_t pf[kDecodeWindowWords / kDecodeThreads];                 // the prefetched window
+  uint64_t pf_w0 = ~0ull;
   __shared__ int32_t sh_state;   // 0 walking headers, 1 sparse walk needs a window, 2 done, 3 indexed sparse table
   __shared__ int32_t sh_t, sh_ntab, sh_k;
   const int b = blockIdx.x;
@@ -124,6 +130,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
           sg->sparse = 1;
           sh_t = t;
           sh_off = off;
+          sh_t0 = off;
           sh_left = (uint64_t)nrows;
           sh_bad = 0;
           if (nrows) sh_state = ix.p[b] ? 3 : 1;
@@ -168,96 +175,134 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
       __syncthreads();
       continue;
     }
-    // B) stage a window starting at the current record (4-byte aligned by construction)
-    const uint64_t w0 = sh_off;
-    uint64_t wbytes = size - w0;
-    if (wbytes > (uint64_t)kDecodeWindowWords * 4) wbytes = (uint64_t)kDecodeWindowWords * 4;
-    const uint32_t nw = (uint32_t)(wbytes / 4);
+    // B) the window of the fixed grid (from the table's first record) that holds the
+    //    current record, plus one halo word; window k+1 was prefetched into registers
+    //    while window k was walked.
+    const uint64_t t0 = sh_t0;
+    const uint64_t w0 = t0 + (sh_off - t0) / kWinBytes * kWinBytes;
+    const uint64_t tot = (size - w0) / 4;                       // whole words from w0
+    const uint32_t nw = (uint32_t)(tot < (uint64_t)kDecodeWindowWords ? tot : (uint64_t)kDecodeWindowWords);
+    const bool halo = tot > nw;
     {
-      // all of a thread's loads in flight before any LDS store (one DRAM round trip per
-      // window instead of one per word)
       constexpr int PER = kDecodeWindowWords / kDecodeThreads;
       const uint32_t *src = reinterpret_cast<const uint32_t *>(p + w0);
-      uint32_t tmp[PER];
+      if (pf_w0 != w0) {
 #pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const uint32_t i = threadIdx.x + (uint32_t)k * kDecodeThreads;
-        tmp[k] = i < nw ? src[i] : 0u;
+        for (int k = 0; k < PER; ++k) {
+          const uint32_t i = threadIdx.x + (uint32_t)k * kDecodeThreads;
+          pf[k] = i < nw ? src[i] : 0u;
+        }
       }
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const uint32_t i = threadIdx.x + (uint32_t)k * kDecodeThreads;
-        if (i < nw) win[i] = tmp[k];
+        if (i < nw) win[i] = pf[k];
+      }
+      if (threadIdx.x == 0) win[nw] = halo ? src[nw] : 0u;
+      // prefetch the next grid window (used if the walk continues there)
+      const uint64_t n0 = w0 + kWinBytes;
+      pf_w0 = ~0ull;
+      if (n0 + 8 <= size) {
+        const uint64_t ntot = (size - n0) / 4;
+        const uint32_t nnw = (uint32_t)(ntot < (uint64_t)kDecodeWindowWords ? ntot : (uint64_t)kDecodeWindowWords);
+        const uint32_t *nsrc = reinterpret_cast<const uint32_t *>(p + n0);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          const uint32_t i = threadIdx.x + (uint32_t)k * kDecodeThreads;
+          pf[k] = i < nnw ? nsrc[i] : 0u;
+        }
+        pf_w0 = n0;
       }
     }
-    // C) jump tables over the window (all threads): j1[q] = word index of the record
-    //    after a record starting at word q, j2 = j1 o j1, j4 = j2 o j2; kUnk where a
-    //    header lies outside the window or the record is malformed.
+    __syncthreads();
+    // C) jump tables over the window (all threads, 16-bit word indices): j1[q] = word of
+    //    the record after a record starting at word q; j2 = j1 o j1, ..., j16; kU16 where
+    //    the next record leaves the window or the header is bad (thread 0 resolves those
+    //    one record at a time from the words themselves).
     const uint64_t wpr = 1 + (uint64_t)dir.vsize[sh_t] / 4;   // words per (col, val) pair
     for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
-      uint32_t v = kUnk;
+      uint16_t v = kU16;
       if (q + 1 < nw) {
         const int32_t n = (int32_t)win[q + 1];
         if (n >= 0) {
           const uint64_t nxt = (uint64_t)q + 2 + (uint64_t)n * wpr;
-          if (w0 + nxt * 4 <= size && nxt < kUnk) v = (uint32_t)nxt;
+          if (nxt < nw && w0 + nxt * 4 <= size) v = (uint16_t)nxt;
         }
       }
-      j1[q] = v;
+      jt[0][q] = v;
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
-      const uint32_t a1 = j1[q];
-      j2[q] = a1 < nw ? j1[a1] : kUnk;
+#pragma unroll
+    for (int lv = 1; lv < kJumpLevels; ++lv) {
+      for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
+        const uint16_t a1 = jt[lv - 1][q];
+        jt[lv][q] = a1 != kU16 ? jt[lv - 1][a1] : kU16;
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
-      const uint32_t a2 = j2[q];
-      j4[q] = a2 < nw ? j2[a2] : kUnk;
-    }
-    __syncthreads();
-    // D) thread 0 hops the chain 4 records at a time, then singly near the window end
+    // D) thread 0 hops the chain 16 records at a time, then 4, then singly (the record
+    //    that leaves the window, a bad header or the table's last records)
     if (threadIdx.x == 0) {
       uint64_t left = sh_left;
       uint32_t w = (uint32_t)((sh_off - w0) / 4);
-      uint32_t nq = 0, ns = 0;
-      int bad = 0;
-      while (left >= 4 && w < nw && j4[w] != kUnk) {
-        qlist[nq++] = w;
-        w = j4[w];
+      uint32_t n16 = 0, n4 = 0, ns = 0;
+      int bad = w >= nw;   // the table's first record header lies past the message end
+      if (bad) left = 0;
+      while (left >= 16 && jt[4][w] != kU16) {
+        a16[n16++] = (uint16_t)w;
+        w = jt[4][w];
+        left -= 16;
+      }
+      while (left >= 4 && jt[2][w] != kU16) {
+        a4[n4++] = (uint16_t)w;
+        w = jt[2][w];
         left -= 4;
       }
-      while (left && w + 1 < nw) {
+      bool out = false;   // the walk left the window (sh_off already set)
+      while (left) {
+        if (w + 1 > nw || (w + 1 == nw && !halo)) { bad = 1; break; }   // header cut by the message end
         const int32_t n = (int32_t)win[w + 1];
         if (n < 0) { bad = 1; break; }
         const uint64_t nxt = (uint64_t)w + 2 + (uint64_t)n * wpr;
         if (w0 + nxt * 4 > size) { bad = 1; break; }
-        slist[ns++] = w;
+        a1s[ns++] = (uint16_t)w;
         --left;
-        if (nxt >= nw) { w = kUnk; sh_off = w0 + nxt * 4; break; }
+        if (nxt >= nw) { out = true; sh_off = w0 + nxt * 4; break; }
         w = (uint32_t)nxt;
       }
-      if (!bad && left && w != kUnk && w + 1 >= nw && w0 + (uint64_t)w * 4 + 8 > size) bad = 1;   // truncated
-      if (w != kUnk) sh_off = w0 + (uint64_t)w * 4;
-      sh_nq = nq;
+      if (!out) sh_off = w0 + (uint64_t)w * 4;
+      sh_n16 = n16;
+      sh_n4 = n4;
       sh_ns = ns;
       sh_bad = bad;
       sh_left = left;
     }
     __syncthreads();
-    // E) expand hops into record offsets (all threads)
+    // E) expand the hops into record offsets (all threads)
     {
-      const uint32_t nq = sh_nq, ns = sh_ns;
+      const uint32_t n16 = sh_n16, n4 = sh_n4, ns = sh_ns;
       const uint64_t rk = sh_rk;
-      for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) {
-        uint32_t q = qlist[i];
+      for (uint32_t i = threadIdx.x; i < n16 * 4; i += blockDim.x) {   // 4 threads per 16-hop
+        uint32_t q = a16[i >> 2];
+        const uint32_t sub = i & 3;
+        for (uint32_t k = 0; k < sub; ++k) q = jt[2][q];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          recoff[rk + 4 * (uint64_t)i + k] = w0 + (uint64_t)q * 4;
-          q = j1[q];
+          recoff[rk + 16 * (uint64_t)(i >> 2) + 4 * sub + k] = w0 + (uint64_t)q * 4;
+          q = jt[0][q];
         }
       }
-      for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) recoff[rk + 4 * (uint64_t)nq + i] = w0 + (uint64_t)slist[i] * 4;
+      const uint64_t r4 = rk + 16 * (uint64_t)n16;
+      for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) {
+        uint32_t q = a4[i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          recoff[r4 + 4 * (uint64_t)i + k] = w0 + (uint64_t)q * 4;
+          q = jt[0][q];
+        }
+      }
+      const uint64_t r1 = r4 + 4 * (uint64_t)n4;
+      for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) recoff[r1 + i] = w0 + (uint64_t)a1s[i] * 4;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -265,7 +310,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
         atomicOr(call_status, kStMalformed);
         sh_state = 2;
       } else {
-        sh_rk = sh_rk + 4 * (uint64_t)sh_nq + sh_ns;
+        sh_rk = sh_rk + 16 * (uint64_t)sh_n16 + 4 * (uint64_t)sh_n4 + sh_ns;
         if (!sh_left) {
           sh_state = 0;
           sh_k = sh_k + 1;

@@ -74,6 +74,9 @@ def parse():
                    help="C2 fraction of rows each batch covers (SURVEY §8(d) C2 variant: 0.125)")
     p.add_argument("--indexed", action="store_true",
                    help="C3 through psx_apply_indexed: producer record indexes replace the sequential sparse walk")
+    p.add_argument("--record-rows", action="store_true",
+                   help="C2 through psx_apply_indexed_rows: the producer's record-row lists (the rows it packed) "
+                        "place the dense records instead of the stream's row ids")
     p.add_argument("--importance", action="store_true",
                    help="C2 with importance accumulation (SSPAggr RelativeMagnitude tables)")
     p.add_argument("--pcie", action="store_true",
@@ -561,6 +564,7 @@ def main():
     streams = []
     nb = max(1, int(round(rows * args.density)))   # records per batch
     touched = torch.zeros(rows, dtype=torch.bool, device="cuda")
+    record_rows = []   # the producer's record-row lists (psx_pack_stream_indexed's record_rows)
     for b in range(B):
         perm = torch.randperm(rows, device="cuda", generator=g)[:nb].to(torch.int32)
         touched[perm.long()] = True
@@ -570,6 +574,8 @@ def main():
             streams.append(wire.dense_stream_torch_f16(1, perm, upd.half()))
         else:
             streams.append(wire.dense_stream_torch(1, perm, upd))
+        if args.record_rows:
+            record_rows.append(perm)
         del upd, perm
     n_touched = int(touched.sum().item())
     del touched
@@ -578,6 +584,8 @@ def main():
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    if args.record_rows:   # the messages are resident before the timed loop: overlap index and apply
+        srv.set_pipeline(1)
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
                                      row_offset=base, max_rows=rows, accum_importance=args.importance,
                                      row_oplog_type=3 if args.f16_records else 0))
@@ -590,7 +598,11 @@ def main():
     ver = [0]
 
     def step():
-        srv.apply_device([(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)])
+        msgs = [(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)]
+        if args.record_rows:
+            srv.apply_indexed_rows(msgs, [r.data_ptr() for r in record_rows])
+        else:
+            srv.apply_device(msgs)
         ver[0] += 1
 
     for _ in range(args.warmup):
@@ -630,8 +642,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    stream_bytes = sum(s.numel() for s in streams)
-    # per GPU: streams + row read/write (+ accum, z, z_max read/write for AdaRevision)
+    stream_bytes = sum(s.numel() for s in streams) + sum(4 * r.numel() for r in record_rows)
+    # per GPU: streams (+ the record-row lists) + row read/write (+ accum, z, z_max read/write
+    # for AdaRevision)
     step_bytes = stream_bytes + (8 if args.adarevision else 2) * n_touched * cap * 4
     total_bytes = step_bytes * args.steps * world
     value = total_bytes / elapsed / 1e9
@@ -685,6 +698,8 @@ def main():
                 "importance": bool(args.importance),
                 "server_table_logic": "AdaRevision" if args.adarevision else None,
                 "record_format": "float16 (row_oplog_type 3)" if args.f16_records else "V[cap] (DenseRowOpLog)",
+                "record_placement": ("producer record-row lists (psx_apply_indexed_rows), row ids checked in the apply"
+                                     if args.record_rows else "row ids read from the stream (dense_index)"),
             },
             "roofline": {
                 "bound": "hbm",

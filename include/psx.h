@@ -86,7 +86,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 4
+#define PSX_ABI_VERSION 5
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -242,6 +242,25 @@ psx_status psx_apply_streams_device(psx_ctx *ctx, const psx_stream *streams, int
  * applied.  Dense tables' entries are counted but not read (fixed stride). */
 psx_status psx_apply_indexed(psx_ctx *ctx, const psx_stream *streams, const uint64_t *const *record_offsets,
                              int32_t n);
+/* psx_apply_indexed plus producer record-row lists: record_rows[i] (device, 4-byte aligned;
+ * NULL = none) holds, for every record of message i, all tables in stream order, the row
+ * id the producer packed into it — psx_pack_stream_indexed's record_rows, i.e. the pack
+ * tables' row_ids in record order.  record_offsets may be NULL (no sparse index).  Dense
+ * tables on the fast path then place records from the lists instead of reading every
+ * record's row id from the stream (a 4-byte read that costs one 128-byte DRAM line per
+ * record), and the apply kernel checks each record's row id against its slot as it loads
+ * the record (same cache line as the payload).  Contract difference, stated: a list that
+ * disagrees with its stream is found during the apply, so the call is PSX_ERR_MALFORMED
+ * at psx_sync with the rows whose records disagree left unchanged (not created, not
+ * dirtied) and every other row of the call applied.  A list entry naming a row twice or
+ * outside the shard leaves its message's claim count short, which is caught before any
+ * apply: the call is replayed from the stream on the ordered path, exactly as for a
+ * duplicate row (exact result; the stream's own row ids decide).  A stream row id that
+ * differs from its list entry — outside the shard or not — is a disagreement like any
+ * other.  Tables whose apply kernel does not check rows (importance, AdaRevision,
+ * partial-coverage and >= 4 GiB calls) ignore the lists. */
+psx_status psx_apply_indexed_rows(psx_ctx *ctx, const psx_stream *streams, const uint64_t *const *record_offsets,
+                                  const int32_t *const *record_rows, int32_t n);
 /* Wait for all queued work and report any device-detected error. */
 psx_status psx_sync(psx_ctx *ctx);
 
@@ -319,6 +338,19 @@ psx_status psx_decode_push_header(const void *msg, size_t msg_size, psx_push_msg
  * larger batches (wire.split_stream).  Default 0: 64-bit offsets, any size. */
 #define PSX_COMPAT_INT32_STREAM_OFFSETS 1
 psx_status psx_ctx_set_compat(psx_ctx *ctx, int32_t flags);
+
+/* Overlap each apply call's index stage (decode, dense index, claim counts) with the
+ * previous call's apply kernels: the stage runs on the context's side stream once call
+ * k-2 has finished, so it may start BEFORE work the caller enqueued on the context stream
+ * after the previous apply call has finished.  Opt-in contract: the messages (and record
+ * lists) of a call are complete when the call is made (e.g. produced before the previous
+ * apply call, or synchronized by the caller).  Modes: 0 off (default); PSX_PIPELINE_LISTED
+ * for calls whose fast dense tables all place records from record-row lists
+ * (psx_apply_indexed_rows with a list for every message: a light index stage); and
+ * PSX_PIPELINE_ALL for every call. */
+#define PSX_PIPELINE_LISTED 1
+#define PSX_PIPELINE_ALL 2
+psx_status psx_ctx_set_pipeline(psx_ctx *ctx, int32_t mode);
 
 /* ServerThread::HandleOpLogMsg's server part (server_thread.cpp:224-266) on a whole
  * ClientSendOpLogMsg in host memory: decode the header, apply the payload
@@ -445,6 +477,10 @@ typedef struct psx_pack_table {
  * record index.  Synchronous on the context stream. */
 psx_status psx_pack_stream(psx_ctx *ctx, const psx_pack_table *tables, int32_t n, void *out,
                            size_t cap, size_t *used, uint64_t *record_offsets);
+/* psx_pack_stream that also writes record_rows (optional, device int32): the row id of
+ * every record in message order, for psx_apply_indexed_rows. */
+psx_status psx_pack_stream_indexed(psx_ctx *ctx, const psx_pack_table *tables, int32_t n, void *out,
+                                   size_t cap, size_t *used, uint64_t *record_offsets, int32_t *record_rows);
 
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);

@@ -150,6 +150,7 @@ def load():
         "psx_apply_stream": ([vp, vp, sz, i32, u32], ctypes.c_int),
         "psx_apply_streams_device": ([vp, P(psx_stream), i32], ctypes.c_int),
         "psx_apply_indexed": ([vp, P(psx_stream), P(vp), i32], ctypes.c_int),
+        "psx_apply_indexed_rows": ([vp, P(psx_stream), P(vp), P(vp), i32], ctypes.c_int),
         "psx_sync": ([vp], ctypes.c_int),
         "psx_serialize_rows": ([vp, i32, vp, i32, vp, sz, P(sz)], ctypes.c_int),
         "psx_serialize_dirty": ([vp, vp, sz, P(sz), i32, i32], ctypes.c_int),
@@ -160,6 +161,7 @@ def load():
         "psx_row_sent": ([vp, i32, vp, i32, i32], ctypes.c_int),
         "psx_adarevision_state": ([vp, i32, i64, i64, vp, vp, vp, P(ctypes.c_uint64)], ctypes.c_int),
         "psx_pack_stream": ([vp, P(psx_pack_table), i32, vp, sz, P(sz), vp], ctypes.c_int),
+        "psx_pack_stream_indexed": ([vp, P(psx_pack_table), i32, vp, sz, P(sz), vp, vp], ctypes.c_int),
         "psx_clock_until": ([vp, i32, i32, P(i32)], ctypes.c_int),
         "psx_min_clock": ([vp, P(i32)], ctypes.c_int),
         "psx_sender_clock": ([vp, i32, P(i32)], ctypes.c_int),
@@ -173,6 +175,7 @@ def load():
         "psx_encode_push_header": ([P(psx_push_msg_header), vp], ctypes.c_int),
         "psx_decode_push_header": ([vp, sz, P(psx_push_msg_header)], ctypes.c_int),
         "psx_ctx_set_compat": ([vp, i32], ctypes.c_int),
+        "psx_ctx_set_pipeline": ([vp, i32], ctypes.c_int),
         "psx_handle_oplog_msg": ([vp, vp, sz, i32, P(i32)], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),

@@ -26,6 +26,8 @@ enum : uint32_t {
   kStUnsupported = 1u << 4,
   kStDuplicateRow = 1u << 5,   // a row appears twice in one message: replay on the ordered path
   kStState = 1u << 6,          // AdaRevision: a record names a (row, version) with no snapshot
+  kStRowsMismatch = 1u << 7,   // a producer record-row list disagrees with its stream (found by the
+                               // apply; not fatal to the rest of the call: see psx_apply_indexed_rows)
 };
 constexpr uint32_t kStFatal = kStMalformed | kStUnknownTable | kStRowRange | kStCapacity |
                               kStUnsupported | kStState;
@@ -53,6 +55,7 @@ struct Seg {
   int64_t rec0;       // byte offset of the first record's row_id, -1 = table absent
   int32_t num_rows;
   int32_t sparse;     // 1: record offsets live in recoff[recoff_base[b] + k]
+  int64_t ord0;       // records of the message before this table (index into a record-row list)
 };
 
 // Inverse-index addressing: entry (slot s, message b) lives at inv[s*ss + b*sb]; the
@@ -85,6 +88,9 @@ struct DenseArgs {
   const uint8_t *zero_chunk;   // >= 2 KiB of zeros, stands in for absent messages
   double *imp;                 // non-null: accumulate NSSumImpCalc importance per slot
   uint64_t *ver;               // non-null: VersionServerRow::version_ per slot (+1 per record)
+  uint32_t rows_mask;          // bit b: message b was placed from the producer's record rows, so
+                               // every record's row id is checked against its slot in the apply
+  int64_t row_offset, row_stride;   // shard geometry (expected row id of a slot)
 };
 
 // AdaRevision server-table logic on one f32 dense table (psx_ada.hip).
@@ -118,9 +124,11 @@ struct AdaArgs {
 
 // Producer-supplied record indexes of one call (psx_apply_indexed): for message b, the
 // byte offset of every record's row id, all tables in stream order (psx_pack_stream's
-// record_offsets); nullptr: walk that message.
+// record_offsets); nullptr: walk that message.  rows[b] (psx_apply_indexed_rows): the row
+// id of every record, all tables in stream order (the rows the producer packed).
 struct IdxSet {
   const uint64_t *p[kMaxFused];
+  const int32_t *rows[kMaxFused];
 };
 
 // Fast-path dense tables of one call (for the duplicate-row gate).

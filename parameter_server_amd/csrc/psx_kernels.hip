@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
     s.rec0 = -1;
     s.num_rows = 0;
     s.sparse = 0;
+    s.ord0 = 0;
     segs[b * kMaxTables + t] = s;
     counters[t * kMaxFused + b] = 0;
     if (b == 0) ntouched[t] = 0;
@@ -117,6 +118,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
           sg->rec0 = (int64_t)off;
           sg->num_rows = nrows;
           sg->sparse = 0;
+          sg->ord0 = (int64_t)sh_kk;
           sh_off = off + need;
           sh_k = sh_k + 1;
           sh_kk = sh_kk + (uint64_t)nrows;
@@ -128,6 +130,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
           sg->rec0 = (int64_t)sh_rk;   // index of the first record offset
           sg->num_rows = nrows;
           sg->sparse = 1;
+          sg->ord0 = (int64_t)sh_kk;
           sh_t = t;
           sh_off = off;
           sh_t0 = off;
@@ -729,6 +732,7 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
   }
   if (dup && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.call_status, kStDuplicateRow);
   skip = skip || dup;
+  const bool rows_mode = a.rows_mask != 0;
 
   const int64_t vec_elems = (a.cap / EPV) * EPV;
   const int64_t row_bytes = a.row_cap * VS;
@@ -755,7 +759,7 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
       }
     }
     if (skip) continue;
-    if (touched) {
+    if (touched && !rows_mode) {
       a.flags[my_slot] = 3;
       if (a.ver) {
         uint64_t n = 0;
@@ -788,6 +792,42 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
           voff[q][b] = (uint32_t)i * stride + lane_off;
         }
       }
+      // Rows mode: records placed from the producer's row lists are checked here.  Lane
+      // q*BMAX + b loads the row id of record (q, b) — it shares the record's first cache
+      // line with the payload loaded next, so the check adds no DRAM traffic — and a row
+      // any of whose records names another row is neither written nor marked.
+      uint32_t okq = (1u << PAIR) - 1;
+      bool chk = false;
+      int32_t rid = 0, rid_want = 0;
+      if (rows_mode) {
+        const uint8_t *cb = a.zero_chunk;
+        uint32_t co = 4;
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q)
+#pragma unroll
+          for (int b = 0; b < BMAX; ++b)
+            if (lane == q * BMAX + b) {
+              chk = ((presm >> (q * BMAX + b)) & 1u) && ((a.rows_mask >> b) & 1u);
+              cb = pay0[b];
+              co = voff[q][b] - lane_off;
+              rid_want = (int32_t)(a.row_offset + (s0 + ks[q]) * a.row_stride);
+            }
+        if (chk) rid = *reinterpret_cast<const int32_t *>(cb + co - 4);
+      }
+      bool verified = !rows_mode;
+      auto verify = [&]() {
+        const uint64_t badm = __ballot(chk && rid != rid_want);
+        if (badm && lane == 0) atomicOr(a.call_status, kStRowsMismatch);
+#pragma unroll
+        for (int q = 0; q < PAIR; ++q) {
+          if ((badm >> (q * BMAX)) & ((1ull << BMAX) - 1)) okq &= ~(1u << q);
+          if (lane == 0 && has[q] && ((okq >> q) & 1u)) {
+            a.flags[s0 + ks[q]] = 3;
+            if (a.ver) a.ver[s0 + ks[q]] += (uint64_t)__builtin_popcount((presm >> (q * BMAX)) & ((1u << BMAX) - 1));
+          }
+        }
+        verified = true;
+      };
       double ib[IMP ? PAIR : 1], imp0[IMP ? PAIR : 1];
 #pragma unroll
       for (int q = 0; q < (IMP ? PAIR : 1); ++q) {
@@ -817,6 +857,7 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
               u[q][b] = gload16<NT>(pay0[b], off);
           }
         }
+        if (!verified) verify();
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
           u32x4 acc = t[q];
@@ -828,14 +869,15 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
               }
               acc = Vec<V>::add(acc, u[q][b]);
             }
-          if (full && has[q]) store16(trow[q] + e0 * VS, acc);
+          if (full && has[q] && ((okq >> q) & 1u)) store16(trow[q] + e0 * VS, acc);
         }
       }
+      if (!verified) verify();
       const int64_t tail = a.cap - vec_elems;
       if (tail) {
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
-          if (has[q] && lane < tail) {
+          if (has[q] && ((okq >> q) & 1u) && lane < tail) {
             const int64_t e = vec_elems + lane;
             V acc = *reinterpret_cast<const V *>(trow[q] + e * VS);
 #pragma unroll
@@ -861,7 +903,7 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
           const double tot = imp0[q] + wave_sum_f64(ib[q]);
-          if (has[q] && lane == 0) a.imp[s0 + ks[q]] = tot;
+          if (has[q] && ((okq >> q) & 1u) && lane == 0) a.imp[s0 + ks[q]] = tot;
         }
       }
     }
@@ -1002,28 +1044,37 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
 }
 
 // dense_index_v2: flattened (message, record) space, UNROLL row-id loads in flight per
-// thread before any store.
-// MODE 0: non-temporal row-id loads; 1: plain loads.  Either way every 4-byte row id costs
-// one 128-B L2->DRAM request (PMC, profiles/r02/pmc_request_sizes_index_apply.json).  Loads
-// issued one lane at a time, with sc0/sc1/nt scope hints (still 128-B requests), or as
-// scalar s_load_dword (64-B requests, but 0.51 vs 0.26 ms) were no faster
+// thread before any store.  A message in rows_mask takes its row ids from the producer's
+// record-row list (contiguous int32s, psx_apply_indexed_rows) instead of the stream.
+// MODE 0: non-temporal row-id loads; 1: plain loads.  Either way every 4-byte row id read
+// from the stream costs one 128-B L2->DRAM request (PMC,
+// profiles/r02/pmc_request_sizes_index_apply.json): 1.07 GB on C2 for 32 MB of row ids.
+// Loads issued one lane at a time, with sc0/sc1/nt scope hints (still 128-B requests), or
+// as scalar s_load_dword (64-B requests, but 0.51 vs 0.26 ms) were no faster
 // (profiles/r02/ab_index_loads.json, ab_index_policy.json).
 template <int UNROLL, int MODE>
-__global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const Seg *segs, int t, int B,
-                                                            int64_t stride, Geo g, int32_t *inv, InvLayout L,
-                                                            uint32_t *call_status) {
+__global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, IdxSet ix, uint32_t rows_mask,
+                                                            const Seg *segs, int t, int B, int64_t stride, Geo g,
+                                                            int32_t *inv, InvLayout L, uint32_t *call_status) {
   __shared__ int64_t pre[kMaxFused + 1];
   __shared__ const uint8_t *base[kMaxFused];
+  __shared__ int64_t sstr[kMaxFused];
   if (threadIdx.x == 0) {
     int64_t acc = 0;
     for (int b = 0; b < kMaxFused; ++b) {
       pre[b] = acc;
       base[b] = nullptr;
+      sstr[b] = stride;
       if (b < B) {
         const Seg sg = segs[b * kMaxTables + t];
         if (sg.rec0 >= 0 && !sg.sparse) {
           acc += sg.num_rows;
-          base[b] = ss.data[b] + sg.rec0;
+          if ((rows_mask >> b) & 1u) {
+            base[b] = reinterpret_cast<const uint8_t *>(ix.rows[b] + sg.ord0);
+            sstr[b] = 4;
+          } else {
+            base[b] = ss.data[b] + sg.rec0;
+          }
         }
       }
     }
@@ -1049,7 +1100,7 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
         while (b + 1 < B && pre[b + 1] <= r) ++b;
         bi[u] = b;
         ii[u] = r - pre[b];
-        ptr[u] = reinterpret_cast<const int32_t *>(base[b] + ii[u] * stride);
+        ptr[u] = reinterpret_cast<const int32_t *>(base[b] + ii[u] * sstr[b]);
       }
     }
 #pragma unroll
@@ -1059,7 +1110,12 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, const
     for (int u = 0; u < UNROLL; ++u) {
       if (bi[u] < 0) continue;
       const int64_t s = slot_of(rid[u], g);
-      if (s < 0) { atomicOr(call_status, kStRowRange); continue; }
+      if (s < 0) {
+        // a listed row outside the shard only drops the claim: the short count replays the
+        // call from the stream, whose own row ids decide (as for a duplicate row)
+        if (!((rows_mask >> bi[u]) & 1u)) atomicOr(call_status, kStRowRange);
+        continue;
+      }
       inv[s * L.ss + bi[u] * L.sb] = (int32_t)ii[u];
     }
   }
@@ -1145,16 +1201,19 @@ static unsigned resident_blocks(K kernel, int64_t want) {
 int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads
 int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact), 3: v3 with plain record loads
 
-hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
-                              int64_t row_offset, int64_t row_stride, int64_t max_rows,
+hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
+                              int64_t stride, int64_t row_offset, int64_t row_stride, int64_t max_rows,
                               int32_t *inv, InvLayout L, uint32_t *call_status, hipStream_t st) {
+  // Listed messages read their row ids from the record-row lists (contiguous).  An
+  // XCD-local form of the scatter (each XCD writing only its eighth of the slots) was
+  // slower, 0.21 vs 0.13 ms on C2 (profiles/r02/ab_index_rows.json).
   Geo g{row_offset, row_stride, max_rows};
   if (g_index_variant == 1)
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, 1>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
-                       call_status);
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, 1>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B,
+                       stride, g, inv, L, call_status);
   else
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, 0>), dim3(2048), dim3(256), 0, st, ss, segs, t, B, stride, g, inv, L,
-                       call_status);
+    hipLaunchKernelGGL((dense_index_v2_kernel<8, 0>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B,
+                       stride, g, inv, L, call_status);
   return hipGetLastError();
 }
 
@@ -1252,6 +1311,14 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
   else if (g_apply_variant == 3) launch_adaptive_v3<V, false, 0, false>(a, st);
   else launch_adaptive_v3<V, false, 0>(a, st);
   return hipGetLastError();
+}
+
+// True when launch_dense_apply runs v3 on these arguments: the only apply kernel that
+// checks producer-placed records (DenseArgs::rows_mask); other tables index from the stream.
+bool dense_apply_checks_rows(const DenseArgs &a, bool rec_f16) {
+  if (a.imp || g_apply_variant == 1 || !v3_ok(a)) return false;
+  if (rec_f16) return true;
+  return !(g_apply_variant == 2 || (g_apply_variant == 0 && sparse_coverage(a)));
 }
 
 hipError_t launch_dense_apply(int dtype, const DenseArgs &a, hipStream_t st, bool rec_f16) {

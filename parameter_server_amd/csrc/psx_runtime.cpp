@@ -23,7 +23,9 @@ namespace psx {
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
                          uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
                          hipStream_t st);
-hipError_t launch_dense_index(StreamSet ss, const Seg *segs, int t, int B, int64_t stride,
+bool dense_apply_checks_rows(const DenseArgs &a, bool rec_f16);
+hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
+                              int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
                               InvLayout L, uint32_t *call_status, hipStream_t st);
 hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, int64_t max_rows,
@@ -188,7 +190,10 @@ struct psx_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_ready[2] = {nullptr, nullptr};    // slot's index stage done (side -> main)
   hipEvent_t ev_free[2] = {nullptr, nullptr};     // slot's apply stage done (main -> side)
-  bool pipeline = false;                          // PSX_PIPELINE=1: overlap (no gain measured, DRAM-bound)
+  int pipeline = 0;     // psx_ctx_set_pipeline: 0 off, PSX_PIPELINE_LISTED (calls whose dense
+                       // tables all place records from record-row lists), PSX_PIPELINE_ALL.
+                       // Walked calls lose (their index stage reads 1 GB of DRAM lines on
+                       // C2), listed calls gain (profiles/r02/s17_bench_*.log)
   uint32_t *d_ndirty = nullptr;          // partial push: dirty-row count
   uint8_t *d_push_body = nullptr;        // psx_apply_push_body: host body staged in HBM
   size_t push_body_cap = 0;
@@ -414,11 +419,9 @@ size_t min_record_bytes(const psx_ctx *c) {
 // the sorted/map capacity dry run), the AdaRevision state check, and the duplicate-row
 // gate — so a call that fails applies nothing.
 psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_ordered,
-                         const uint64_t *const *record_offsets = nullptr) {
+                         const uint64_t *const *record_offsets = nullptr,
+                         const int32_t *const *record_rows = nullptr) {
   const int slot = (int)(c->call_seq & 1);
-  // Stage 1 (decode, index, verify) runs on the side stream once the slot's previous
-  // user (call k-2) has finished applying; stage 2 runs on the main stream after it.
-  hipStream_t prep = c->pipeline ? c->side : c->stream;
   psx::StreamSet ss{};
   ss.n = n;
   size_t rec_need = 0, list_need = 0;
@@ -458,7 +461,38 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     }
   }
   psx::IdxSet ix{};
-  for (int i = 0; i < n && record_offsets; ++i) ix.p[i] = record_offsets[i];
+  uint32_t rows_given = 0;
+  for (int i = 0; i < n; ++i) {
+    if (record_offsets) ix.p[i] = record_offsets[i];
+    if (record_rows && record_rows[i] && !force_ordered) {
+      ix.rows[i] = record_rows[i];
+      rows_given |= 1u << i;
+    }
+  }
+  // Producer record rows replace the stream's row ids for fast tables whose apply kernel
+  // checks them (rows_mask[ti]); the others index from the stream.
+  std::vector<uint32_t> rows_mask(c->tables.size(), 0);
+  const uint32_t all_msgs = n >= 32 ? ~0u : ((1u << n) - 1);
+  bool light = rows_given == all_msgs;   // no fast table reads row ids from the stream
+  for (size_t ti = 0; ti < c->tables.size(); ++ti) {
+    TableState &t = c->tables[ti];
+    if (!t.fast() || force_ordered) continue;
+    if (rows_given && !t.ada) {
+      psx::DenseArgs probe{};
+      probe.ss = ss;
+      probe.B = n;
+      probe.stride = t.dense_stride();
+      probe.max_rows = t.cfg.max_rows;
+      probe.imp = t.d_imp;
+      if (psx::dense_apply_checks_rows(probe, t.rec_f16())) rows_mask[ti] = rows_given;
+    }
+    if (rows_mask[ti] != all_msgs) light = false;
+  }
+  // Stage 1 (decode, index, verify) runs on the side stream once the slot's previous
+  // user (call k-2) has finished applying, overlapping call k-1's apply; stage 2 runs on
+  // the main stream after it.
+  const bool pipelined = c->pipeline == PSX_PIPELINE_ALL || (c->pipeline == PSX_PIPELINE_LISTED && light);
+  hipStream_t prep = pipelined ? c->side : c->stream;
   psx::TableDir dir{};
   dir.n = (int32_t)c->tables.size();
   for (size_t i = 0; i < c->tables.size(); ++i) {
@@ -473,7 +507,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   uint32_t *call_log = c->d_status + 1 + kRing + ring;
   psx::Seg *segs = c->d_segs[slot];
   uint32_t *counters = c->d_counters[slot];
-  if (c->pipeline) HIP_TRY(c, hipStreamWaitEvent(prep, c->ev_free[slot], 0));
+  if (pipelined) HIP_TRY(c, hipStreamWaitEvent(prep, c->ev_free[slot], 0));
   psx_status st = timed(
       c, "decode_streams",
       [&] {
@@ -494,8 +528,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     st = timed(
         c, "dense_index",
         [&] {
-          return psx::launch_dense_index(ss, segs, (int)ti, n, stride, t.cfg.row_offset, t.cfg.row_stride,
-                                         t.cfg.max_rows, t.d_inv[slot], L, call_st, prep);
+          return psx::launch_dense_index(ss, ix, rows_mask[ti], segs, (int)ti, n, stride, t.cfg.row_offset,
+                                         t.cfg.row_stride, t.cfg.max_rows, t.d_inv[slot], L, call_st, prep);
         },
         prep);
     if (st) return st;
@@ -505,7 +539,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
         prep);
     if (st) return st;
   }
-  if (c->pipeline) {
+  if (pipelined) {
     HIP_TRY(c, hipEventRecord(c->ev_ready[slot], prep));
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_ready[slot], 0));
   }
@@ -623,12 +657,16 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.call_status = call_st;
     a.zero_chunk = c->d_zero;
     a.imp = t.d_imp;
+    a.rows_mask = rows_mask[ti];
+    a.row_offset = t.cfg.row_offset;
+    a.row_stride = t.cfg.row_stride;
     st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream, t.rec_f16()); });
     if (st) return st;
   }
   st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
   if (st) return st;
-  if (c->pipeline) HIP_TRY(c, hipEventRecord(c->ev_free[slot], c->stream));
+  // every call marks its slot free (a later pipelined call's stage 1 waits on it)
+  HIP_TRY(c, hipEventRecord(c->ev_free[slot], c->stream));
   PendingCall pc;
   pc.streams.assign(s, s + n);
   pc.ring = ring;
@@ -699,6 +737,10 @@ psx_status ada_rows_sent(psx_ctx *c, TableState &t, int ti, const int32_t *list,
 psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
   if (sticky & psx::kStUnknownTable) return fail(c, PSX_ERR_UNKNOWN_TABLE, "unknown table id in a device stream");
   if (sticky & psx::kStMalformed) return fail(c, PSX_ERR_MALFORMED, "malformed device stream");
+  if (sticky & psx::kStRowsMismatch)
+    return fail(c, PSX_ERR_MALFORMED,
+                "producer record rows disagree with the stream's row ids: the rows whose records disagree were "
+                "left unchanged, every other row of the call was applied");
   if (sticky & psx::kStRowRange) return fail(c, PSX_ERR_ROW_RANGE, "row id outside this shard's range");
   if (sticky & psx::kStState)
     return fail(c, PSX_ERR_STATE, "AdaRevision: a record names a (row, version) without a snapshot");
@@ -853,7 +895,7 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
     if (hipMemset(c->d_counters[k], 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
       return cleanup(PSX_ERR_DEVICE);
   }
-  if (const char *pv = getenv("PSX_PIPELINE")) c->pipeline = atoi(pv) != 0;
+  if (const char *pv = getenv("PSX_PIPELINE")) c->pipeline = atoi(pv);   // A/B runs
   if (hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
       hipMalloc(&c->d_zero, 4096) != hipSuccess)
     return cleanup(PSX_ERR_OOM);
@@ -1180,7 +1222,8 @@ psx_status psx_row_versions(psx_ctx *c, int32_t table_id, int64_t first_row, int
 }
 
 static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
-                                    const uint64_t *const *record_offsets);
+                                    const uint64_t *const *record_offsets,
+                                    const int32_t *const *record_rows = nullptr);
 
 psx_status psx_apply_indexed(psx_ctx *c, const psx_stream *s, const uint64_t *const *record_offsets, int32_t n) {
   if (!c || !s || !record_offsets || n <= 0 || n > PSX_MAX_FUSED_STREAMS) return PSX_ERR_INVALID_ARG;
@@ -1190,13 +1233,26 @@ psx_status psx_apply_indexed(psx_ctx *c, const psx_stream *s, const uint64_t *co
   return apply_device_impl(c, s, n, record_offsets);
 }
 
+psx_status psx_apply_indexed_rows(psx_ctx *c, const psx_stream *s, const uint64_t *const *record_offsets,
+                                  const int32_t *const *record_rows, int32_t n) {
+  if (!c || !s || (!record_offsets && !record_rows) || n <= 0 || n > PSX_MAX_FUSED_STREAMS)
+    return PSX_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i) {
+    if (record_offsets && record_offsets[i] && ((uintptr_t)record_offsets[i] & 7))
+      return fail(c, PSX_ERR_INVALID_ARG, "record_offsets must be 8-byte aligned device arrays");
+    if (record_rows && record_rows[i] && ((uintptr_t)record_rows[i] & 3))
+      return fail(c, PSX_ERR_INVALID_ARG, "record_rows must be 4-byte aligned device arrays");
+  }
+  return apply_device_impl(c, s, n, record_offsets, record_rows);
+}
+
 psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) {
   if (!c || !s || n <= 0 || n > PSX_MAX_FUSED_STREAMS) return PSX_ERR_INVALID_ARG;
   return apply_device_impl(c, s, n, nullptr);
 }
 
 static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
-                                    const uint64_t *const *record_offsets) {
+                                    const uint64_t *const *record_offsets, const int32_t *const *record_rows) {
   // Version rule of Server::ApplyOpLogUpdateVersion (server.cpp:124-126), checked for
   // the whole batch before anything is enqueued.
   std::map<int32_t, int64_t> v = c->versions;
@@ -1218,7 +1274,7 @@ static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
     psx_status d = sync_impl(c);
     if (d != PSX_OK) c->deferred = d;
   }
-  psx_status st = enqueue_apply(c, s, n, false, record_offsets);
+  psx_status st = enqueue_apply(c, s, n, false, record_offsets, record_rows);
   if (st) return st;
   c->versions = v;
   return PSX_OK;
@@ -1661,6 +1717,11 @@ psx_status psx_adarevision_state(psx_ctx *c, int32_t table_id, int64_t first_row
 
 psx_status psx_pack_stream(psx_ctx *c, const psx_pack_table *tables, int32_t n, void *out, size_t cap,
                            size_t *used, uint64_t *record_offsets) {
+  return psx_pack_stream_indexed(c, tables, n, out, cap, used, record_offsets, nullptr);
+}
+
+psx_status psx_pack_stream_indexed(psx_ctx *c, const psx_pack_table *tables, int32_t n, void *out, size_t cap,
+                                   size_t *used, uint64_t *record_offsets, int32_t *record_rows) {
   if (!c || !used || n < 0 || n > PSX_MAX_TABLES || (n && !tables)) return PSX_ERR_INVALID_ARG;
   *used = 0;
   if (out && ((uintptr_t)out & 3)) return fail(c, PSX_ERR_INVALID_ARG, "pack output must be 4-byte aligned");
@@ -1740,8 +1801,13 @@ psx_status psx_pack_stream(psx_ctx *c, const psx_pack_table *tables, int32_t n, 
   }
   *used = (size_t)pos;
   if (!out || (size_t)pos > cap) return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "pack: *used bytes needed");
-  for (size_t k = 0; k < live.size(); ++k)
+  for (size_t k = 0; k < live.size(); ++k) {
     HIP_TRY(c, psx::launch_pack_emit(live[k]->dtype, pt[k], (uint8_t *)out, record_offsets, c->stream));
+    // the record-row list: the rows packed, in record order (what the producer already holds)
+    if (record_rows)
+      HIP_TRY(c, hipMemcpyAsync(record_rows + pt[k].rec_base, live[k]->row_ids, sizeof(int32_t) * live[k]->num_rows,
+                                hipMemcpyDeviceToDevice, c->stream));
+  }
   HIP_TRY(c, psx::launch_pack_header((uint8_t *)out, h, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return PSX_OK;
@@ -2064,6 +2130,12 @@ psx_status psx_decode_push_header(const void *msg, size_t msg_size, psx_push_msg
   h->version = rd32h(p + 32);
   h->is_clock = p[36] ? 1 : 0;
   if (h->avai_size > msg_size - PSX_PUSH_MSG_HEADER_BYTES) return PSX_ERR_MALFORMED;
+  return PSX_OK;
+}
+
+psx_status psx_ctx_set_pipeline(psx_ctx *c, int32_t mode) {
+  if (!c || mode < 0 || mode > PSX_PIPELINE_ALL) return PSX_ERR_INVALID_ARG;
+  c->pipeline = mode;
   return PSX_OK;
 }
 

@@ -80,6 +80,12 @@ class Server:
     def set_stream(self, hip_stream_handle):
         _check(self._L, self._ctx, self._L.psx_ctx_set_stream(self._ctx, hip_stream_handle))
 
+    def set_pipeline(self, mode):
+        """psx_ctx_set_pipeline: 0 off, 1 calls whose dense tables are all placed from
+        record-row lists, 2 every call.  Opt-in: a call's messages must be complete when
+        the call is made (its index stage may overlap the previous call's apply)."""
+        _check(self._L, self._ctx, self._L.psx_ctx_set_pipeline(self._ctx, int(mode)))
+
     # -- Server API (server.hpp) ----------------------------------------------
     def CreateTable(self, table_id, info: TableInfo):
         cfg = psx_table_config(
@@ -131,6 +137,21 @@ class Server:
             arr[i].version = ver
         offs = (ctypes.c_void_p * n)(*[o or None for o in record_offsets])
         _check(self._L, self._ctx, self._L.psx_apply_indexed(self._ctx, arr, offs, n))
+
+    def apply_indexed_rows(self, streams, record_rows, record_offsets=None):
+        """apply_device with producer record-row lists (psx_apply_indexed_rows):
+        record_rows[i] is the device pointer of message i's int32 row ids in record order
+        (psx_pack_stream_indexed's), or None; record_offsets as in apply_indexed."""
+        n = len(streams)
+        arr = (psx_stream * n)()
+        for i, (ptr, nbytes, bg, ver) in enumerate(streams):
+            arr[i].data = ptr
+            arr[i].size = nbytes
+            arr[i].bg_id = bg
+            arr[i].version = ver
+        rows = (ctypes.c_void_p * n)(*[r or None for r in record_rows])
+        offs = (ctypes.c_void_p * n)(*[o or None for o in record_offsets]) if record_offsets else None
+        _check(self._L, self._ctx, self._L.psx_apply_indexed_rows(self._ctx, arr, offs, rows, n))
 
     def sync(self):
         _check(self._L, self._ctx, self._L.psx_sync(self._ctx))
@@ -314,13 +335,14 @@ class Server:
             1 if insert_missing else 0))
 
     # -- client-side pack -------------------------------------------------------------
-    def pack_stream(self, tables, with_index=False):
+    def pack_stream(self, tables, with_index=False, with_rows=False):
         """Pack per-table oplog rows into one message on the device (psx_pack_stream).
 
         tables: dicts {table_id, dtype (psx dtype), dense_serialized, row_ids (CUDA int32
         [n]), oplogs (CUDA [n, capacity])}.  Returns a CUDA uint8 tensor holding the
         message (empty for an all-empty pack) and, with with_index, the CUDA int64 tensor
-        of record offsets."""
+        of record offsets; with with_rows (psx_pack_stream_indexed), also the CUDA int32
+        tensor of record rows (appended to the returned tuple)."""
         import torch
         torch.cuda.current_stream(self.device).synchronize()   # inputs come from torch's stream
         n = len(tables)
@@ -346,12 +368,18 @@ class Server:
         dev = torch.device("cuda", self.device)
         out = torch.empty((used.value + 3) // 4, dtype=torch.int32, device=dev).view(torch.uint8)
         idx = torch.empty(max(nrec, 1), dtype=torch.int64, device=dev) if with_index else None
+        rws = torch.empty(max(nrec, 1), dtype=torch.int32, device=dev) if with_rows else None
         if used.value:
-            _check(self._L, self._ctx, self._L.psx_pack_stream(
+            _check(self._L, self._ctx, self._L.psx_pack_stream_indexed(
                 self._ctx, arr, n, out.data_ptr(), out.numel(), ctypes.byref(used),
-                idx.data_ptr() if idx is not None else None))
+                idx.data_ptr() if idx is not None else None, rws.data_ptr() if rws is not None else None))
         out = out[:used.value]
-        return (out, idx[:nrec]) if with_index else out
+        res = (out,)
+        if with_index:
+            res += (idx[:nrec],)
+        if with_rows:
+            res += (rws[:nrec],)
+        return res if len(res) > 1 else out
 
     # -- timing ------------------------------------------------------------------------
     def timing(self, on=True):

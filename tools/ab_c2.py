@@ -3,7 +3,8 @@ rule 24): the headline workload of bench.py, then R rounds; each round runs ever
 configuration for K steps and records the per-kernel HIP-event times.  Prints JSON with
 the median ms of every kernel per configuration.
 Usage: python tools/ab_c2.py --configs 0:0,1:0,2:0 [--rounds 5 --steps 5]
-       (index_variant:apply_variant, include/psx_debug.h)"""
+       (index_variant:apply_variant[:rows], include/psx_debug.h; rows = 1 applies through
+       psx_apply_indexed_rows with the batches' record-row lists)"""
 import argparse
 import json
 import os
@@ -31,11 +32,12 @@ def main():
     rows, cap, B = args.rows, args.cols, args.batches
     g = torch.Generator(device="cuda").manual_seed(1234)
     table0 = torch.randn(rows, cap, device="cuda", generator=g) * 0.1
-    streams = []
+    streams, lists = [], []
     for b in range(B):
         perm = torch.randperm(rows, device="cuda", generator=g).to(torch.int32)
         upd = torch.randn(rows, cap, device="cuda", generator=g) * 0.01
         streams.append(wire.dense_stream_torch(1, perm, upd))
+        lists.append(perm)
         del upd, perm
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(device=0, server_id=1, bg_ids=bgs)
@@ -45,7 +47,7 @@ def main():
     del table0
     ver = [0]
     kernels = ("decode_streams", "dense_index", "dense_verify", "dense_apply", "finish_call")
-    configs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
+    configs = [tuple(int(x) for x in (c + ":0").split(":")[:3]) for c in args.configs.split(",")]
     res = {c: {k: [] for k in kernels + ("step",)} for c in configs}
 
     def run(c, steps):
@@ -56,7 +58,11 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            srv.apply_device([(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)])
+            msgs = [(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)]
+            if c[2]:
+                srv.apply_indexed_rows(msgs, [r.data_ptr() for r in lists])
+            else:
+                srv.apply_device(msgs)
             ver[0] += 1
         srv.sync()
         torch.cuda.synchronize()
@@ -74,7 +80,7 @@ def main():
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))
             res[c]["step"].append(step_ms)
-    out = {f"index{c[0]}_apply{c[1]}": {k: round(statistics.median(v), 4) for k, v in res[c].items()}
+    out = {f"index{c[0]}_apply{c[1]}" + ("_rows" if c[2] else ""): {k: round(statistics.median(v), 4) for k, v in res[c].items()}
            for c in configs}
     print(json.dumps(out, indent=1))
     srv.close()

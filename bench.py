@@ -6,8 +6,15 @@ batches, each a full Appendix-A stream (ClientSendOpLogMsg payload) holding one 
 record per row in a per-batch random row order, updates N(0, 0.01).  Streams and table
 are resident in HBM before the timed region.  Synthetic data, generated on the GPU.
 
-Algorithmic bytes per step: sum_b (20 + N_b*(4 + 4R)) + 2 * N_touched * 4R
-(N_b = N at full density; --density 0.125 gives the §8(d) partial-coverage variant).
+Records are placed from the producer's record-row lists (psx_apply_indexed_rows: the rows
+psx_pack_stream_indexed packed, 4 B per record; every record's row id is still checked
+against its row inside the apply) with each call's index stage overlapping the previous
+call's apply; the same messages through the walked path (row ids read from the stream,
+psx_apply_streams_device) are timed after it and reported as `walked` (--walked: only that).
+
+Algorithmic bytes per step: sum_b (20 + N_b*(4 + 4R)) + 2 * N_touched * 4R,
+plus 4 * N_b per listed message (N_b = N at full density; --density 0.125 gives the §8(d)
+partial-coverage variant).
 value = bytes of all ranks / max-over-ranks wall time.  Multi-GPU: each rank owns a
 2^20-row shard (row range) and receives its own already-split batches, as the reference
 client splits oplogs by owning server (abstract_bg_worker.cpp:590-649): no collective,
@@ -74,9 +81,13 @@ def parse():
                    help="C2 fraction of rows each batch covers (SURVEY §8(d) C2 variant: 0.125)")
     p.add_argument("--indexed", action="store_true",
                    help="C3 through psx_apply_indexed: producer record indexes replace the sequential sparse walk")
-    p.add_argument("--record-rows", action="store_true",
-                   help="C2 through psx_apply_indexed_rows: the producer's record-row lists (the rows it packed) "
-                        "place the dense records instead of the stream's row ids")
+    p.add_argument("--walked", action="store_true",
+                   help="C2 through psx_apply_streams_device only: every record's row id read from the stream to "
+                        "place it (the default run measures the producer record-row path, psx_apply_indexed_rows, "
+                        "and reports this walked path beside it)")
+    p.add_argument("--skip-walked", action="store_true",
+                   help="do not time the walked path after the record-row run (profiler passes: every "
+                        "dense_apply launch then belongs to the measured configuration)")
     p.add_argument("--importance", action="store_true",
                    help="C2 with importance accumulation (SSPAggr RelativeMagnitude tables)")
     p.add_argument("--pcie", action="store_true",
@@ -410,7 +421,11 @@ def run_c4(args):
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "exchange_ms_per_step": round(t_x[0] / args.steps * 1e3, 3),
-            "exchange_algbw_GBps": round(sent * args.steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
+            # nccl-tests all-to-all convention: algbw = bytes per rank / time, busbw =
+            # algbw * (n-1)/n (the bytes that actually cross xGMI per rank)
+            "exchange_algbw_GBps": round(per_rank_stream * args.steps / t_x[0] / 1e9, 2)
+            if world > 1 and t_x[0] > 0 else None,
+            "exchange_busbw_GBps": round(sent * args.steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
             "apply_kernel_ms": round(apply_ms / max(apply_n, 1), 3),
             "index_kernel_ms": round(idx_ms / max(apply_n, 1), 3),
             "higher_is_better": True, "scaling": "strong", "dtype": "f32",
@@ -558,6 +573,9 @@ def main():
     from parameter_server_amd import wire
 
     rows, cap, B = args.rows, args.cols, args.batches
+    # record-row lists only where the apply kernel uses them (v3: full coverage, no
+    # importance, no AdaRevision); the other variants place records from the stream
+    use_rows = not (args.walked or args.adarevision or args.importance or args.density != 1.0)
     base = rank * rows                       # this shard's first row id
     g = torch.Generator(device="cuda").manual_seed(1234 + 7919 * rank)
     table0 = torch.randn(rows, cap, device="cuda", generator=g) * 0.1
@@ -574,7 +592,7 @@ def main():
             streams.append(wire.dense_stream_torch_f16(1, perm, upd.half()))
         else:
             streams.append(wire.dense_stream_torch(1, perm, upd))
-        if args.record_rows:
+        if use_rows:
             record_rows.append(perm)
         del upd, perm
     n_touched = int(touched.sum().item())
@@ -584,7 +602,7 @@ def main():
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
-    if args.record_rows:   # the messages are resident before the timed loop: overlap index and apply
+    if use_rows:   # the messages are resident before the timed loop: overlap index and apply
         srv.set_pipeline(1)
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
                                      row_offset=base, max_rows=rows, accum_importance=args.importance,
@@ -597,9 +615,9 @@ def main():
 
     ver = [0]
 
-    def step():
+    def step(walked=False):
         msgs = [(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)]
-        if args.record_rows:
+        if use_rows and not walked:
             srv.apply_indexed_rows(msgs, [r.data_ptr() for r in record_rows])
         else:
             srv.apply_device(msgs)
@@ -636,18 +654,48 @@ def main():
     kernels = {k: srv.timing_read(k) for k in ("decode_streams", "dense_index", "dense_verify",
                                                apply_kernel, "finish_call")}
     srv.timing(False)
+    # The walked path (row ids read from the stream, no overlap) on the same messages, timed
+    # the same way, reported beside `value`.
+    walked = None
+    if use_rows and not args.skip_walked:
+        srv.set_pipeline(0)
+        for _ in range(2):
+            step(walked=True)
+        srv.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(walked=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el_w = time.perf_counter() - t0
+        srv.sync()
+        if world > 1:
+            t = torch.tensor([el_w], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_w = float(t.item())
 
     if world > 1:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    stream_bytes = sum(s.numel() for s in streams) + sum(4 * r.numel() for r in record_rows)
+    list_bytes = sum(4 * r.numel() for r in record_rows)
+    stream_bytes = sum(s.numel() for s in streams) + list_bytes
     # per GPU: streams (+ the record-row lists) + row read/write (+ accum, z, z_max read/write
     # for AdaRevision)
     step_bytes = stream_bytes + (8 if args.adarevision else 2) * n_touched * cap * 4
     total_bytes = step_bytes * args.steps * world
     value = total_bytes / elapsed / 1e9
+    if walked is None and use_rows and not args.skip_walked:
+        wb = step_bytes - list_bytes
+        walked = {"value": round(wb * args.steps * world / el_w / 1e9, 2), "unit": "GB/s",
+                  "ms_per_step": round(el_w / args.steps * 1e3, 4),
+                  "what": "the same messages through psx_apply_streams_device: row ids read from the stream "
+                          "(dense_index), no index/apply overlap; algorithmic bytes without the lists"}
 
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
@@ -698,8 +746,10 @@ def main():
                 "importance": bool(args.importance),
                 "server_table_logic": "AdaRevision" if args.adarevision else None,
                 "record_format": "float16 (row_oplog_type 3)" if args.f16_records else "V[cap] (DenseRowOpLog)",
-                "record_placement": ("producer record-row lists (psx_apply_indexed_rows), row ids checked in the apply"
-                                     if args.record_rows else "row ids read from the stream (dense_index)"),
+                "record_placement": ("producer record-row lists (psx_apply_indexed_rows, psx_pack_stream_indexed's "
+                                     "record_rows; 4 B per record counted), every record's row id checked in the apply; "
+                                     "index stage overlapped with the previous call's apply (psx_ctx_set_pipeline)"
+                                     if use_rows else "row ids read from the stream (dense_index)"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -718,6 +768,8 @@ def main():
             "kernel_ms_per_launch_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},
             "cpu_baseline": cpu,
         }
+        if walked:
+            line["walked"] = walked
         if pcie:
             line["pcie_inclusive"] = pcie
         print(json.dumps(line), flush=True)

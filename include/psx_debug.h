@@ -1,9 +1,10 @@
 /*
  * psx_debug.h — kernel selectors of libpsx (not part of the reference boundary).
  * The defaults are the measured winners; the alternatives are the kernels the product
- * itself falls back to (v2 for >= 4 GiB streams, v4 for partially covered calls) plus
- * two load-form knobs, selectable so the parity suite covers every kernel and A/B runs
- * stay interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
+ * itself falls back to (v2 for >= 4 GiB streams, v4 for partially covered calls),
+ * selectable so the parity suite covers every kernel and A/B runs stay interleaved in one
+ * process (cdna_hip_programming.md §5.4 rule 24).  Variants that lost their A/B are
+ * removed (their logs stay under profiles/).
  */
 #ifndef PSX_DEBUG_H_
 #define PSX_DEBUG_H_
@@ -13,9 +14,7 @@ extern "C" {
 #endif
 
 enum {
-  PSX_VARIANT_DENSE_INDEX = 0,  /* 0: non-temporal row-id loads (default), 1: plain loads */
-  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact,
-                                   3: v3 with plain record loads */
+  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact */
   PSX_VARIANT_ORD_SPLIT = 6     /* 1: rows of sorted/map tables with 256 < max_entries <= 1024
                                    classified into a 256- and a 1,024-entry image launch that
                                    run concurrently (default), 0: one 1,024-entry launch */

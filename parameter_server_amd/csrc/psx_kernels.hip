@@ -733,6 +733,13 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
   if (dup && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.call_status, kStDuplicateRow);
   skip = skip || dup;
   const bool rows_mode = a.rows_mask != 0;
+  const int wib = threadIdx.x >> 6;
+  __shared__ int32_t s_idx[4][TILE * BMAX];     // rows mode: the tile's record numbers
+  __shared__ const uint8_t *s_pay0[BMAX];
+#pragma unroll
+  for (int b = 0; b < BMAX; ++b)
+    if (threadIdx.x == b) s_pay0[b] = pay0[b];
+  __syncthreads();
 
   const int64_t vec_elems = (a.cap / EPV) * EPV;
   const int64_t row_bytes = a.row_cap * VS;
@@ -759,6 +766,18 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
       }
     }
     if (skip) continue;
+    // Rows mode (records placed from the producer's record-row lists): the tile's record
+    // numbers go to LDS so that, per row pair, lane q*BMAX + b can load the row id of
+    // record (q, b) right beside the pair's payload loads (same first cache line: no added
+    // DRAM traffic); a row any of whose records names another row is neither written nor
+    // marked.  Loading each slot's row ids in the tile prologue instead needs no LDS but
+    // re-fetches ~half of those lines (PMC 11.32 vs 10.77 GB read per launch: evicted before
+    // the pair that uses them), and a 16-way select chain for the addressing costs 1.7% of
+    // the apply (profiles/r02/ab_rows_check.json).
+    if (rows_mode && mine) {
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) s_idx[wib][lane * BMAX + b] = idx[b];
+    }
     if (touched && !rows_mode) {
       a.flags[my_slot] = 3;
       if (a.ver) {
@@ -792,27 +811,21 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
           voff[q][b] = (uint32_t)i * stride + lane_off;
         }
       }
-      // Rows mode: records placed from the producer's row lists are checked here.  Lane
-      // q*BMAX + b loads the row id of record (q, b) — it shares the record's first cache
-      // line with the payload loaded next, so the check adds no DRAM traffic — and a row
-      // any of whose records names another row is neither written nor marked.
-      uint32_t okq = (1u << PAIR) - 1;
+      uint32_t okq = (1u << PAIR) - 1;   // bit q: row q may be stored (rows mode)
       bool chk = false;
       int32_t rid = 0, rid_want = 0;
       if (rows_mode) {
-        const uint8_t *cb = a.zero_chunk;
-        uint32_t co = 4;
+        const int qj = lane / BMAX, bj = lane % BMAX;
+        int ksj = ks[0];
 #pragma unroll
-        for (int q = 0; q < PAIR; ++q)
-#pragma unroll
-          for (int b = 0; b < BMAX; ++b)
-            if (lane == q * BMAX + b) {
-              chk = ((presm >> (q * BMAX + b)) & 1u) && ((a.rows_mask >> b) & 1u);
-              cb = pay0[b];
-              co = voff[q][b] - lane_off;
-              rid_want = (int32_t)(a.row_offset + (s0 + ks[q]) * a.row_stride);
-            }
-        if (chk) rid = *reinterpret_cast<const int32_t *>(cb + co - 4);
+        for (int q = 1; q < PAIR; ++q)
+          if (qj == q) ksj = ks[q];
+        chk = lane < PAIR * BMAX && ((presm >> lane) & 1u) && ((a.rows_mask >> bj) & 1u);
+        rid_want = (int32_t)(a.row_offset + (s0 + ksj) * a.row_stride);
+        if (chk) {
+          const int32_t i = s_idx[wib][ksj * BMAX + bj];
+          rid = *reinterpret_cast<const int32_t *>(s_pay0[bj] + (uint32_t)i * stride - 4);
+        }
       }
       bool verified = !rows_mode;
       auto verify = [&]() {
@@ -1046,13 +1059,13 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
 // dense_index_v2: flattened (message, record) space, UNROLL row-id loads in flight per
 // thread before any store.  A message in rows_mask takes its row ids from the producer's
 // record-row list (contiguous int32s, psx_apply_indexed_rows) instead of the stream.
-// MODE 0: non-temporal row-id loads; 1: plain loads.  Either way every 4-byte row id read
-// from the stream costs one 128-B L2->DRAM request (PMC,
+// Every 4-byte row id read from the stream costs one 128-B L2->DRAM request (PMC,
 // profiles/r02/pmc_request_sizes_index_apply.json): 1.07 GB on C2 for 32 MB of row ids.
-// Loads issued one lane at a time, with sc0/sc1/nt scope hints (still 128-B requests), or
-// as scalar s_load_dword (64-B requests, but 0.51 vs 0.26 ms) were no faster
-// (profiles/r02/ab_index_loads.json, ab_index_policy.json).
-template <int UNROLL, int MODE>
+// Plain loads, loads issued one lane at a time, sc0/sc1/nt scope hints (still 128-B
+// requests) and scalar s_load_dword (64-B requests, but 0.51 vs 0.26 ms) were no faster
+// than the non-temporal vector loads kept here (profiles/r02/ab_index_loads.json,
+// ab_index_policy.json).
+template <int UNROLL>
 __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, IdxSet ix, uint32_t rows_mask,
                                                             const Seg *segs, int t, int B, int64_t stride, Geo g,
                                                             int32_t *inv, InvLayout L, uint32_t *call_status) {
@@ -1105,7 +1118,7 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, IdxSe
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
-      if (ptr[u]) rid[u] = MODE == 0 ? __builtin_nontemporal_load(ptr[u]) : *ptr[u];
+      if (ptr[u]) rid[u] = __builtin_nontemporal_load(ptr[u]);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       if (bi[u] < 0) continue;
@@ -1198,8 +1211,7 @@ static unsigned resident_blocks(K kernel, int64_t want) {
 // Run-time selectors (include/psx_debug.h): the defaults are the measured winners; the
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
-int g_index_variant = 0;   // 0: non-temporal row-id loads, 1: plain loads
-int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact), 3: v3 with plain record loads
+int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact)
 
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride, int64_t row_offset, int64_t row_stride, int64_t max_rows,
@@ -1208,12 +1220,8 @@ hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask
   // XCD-local form of the scatter (each XCD writing only its eighth of the slots) was
   // slower, 0.21 vs 0.13 ms on C2 (profiles/r02/ab_index_rows.json).
   Geo g{row_offset, row_stride, max_rows};
-  if (g_index_variant == 1)
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, 1>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B,
-                       stride, g, inv, L, call_status);
-  else
-    hipLaunchKernelGGL((dense_index_v2_kernel<8, 0>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B,
-                       stride, g, inv, L, call_status);
+  hipLaunchKernelGGL((dense_index_v2_kernel<8>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B, stride,
+                     g, inv, L, call_status);
   return hipGetLastError();
 }
 
@@ -1245,13 +1253,13 @@ static void launch_v3(const DenseArgs &a, hipStream_t st) {
 
 // BMAX is the next power of two >= B and the rows in flight per wave grow as B shrinks,
 // so every wave keeps ~8-18 16-byte loads in flight whatever the batch width.
-template <typename V, bool IMP, int H16, bool NT = true>
+template <typename V, bool IMP, int H16>
 static void launch_adaptive_v3(const DenseArgs &a, hipStream_t st) {
-  if (a.B <= 1) launch_v3<V, 1, 16, NT, 8, IMP, H16>(a, st);
-  else if (a.B <= 2) launch_v3<V, 2, 16, NT, 4, IMP, H16>(a, st);
-  else if (a.B <= 4) launch_v3<V, 4, 16, NT, 3, IMP, H16>(a, st);
-  else if (a.B <= 8) launch_v3<V, 8, 16, NT, 2, IMP, H16>(a, st);
-  else launch_v3<V, 16, 16, NT, 1, IMP, H16>(a, st);
+  if (a.B <= 1) launch_v3<V, 1, 16, true, 8, IMP, H16>(a, st);
+  else if (a.B <= 2) launch_v3<V, 2, 16, true, 4, IMP, H16>(a, st);
+  else if (a.B <= 4) launch_v3<V, 4, 16, true, 3, IMP, H16>(a, st);
+  else if (a.B <= 8) launch_v3<V, 8, 16, true, 2, IMP, H16>(a, st);
+  else launch_v3<V, 16, 16, true, 1, IMP, H16>(a, st);
 }
 
 // v2 (64-bit record pointers): streams of >= 4 GiB, which v3's 32-bit offsets cannot reach.
@@ -1308,7 +1316,6 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
   if (a.imp) launch_adaptive_imp<V, 0>(a, st);
   else if (g_apply_variant == 1 || !v3_ok(a)) launch_adaptive_v2<V, 0>(a, st);
   else if (g_apply_variant == 2 || (g_apply_variant == 0 && sparse_coverage(a))) launch_v4<V>(a, st);
-  else if (g_apply_variant == 3) launch_adaptive_v3<V, false, 0, false>(a, st);
   else launch_adaptive_v3<V, false, 0>(a, st);
   return hipGetLastError();
 }

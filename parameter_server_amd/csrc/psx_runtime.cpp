@@ -2197,14 +2197,12 @@ psx_status psx_timing_reset(psx_ctx *c) {
 // ---- kernel selectors (include/psx_debug.h) ------------------------------------
 #include "../../include/psx_debug.h"
 namespace psx {
-extern int g_index_variant;
 extern int g_apply_variant;
 extern int g_ord_split;
 }  // namespace psx
 
 static int *variant_slot(int32_t which) {
   switch (which) {
-    case PSX_VARIANT_DENSE_INDEX: return &psx::g_index_variant;
     case PSX_VARIANT_DENSE_APPLY: return &psx::g_apply_variant;
     case PSX_VARIANT_ORD_SPLIT: return &psx::g_ord_split;
     default: return nullptr;
@@ -2225,11 +2223,10 @@ extern "C" int32_t psx_debug_get_variant(int32_t which) {
 }
 
 namespace {
-// PSX_INDEX_VARIANT / PSX_APPLY_VARIANT / PSX_ORD_SPLIT override the defaults at load time
+// PSX_APPLY_VARIANT / PSX_ORD_SPLIT override the defaults at load time
 // (A/B runs of bench.py and the parity suite).
 struct VariantEnv {
   VariantEnv() {
-    if (const char *v = getenv("PSX_INDEX_VARIANT")) psx::g_index_variant = atoi(v);
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
   }

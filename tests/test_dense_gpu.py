@@ -168,15 +168,8 @@ def test_version_gap_applies_nothing():
     assert srv.GetBgVersion(100) == -1
 
 
-@pytest.mark.parametrize("index_variant", [0, 1], ids=["nt", "plain"])
-def test_device_stream_errors_reported_at_sync(index_variant):
-    from parameter_server_amd import _abi
-    L = _abi.load()
-    old = L.psx_debug_set_variant(0, index_variant)
-    try:
-        _device_stream_errors()
-    finally:
-        L.psx_debug_set_variant(0, old)
+def test_device_stream_errors_reported_at_sync():
+    _device_stream_errors()
 
 
 def _device_stream_errors():
@@ -250,19 +243,17 @@ def test_smoke_entry():
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3], ids=["auto", "v2", "v4", "v3plain"])
-@pytest.mark.parametrize("index_variant", [0, 1], ids=["nt", "plain"])
-def test_every_kernel_variant_bit_exact(apply_variant, index_variant):
+@pytest.mark.parametrize("apply_variant", [0, 1, 2], ids=["auto", "v2", "v4"])
+def test_every_kernel_variant_bit_exact(apply_variant):
     """Every dense kernel the product can launch (include/psx_debug.h: v3 default, v2 the
-    >= 4 GiB fallback, v4 the partial-coverage kernel, plain-load forms) matches the
-    oracle, including a ragged row tail (cap 301) and 8-byte values."""
+    >= 4 GiB fallback, v4 the partial-coverage kernel) matches the oracle, including a
+    ragged row tail (cap 301) and 8-byte values."""
     from parameter_server_amd import _abi
     L = _abi.load()
     old_a = L.psx_debug_set_variant(1, apply_variant)
-    old_i = L.psx_debug_set_variant(0, index_variant)
     try:
         for dt, cap, B in [(F32, 301, 9), (F64, 130, 8), (I32, 64, 3)]:
-            rng = np.random.RandomState(apply_variant * 10 + index_variant + cap)
+            rng = np.random.RandomState(apply_variant * 10 + cap)
             rows = 333
             srv, orc = _pair(dt, rows, cap)
             init = _vals(rng, (rows, cap), dt)
@@ -278,4 +269,3 @@ def test_every_kernel_variant_bit_exact(apply_variant, index_variant):
             srv.close()
     finally:
         L.psx_debug_set_variant(1, old_a)
-        L.psx_debug_set_variant(0, old_i)

@@ -2,8 +2,8 @@
 rule 24): the headline workload of bench.py, then R rounds; each round runs every
 configuration for K steps and records the per-kernel HIP-event times.  Prints JSON with
 the median ms of every kernel per configuration.
-Usage: python tools/ab_c2.py --configs 0:0,1:0,2:0 [--rounds 5 --steps 5]
-       (index_variant:apply_variant[:rows], include/psx_debug.h; rows = 1 applies through
+Usage: python tools/ab_c2.py --configs 0,0:1,2 [--rounds 5 --steps 5]
+       (apply_variant[:rows], include/psx_debug.h; rows = 1 applies through
        psx_apply_indexed_rows with the batches' record-row lists)"""
 import argparse
 import json
@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="0:0,1:0")
+    ap.add_argument("--configs", default="0,0:1")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rows", type=int, default=1 << 20)
@@ -47,19 +47,18 @@ def main():
     del table0
     ver = [0]
     kernels = ("decode_streams", "dense_index", "dense_verify", "dense_apply", "finish_call")
-    configs = [tuple(int(x) for x in (c + ":0").split(":")[:3]) for c in args.configs.split(",")]
+    configs = [tuple(int(x) for x in (c + ":0").split(":")[:2]) for c in args.configs.split(",")]
     res = {c: {k: [] for k in kernels + ("step",)} for c in configs}
 
     def run(c, steps):
-        L.psx_debug_set_variant(0, c[0])
-        L.psx_debug_set_variant(1, c[1])
+        L.psx_debug_set_variant(1, c[0])
         srv.timing(True)
         srv.timing_reset()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             msgs = [(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)]
-            if c[2]:
+            if c[1]:
                 srv.apply_indexed_rows(msgs, [r.data_ptr() for r in lists])
             else:
                 srv.apply_device(msgs)
@@ -80,7 +79,7 @@ def main():
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))
             res[c]["step"].append(step_ms)
-    out = {f"index{c[0]}_apply{c[1]}" + ("_rows" if c[2] else ""): {k: round(statistics.median(v), 4) for k, v in res[c].items()}
+    out = {f"apply{c[0]}" + ("_rows" if c[1] else ""): {k: round(statistics.median(v), 4) for k, v in res[c].items()}
            for c in configs}
     print(json.dumps(out, indent=1))
     srv.close()

@@ -240,6 +240,52 @@ def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234, with_reco
     return streams, nupd
 
 
+C3_LATENCY_JSON = os.path.join(ROOT, "profiles", "r02", "c3_inc_latency.json")
+C3_WAVES_PER_SIMD = {4: 7, 16: 2}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
+
+
+def c3_model(batches, rows, K, apply_ms):
+    """The sorted-map apply's bound ("C3 bound").  Every Inc of a row is a
+    dependent chain in one wave (FindIndex ballots over the image, then the add or the
+    LinearSearchAndMove shift), so a row costs t_r = k_r x L(n_r): k_r Incs per step at
+    image size n_r, L(n) the measured per-Inc latency of a lone wave on the kernel the row
+    takes (tools/probe_inc_latency.py -> profiles/r02/c3_inc_latency.json, "found" keys: at
+    steady state every column of a step already exists).  Rows are independent waves, w of them
+    resident per SIMD (7 for the 256-entry image, 2 for the 1,024-entry one), 1,024 SIMDs:
+        T >= max( max_r t_r ,  sum_r t_r / (w_r x 1024) )
+    (critical path vs latency-interleave throughput; optimistic: no issue contention).
+    n_r = columns with a nonzero net value over the step's batches (the image after the
+    first step, since the same batches repeat)."""
+    import numpy as np
+    if not os.path.exists(C3_LATENCY_JSON):
+        return None
+    js = json.load(open(C3_LATENCY_JSON))
+
+    def curve(name):
+        lat = js.get(name) or js["found_ns"]
+        xs = np.array(sorted(int(k) for k in lat), dtype=np.float64)
+        return xs, np.array([lat[str(int(x))] for x in xs], dtype=np.float64)
+    r = np.concatenate([np.full(len(c), rid, np.int64) for recs in batches for rid, c, _ in recs])
+    c = np.concatenate([c for recs in batches for _, c, _ in recs]).astype(np.int64)
+    v = np.concatenate([v for recs in batches for _, _, v in recs]).astype(np.int64)
+    k_r = np.bincount(r, minlength=rows).astype(np.float64)
+    uniq, inv = np.unique(r * K + c, return_inverse=True)
+    net = np.bincount(inv, weights=v)
+    n_r = np.bincount(uniq[net != 0] // K, minlength=rows).astype(np.float64)
+    big = n_r + k_r > 256                                          # the 1,024-entry launch
+    x16, y16 = curve("found_ns")                                   # 1,024-entry image
+    x4, y4 = curve("found_small_ns")                               # 256-entry image
+    t_r = k_r * np.where(big, np.interp(n_r, x16, y16), np.interp(n_r, x4, y4)) * 1e-6   # ms
+    chain = float(t_r.max())
+    tput = float((t_r[~big].sum() / C3_WAVES_PER_SIMD[4] + t_r[big].sum() / C3_WAVES_PER_SIMD[16]) / 1024)
+    bound = max(chain, tput)
+    return {"bound_ms": round(bound, 4), "critical_path_ms": round(chain, 4), "interleave_ms": round(tput, 4),
+            "ordered_apply_ms": round(apply_ms, 4), "frac_of_bound": round(bound / apply_ms, 3) if apply_ms else None,
+            "rows_touched": int((k_r > 0).sum()), "rows_1024_image": int(big.sum()),
+            "max_incs_per_row": int(k_r.max()), "max_image": int(n_r.max()),
+            "latency_source": os.path.relpath(C3_LATENCY_JSON, ROOT)}
+
+
 def c3_cpu_baseline(args, batches, nupd, bgs):
     """The oracle on the same C3 batches as T server threads: rows sharded row % T (the
     reference's comm-channel placement, context.hpp:291-304), each thread applying its
@@ -314,7 +360,8 @@ def run_c3(args):
     for _ in range(args.warmup):
         step()
     srv.sync()
-    srv.timing(True)
+    # timed region: events only around the apply launches (timing mode 2)
+    srv.timing(2)
     srv.timing_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -323,8 +370,17 @@ def run_c3(args):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     srv.sync()
-    kern = {k: srv.timing_read(k) for k in ("decode_streams", "ordered_apply", "finish_call")}
+    apply_ms, apply_n = srv.timing_read("ordered_apply")
+    # per-kernel breakdown: a separate pass with events around every kernel
+    srv.timing(1)
+    srv.timing_reset()
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+    srv.sync()
+    kern = {k: srv.timing_read(k) for k in ("decode_streams", "ordered_prep", "ordered_apply", "finish_call")}
+    srv.timing(False)
     stream_bytes = sum(s.size for s in streams)
+    model = c3_model(batches, rows, K, apply_ms / max(apply_n, 1))
     cpu = c3_cpu_baseline(args, batches, nupd, bgs) if args.cpu_seconds > 0 else None
     print(json.dumps({
         "metric": "sparse int row-update apply (SortedVectorMapRow<int32>), C3",
@@ -336,7 +392,9 @@ def run_c3(args):
         "config": {"workload": f"C3: {rows} rows x K={K}, {B} batches x 10000 rows/step"
                                + (", producer record index (psx_apply_indexed)" if args.indexed else ""),
                    "updates_per_step": nupd, "stream_bytes_per_step": stream_bytes},
-        "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
+        "ordered_apply_ms_per_step": round(apply_ms / max(apply_n, 1), 4),
+        "kernel_ms_per_step_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
+        "latency_model": model,
         "cpu_baseline": cpu}), flush=True)
     srv.close()
 

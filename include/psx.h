@@ -16,13 +16,19 @@
  *                                                        src/petuum_ps/server/server.hpp:46-48,
  *                                                        src/petuum_ps/server/server.cpp:120-179
  *   psx_apply_streams_device  the same, for K device-resident messages applied in order
+ *   psx_apply_indexed       the same with producer record offsets: replaces
+ *                           SerializedOpLogReader::Next's size chain
+ *                                                        src/petuum_ps/server/serialized_oplog_reader.hpp:57-84
+ *   psx_apply_indexed_rows  the same with producer record-row lists: dense records placed
+ *                           without reading their row ids from the stream (checked in the apply)
+ *   psx_ctx_set_pipeline    (new) overlap a call's index stage with the previous call's apply
  *   psx_table_load_rows     AbstractRow::ResetRowData    src/petuum_ps_common/storage/numeric_store_row.hpp:142-145
  *   psx_table_read_rows     VectorStore::CopyToMem       src/petuum_ps_common/storage/vector_store.hpp:115-118
  *   psx_serialize_rows      ServerRow::Serialize         src/petuum_ps/server/server_row.hpp:65-71
  *   psx_serialize_dirty     Server::CreateSendServerPushRowMsgs  src/petuum_ps/server/server.cpp:189-309
  *   psx_row_flags           ServerRow::IsDirty / FindRow src/petuum_ps/server/server_row.hpp:90-96,
  *                                                        src/petuum_ps/server/server_table.cpp:136-141
- *   psx_pack_stream         CreateOpLogMsgs + OpLogSerializer + RowOpLogSerializer (client pack)
+ *   psx_pack_stream(_indexed) CreateOpLogMsgs + OpLogSerializer + RowOpLogSerializer (client pack)
  *                                                        src/petuum_ps/thread/abstract_bg_worker.cpp:590-649,
  *                                                        src/petuum_ps/client/oplog_serializer.hpp:12-37,
  *                                                        src/petuum_ps/thread/row_oplog_serializer.hpp:139-166,
@@ -68,7 +74,9 @@
  * Here every call returns a psx_status instead; a failed call applies nothing: every
  * check of an apply call (framing, tables, row range, columns, the sorted/map capacity
  * dry run, AdaRevision snapshots, duplicate rows) runs on the device before any table is
- * touched.  Errors discovered by device kernels are reported by the next psx_sync() —
+ * touched.  The one stated exception is a producer record-row list that disagrees with
+ * its stream (psx_apply_indexed_rows): that is found inside the apply, so only the rows
+ * concerned are left unchanged.  Errors discovered by device kernels are reported by the next psx_sync() —
  * or by the next call that reads or serves rows, which first settles the calls in
  * flight (so it sees every accepted message, as the reference server thread does).
  *

@@ -527,6 +527,21 @@ __device__ __forceinline__ T bcast(T x, int src) {
   }
 }
 
+// Found-key update of a striped image: entry (jj, l) += d, returning its new value.  jj
+// is wave-uniform, so a binary search over the J registers costs log2(J) uniform branches
+// instead of J guarded blocks.
+template <int LO, int HI, int J, typename V>
+__device__ __forceinline__ V add_at(V (&val)[J], int jj, int l, int lane, V d) {
+  if constexpr (HI - LO == 1) {
+    if (lane == l) val[LO] = OV<V>::add(val[LO], d);
+    return bcast(val[LO], l);
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (jj < MID) return add_at<LO, MID, J, V>(val, jj, l, lane, d);
+    return add_at<MID, HI, J, V>(val, jj, l, lane, d);
+  }
+}
+
 // Split tables run two launches of this kernel concurrently, over the touched rows
 // ordered_classify put in the 256- and the 1,024-entry list (a.touched / a.ntouched point
 // at one list each).
@@ -535,11 +550,17 @@ template <typename V, int KIND, int J, bool DRY = false>
 __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
   __shared__ int32_t sort_scratch[4][64];
+  // Key -> entry-index map of the wave's row (FindIndex in one LDS read instead of J
+  // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
+  // per row at load): int16 per key, -1 = absent.
+  __shared__ int16_t s_pos[4][1024];   // the register kernels serve max_entries <= 1,024
   if (threadIdx.x == 0) build_space(a, rs);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const bool go = o_gate(a) && (!DRY || *a.keyflag);
+  const bool pos_ok = a.keyflag && !*a.keyflag && a.max_entries <= 1024;
+  int16_t *pos = s_pos[wib];
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + wib;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
@@ -591,6 +612,22 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         const int32_t i = j * 64 + lane;
         key[j] = i < n ? o_ld32(row + (int64_t)i * ES) : 0;
         val[j] = i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
+      }
+      bool use_pos = pos_ok;
+      if (use_pos) {
+        bool out = false;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          out = out || (j * 64 + lane < n && (key[j] < 0 || key[j] >= (int32_t)a.max_entries));
+        use_pos = __ballot(out) == 0;
+      }
+      if (use_pos) {
+        for (int32_t k = lane; k < (int32_t)a.max_entries; k += 64) pos[k] = -1;
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (j * 64 + lane < n) pos[key[j]] = (int16_t)(j * 64 + lane);
+        wave_sync();
       }
       double impt = a.imp ? a.imp[slot] : 0.0;
       bool over = false;   // DRY: this row would exceed max_entries
@@ -648,16 +685,29 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
           const int32_t my_col = c0 == 0 ? col0 : (pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0);
           const V my_d = c0 == 0 ? d0 : (pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0));
           const int32_t cnt = nn - c0 < 64 ? nn - c0 : 64;
+          // With the key map, lane t looks up its own column once for the whole chunk
+          // (a record's columns are distinct, so an Inc moves no other key except by an
+          // insert/remove shift, after which the chunk's lookups are re-read).
+          int32_t my_idx = -1;
+          bool stale = true;
           for (int32_t t = 0; t < cnt && !over; ++t) {
             const int32_t c = __builtin_amdgcn_readlane(my_col, t);
             const V d = bcast(my_d, t);
             if (d == V(0)) continue;                                  // :306
             int32_t idx = -1;                                         // FindIndex :230-238
+            if (use_pos) {
+              if (stale) {
+                my_idx = lane < cnt ? (int32_t)pos[my_col] : -1;
+                stale = false;
+              }
+              idx = __builtin_amdgcn_readlane(my_idx, t);
+            } else {
 #pragma unroll
-            for (int j = 0; j < J; ++j) {
-              if (j * 64 < n && idx < 0) {
-                const uint64_t bal = __ballot(j * 64 + lane < n && key[j] == c);
-                if (bal) idx = j * 64 + __builtin_ctzll(bal);
+              for (int j = 0; j < J; ++j) {
+                if (j * 64 < n && idx < 0) {
+                  const uint64_t bal = __ballot(j * 64 + lane < n && key[j] == c);
+                  if (bal) idx = j * 64 + __builtin_ctzll(bal);
+                }
               }
             }
             if (idx < 0) {
@@ -708,14 +758,19 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
                   val[j] = d;
                 }
               ++n;
+              if (use_pos) {   // entries [p, n) moved or arrived: their new indices
+                stale = true;
+                wave_sync();
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                  const int32_t i = j * 64 + lane;
+                  if (i >= p && i < n) pos[key[j]] = (int16_t)i;
+                }
+                wave_sync();
+              }
             } else {
               // found: add in place (:325-327), remove on zero (:329-334)
-              V nv = V(0);
-#pragma unroll
-              for (int j = 0; j < J; ++j) {
-                if (j * 64 + lane == idx) val[j] = OV<V>::add(val[j], d);
-                if (j == (idx >> 6)) nv = bcast(val[j], idx & 63);
-              }
+              const V nv = add_at<0, J>(val, idx >> 6, idx & 63, lane, d);
               if (nv == V(0)) {
                 if (KIND == 1) {
                   // entries (idx, n) move to i - 1: ascending j, rotate left by one lane
@@ -740,6 +795,18 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
                       }
                     }
                   }
+                  if (use_pos) {   // c leaves; entries (idx, n) moved down one
+                    stale = true;
+                    wave_sync();
+                    if (lane == 0) pos[c] = -1;
+                    wave_sync();
+#pragma unroll
+                    for (int j = 0; j < J; ++j) {
+                      const int32_t i = j * 64 + lane;
+                      if (i >= idx && i < n - 1) pos[key[j]] = (int16_t)i;
+                    }
+                    wave_sync();
+                  }
                 } else {
                   // MapStore erase; unordered: the last entry fills the hole
                   int32_t lk = 0;
@@ -756,6 +823,15 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
                       key[j] = lk;
                       val[j] = lv;
                     }
+                  if (use_pos) {   // c leaves; the last entry takes its index
+                    stale = true;
+                    wave_sync();
+                    if (lane == 0) {
+                      pos[c] = -1;
+                      if (idx != n - 1) pos[lk] = (int16_t)idx;
+                    }
+                    wave_sync();
+                  }
                 }
                 --n;
               }

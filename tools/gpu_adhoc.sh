@@ -1,9 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/s23; mkdir -p $O; export TMPDIR=/tmp
-echo "== rows tests"
-timeout -k 10 600 python -u -m pytest tests/test_indexed_rows_gpu.py tests/test_dense_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
-echo "== A/B"; timeout -k 10 300 python -u tools/ab_c2.py --configs 0,0:1 --rounds 7 --steps 5 > $O/ab.json 2>&1 || { tail -20 $O/ab.json; exit 1; }
-cat $O/ab.json
-TAG=s23 bash tools/gpu_run.sh pmc bench
+O=gpurun_out/s29; mkdir -p $O; export TMPDIR=/tmp
+echo "== probe"; timeout -k 10 300 python -u tools/probe_inc_latency.py --out $O/c3_inc_latency.json > $O/probe.log 2>&1 || { tail -20 $O/probe.log; exit 1; }
+grep ns/Inc $O/probe.log | tr '\n' ' '; echo
+cp $O/c3_inc_latency.json profiles/r02/c3_inc_latency.json
+TAG=s29 bash tools/gpu_run.sh c3 c3idx stats3

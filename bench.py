@@ -241,7 +241,7 @@ def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234, with_reco
 
 
 C3_LATENCY_JSON = os.path.join(ROOT, "profiles", "r02", "c3_inc_latency.json")
-C3_WAVES_PER_SIMD = {4: 7, 16: 2}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
+C3_WAVES_PER_SIMD = {4: 7, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
 
 
 def c3_model(batches, rows, K, apply_ms):
@@ -251,7 +251,7 @@ def c3_model(batches, rows, K, apply_ms):
     image size n_r, L(n) the measured per-Inc latency of a lone wave on the kernel the row
     takes (tools/probe_inc_latency.py -> profiles/r02/c3_inc_latency.json, "found" keys: at
     steady state every column of a step already exists).  Rows are independent waves, w of them
-    resident per SIMD (7 for the 256-entry image, 2 for the 1,024-entry one), 1,024 SIMDs:
+    resident per SIMD (7 for the 256-entry image, 3 for the 1,024-entry one), 1,024 SIMDs:
         T >= max( max_r t_r ,  sum_r t_r / (w_r x 1024) )
     (critical path vs latency-interleave throughput; optimistic: no issue contention).
     n_r = columns with a nonzero net value over the step's batches (the image after the
@@ -532,14 +532,17 @@ def run_pcie(args, srv, streams, rows, cap, bgs, ver):
 
 
 def run_c5(args):
-    """mixed dense + sparse tables, continuous stream with clocks.
-    Every clock, 8 workers each send one message carrying both tables (a C2-like dense
-    f32 table, 2^18 x 256, half the rows per worker; a C3-like SortedVectorMapRow<int32>
-    table, 100K x 1024, 1250 Zipf rows per worker); the server applies the 8 messages
-    (one fused call) and, as the min clock advances, serves every dirty row back to host
-    memory (Server::CreateSendServerPushRowMsgs, server.cpp:189-309).  SSP staleness 4
-    lets workers run ahead on the client side; the server sees the same continuous
-    stream.  Reports clocks/s and the apply + serve-back rate in algorithmic GB/s."""
+    """mixed dense + sparse tables, a continuous stream with clocks under
+    SSPPush.  8 workers (= 8 clients) each send one message per clock carrying both tables
+    (a C2-like dense f32 table, 2^18 x 256, half the rows per worker; a C3-like
+    SortedVectorMapRow<int32> table, 100K x 1024, 1250 Zipf rows per worker); each client
+    subscribed to the rows of its messages (its row requests, server_thread.cpp:185-200).
+    Per clock the server applies the 8 messages (one fused call), advances every sender's
+    clock (Server::ClockUntil, server.cpp:62-79) and, when the min clock moves
+    (server_thread.cpp:262-288), builds one push body per client from its subscriptions
+    (CreateSendServerPushRowMsgs, server.cpp:189-309) into host memory.  Staleness 4 is the
+    client's Get gate (ssp_push_consistency_controller.cpp:70-88): workers may run up to 4
+    clocks ahead, and the server sees the same stream.  Reports clocks/s and the split."""
     import numpy as np
     import torch
     import parameter_server_amd as psa
@@ -548,7 +551,7 @@ def run_c5(args):
     rng = np.random.RandomState(77)
     p = 1.0 / np.arange(1, rows_s + 1)
     p /= p.sum()
-    msgs = []
+    msgs, subs = [], []
     for b in range(B):
         ids_d = rng.permutation(rows_d)[: rows_d // 2].astype(np.int32)
         upd = rng.normal(0, 0.01, size=(ids_d.size, cap)).astype(np.float32)
@@ -560,6 +563,7 @@ def run_c5(args):
         msgs.append(wire.pack_np([
             dict(table_id=1, dense_serialized=True, row_ids=ids_d, oplogs=upd),
             dict(table_id=3, dense_serialized=False, row_ids=ids_s, oplogs=cnt)]))
+        subs.append((ids_d, ids_s))
     dev = [torch.from_numpy(m).cuda() for m in msgs]
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(0, 1, bgs)
@@ -567,22 +571,33 @@ def run_c5(args):
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows_d))
     srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
                                      oplog_dense_serialized=False, max_rows=rows_s, max_entries=K))
+    srv.set_num_clients(B)
+    for b, (ids_d, ids_s) in enumerate(subs):
+        srv.subscribe(1, ids_d, b)
+        srv.subscribe(3, ids_s, b)
     ver = [0]
-    served = [0]
-    t_apply = [0.0]
+    pushed, pushes = [0], [0]
+    t_apply, t_clock = [0.0], [0.0]
 
     def clock():
         t = time.perf_counter()
         srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
         srv.sync()
-        t_apply[0] += time.perf_counter() - t
+        t2 = time.perf_counter()
+        t_apply[0] += t2 - t
+        changed = 0
+        for bg in bgs:                       # each worker's clock message (is_clock, bg_clock)
+            changed = srv.ClockUntil(bg, ver[0] + 1) or changed
+        if changed:                          # the min clock moved: one push body per client
+            pushed[0] += sum(x.size for x in srv.serialize_push(clear=True, as_bytes=False))
+            pushes[0] += 1
+        t_clock[0] += time.perf_counter() - t2
         ver[0] += 1
-        served[0] += len(srv.serialize_dirty(clear=True))
 
     for _ in range(args.warmup):
         clock()
-    served[0] = 0
-    t_apply[0] = 0.0
+    pushed[0] = pushes[0] = 0
+    t_apply[0] = t_clock[0] = 0.0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -590,18 +605,19 @@ def run_c5(args):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     msg_bytes = sum(m.size for m in msgs)
-    dirty_dense = rows_d                     # 8 half-coverage batches touch ~all rows
-    step_bytes = msg_bytes + 2 * dirty_dense * cap * 4 + served[0] / args.steps
+    step_bytes = msg_bytes + 2 * rows_d * cap * 4 + pushed[0] / args.steps
     print(json.dumps({
-        "metric": "C5 mixed dense+sparse clock (apply + serve-back to host)",
+        "metric": "C5 mixed dense+sparse clock under SSPPush (apply + ClockUntil + per-client push to host)",
         "value": round(args.steps / el, 2), "unit": "clocks/s",
         "GBps_algorithmic": round(step_bytes * args.steps / el / 1e9, 2),
         "ms_per_clock": round(el / args.steps * 1e3, 3),
         "apply_ms_per_clock": round(t_apply[0] / args.steps * 1e3, 3),
-        "serve_ms_per_clock": round((el - t_apply[0]) / args.steps * 1e3, 3),
-        "served_bytes_per_clock": int(served[0] / args.steps), "message_bytes_per_clock": msg_bytes,
+        "clock_and_push_ms_per_clock": round(t_clock[0] / args.steps * 1e3, 3),
+        "pushes": pushes[0], "pushed_bytes_per_clock": int(pushed[0] / args.steps),
+        "message_bytes_per_clock": msg_bytes,
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "dtype": "f32+int32",
-        "data": "synthetic", "config": {"workload": "C5: dense 2^18x256 f32 + sorted-map 100Kx1024 int32, 8 msgs/clock"},
+        "data": "synthetic", "config": {"workload": "C5: dense 2^18x256 f32 + sorted-map 100Kx1024 int32, "
+                                                    "8 clients x 1 msg/clock, SSPPush, staleness 4 (client gate)"},
     }), flush=True)
     srv.close()
 

@@ -529,7 +529,9 @@ __device__ __forceinline__ T bcast(T x, int src) {
 
 // Found-key update of a striped image: entry (jj, l) += d, returning its new value.  jj
 // is wave-uniform, so a binary search over the J registers costs log2(J) uniform branches
-// instead of J guarded blocks.
+// instead of J guarded blocks.  (A branch-free form — one compare of every register's
+// entry index against idx — was slower: 420 vs 380 ns per Inc on the 1,024-entry image,
+// C3 apply 0.248 vs 0.230 ms.)
 template <int LO, int HI, int J, typename V>
 __device__ __forceinline__ V add_at(V (&val)[J], int jj, int l, int lane, V d) {
   if constexpr (HI - LO == 1) {

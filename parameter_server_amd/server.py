@@ -305,21 +305,33 @@ class Server:
                                                                    ctypes.c_void_p(out.ctypes.data)))
         return out
 
-    def serialize_push(self, clear=True):
+    def serialize_push(self, clear=True, as_bytes=True):
         """Server::CreateSendServerPushRowMsgs with subscriptions (server.cpp:189-309): a list
-        of num_clients push bodies (bytes), one per client."""
+        of num_clients push bodies, one per client.  The bodies land in page-locked host
+        buffers kept by this object; as_bytes=False returns numpy views of them (valid
+        until the next call) instead of bytes copies."""
         C = getattr(self, "num_clients", 1)
         caps = (ctypes.c_size_t * C)()
         used = (ctypes.c_size_t * C)()
         st = self._L.psx_serialize_push(self._ctx, None, caps, used, 0, 0)
         if st not in (_abi.PSX_OK, 9):
             _check(self._L, self._ctx, st)
-        bufs = [np.zeros(max(used[k], 1), np.uint8) for k in range(C)]
+        pinned = getattr(self, "_push_pinned", None)
+        if pinned is None or len(pinned) != C:
+            pinned = self._push_pinned = [None] * C
+        import torch
+        for k in range(C):
+            need = max(used[k], 1)
+            if pinned[k] is None or pinned[k].numel() < need:
+                pinned[k] = torch.empty(need + need // 4, dtype=torch.uint8, pin_memory=True)
+        bufs = [t.numpy() for t in pinned]
         ptrs = (ctypes.c_void_p * C)(*[b.ctypes.data for b in bufs])
         for k in range(C):
             caps[k] = bufs[k].size
         _check(self._L, self._ctx, self._L.psx_serialize_push(self._ctx, ptrs, caps, used, 0, 1 if clear else 0))
-        return [bufs[k][:used[k]].tobytes() for k in range(C)]
+        if as_bytes:
+            return [bufs[k][:used[k]].tobytes() for k in range(C)]
+        return [bufs[k][:used[k]] for k in range(C)]
 
     # -- client side of serve-back ------------------------------------------------------
     def apply_push_body(self, body, insert_missing=False, device_ptr=None, size=None):

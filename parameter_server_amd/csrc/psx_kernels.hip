@@ -1325,6 +1325,9 @@ static hipError_t launch_dense_apply_t(const DenseArgs &a, hipStream_t st) {
 bool dense_apply_checks_rows(const DenseArgs &a, bool rec_f16) {
   if (a.imp || g_apply_variant == 1 || !v3_ok(a)) return false;
   if (rec_f16) return true;
+  // v4 (partial coverage) does not check lists: a form that did (lane j checking slot-list
+  // entry j before the group's payload loads) made its apply 40% slower on the 12.5%-density
+  // C2 variant, 0.907 vs 0.65 ms (profiles/r02/ab_v4_rows.json)
   return !(g_apply_variant == 2 || (g_apply_variant == 0 && sparse_coverage(a)));
 }
 

@@ -20,6 +20,11 @@ value = bytes of all ranks / max-over-ranks wall time.  Multi-GPU: each rank own
 client splits oplogs by owning server (abstract_bg_worker.cpp:590-649): no collective,
 weak scaling.
 
+After the timed region the bare run (no variant flags) also records the PCIe-inclusive
+rate and C3 walked/indexed (N = 1), or the exchange-bearing step (N > 1: each rank's batch
+spans every shard, one RCCL all-to-all over xGMI, then the owners' fused applies) —
+`--no-extras` leaves them out.
+
 cpu_baseline: the CPU oracle (restated Server::ApplyOpLogUpdateVersion loop, one
 thread = one reference server thread) on a bounded sample of the same workload.
 """
@@ -93,6 +98,9 @@ def parse():
     p.add_argument("--pcie", action="store_true",
                    help="also time the host-buffer form: pinned H2D of the 8 messages + apply + D2H of "
                         "every (dirty) row, i.e. the rate including PCIe (reported, never `value`)")
+    p.add_argument("--no-extras", dest="extras", action="store_false",
+                   help="plain C2 line only: no PCIe-inclusive pass, no C3 (N = 1), no exchange step (N > 1) "
+                        "after the timed region (profiler passes)")
     p.add_argument("--master-port", type=int, default=29531,
                    help="rendezvous port when bench.py launches its own ranks (--gpus N, WORLD_SIZE unset)")
     p.add_argument("--selftest-launch", action="store_true",
@@ -214,12 +222,19 @@ def cpu_baseline(args):
                       f"server.cpp:120-179)"}
 
 
+_C3_CACHE = {}
+
+
 def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234, with_records=False):
     """SortedVectorMapRow<int32> rows, K columns; B batches of per_batch
     distinct Zipf(s=1) rows, nnz uniform [1, 32], ascending unique columns, values
     +-{1..3} (first batch positive)."""
     import numpy as np
     from parameter_server_amd import wire
+    key = (rows, K, B, per_batch, seed)
+    if key in _C3_CACHE:        # the default run measures walked and indexed on the same batches
+        streams, nupd, batches = _C3_CACHE[key]
+        return (streams, nupd, batches) if with_records else (streams, nupd)
     rng = np.random.RandomState(seed)
     p = 1.0 / np.arange(1, rows + 1)
     p /= p.sum()
@@ -235,6 +250,7 @@ def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234, with_reco
         nupd += int(ks.sum())
         streams.append(wire.sparse_stream_np(3, 4, recs))
         batches.append(recs)
+    _C3_CACHE[key] = (streams, nupd, batches)
     if with_records:
         return streams, nupd, batches
     return streams, nupd
@@ -286,7 +302,7 @@ def c3_model(batches, rows, K, apply_ms):
             "latency_source": os.path.relpath(C3_LATENCY_JSON, ROOT)}
 
 
-def c3_cpu_baseline(args, batches, nupd, bgs):
+def c3_cpu_baseline(args, batches, nupd, bgs, seconds):
     """The oracle on the same C3 batches as T server threads: rows sharded row % T (the
     reference's comm-channel placement, context.hpp:291-304), each thread applying its
     shard's sub-messages in batch order (the client splits per server,
@@ -322,16 +338,17 @@ def c3_cpu_baseline(args, batches, nupd, bgs):
             o.close()
         return nupd * n / el / 1e6, n, el
 
-    v1, n1, e1 = timed_run(1, args.cpu_seconds / 3)
-    vt, nt, et = timed_run(T, args.cpu_seconds * 2 / 3) if T > 1 else (v1, n1, e1)
+    v1, n1, e1 = timed_run(1, seconds / 3)
+    vt, nt, et = timed_run(T, seconds * 2 / 3) if T > 1 else (v1, n1, e1)
     return {"value": round(vt, 3), "unit": "M updates/s", "cores": T, "kind": "port",
             "single_thread": round(v1, 3),
             "sample": f"the same {len(batches)} batches; {T} threads (rows % {T} shards): {nt} steps in {et:.1f} s; "
                       f"1 thread: {n1} steps in {e1:.1f} s (oracle restatement of sorted_vector_map_store.hpp Inc)"}
 
 
-def run_c3(args):
-    """Sparse int count rows (C3): reports updates/s (and stream GB/s) on 1 GPU."""
+def c3_measure(args, indexed, steps, warmup, cpu_seconds):
+    """Sparse int count rows (C3) on 1 GPU: updates/s (and stream GB/s), the ordered apply
+    against its latency model, and (cpu_seconds > 0) the CPU port on the same batches."""
     import numpy as np
     import torch
     import parameter_server_amd as psa
@@ -345,7 +362,7 @@ def run_c3(args):
                                      oplog_dense_serialized=False, max_rows=rows, max_entries=K))
     ver = [0]
     idx = None
-    if args.indexed:   # the producer's record index (psx_pack_stream emits the same), built before timing
+    if indexed:   # the producer's record index (psx_pack_stream emits the same), built before timing
         from parameter_server_amd import wire as _w
         idx = [torch.from_numpy(_w.stream_record_offsets(s, {3: None}).view(np.int64)).cuda() for s in streams]
 
@@ -357,7 +374,7 @@ def run_c3(args):
             srv.apply_device(msgs)
         ver[0] += 1
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     srv.sync()
     # timed region: events only around the apply launches (timing mode 2)
@@ -365,7 +382,7 @@ def run_c3(args):
     srv.timing_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -374,51 +391,50 @@ def run_c3(args):
     # per-kernel breakdown: a separate pass with events around every kernel
     srv.timing(1)
     srv.timing_reset()
-    for _ in range(max(3, min(args.steps, 10))):
+    for _ in range(max(3, min(steps, 10))):
         step()
     srv.sync()
     kern = {k: srv.timing_read(k) for k in ("decode_streams", "ordered_prep", "ordered_apply", "finish_call")}
     srv.timing(False)
+    srv.close()
     stream_bytes = sum(s.size for s in streams)
     model = c3_model(batches, rows, K, apply_ms / max(apply_n, 1))
-    cpu = c3_cpu_baseline(args, batches, nupd, bgs) if args.cpu_seconds > 0 else None
-    print(json.dumps({
+    cpu = c3_cpu_baseline(args, batches, nupd, bgs, cpu_seconds) if cpu_seconds > 0 else None
+    return {
         "metric": "sparse int row-update apply (SortedVectorMapRow<int32>), C3",
-        "value": round(nupd * args.steps / el / 1e6, 3), "unit": "M updates/s",
-        "stream_GBps": round(stream_bytes * args.steps / el / 1e9, 3),
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+        "value": round(nupd * steps / el / 1e6, 3), "unit": "M updates/s",
+        "stream_GBps": round(stream_bytes * steps / el / 1e9, 3),
+        "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(el / steps * 1e3, 4), "higher_is_better": True,
         "dtype": "int32", "data": "synthetic (Zipf rows, uniform nnz 1..32, values +-1..3)",
         "config": {"workload": f"C3: {rows} rows x K={K}, {B} batches x 10000 rows/step"
-                               + (", producer record index (psx_apply_indexed)" if args.indexed else ""),
+                               + (", producer record index (psx_apply_indexed)" if indexed else ""),
                    "updates_per_step": nupd, "stream_bytes_per_step": stream_bytes},
         "ordered_apply_ms_per_step": round(apply_ms / max(apply_n, 1), 4),
         "kernel_ms_per_step_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
         "latency_model": model,
-        "cpu_baseline": cpu}), flush=True)
-    srv.close()
+        "cpu_baseline": cpu}
 
 
-def run_c4(args):
-    """SURVEY §8(d) C4: a dense f32 gradient table of c4_rows x 1024, row-range sharded
-    over the ranks.  Per step every rank (one worker) holds a full-coverage batch, packed
-    per owner shard (rows in random order) as the reference client does; one all-to-all
-    (RCCL over xGMI) delivers each owner its world_size messages, which one fused,
-    order-preserving apply adds to the shard (bit-exact vs sequential application)."""
+def run_c3(args):
+    print(json.dumps(c3_measure(args, args.indexed, args.steps, args.warmup, args.cpu_seconds)), flush=True)
+
+
+def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242):
+    """The exchange-bearing step (SURVEY §8(d) C4 shape): a dense f32 table of rows_total x
+    cap, row-range sharded over the ranks.  Per step every rank (one worker) holds a
+    full-coverage batch, packed per owner shard (rows in random order) as the reference
+    client does (abstract_bg_worker.cpp:590-649); one all-to-all (RCCL over xGMI) delivers
+    each owner its world_size messages, which one fused, order-preserving apply adds to the
+    shard (bit-exact vs sequential application).  The process group is already up.
+    Returns the measurement (max over ranks) as a dict."""
     import torch
     import torch.distributed as dist
     import parameter_server_amd as psa
     from parameter_server_amd import wire
     from parameter_server_amd.exchange import alltoall_streams, split
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    cap = 1024
-    shard = args.c4_rows // world
-    g = torch.Generator(device="cuda").manual_seed(4242 + rank)
+    shard = rows_total // world
+    g = torch.Generator(device="cuda").manual_seed(seed + rank)
     parts = []
     for owner in range(world):
         perm = torch.randperm(shard, device="cuda", generator=g).to(torch.int32) + owner * shard
@@ -450,7 +466,7 @@ def run_c4(args):
         srv.sync()
         ver[0] += 1
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     t_x[0] = 0.0
     srv.timing(True)
@@ -459,40 +475,60 @@ def run_c4(args):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
     apply_ms, apply_n = srv.timing_read("dense_apply")
     idx_ms, _ = srv.timing_read("dense_index")
+    srv.close()
+    del send
+    torch.cuda.empty_cache()
     if world > 1:
         t = torch.tensor([el, t_x[0]], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, t_x[0] = (float(x) for x in t.tolist())
     per_rank_stream = sum(sizes)
     apply_bytes = per_rank_stream + 2 * shard * cap * 4    # per owner per step (same totals)
+    sent = per_rank_stream * (world - 1) / world
+    return {
+        "value": round(apply_bytes * world * steps / el / 1e9, 2), "unit": "GB/s (algorithmic, all ranks)",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(el / steps * 1e3, 3),
+        "exchange_ms_per_step": round(t_x[0] / steps * 1e3, 3),
+        # nccl-tests all-to-all convention: algbw = bytes per rank / time, busbw =
+        # algbw * (n-1)/n (the bytes that actually cross xGMI per rank)
+        "exchange_algbw_GBps": round(per_rank_stream * steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
+        "exchange_busbw_GBps": round(sent * steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
+        "apply_kernel_ms": round(apply_ms / max(apply_n, 1), 3),
+        "index_kernel_ms": round(idx_ms / max(apply_n, 1), 3),
+        "config": {"workload": f"{rows_total} rows x {cap} f32, row-range shards x{world}",
+                   "shard_rows": shard, "stream_bytes_per_rank": per_rank_stream,
+                   "parallelism": f"{world} shards, RCCL all-to-all of per-owner messages"},
+    }
+
+
+def run_c4(args):
+    """SURVEY §8(d) C4: a dense f32 gradient table of c4_rows x 1024, row-range sharded
+    over the ranks, one all-to-all exchange per step (exchange_measure)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    m = exchange_measure(args.c4_rows, 1024, args.steps, args.warmup, world, rank, local)
     if rank == 0:
-        sent = per_rank_stream * (world - 1) / world
-        print(json.dumps({
-            "metric": "C4 dense gradient apply with all-to-all exchange",
-            "value": round(apply_bytes * world * args.steps / el / 1e9, 2), "unit": "GB/s (algorithmic, all ranks)",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3),
-            "exchange_ms_per_step": round(t_x[0] / args.steps * 1e3, 3),
-            # nccl-tests all-to-all convention: algbw = bytes per rank / time, busbw =
-            # algbw * (n-1)/n (the bytes that actually cross xGMI per rank)
-            "exchange_algbw_GBps": round(per_rank_stream * args.steps / t_x[0] / 1e9, 2)
-            if world > 1 and t_x[0] > 0 else None,
-            "exchange_busbw_GBps": round(sent * args.steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
-            "apply_kernel_ms": round(apply_ms / max(apply_n, 1), 3),
-            "index_kernel_ms": round(idx_ms / max(apply_n, 1), 3),
-            "higher_is_better": True, "scaling": "strong", "dtype": "f32",
-            "data": "synthetic (GPU-generated N(0,0.01) gradients, full coverage, random row order)",
-            "config": {"workload": f"C4: {args.c4_rows} rows x {cap} f32, row-range shards x{world}",
-                       "shard_rows": shard, "stream_bytes_per_rank": per_rank_stream,
-                       "parallelism": f"{world} shards, RCCL all-to-all of per-owner messages"},
-        }), flush=True)
-    srv.close()
+        m["config"]["workload"] = "C4: " + m["config"]["workload"]
+        line = {"metric": "C4 dense gradient apply with all-to-all exchange"}
+        line.update(m)
+        line.update({"higher_is_better": True, "scaling": "strong", "dtype": "f32",
+                     "data": "synthetic (GPU-generated N(0,0.01) gradients, full coverage, random row order)"})
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -789,7 +825,35 @@ def main():
     elif c2_dims:
         traffic_note = "no PMC JSON for this tree"
 
-    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie else None
+    # The driver runs the bare `python bench.py [--gpus N]`: on the plain C2 configuration
+    # the same run also records, beside `value`, the PCIe-inclusive rate and C3 (N = 1), or
+    # the exchange-bearing step over xGMI (N > 1).  None of it is inside the timed region.
+    extras = args.extras and c2_dims and not args.adarevision and not args.walked
+    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie or (extras and world == 1) else None
+    srv.close()
+    del streams, record_rows
+    torch.cuda.empty_cache()
+    other, exchange = None, None
+    if extras and world > 1:
+        try:
+            exchange = exchange_measure(world * rows, cap, min(args.steps, 10), 2, world, rank, local)
+            exchange["what"] = ("a worker batch spanning every shard: per-owner sub-streams of each rank's full-coverage "
+                                "batch, one RCCL all-to-all over xGMI, then the owner's fused apply of the N messages "
+                                "in source-rank order (C4's step at C2's row width)")
+        except Exception as e:   # reported, never allowed to drop the headline line
+            exchange = {"error": repr(e)[:400]}
+    if extras and world == 1:
+        other = {}
+        for name, ix in (("C3_walked", False), ("C3_indexed", True)):
+            try:
+                m = c3_measure(args, ix, 20, 3, min(args.cpu_seconds, 6.0) if not ix else 0.0)
+                other[name] = {k: m[k] for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step",
+                                                 "kernel_ms_per_step_breakdown_pass", "cpu_baseline")}
+                other[name]["config"] = m["config"]["workload"]
+                lm = m.get("latency_model") or {}
+                other[name]["ordered_apply_frac_of_latency_bound"] = lm.get("frac_of_bound")
+            except Exception as e:
+                other[name] = {"error": repr(e)[:400]}
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
@@ -846,8 +910,11 @@ def main():
             line["walked"] = walked
         if pcie:
             line["pcie_inclusive"] = pcie
+        if exchange:
+            line["exchange"] = exchange
+        if other:
+            line["other_configs"] = other
         print(json.dumps(line), flush=True)
-    srv.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -17,7 +17,11 @@ enum {
   PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact */
   PSX_VARIANT_ORD_SPLIT = 6     /* 1: rows of sorted/map tables with 256 < max_entries <= 1024
                                    classified into a 256- and a 1,024-entry image launch that
-                                   run concurrently (default), 0: one 1,024-entry launch */
+                                   run concurrently (default), 0: one 1,024-entry launch */,
+  PSX_VARIANT_DECODE = 7        /* 1: walked messages with sparse tables decode window-parallel
+                                   (psx_walk.hip; default where eligible), 0: one workgroup per
+                                   message (decode_streams) */,
+  PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

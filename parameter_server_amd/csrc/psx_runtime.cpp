@@ -24,6 +24,12 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
                          uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
                          hipStream_t st);
 bool dense_apply_checks_rows(const DenseArgs &a, bool rec_f16);
+hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
+                       uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
+                       uint32_t epoch, hipStream_t st);
+size_t walk_ws_bytes(uint64_t items);
+int g_decode_walk = 1;   // PSX_VARIANT_DECODE
+int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
@@ -185,6 +191,9 @@ struct psx_ctx {
   uint32_t *d_ntouched[2] = {nullptr, nullptr};   // ordered path: touched-row count per table
   uint64_t *d_recoff[2] = {nullptr, nullptr};
   size_t recoff_cap[2] = {0, 0};                  // entries
+  void *d_walk[2] = {nullptr, nullptr};           // window-parallel decode workspace (psx_walk.hip)
+  size_t walk_cap[2] = {0, 0};                    // bytes
+  uint32_t walk_epoch[2] = {0, 0};                // granule tag of the slot's last call
   hipStream_t side = nullptr;                     // decode/index/verify stage
   hipStream_t aux = nullptr;                      // launches beside the context stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -401,6 +410,19 @@ bool has_sparse_serialized(const psx_ctx *c) {
   return false;
 }
 
+// Window-parallel decode (psx_walk.hip): 32 KiB windows; a call runs it when its messages
+// have at most kWalkMaxItems (message, window) items (B x the largest message's windows:
+// 4 GiB of windows), on one 1,024-thread block per CU.
+constexpr uint64_t kWalkWindowBytes = 32768;
+constexpr uint64_t kWalkMaxItems = 1u << 17;
+
+unsigned walk_blocks(psx_ctx *c) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
+    cus = 256;
+  return (unsigned)cus;
+}
+
 // Smallest record of any table in the context: bounds the records a message can hold
 // (ordered-path record lists are sized by it).  Sparse records are >= 8 bytes
 // ({int32 row_id; int32 n}); dense ones 4 + dense_body.
@@ -508,9 +530,46 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   psx::Seg *segs = c->d_segs[slot];
   uint32_t *counters = c->d_counters[slot];
   if (pipelined) HIP_TRY(c, hipStreamWaitEvent(prep, c->ev_free[slot], 0));
+  // Walked messages with sparse tables: the window-parallel decode (psx_walk.hip) when every
+  // sparse table of the context has one record pair size and the window items are bounded;
+  // otherwise (and for producer record offsets) one workgroup per message.
+  uint32_t spec_wpr = 0;
+  bool walk = psx::g_decode_walk && sparse;
+  for (int i = 0; i < n; ++i)
+    if (ix.p[i]) walk = false;
+  for (auto &t : c->tables) {
+    if (t.cfg.oplog_dense_serialized) continue;
+    const uint32_t w = 1 + (uint32_t)t.vsize / 4;
+    if (spec_wpr && spec_wpr != w) walk = false;
+    spec_wpr = w;
+  }
+  uint64_t maxw = 0;
+  for (int i = 0; i < n; ++i) maxw = std::max<uint64_t>(maxw, (s[i].size + kWalkWindowBytes - 1) / kWalkWindowBytes);
+  const uint64_t items = (uint64_t)n * maxw;
+  if (items == 0 || items > kWalkMaxItems) walk = false;
+  if (walk) {
+    const size_t need = psx::walk_ws_bytes(items);
+    if (need > c->walk_cap[slot]) {
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->side));
+      if (c->d_walk[slot]) hipFree(c->d_walk[slot]);
+      c->d_walk[slot] = nullptr;
+      c->walk_cap[slot] = 0;
+      HIP_TRY(c, hipMalloc(&c->d_walk[slot], need));
+      HIP_TRY(c, hipMemset(c->d_walk[slot], 0, need));   // no stale granule tag can match
+      c->walk_cap[slot] = need;
+      c->walk_epoch[slot] = 0;
+    }
+    if (++c->walk_epoch[slot] == 0) c->walk_epoch[slot] = 1;
+    ++psx::g_walk_calls;
+  }
   psx_status st = timed(
       c, "decode_streams",
       [&] {
+        if (walk)
+          return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
+                                  c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
+                                  c->walk_epoch[slot], prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -924,6 +983,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
     if (c->d_counters[k]) hipFree(c->d_counters[k]);
     if (c->d_ntouched[k]) hipFree(c->d_ntouched[k]);
     if (c->d_recoff[k]) hipFree(c->d_recoff[k]);
+    if (c->d_walk[k]) hipFree(c->d_walk[k]);
     if (c->ev_ready[k]) hipEventDestroy(c->ev_ready[k]);
     if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
   }
@@ -2205,6 +2265,8 @@ static int *variant_slot(int32_t which) {
   switch (which) {
     case PSX_VARIANT_DENSE_APPLY: return &psx::g_apply_variant;
     case PSX_VARIANT_ORD_SPLIT: return &psx::g_ord_split;
+    case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
+    case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     default: return nullptr;
   }
 }
@@ -2229,6 +2291,7 @@ struct VariantEnv {
   VariantEnv() {
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
+    if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
   }
 } variant_env;
 }  // namespace

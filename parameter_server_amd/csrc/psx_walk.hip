@@ -1,0 +1,460 @@
+// psx_walk.hip — window-parallel decode of walked messages that hold sparse tables.
+//
+// The record chain of a sparse table (SerializedOpLogReader::Next,
+// src/petuum_ps/server/serialized_oplog_reader.hpp:50-85: each record's size comes from its
+// own n, so record k+1 starts where record k ends) is sequential.  decode_streams walks it
+// with one workgroup per message, one 32 KiB window after another.  Here every window of
+// every message is its own work item, and the work that does not depend on where the chain
+// enters the window runs in parallel, before the chain arrives:
+//
+//   walk_head   one small block per message: per-call resets, the table headers up to the
+//               first sparse table with records (dense tables are O(1) each), the message's
+//               window range, the walker state at that table's first record.
+//   walk        persistent blocks of 1,024 threads take (window, message) tickets in
+//               window-major order.  Per window, speculatively for EVERY word q as a record
+//               start: the 1/2/4/8/16-record jump tables, then pointer jumping to the LAST
+//               record start on q's chain inside the window and the record count up to it
+//               (the window's exit map).  Then one wave waits for the predecessor window's
+//               walker state (8-byte {tag, value} granules written by atomics: the data is
+//               the flag, no fence — cdna_hip_programming.md, publish/consume recipe R2),
+//               resolves its own state in O(1) per table (one exit-map lookup per sparse
+//               table, headers read directly), publishes, and only then expands its records'
+//               offsets into recoff with the jump tables.
+//
+// The chain between windows costs one granule hand-off per window instead of a full window
+// walk.  Output (segs, recoff, counters, the status bits) is exactly decode_streams'.
+// Eligible calls (psx_runtime.cpp): no producer record offsets, every sparse table of the
+// context with one value size (the speculation uses that record pair size), and at most
+// kWalkMaxItems window items; the others run decode_streams.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "psx_device.hpp"
+
+namespace psx {
+
+constexpr int kWalkThreads = 1024;
+constexpr int kWW = 8192;                       // words per window (32 KiB)
+constexpr uint64_t kWBytes = (uint64_t)kWW * 4;
+constexpr int kWLevels = 5;                     // jump tables: 1, 2, 4, 8, 16 records
+constexpr uint16_t kNo = 0xFFFFu;               // next record outside the window / bad header
+constexpr int kGran = 14;                       // granules per published walker state
+constexpr int kMaxSegs = kMaxTables;            // sparse tables with records in one window
+
+typedef unsigned long long __attribute__((address_space(1))) gu64;
+
+// Workspace of one call slot: [WalkCtl][WalkHead][granules: kGran per window item].  Only
+// the WalkCtl (16 bytes) is zeroed per call; the granules carry the call's epoch as tag.
+constexpr size_t kWalkHeadOff = 256;
+
+// Walker state between windows.  mode 0: the next table header is at pos; 1: inside sparse
+// table t, `left` records still to walk, the next one at pos; 2: message done (or failed).
+struct WalkState {
+  uint64_t pos, left, rk, kk, seen;   // rk: next recoff index; kk: records before pos (all tables);
+  int32_t k, t, mode, ntab;           // seen: bit t = table t met in this message (duplicate check)
+};
+
+struct WalkCtl {      // zeroed (hipMemsetAsync, 16 bytes) before every call
+  uint32_t ticket;
+  uint32_t maxwin;    // max over messages of their window count
+  uint32_t pad[2];
+};
+
+struct WalkHead {     // written by walk_head, read by the first window of each message
+  WalkState st[kMaxFused];
+  uint32_t wfirst[kMaxFused];   // the message's first window (32 KiB grid from byte 0)
+  uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
+};
+constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
+
+size_t walk_ws_bytes(uint64_t items) { return kWalkGranOff + items * kGran * 8; }
+
+// One table header at s.pos (SerializedOpLogReader::StartNewTable, :87-121), read directly
+// from the message.  Returns false when the message is done or failed (s.mode = 2).
+__device__ bool walk_header(const uint8_t *p, uint64_t size, const TableDir &dir, Seg *segs_b, WalkState &s,
+                            uint32_t *call_status) {
+  if (s.k >= s.ntab) { s.mode = 2; return false; }
+  uint64_t off = s.pos;
+  if (off + 16 > size) { atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
+  const int32_t tid = *reinterpret_cast<const int32_t *>(p + off);
+  const uint64_t usz = (uint64_t) * reinterpret_cast<const uint32_t *>(p + off + 4) |
+                       ((uint64_t) * reinterpret_cast<const uint32_t *>(p + off + 8) << 32);
+  const int32_t nrows = *reinterpret_cast<const int32_t *>(p + off + 12);
+  off += 16;
+  int t = -1;
+  for (int i = 0; i < dir.n; ++i)
+    if (dir.table_id[i] == tid) t = i;
+  if (t < 0) { atomicOr(call_status, kStUnknownTable); s.mode = 2; return false; }
+  if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
+  if ((s.seen >> t) & 1ull) { atomicOr(call_status, kStUnsupported); s.mode = 2; return false; }
+  s.seen |= 1ull << t;
+  Seg *sg = &segs_b[t];
+  if (dir.dense_serialized[t]) {
+    const uint64_t stride = 4 + (uint64_t)dir.dense_body[t];
+    const uint64_t need = (uint64_t)nrows * stride;
+    if (off + need > size) { atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
+    Seg v;
+    v.rec0 = (int64_t)off;
+    v.num_rows = nrows;
+    v.sparse = 0;
+    v.ord0 = (int64_t)s.kk;
+    *sg = v;
+    s.pos = off + need;
+    s.k += 1;
+    s.kk += (uint64_t)nrows;
+    return true;
+  }
+  if (off & 3) { atomicOr(call_status, kStUnsupported); s.mode = 2; return false; }
+  Seg v;
+  v.rec0 = (int64_t)s.rk;
+  v.num_rows = nrows;
+  v.sparse = 1;
+  v.ord0 = (int64_t)s.kk;
+  *sg = v;
+  s.pos = off;
+  if (nrows) {
+    s.mode = 1;
+    s.t = t;
+    s.left = (uint64_t)nrows;
+  } else {
+    s.k += 1;
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir dir, Seg *segs, uint32_t *call_status,
+                                                        uint32_t *counters, uint32_t *ntouched, WalkCtl *ctl,
+                                                        WalkHead *head) {
+  const int b = blockIdx.x;
+  for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
+    Seg s;
+    s.rec0 = -1;
+    s.num_rows = 0;
+    s.sparse = 0;
+    s.ord0 = 0;
+    segs[b * kMaxTables + t] = s;
+    counters[t * kMaxFused + b] = 0;
+    if (b == 0) ntouched[t] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint8_t *p = ss.data[b];
+  const uint64_t size = ss.size[b];
+  WalkState s{};
+  s.pos = 4;
+  s.rk = ss.recoff_base[b];
+  s.mode = 2;
+  if (size == 0) {
+    // empty message (server.cpp:128)
+  } else if (size < 4 || *reinterpret_cast<const int32_t *>(p) < 0) {
+    atomicOr(call_status, kStMalformed);
+  } else {
+    s.ntab = *reinterpret_cast<const int32_t *>(p);
+    s.mode = 0;
+    while (s.mode == 0 && walk_header(p, size, dir, segs + b * kMaxTables, s, call_status)) {
+    }
+  }
+  uint32_t nwin = 0, wf = 0;
+  if (s.mode == 1 && s.pos + 8 > size) {   // the first record's header past the message end
+    atomicOr(call_status, kStMalformed);
+    s.mode = 2;
+  }
+  if (s.mode == 1) {
+    wf = (uint32_t)(s.pos / kWBytes);
+    nwin = (uint32_t)((size + kWBytes - 1) / kWBytes) - wf;
+    atomicMax(&ctl->maxwin, nwin);
+  }
+  head->st[b] = s;
+  head->wfirst[b] = wf;
+  head->nwin[b] = nwin;
+}
+
+__device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
+  switch (i) {
+    case 0: return (uint32_t)s.pos;
+    case 1: return (uint32_t)(s.pos >> 32);
+    case 2: return (uint32_t)s.left;
+    case 3: return (uint32_t)(s.left >> 32);
+    case 4: return (uint32_t)s.rk;
+    case 5: return (uint32_t)(s.rk >> 32);
+    case 6: return (uint32_t)s.kk;
+    case 7: return (uint32_t)(s.kk >> 32);
+    case 8: return (uint32_t)s.seen;
+    case 9: return (uint32_t)(s.seen >> 32);
+    case 10: return (uint32_t)s.k;
+    case 11: return (uint32_t)s.t;
+    case 12: return (uint32_t)s.mode;
+    default: return (uint32_t)s.ntab;
+  }
+}
+
+__global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
+                                                            uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
+                                                            unsigned long long *gran_p, uint32_t spec_wpr,
+                                                            uint32_t epoch) {
+  gu64 *gran = (gu64 *)gran_p;
+  __shared__ uint32_t win[kWW + 1];                 // + 1 halo word
+  __shared__ uint16_t jt[kWLevels][kWW];            // jt[l][q]: the record 2^l on from q, kNo if outside
+  __shared__ uint16_t xp[kWW];                      // exit map: last record start on q's chain in the window
+  __shared__ uint16_t xc[kWW];                      //           records from q up to it (exclusive)
+  __shared__ uint16_t seg_q[kMaxSegs];
+  __shared__ uint16_t seg_n[kMaxSegs];
+  __shared__ uint64_t seg_rk[kMaxSegs];
+  __shared__ uint16_t a16[kWW / 16 + 1], a4[4], a1[4];
+  __shared__ uint32_t sh_nseg, sh_n16, sh_n4, sh_n1, sh_ticket;
+  const int tid = threadIdx.x;
+  const int B = ss.n;
+  const uint32_t items = (uint32_t)B * ctl->maxwin;
+
+  for (;;) {
+    if (tid == 0) sh_ticket = atomicAdd(&ctl->ticket, 1u);
+    __syncthreads();
+    const uint32_t tk = sh_ticket;
+    if (tk >= items) break;
+    const int b = (int)(tk % (uint32_t)B);
+    const uint32_t j = tk / (uint32_t)B;
+    const uint32_t nwin_b = head->nwin[b];
+    if (j >= nwin_b) {
+      __syncthreads();   // sh_ticket is rewritten at the top
+      continue;
+    }
+    const uint8_t *p = ss.data[b];
+    const uint64_t size = ss.size[b];
+    const uint64_t W0 = ((uint64_t)head->wfirst[b] + j) * kWBytes;
+    const uint64_t tot = (size - W0) / 4;                   // whole words from W0
+    const uint32_t nw = (uint32_t)(tot < (uint64_t)kWW ? tot : (uint64_t)kWW);
+    const bool halo = tot > nw;
+    const bool last = j + 1 == nwin_b;
+    // 1) the window (and its halo word) into LDS
+    {
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(p + W0);
+      constexpr int PER = kWW / kWalkThreads;
+      uint32_t r[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)k * kWalkThreads;
+        r[k] = i < nw ? src[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) win[tid + k * kWalkThreads] = r[k];
+      if (tid == 0) win[nw] = halo ? src[nw] : 0u;
+    }
+    __syncthreads();
+    // 2) jump tables (every word a speculative record start): next = q + 2 + n * wpr
+    for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
+      uint16_t v = kNo;
+      if (q + 1 < nw) {
+        const int32_t n = (int32_t)win[q + 1];
+        if (n >= 0) {
+          const uint64_t nxt = (uint64_t)q + 2 + (uint64_t)n * spec_wpr;
+          if (nxt < nw && W0 + nxt * 4 <= size) v = (uint16_t)nxt;
+        }
+      }
+      jt[0][q] = v;
+      xp[q] = v == kNo ? (uint16_t)q : v;
+      xc[q] = v == kNo ? 0 : 1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int lv = 1; lv < kWLevels; ++lv) {
+      for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
+        const uint16_t a = jt[lv - 1][q];
+        jt[lv][q] = a != kNo ? jt[lv - 1][a] : kNo;
+      }
+      __syncthreads();
+    }
+    // 3) exit map by pointer jumping (terminal records point to themselves with count 0)
+    for (;;) {
+      constexpr int PER = kWW / kWalkThreads;
+      uint16_t np[PER], nc[PER];
+      bool changed = false;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
+        const uint16_t a = xp[q];
+        np[k] = xp[a];
+        nc[k] = (uint16_t)(xc[q] + xc[a]);
+        changed |= np[k] != a;
+      }
+      const int any = __syncthreads_or(changed);
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
+        xp[q] = np[k];
+        xc[q] = nc[k];
+      }
+      __syncthreads();
+      if (!any) break;
+    }
+    // 4) wave 0: wait for the predecessor's state, resolve this window, publish
+    if (tid < 64) {
+      const int lane = tid;
+      WalkState s;
+      if (j == 0) {
+        s = head->st[b];
+      } else {
+        const gu64 *g = gran + (uint64_t)(tk - (uint32_t)B) * kGran;
+        uint32_t v = 0;
+        bool ok = false;
+        for (uint32_t spins = 0;; ++spins) {
+          uint64_t x = (uint64_t)epoch << 32;
+          if (lane < kGran) x = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = (uint32_t)x;
+          if (__all((uint32_t)(x >> 32) == epoch)) { ok = true; break; }
+          if (spins > (1u << 24)) break;        // bounded: a lost hand-off fails the call
+          __builtin_amdgcn_s_sleep(1);
+        }
+        auto lo_hi = [&](int i) { return (uint64_t)(uint32_t)__shfl((int)v, i) | ((uint64_t)(uint32_t)__shfl((int)v, i + 1) << 32); };
+        s.pos = lo_hi(0);
+        s.left = lo_hi(2);
+        s.rk = lo_hi(4);
+        s.kk = lo_hi(6);
+        s.seen = lo_hi(8);
+        s.k = __shfl((int)v, 10);
+        s.t = __shfl((int)v, 11);
+        s.mode = __shfl((int)v, 12);
+        s.ntab = __shfl((int)v, 13);
+        if (!ok) {
+          if (lane == 0) atomicOr(call_status, kStUnsupported);
+          s.mode = 2;
+        }
+      }
+      if (lane == 0) {
+        const uint64_t Wend = W0 + kWBytes;
+        uint32_t nseg = 0;
+        Seg *segs_b = segs + b * kMaxTables;
+        for (;;) {
+          if (s.mode == 2) break;
+          if (s.pos >= Wend && !last) break;          // the walk continues in a later window
+          if (s.mode == 0) {
+            walk_header(p, size, dir, segs_b, s, call_status);
+            continue;
+          }
+          // sparse records from s.pos: one exit-map lookup
+          const uint64_t q = (s.pos - W0) / 4;
+          if (q >= nw) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }   // header past the end
+          const uint32_t T = xp[q];
+          const uint64_t c = (uint64_t)xc[q] + 1;                                    // records q .. T
+          const uint64_t take = s.left < c ? s.left : c;
+          uint64_t endT = 0;
+          if (take == c) {
+            // the table holds T's record (before T every link is a checked jump-table link;
+            // past the table's end the speculative chain may be garbage): its header inside
+            // the message, n >= 0, its end inside the message
+            if (T + 1 > nw || (T + 1 == nw && !halo)) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
+            const int32_t nT = (int32_t)win[T + 1];
+            if (nT < 0) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
+            endT = W0 + ((uint64_t)T + 2 + (uint64_t)nT * spec_wpr) * 4;
+            if (endT > size) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
+          }
+          seg_q[nseg] = (uint16_t)q;
+          seg_n[nseg] = (uint16_t)take;
+          seg_rk[nseg] = s.rk;
+          ++nseg;
+          s.rk += take;
+          s.kk += take;
+          s.left -= take;
+          if (take == c) {
+            s.pos = endT;
+          } else {
+            // the table ends inside the chain: the record `take` on from q (binary lifting)
+            uint32_t w = (uint32_t)q;
+            uint64_t r = take;
+            for (int lv = kWLevels - 1; lv >= 0; --lv)
+              while (r >= (1ull << lv)) { w = jt[lv][w]; r -= 1ull << lv; }
+            s.pos = W0 + (uint64_t)w * 4;
+          }
+          if (s.left == 0) {
+            s.k += 1;
+            s.mode = 0;
+          }
+        }
+        sh_nseg = nseg;
+      }
+      // lane i publishes granule i of lane 0's state
+      uint32_t mine = 0;
+#pragma unroll
+      for (int i = 0; i < kGran; ++i) {
+        const uint32_t w = (uint32_t)__shfl((int)gran_value(s, i), 0);
+        if (lane == i) mine = w;
+      }
+      if (!last && lane < kGran) {
+        gu64 *g = gran + (uint64_t)tk * kGran;
+        __hip_atomic_store(g + lane, ((uint64_t)epoch << 32) | (uint64_t)mine, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    // 5) expand the window's record offsets (thread 0 collects hop starts, all threads fill)
+    const uint32_t nseg = sh_nseg;
+    for (uint32_t si = 0; si < nseg; ++si) {
+      if (tid == 0) {
+        uint32_t w = seg_q[si];
+        uint32_t rem = seg_n[si];
+        uint32_t n16 = 0, n4 = 0, n1 = 0;
+        while (rem >= 16) {
+          a16[n16++] = (uint16_t)w;
+          rem -= 16;
+          if (rem) w = jt[4][w];
+        }
+        while (rem >= 4) {
+          a4[n4++] = (uint16_t)w;
+          rem -= 4;
+          if (rem) w = jt[2][w];
+        }
+        while (rem) {
+          a1[n1++] = (uint16_t)w;
+          if (--rem) w = jt[0][w];
+        }
+        sh_n16 = n16;
+        sh_n4 = n4;
+        sh_n1 = n1;
+      }
+      __syncthreads();
+      const uint32_t n16 = sh_n16, n4 = sh_n4, n1 = sh_n1;
+      const uint64_t rk = seg_rk[si];
+      for (uint32_t i = tid; i < n16 * 4; i += kWalkThreads) {   // 4 threads per 16-record hop
+        uint32_t q = a16[i >> 2];
+        const uint32_t sub = i & 3;
+        for (uint32_t k = 0; k < sub; ++k) q = jt[2][q];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          recoff[rk + 16 * (uint64_t)(i >> 2) + 4 * sub + k] = W0 + (uint64_t)q * 4;
+          if (k < 3) q = jt[0][q];
+        }
+      }
+      const uint64_t r4 = rk + 16 * (uint64_t)n16;
+      if (tid < n4) {
+        uint32_t q = a4[tid];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          recoff[r4 + 4 * (uint64_t)tid + k] = W0 + (uint64_t)q * 4;
+          if (k < 3) q = jt[0][q];
+        }
+      }
+      const uint64_t r1 = r4 + 4 * (uint64_t)n4;
+      if (tid < n1) recoff[r1 + tid] = W0 + (uint64_t)a1[tid] * 4;
+      __syncthreads();
+    }
+  }
+}
+
+// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 32 KiB window count);
+// epoch: nonzero, different from the previous call's on this workspace (granule tags).
+hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
+                       uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
+                       uint32_t epoch, hipStream_t st) {
+  WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
+  WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
+  unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(WalkCtl), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(walk_head_kernel, dim3(ss.n), dim3(256), 0, st, ss, dir, segs, call_status, counters, ntouched,
+                     ctl, head);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
+                     head, gran, spec_wpr, epoch);
+  return hipGetLastError();
+}
+
+}  // namespace psx

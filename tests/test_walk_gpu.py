@@ -1,0 +1,241 @@
+"""The window-parallel decode (psx_walk.hip) against the one-workgroup-per-message decode
+(decode_streams) and the CPU oracle, on the record-chain shapes that stress it: records
+spanning several 32 KiB windows, windows holding 4,096 records, tables ending mid-window and
+exactly on a window boundary, several sparse and dense tables in one message, empty sparse
+tables, messages of different lengths in one call, and malformed chains (the same error and
+nothing applied).  Reference: SerializedOpLogReader (serialized_oplog_reader.hpp:30-133)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import parameter_server_amd as psa
+from parameter_server_amd import wire, PsxError, _abi
+from oracle.oracle import OracleServer, DENSE, SORTED_MAP, MAP, F32, F64, I32, I64
+
+pytestmark = pytest.mark.gpu
+DECODE, WALK_CALLS = 7, 8
+NP = {F32: np.float32, F64: np.float64, I32: np.int32, I64: np.int64}
+VS = {F32: 4, F64: 8, I32: 4, I64: 8}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built_lib, oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _message(tables):
+    """tables: list of (table_id, vsize, rows) for sparse tables or (table_id, 'dense', ids,
+    payload) for dense ones, in the given order (empty tables kept)."""
+    parts = [np.array([len(tables)], np.int32).view(np.uint8)]
+    for t in tables:
+        if t[1] == "dense":
+            parts.append(wire.dense_stream_np(t[0], np.asarray(t[2], np.int32), t[3])[4:])
+        else:
+            parts.append(wire.sparse_stream_np(t[0], t[1], t[2])[4:])
+    return np.concatenate(parts)
+
+
+def _rows(rng, ids, ncols, dt, nnz):
+    out = []
+    for rid, k in zip(ids, nnz):
+        cols = np.sort(rng.choice(ncols, size=k, replace=False)).astype(np.int32)
+        v = rng.randint(1, 4, size=k) if dt in (I32, I64) else rng.normal(0, 1, size=k)
+        out.append((int(rid), cols, v.astype(NP[dt])))
+    return out
+
+
+class _Setup:
+    """A libpsx server and the oracle with the same tables."""
+
+    def __init__(self, tables, bgs):
+        self.bgs = list(bgs)
+        self.srv = psa.Server(0, 1, self.bgs)
+        self.orc = OracleServer(self.bgs)
+        self.tables = tables
+        for tid, kind, dt, ncols, dense_ser, rows in tables:
+            self.srv.CreateTable(tid, psa.TableInfo(row_kind=kind, dtype=dt, row_capacity=ncols,
+                                                    oplog_dense_serialized=dense_ser, max_rows=rows,
+                                                    max_entries=ncols if kind != DENSE else 0))
+            self.orc.create_table(tid, kind, dt, ncols if kind == DENSE else 0, oplog_dense_serialized=dense_ser)
+
+    def snapshot(self):
+        return {t[0]: self.srv.serialize_rows(t[0], list(range(t[5]))) for t in self.tables}
+
+    def oracle_snapshot(self):
+        return {t[0]: self.orc.serialize_records(t[0], list(range(t[5]))) for t in self.tables}
+
+    def apply(self, streams, ver, oracle=True):
+        dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+        torch.cuda.synchronize()
+        self.srv.apply_device([(d.data_ptr(), d.numel(), bg, ver) for d, bg in zip(dev, self.bgs)])
+        self.srv.sync()
+        if oracle:
+            for s, bg in zip(streams, self.bgs):
+                assert self.orc.apply_stream(s, bg, ver) == 0
+
+    def close(self):
+        self.srv.close()
+        self.orc.close()
+
+
+def _run_both(tables, streams):
+    """Apply the streams with the window-parallel decode and with decode_streams (fresh
+    servers); both must equal the oracle, and the walk must have run."""
+    L = _abi.load()
+    out = []
+    for variant in (1, 0):
+        old = L.psx_debug_set_variant(DECODE, variant)
+        L.psx_debug_set_variant(WALK_CALLS, 0)
+        try:
+            st = _Setup(tables, range(100, 100 + len(streams)))
+            st.apply(streams, 0)
+            got, want = st.snapshot(), st.oracle_snapshot()
+            st.close()
+            walked = L.psx_debug_get_variant(WALK_CALLS)
+        finally:
+            L.psx_debug_set_variant(DECODE, old)
+        assert got == want, f"decode variant {variant} differs from the oracle"
+        assert (walked > 0) == (variant == 1)
+        out.append(got)
+    return out
+
+
+def test_c3_shaped_messages_every_window():
+    """Zipf rows, nnz 1..32, 8 messages of ~46 windows each into sorted-map rows."""
+    rng = np.random.RandomState(5)
+    rows, K = 20_000, 1024
+    p = 1.0 / np.arange(1, rows + 1)
+    p /= p.sum()
+    streams = []
+    for b in range(8):
+        ids = rng.choice(rows, size=10_000, replace=False, p=p)
+        streams.append(wire.sparse_stream_np(3, 4, _rows(rng, ids, K, I32, rng.randint(1, 33, size=ids.size))))
+    _run_both([(3, SORTED_MAP, I32, K, False, rows)], streams)
+
+
+@pytest.mark.parametrize("dt", [F32, F64])
+def test_records_spanning_windows_and_tiny_records(dt):
+    """Records of 8,000-24,000 (col, val) pairs (up to 6 windows each) between runs of
+    one-pair records (2,048 per window), then a table of zero-pair records (4,096 per
+    window) and one-pair records."""
+    rng = np.random.RandomState(9)
+    RA, KA, RB, KB = 1024, 24_000, 8192, 16
+    ids = rng.permutation(RA)
+    recs, i = [], 0
+    for blk in range(6):
+        for _ in range(2):
+            recs += _rows(rng, [ids[i]], KA, dt, [rng.randint(8_000, 24_000)])
+            i += 1
+        recs += _rows(rng, ids[i:i + 150], KA, dt, [1] * 150)
+        i += 150
+    idb = rng.permutation(RB)
+    tiny = [(int(r), np.zeros(0, np.int32), np.zeros(0, NP[dt])) for r in idb[:6000]]
+    tiny += _rows(rng, idb[6000:7000], KB, dt, [1] * 1000)
+    s = _message([(3, VS[dt], recs), (4, VS[dt], tiny)])
+    _run_both([(3, DENSE, dt, KA, False, RA), (4, DENSE, dt, KB, False, RB)], [s])
+
+
+def test_several_tables_per_message_ending_anywhere():
+    """dense, sparse, dense, sparse, empty sparse, sparse tables in one message; table ends
+    mid-window, on a window boundary (padded to 32 KiB exactly) and at the message end;
+    messages of different lengths in one call of 16."""
+    rng = np.random.RandomState(13)
+    R, K, CAP = 3000, 512, 64
+    tabs = [(1, DENSE, F32, CAP, True, R), (2, SORTED_MAP, I32, K, False, R), (4, DENSE, F32, CAP, True, R),
+            (5, SORTED_MAP, I32, K, False, R), (6, SORTED_MAP, I32, K, False, R), (7, DENSE, I32, K, False, R)]
+    streams = []
+    for b in range(16):
+        n = int(rng.randint(0, 600)) if b % 3 else 1
+        ids = [rng.permutation(R)[:n] for _ in range(6)]
+        parts = [(1, "dense", ids[0][: n // 2], rng.normal(0, 1, (n // 2, CAP)).astype(np.float32)),
+                 (2, 4, _rows(rng, ids[1], K, I32, rng.randint(1, 40, size=n))),
+                 (4, "dense", ids[2][:7], rng.normal(0, 1, (min(7, n), CAP)).astype(np.float32)),
+                 (5, 4, _rows(rng, ids[3], K, I32, rng.randint(1, 9, size=n))),
+                 (6, 4, []),
+                 (7, 4, _rows(rng, ids[5], K, I32, rng.randint(0, 200, size=n)))]
+        if b == 4:
+            # table 2's records end exactly on the first 32 KiB boundary of the message
+            parts[0] = (1, "dense", ids[0][:1], rng.normal(0, 1, (1, CAP)).astype(np.float32))
+            head = 4 + 16 + 1 * (4 + 4 * CAP) + 16
+            recs, used = [], head
+            while used + 8 + 8 * 64 < 32768:
+                recs += _rows(rng, [len(recs)], K, I32, [64])
+                used += 8 + 8 * 64
+            assert (32768 - used - 8) % 8 == 0
+            recs += _rows(rng, [len(recs)], K, I32, [(32768 - used - 8) // 8])
+            parts[1] = (2, 4, recs)
+        streams.append(_message(parts))
+    assert any(s.size > 65536 for s in streams) and len({s.size for s in streams}) > 8
+    _run_both(tabs, streams)
+
+
+def test_mixed_value_sizes_fall_back_to_block_decode():
+    """Sparse tables of 4- and 8-byte values in one context: the speculation needs one
+    record pair size, so the call takes decode_streams (and still matches the oracle)."""
+    L = _abi.load()
+    rng = np.random.RandomState(17)
+    R, K = 500, 128
+    tabs = [(2, SORTED_MAP, I32, K, False, R), (3, MAP, F64, K, False, R)]
+    s = _message([(2, 4, _rows(rng, rng.permutation(R)[:300], K, I32, rng.randint(1, 20, size=300))),
+                  (3, 8, _rows(rng, rng.permutation(R)[:300], K, F64, rng.randint(1, 20, size=300)))])
+    L.psx_debug_set_variant(WALK_CALLS, 0)
+    st = _Setup(tabs, [100])
+    st.apply([s], 0)
+    assert st.snapshot() == st.oracle_snapshot()
+    assert L.psx_debug_get_variant(WALK_CALLS) == 0
+    st.close()
+
+
+def _malformed_cases():
+    rng = np.random.RandomState(21)
+    R, K = 4000, 256
+    good = wire.sparse_stream_np(3, 4, _rows(rng, rng.permutation(R)[:3000], K, I32, rng.randint(1, 30, size=3000)))
+    n0 = int(np.frombuffer(good[16:20], np.int32)[0])
+    cases = {}
+    cases["truncated"] = good[: good.size - 12]
+    words = good.view(np.int32).copy()
+    # record 1500's n negative: walk to it
+    off, w = 5, []
+    for r in range(2000):
+        w.append(off)
+        off += 2 + 2 * int(words[off + 1])
+    bad = words.copy()
+    bad[w[1500] + 1] = -3
+    cases["negative_n"] = bad.view(np.uint8)
+    bad = words.copy()
+    bad[w[1999] + 1] = 1 << 28
+    cases["n_past_end"] = bad.view(np.uint8)
+    two = _message([(3, 4, _rows(rng, rng.permutation(R)[:2000], K, I32, rng.randint(1, 30, size=2000))),
+                    (9, 4, _rows(rng, [1, 2], K, I32, [3, 3]))])
+    cases["unknown_table_after_sparse"] = two
+    dup = _message([(3, 4, _rows(rng, rng.permutation(R)[:2000], K, I32, rng.randint(1, 30, size=2000))),
+                    (3, 4, _rows(rng, [1, 2], K, I32, [3, 3]))])
+    cases["table_twice"] = dup
+    more = words.copy()
+    more[4] = n0 + 1          # one record more than the message holds
+    cases["rows_past_end"] = more.view(np.uint8)
+    return R, K, good, cases
+
+
+@pytest.mark.parametrize("case", ["truncated", "negative_n", "n_past_end", "unknown_table_after_sparse",
+                                  "table_twice", "rows_past_end"])
+def test_malformed_chain_same_error_nothing_applied(case):
+    L = _abi.load()
+    R, K, good, cases = _malformed_cases()
+    errs = []
+    for variant in (1, 0):
+        old = L.psx_debug_set_variant(DECODE, variant)
+        try:
+            st = _Setup([(3, SORTED_MAP, I32, K, False, R)], [100, 101])
+            st.apply([good, np.zeros(0, np.uint8)], 0)
+            before = st.snapshot()
+            with pytest.raises(PsxError) as ei:
+                st.apply([good, cases[case]], 1, oracle=False)
+            errs.append(ei.value.status)
+            assert st.snapshot() == before, f"variant {variant}: a failed call applied something"
+            st.close()
+        finally:
+            L.psx_debug_set_variant(DECODE, old)
+    assert errs[0] == errs[1]

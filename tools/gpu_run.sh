@@ -32,7 +32,7 @@ for s in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python -u bench.py --steps 20 --warmup 5 --pmc-json "$PMC_JSON" ;;
     walked) run walked 300 python -u bench.py --walked --steps 20 --warmup 5 --cpu-seconds 0 ;;
-    stats) run stats 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o c2 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --skip-walked
+    stats) run stats 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o c2 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --skip-walked --no-extras
            python3 tools/kernel_stats.py "$(find "$O/stats" -name '*.db' | head -1)" "$O/c2_kernel_stats.csv" && head -4 "$O/c2_kernel_stats.csv" | cut -c1-160 ;;
     stats3) run stats3 300 rocprofv3 --kernel-trace --stats -d "$O/stats3" -o c3 -- python3 bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0
            python3 tools/kernel_stats.py "$(find "$O/stats3" -name '*.db' | head -1)" "$O/c3_kernel_stats.csv" && head -6 "$O/c3_kernel_stats.csv" | cut -c1-160 ;;
@@ -40,7 +40,7 @@ for s in "$@"; do
       P=1
       for ctrs in "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" "FETCH_SIZE" "WRITE_SIZE"; do
         say "pmc pass $P: $ctrs"
-        timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$O/pmc/p$P" -o pmc -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --skip-walked \
+        timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$O/pmc/p$P" -o pmc -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --skip-walked --no-extras \
           > "$O/pmc_p$P.log" 2>&1 || { echo "!! pmc pass $P"; tail -5 "$O/pmc_p$P.log"; exit 1; }
         P=$((P+1))
       done

@@ -257,48 +257,52 @@ def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234, with_reco
 
 
 C3_LATENCY_JSON = os.path.join(ROOT, "profiles", "r02", "c3_inc_latency.json")
-C3_WAVES_PER_SIMD = {4: 7, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
+C3_WAVES_PER_SIMD = {4: 5, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
 
 
 def c3_model(batches, rows, K, apply_ms):
-    """The sorted-map apply's bound ("C3 bound").  Every Inc of a row is a
-    dependent chain in one wave (FindIndex ballots over the image, then the add or the
-    LinearSearchAndMove shift), so a row costs t_r = k_r x L(n_r): k_r Incs per step at
-    image size n_r, L(n) the measured per-Inc latency of a lone wave on the kernel the row
-    takes (tools/probe_inc_latency.py -> profiles/r02/c3_inc_latency.json, "found" keys: at
-    steady state every column of a step already exists).  Rows are independent waves, w of them
-    resident per SIMD (7 for the 256-entry image, 3 for the 1,024-entry one), 1,024 SIMDs:
+    """The sorted-map apply's bound ("C3 bound").  A row's records are one
+    dependent chain in one wave; each record's found keys (a chunk of <= 64 columns) are
+    added at once (found_run), so at steady state (every column of a step already present)
+    a row costs t_r = R_r x L(n_r): R_r records per step at image size n_r, L(n) the
+    measured per-record latency of a lone wave on the kernel the row takes
+    (tools/probe_inc_latency.py -> profiles/r02/c3_inc_latency.json).  Rows are independent
+    waves, w of them resident per SIMD (5 for the 256-entry image, 3 for the 1,024-entry
+    one), 1,024 SIMDs:
         T >= max( max_r t_r ,  sum_r t_r / (w_r x 1024) )
-    (critical path vs latency-interleave throughput; optimistic: no issue contention).
-    n_r = columns with a nonzero net value over the step's batches (the image after the
-    first step, since the same batches repeat)."""
+    (critical path vs latency-interleave throughput; optimistic: no issue contention, no
+    inserts).  n_r = columns with a nonzero net value over the step's batches."""
     import numpy as np
     if not os.path.exists(C3_LATENCY_JSON):
         return None
     js = json.load(open(C3_LATENCY_JSON))
+    if "found_rec_ns" not in js:
+        return None
 
     def curve(name):
-        lat = js.get(name) or js["found_ns"]
+        lat = js[name]
         xs = np.array(sorted(int(k) for k in lat), dtype=np.float64)
-        return xs, np.array([lat[str(int(x))] for x in xs], dtype=np.float64)
-    r = np.concatenate([np.full(len(c), rid, np.int64) for recs in batches for rid, c, _ in recs])
+        return xs, np.array([max(lat[str(int(x))], 0.0) for x in xs], dtype=np.float64)
+    r = np.array([rid for recs in batches for rid, _, _ in recs], np.int64)
+    rc = np.concatenate([np.full(len(c), rid, np.int64) for recs in batches for rid, c, _ in recs])
     c = np.concatenate([c for recs in batches for _, c, _ in recs]).astype(np.int64)
     v = np.concatenate([v for recs in batches for _, _, v in recs]).astype(np.int64)
-    k_r = np.bincount(r, minlength=rows).astype(np.float64)
-    uniq, inv = np.unique(r * K + c, return_inverse=True)
+    R_r = np.bincount(r, minlength=rows).astype(np.float64)
+    k_r = np.bincount(rc, minlength=rows).astype(np.float64)
+    uniq, inv = np.unique(rc * K + c, return_inverse=True)
     net = np.bincount(inv, weights=v)
     n_r = np.bincount(uniq[net != 0] // K, minlength=rows).astype(np.float64)
     big = n_r + k_r > 256                                          # the 1,024-entry launch
-    x16, y16 = curve("found_ns")                                   # 1,024-entry image
-    x4, y4 = curve("found_small_ns")                               # 256-entry image
-    t_r = k_r * np.where(big, np.interp(n_r, x16, y16), np.interp(n_r, x4, y4)) * 1e-6   # ms
+    x16, y16 = curve("found_rec_ns")                               # 1,024-entry image
+    x4, y4 = curve("found_small_rec_ns")                           # 256-entry image
+    t_r = R_r * np.where(big, np.interp(n_r, x16, y16), np.interp(n_r, x4, y4)) * 1e-6   # ms
     chain = float(t_r.max())
     tput = float((t_r[~big].sum() / C3_WAVES_PER_SIMD[4] + t_r[big].sum() / C3_WAVES_PER_SIMD[16]) / 1024)
     bound = max(chain, tput)
     return {"bound_ms": round(bound, 4), "critical_path_ms": round(chain, 4), "interleave_ms": round(tput, 4),
             "ordered_apply_ms": round(apply_ms, 4), "frac_of_bound": round(bound / apply_ms, 3) if apply_ms else None,
-            "rows_touched": int((k_r > 0).sum()), "rows_1024_image": int(big.sum()),
-            "max_incs_per_row": int(k_r.max()), "max_image": int(n_r.max()),
+            "rows_touched": int((R_r > 0).sum()), "rows_1024_image": int(big.sum()),
+            "max_records_per_row": int(R_r.max()), "max_incs_per_row": int(k_r.max()), "max_image": int(n_r.max()),
             "latency_source": os.path.relpath(C3_LATENCY_JSON, ROOT)}
 
 

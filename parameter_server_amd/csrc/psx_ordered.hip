@@ -544,6 +544,75 @@ __device__ __forceinline__ V add_at(V (&val)[J], int jj, int l, int lane, V d) {
   }
 }
 
+// A run of found-key Incs of one record chunk (lanes with distinct keys, all present,
+// delta != 0, before the chunk's next insert), applied at once.  Sequentially each adds in
+// place (sorted_vector_map_store.hpp:325-327) and an entry that reaches zero is removed with
+// an order-preserving memmove (:329-334, RemoveOneEntryAndCompact :289-303): the adds touch
+// distinct entries and move nothing, and the removals of several entries leave the same
+// sequence in any order, so the run equals: every delta added to its entry, then every
+// entry of the run that reached zero removed by one stable compaction.  sv (V[J*64], zero
+// between runs) and ck (int32[J*64]) are the wave's LDS scratch; pos is the key map.
+template <typename V, int J>
+__device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int32_t n, bool run, int32_t my_idx,
+                                             V my_d, int lane, V *sv, int32_t *ck, int16_t *pos, bool &stale) {
+  if (run) sv[my_idx] = my_d;
+  wave_sync();
+  uint64_t rmm[J];
+  bool anyrm = false;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    rmm[j] = 0;
+    if (j * 64 < n) {
+      const int32_t i = j * 64 + lane;
+      const V dv = sv[i];
+      const bool hit = dv != V(0);
+      if (hit) {
+        val[j] = OV<V>::add(val[j], dv);
+        sv[i] = V(0);
+      }
+      rmm[j] = __ballot(hit && val[j] == V(0));
+      anyrm = anyrm || rmm[j] != 0;
+    }
+  }
+  if (!anyrm) return n;
+  // stable compaction: kept entries to LDS at their new index, the key map updated
+  int32_t gone = 0;
+  const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if (j * 64 < n) {
+      const int32_t i = j * 64 + lane;
+      if (i < n) {
+        if ((rmm[j] >> lane) & 1ull) {
+          pos[key[j]] = -1;
+        } else {
+          const int32_t ni = i - gone - __builtin_popcountll(rmm[j] & lt);
+          ck[ni] = key[j];
+          sv[ni] = val[j];
+          pos[key[j]] = (int16_t)ni;
+        }
+      }
+      gone += __builtin_popcountll(rmm[j]);
+    }
+  }
+  wave_sync();
+  const int32_t n2 = n - gone;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if (j * 64 < n) {
+      const int32_t i = j * 64 + lane;
+      if (i < n2) {
+        key[j] = ck[i];
+        val[j] = sv[i];
+        sv[i] = V(0);
+      }
+    }
+  }
+  wave_sync();
+  stale = true;
+  return n2;
+}
+
 // Split tables run two launches of this kernel concurrently, over the touched rows
 // ordered_classify put in the 256- and the 1,024-entry list (a.touched / a.ntouched point
 // at one list each).
@@ -556,10 +625,14 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
   // per row at load): int16 per key, -1 = absent.
   __shared__ int16_t s_pos[4][1024];   // the register kernels serve max_entries <= 1,024
+  __shared__ V s_sv[4][J * 64];        // found_run: deltas by entry (zero between runs), compaction values
+  __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
   if (threadIdx.x == 0) build_space(a, rs);
-  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
+  __syncthreads();
   const bool go = o_gate(a) && (!DRY || *a.keyflag);
   const bool pos_ok = a.keyflag && !*a.keyflag && a.max_entries <= 1024;
   int16_t *pos = s_pos[wib];
@@ -693,6 +766,24 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
           int32_t my_idx = -1;
           bool stale = true;
           for (int32_t t = 0; t < cnt && !over; ++t) {
+            if constexpr (KIND == 1) {
+              if (use_pos) {
+                // the found keys up to the chunk's next insert, at once (found_run)
+                if (stale) {
+                  my_idx = lane < cnt ? (int32_t)pos[my_col] : -1;
+                  stale = false;
+                }
+                const bool live = lane >= t && lane < cnt && my_d != V(0);
+                const uint64_t ins = __ballot(live && my_idx < 0);
+                const int32_t run_end = ins ? (int32_t)__builtin_ctzll(ins) : cnt;
+                if (run_end > t) {
+                  const bool run = live && lane < run_end;
+                  if (__ballot(run)) n = found_run<V, J>(key, val, n, run, my_idx, my_d, lane, s_sv[wib], s_ck[wib], pos, stale);
+                  t = run_end - 1;
+                  continue;
+                }
+              }
+            }
             const int32_t c = __builtin_amdgcn_readlane(my_col, t);
             const V d = bcast(my_d, t);
             if (d == V(0)) continue;                                  // :306

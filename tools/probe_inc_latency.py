@@ -1,4 +1,4 @@
-"""Per-Inc latency of the sorted-map apply (SortedVectorMapStore::Inc,
+"""Per-record latency of the sorted-map apply (SortedVectorMapStore::Inc,
 sorted_vector_map_store.hpp:305-337) on MI355X, for the C3 cost model.
 
 One row, one wave: the row's image is first filled to n entries, then one call of 16
@@ -61,31 +61,30 @@ def main():
         srv.close()
         return ms * 1e6, incs
 
-    res = {"found": {}, "found_small": {}, "insert": {}, "fixed_ns_small": {}}
-    for mode in ("found", "insert"):
-        # found: 16 x 64 Incs (the call can add 1,024 entries: the 1,024-entry image);
-        # insert: 4 x 64 new keys, n -> n + 256
-        nmsg = {"found": 16, "insert": 4}[mode]
-        for n in {"found": (32, 64, 128, 192, 256, 384, 512, 768, 960), "insert": (0, 128, 256, 512, 768)}[mode]:
-            t = [one_call(n, nmsg, mode, rep) for rep in range(args.reps)]
-            res[mode][n] = round(float(np.median([a / b for a, b in t])), 1)
-            print(mode, n, res[mode][n], "ns/Inc", flush=True)
-    # found_small: the 256-entry image (n + the call's Incs <= 256): one call of 64 Incs and
-    # one of 128-192, the per-Inc latency from the difference (the launch's fixed cost cancels)
-    for n in (32, 64, 96, 128):
-        k2 = min(3, (256 - n) // 64)
-        t1 = np.median([one_call(n, 1, "found", rep)[0] for rep in range(args.reps)])
-        t2 = np.median([one_call(n, k2, "found", rep)[0] for rep in range(args.reps)])
-        res["found_small"][n] = round(float((t2 - t1) / (64 * (k2 - 1))), 1)
-        res["fixed_ns_small"][n] = round(float(t1 - 64 * res["found_small"][n]), 1)
-        print("found_small", n, res["found_small"][n], "ns/Inc, fixed", res["fixed_ns_small"][n], "ns", flush=True)
-    out = {"what": "ns per SortedVectorMapStore::Inc in one wave's dependent chain (one row, one wave; median of "
-                   "reps; ordered_apply launch time / Incs). found: 16 records x 64 existing keys (add in place) on "
-                   "an image of n entries, the 1,024-entry register image; found_small: the 256-entry image, from "
-                   "calls of 64 and 128-192 existing-key Incs (fixed_ns_small: the launch's fixed part). insert: 4 records x 64 "
-                   "new keys, the image growing n -> n + 256.",
-           "found_ns": res["found"], "found_small_ns": res["found_small"], "insert_ns": res["insert"],
-           "fixed_ns_small": res["fixed_ns_small"]}
+    # Per RECORD of found keys (the sorted-map apply adds a record chunk's found keys at once,
+    # found_run in psx_ordered.hip): the difference of two calls' launch times cancels the
+    # launch's fixed part.  found: 16 vs 4 records of 64 existing keys (the 1,024-entry
+    # image); found_small: 3 vs 1 records (n + 192 <= 256: the 256-entry image).  insert:
+    # ns per new key, 4 records x 64 new keys (n -> n + 256), launch time / Incs.
+    def med(n, nmsg, mode):
+        return float(np.median([one_call(n, nmsg, mode, rep)[0] for rep in range(args.reps)]))
+    res = {"found_rec": {}, "found_small_rec": {}, "insert": {}}
+    for n in (64, 128, 192, 256, 384, 512, 768, 960):
+        res["found_rec"][n] = round((med(n, 16, "found") - med(n, 4, "found")) / 12, 1)
+        print("found_rec", n, res["found_rec"][n], "ns/record", flush=True)
+    for n in (32, 64):
+        res["found_small_rec"][n] = round((med(n, 3, "found") - med(n, 1, "found")) / 2, 1)
+        print("found_small_rec", n, res["found_small_rec"][n], "ns/record", flush=True)
+    for n in (0, 128, 256, 512, 768):
+        t = [one_call(n, 4, "insert", rep) for rep in range(args.reps)]
+        res["insert"][n] = round(float(np.median([a / b for a, b in t])), 1)
+        print("insert", n, res["insert"][n], "ns/Inc", flush=True)
+    out = {"what": "ns per record of 64 found keys in one wave's dependent chain (one row, one wave; median of reps; "
+                   "difference of two ordered_apply launch times, so the launch's fixed part cancels): found_rec on "
+                   "the 1,024-entry register image (16 vs 4 records), found_small_rec on the 256-entry image (3 vs 1 "
+                   "records); insert: ns per new key (4 records x 64 new keys, the image growing n -> n + 256, launch "
+                   "time / Incs).",
+           "found_rec_ns": res["found_rec"], "found_small_rec_ns": res["found_small_rec"], "insert_ns": res["insert"]}
     print(json.dumps(out))
     if args.out:
         json.dump(out, open(args.out, "w"), indent=1)

@@ -260,18 +260,20 @@ C3_LATENCY_JSON = os.path.join(ROOT, "profiles", "r02", "c3_inc_latency.json")
 C3_WAVES_PER_SIMD = {4: 5, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
 
 
-def c3_model(batches, rows, K, apply_ms):
+def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20):
     """The sorted-map apply's bound ("C3 bound").  A row's records are one
-    dependent chain in one wave; each record's found keys (a chunk of <= 64 columns) are
-    added at once (found_run), so at steady state (every column of a step already present)
-    a row costs t_r = R_r x L(n_r): R_r records per step at image size n_r, L(n) the
-    measured per-record latency of a lone wave on the kernel the row takes
-    (tools/probe_inc_latency.py -> profiles/r02/c3_inc_latency.json).  Rows are independent
-    waves, w of them resident per SIMD (5 for the 256-entry image, 3 for the 1,024-entry
-    one), 1,024 SIMDs:
+    dependent chain in one wave: each record's found keys (a chunk of <= 64 columns) are
+    added at once (found_run), each new key is one LinearSearchAndMove insert.  So a row
+    costs t_r = R_r x Lrec(n_r) + I_r x Lins(n_r): R_r records and I_r inserts per step at
+    image size n_r, Lrec / Lins the measured latencies of a lone wave on the kernel the row
+    takes (tools/probe_inc_latency.py -> profiles/r02/c3_inc_latency.json).  I_r is exact
+    for the timed steps: the bench repeats the same batches, so the value of (row, col)
+    before its k-th Inc of step s is s x S + P_k (S its net per step, P_k the partial sum
+    before the Inc in message order), and the Inc inserts iff that is 0.  Rows are
+    independent waves, w of them resident per SIMD (5 for the 256-entry image, 3 for the
+    1,024-entry one), 1,024 SIMDs:
         T >= max( max_r t_r ,  sum_r t_r / (w_r x 1024) )
-    (critical path vs latency-interleave throughput; optimistic: no issue contention, no
-    inserts).  n_r = columns with a nonzero net value over the step's batches."""
+    (critical path vs latency-interleave throughput; optimistic: no issue contention)."""
     import numpy as np
     if not os.path.exists(C3_LATENCY_JSON):
         return None
@@ -289,20 +291,42 @@ def c3_model(batches, rows, K, apply_ms):
     v = np.concatenate([v for recs in batches for _, _, v in recs]).astype(np.int64)
     R_r = np.bincount(r, minlength=rows).astype(np.float64)
     k_r = np.bincount(rc, minlength=rows).astype(np.float64)
-    uniq, inv = np.unique(rc * K + c, return_inverse=True)
-    net = np.bincount(inv, weights=v)
+    key = rc * K + c
+    order = np.argsort(key, kind="stable")                     # message order within a key
+    ks, vs = key[order], v[order]
+    uniq, start, cnt = np.unique(ks, return_index=True, return_counts=True)
+    grp = np.repeat(np.arange(uniq.size), cnt)
+    csum = np.cumsum(vs)
+    base = np.repeat(csum[start] - vs[start], cnt)
+    before = csum - vs - base                                  # P_k
+    S = np.repeat(np.add.reduceat(vs, start), cnt)
+    nz = vs != 0
+    ins = np.zeros(vs.size, np.float64)
+    zero_S = (S == 0) & nz
+    ins[zero_S] = (before[zero_S] == 0)
+    m = (S != 0) & nz & (before % np.where(S == 0, 1, S) == 0)
+    sk = -before[m] // S[m]
+    ins[m] = ((sk >= warmup) & (sk < warmup + steps)) / steps
+    I_r = np.bincount(uniq[grp] // K, weights=ins, minlength=rows)
+    net = np.add.reduceat(vs, start)
     n_r = np.bincount(uniq[net != 0] // K, minlength=rows).astype(np.float64)
-    big = n_r + k_r > 256                                          # the 1,024-entry launch
-    x16, y16 = curve("found_rec_ns")                               # 1,024-entry image
-    x4, y4 = curve("found_small_rec_ns")                           # 256-entry image
-    t_r = R_r * np.where(big, np.interp(n_r, x16, y16), np.interp(n_r, x4, y4)) * 1e-6   # ms
+    big = n_r + k_r > 256                                      # the 1,024-entry launch
+    x16, y16 = curve("found_rec_ns")                           # 1,024-entry image
+    x4, y4 = curve("found_small_rec_ns")                       # 256-entry image
+    xi, yi = curve("insert_ns")
+    t_r = (R_r * np.where(big, np.interp(n_r, x16, y16), np.interp(n_r, x4, y4))
+           + I_r * np.interp(n_r, xi, yi)) * 1e-6              # ms
     chain = float(t_r.max())
     tput = float((t_r[~big].sum() / C3_WAVES_PER_SIMD[4] + t_r[big].sum() / C3_WAVES_PER_SIMD[16]) / 1024)
     bound = max(chain, tput)
+    hot = int(np.argmax(t_r))
     return {"bound_ms": round(bound, 4), "critical_path_ms": round(chain, 4), "interleave_ms": round(tput, 4),
             "ordered_apply_ms": round(apply_ms, 4), "frac_of_bound": round(bound / apply_ms, 3) if apply_ms else None,
             "rows_touched": int((R_r > 0).sum()), "rows_1024_image": int(big.sum()),
-            "max_records_per_row": int(R_r.max()), "max_incs_per_row": int(k_r.max()), "max_image": int(n_r.max()),
+            "inserts_per_step": round(float(I_r.sum()), 1),
+            "hot_row": {"records": int(R_r[hot]), "incs": int(k_r[hot]), "inserts": round(float(I_r[hot]), 1),
+                        "image": int(n_r[hot])},
+            "max_incs_per_row": int(k_r.max()), "max_image": int(n_r.max()),
             "latency_source": os.path.relpath(C3_LATENCY_JSON, ROOT)}
 
 
@@ -350,9 +374,11 @@ def c3_cpu_baseline(args, batches, nupd, bgs, seconds):
                       f"1 thread: {n1} steps in {e1:.1f} s (oracle restatement of sorted_vector_map_store.hpp Inc)"}
 
 
-def c3_measure(args, indexed, steps, warmup, cpu_seconds):
+def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
     """Sparse int count rows (C3) on 1 GPU: updates/s (and stream GB/s), the ordered apply
-    against its latency model, and (cpu_seconds > 0) the CPU port on the same batches."""
+    against its latency model, and (cpu_seconds > 0) the CPU port on the same batches.
+    pipeline: psx_ctx_set_pipeline(PSX_PIPELINE_ALL) — each call's decode runs on the side
+    stream beside the previous call's apply (the messages are resident before the call)."""
     import numpy as np
     import torch
     import parameter_server_amd as psa
@@ -364,6 +390,8 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds):
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
     srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
                                      oplog_dense_serialized=False, max_rows=rows, max_entries=K))
+    if pipeline:
+        srv.set_pipeline(2)
     ver = [0]
     idx = None
     if indexed:   # the producer's record index (psx_pack_stream emits the same), built before timing
@@ -412,7 +440,9 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds):
         "ms_per_step": round(el / steps * 1e3, 4), "higher_is_better": True,
         "dtype": "int32", "data": "synthetic (Zipf rows, uniform nnz 1..32, values +-1..3)",
         "config": {"workload": f"C3: {rows} rows x K={K}, {B} batches x 10000 rows/step"
-                               + (", producer record index (psx_apply_indexed)" if indexed else ""),
+                               + (", producer record index (psx_apply_indexed)" if indexed else "")
+                               + (", decode overlapped with the previous call's apply (PSX_PIPELINE_ALL)"
+                                  if pipeline else ""),
                    "updates_per_step": nupd, "stream_bytes_per_step": stream_bytes},
         "ordered_apply_ms_per_step": round(apply_ms / max(apply_n, 1), 4),
         "kernel_ms_per_step_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
@@ -421,7 +451,11 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds):
 
 
 def run_c3(args):
-    print(json.dumps(c3_measure(args, args.indexed, args.steps, args.warmup, args.cpu_seconds)), flush=True)
+    m = c3_measure(args, args.indexed, args.steps, args.warmup, args.cpu_seconds)
+    p = c3_measure(args, args.indexed, args.steps, args.warmup, 0.0, pipeline=True)
+    m["pipelined"] = {k: p[k] for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step")}
+    m["pipelined"]["what"] = p["config"]["workload"]
+    print(json.dumps(m), flush=True)
 
 
 def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242):
@@ -848,9 +882,10 @@ def main():
             exchange = {"error": repr(e)[:400]}
     if extras and world == 1:
         other = {}
-        for name, ix in (("C3_walked", False), ("C3_indexed", True)):
+        for name, ix, pl in (("C3_walked", False, False), ("C3_walked_pipelined", False, True),
+                             ("C3_indexed", True, False)):
             try:
-                m = c3_measure(args, ix, 20, 3, min(args.cpu_seconds, 6.0) if not ix else 0.0)
+                m = c3_measure(args, ix, 20, 3, min(args.cpu_seconds, 6.0) if not (ix or pl) else 0.0, pipeline=pl)
                 other[name] = {k: m[k] for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step",
                                                  "kernel_ms_per_step_breakdown_pass", "cpu_baseline")}
                 other[name]["config"] = m["config"]["workload"]

@@ -81,9 +81,30 @@ __device__ __forceinline__ void locate(const OrdArgs &a, const RecSpace &rs, int
   off = rs.sparse[b] ? a.recoff[rs.first[b] + k] : (uint64_t)(rs.first[b] + k * a.stride);
 }
 
+// Does any column of the sparse record at p lie outside [0, lim)?  Eight loads in flight
+// per step, no early exit (the columns are one record's, a few cache lines).
+__device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
+  const int32_t n = o_ld32(p + 4);
+  const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
+  const uint32_t ul = lim > 0x7fffffff ? 0xffffffffu : (uint32_t)lim;
+  bool bad = false;
+  int32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = (uint32_t)cols[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bad |= c[k] >= ul;   // negative columns wrap above lim
+  }
+  for (; i < n; ++i) bad |= (uint32_t)cols[i] >= ul;
+  return bad;
+}
+
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
+  // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
+  if (!o_gate(a)) return;
   if (threadIdx.x == 0) build_space(a, rs);
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
@@ -107,17 +128,11 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
       } else {
         if (!a.dense_records && a.kind == 0) {
           // sparse record into a dense row: every column must lie inside the row
-          const int32_t n = o_ld32(p + 4);
-          const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
-          for (int32_t i = 0; i < n; ++i)
-            if (cols[i] < 0 || cols[i] >= a.row_cap) { atomicOr(a.call_status, kStCapacity); break; }
+          if (cols_outside(p, a.row_cap)) atomicOr(a.call_status, kStCapacity);
         } else if (a.kind != 0 && a.keyflag && !*a.keyflag) {
           // sorted/map rows: while every key stays in [0, max_entries) no row can hold
           // more than max_entries entries and the capacity dry run is skipped
-          const int32_t n = o_ld32(p + 4);
-          const int32_t *cols = reinterpret_cast<const int32_t *>(p + 8);
-          for (int32_t i = 0; i < n; ++i)
-            if (cols[i] < 0 || cols[i] >= a.max_entries) { atomicOr(a.keyflag, 1u); break; }
+          if (cols_outside(p, a.max_entries)) atomicOr(a.keyflag, 1u);
         }
         if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
         first = atomicAdd(&a.cnt[s], 1) == 0;
@@ -145,6 +160,7 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
   if (a.nsplit && blockIdx.x == 0 && threadIdx.x < 2) a.nsplit[threadIdx.x] = 0;
+  if (!o_gate(a)) return;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
     int b;
     uint64_t off;
@@ -627,13 +643,15 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
   __shared__ int16_t s_pos[4][1024];   // the register kernels serve max_entries <= 1,024
   __shared__ V s_sv[4][J * 64];        // found_run: deltas by entry (zero between runs), compaction values
   __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
-  if (threadIdx.x == 0) build_space(a, rs);
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
+  const bool go = o_gate(a) && (!DRY || *a.keyflag);
+  // blocks past the touched rows leave before any setup (the grid is sized by max_rows)
+  if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched) return;
+  if (threadIdx.x == 0) build_space(a, rs);
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
   __syncthreads();
-  const bool go = o_gate(a) && (!DRY || *a.keyflag);
   const bool pos_ok = a.keyflag && !*a.keyflag && a.max_entries <= 1024;
   int16_t *pos = s_pos[wib];
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
@@ -689,6 +707,7 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
         val[j] = i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
       }
       bool use_pos = pos_ok;
+      bool pos_dirty = false;   // sorted rows: inserts not yet written to the key map
       if (use_pos) {
         bool out = false;
 #pragma unroll
@@ -770,6 +789,16 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
               if (use_pos) {
                 // the found keys up to the chunk's next insert, at once (found_run)
                 if (stale) {
+                  if (pos_dirty) {   // inserts since the map was last written: rewrite it
+                    wave_sync();
+#pragma unroll
+                    for (int j = 0; j < J; ++j) {
+                      const int32_t i = j * 64 + lane;
+                      if (j * 64 < n && i < n) pos[key[j]] = (int16_t)i;
+                    }
+                    wave_sync();
+                    pos_dirty = false;
+                  }
                   my_idx = lane < cnt ? (int32_t)pos[my_col] : -1;
                   stale = false;
                 }
@@ -778,7 +807,10 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
                 const int32_t run_end = ins ? (int32_t)__builtin_ctzll(ins) : cnt;
                 if (run_end > t) {
                   const bool run = live && lane < run_end;
-                  if (__ballot(run)) n = found_run<V, J>(key, val, n, run, my_idx, my_d, lane, s_sv[wib], s_ck[wib], pos, stale);
+                  if (__ballot(run)) {
+                    n = found_run<V, J>(key, val, n, run, my_idx, my_d, lane, s_sv[wib], s_ck[wib], pos, stale);
+                    if (stale) pos_dirty = false;   // the compaction rewrote the whole map
+                  }
                   t = run_end - 1;
                   continue;
                 }
@@ -851,7 +883,12 @@ __global__ void __launch_bounds__(256) ordered_apply_reg_kernel(OrdArgs a) {
                   val[j] = d;
                 }
               ++n;
-              if (use_pos) {   // entries [p, n) moved or arrived: their new indices
+              if (KIND == 1 && use_pos) {
+                // entries [p, n) moved up one: the chunk's other looked-up indices follow
+                // arithmetically; the key map is rewritten before the next lookup
+                my_idx += my_idx >= p ? 1 : 0;
+                pos_dirty = true;
+              } else if (use_pos) {   // entries [p, n) moved or arrived: their new indices
                 stale = true;
                 wave_sync();
 #pragma unroll

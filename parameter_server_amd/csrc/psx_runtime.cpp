@@ -412,7 +412,11 @@ bool has_sparse_serialized(const psx_ctx *c) {
 
 // Window-parallel decode (psx_walk.hip): 32 KiB windows; a call runs it when its messages
 // have at most kWalkMaxItems (message, window) items (B x the largest message's windows:
-// 4 GiB of windows), on one 1,024-thread block per CU.
+// 4 GiB of windows), on 1,024-thread blocks (147 KB of LDS: one per CU) on half the CUs.
+// The walk is bound by its window-to-window hand-offs (~1.7 us each), which ~100 blocks
+// keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
+// work takes ~15-20 us); the other half of the chip stays free for the previous call's
+// apply when the decode is pipelined (psx_ctx_set_pipeline).
 constexpr uint64_t kWalkWindowBytes = 32768;
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
@@ -420,7 +424,7 @@ unsigned walk_blocks(psx_ctx *c) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
     cus = 256;
-  return (unsigned)cus;
+  return (unsigned)std::max(1, cus / 2);
 }
 
 // Smallest record of any table in the context: bounds the records a message can hold

@@ -46,7 +46,8 @@ def main():
         msgs = []
         for b in range(nmsg):
             if mode != "insert":
-                cols = np.sort(rng.choice(have, size=min(64, n), replace=False)).astype(np.int32)
+                k = min(24 if mode == "found24" else 64, n)
+                cols = np.sort(rng.choice(have, size=k, replace=False)).astype(np.int32)
             else:
                 cols = np.sort(fresh[64 * b:64 * (b + 1)]).astype(np.int32)
             msgs.append(wire.sparse_stream_np(3, 4, [(0, cols, np.ones(cols.size, np.int32))]))
@@ -72,8 +73,8 @@ def main():
     for n in (64, 128, 192, 256, 384, 512, 768, 960):
         res["found_rec"][n] = round((med(n, 16, "found") - med(n, 4, "found")) / 12, 1)
         print("found_rec", n, res["found_rec"][n], "ns/record", flush=True)
-    for n in (32, 64):
-        res["found_small_rec"][n] = round((med(n, 3, "found") - med(n, 1, "found")) / 2, 1)
+    for n in (32, 64):   # records of 24 keys: 8 of them add <= 192 entries (n + 192 <= 256)
+        res["found_small_rec"][n] = round((med(n, 8, "found24") - med(n, 2, "found24")) / 6, 1)
         print("found_small_rec", n, res["found_small_rec"][n], "ns/record", flush=True)
     for n in (0, 128, 256, 512, 768):
         t = [one_call(n, 4, "insert", rep) for rep in range(args.reps)]
@@ -81,8 +82,8 @@ def main():
         print("insert", n, res["insert"][n], "ns/Inc", flush=True)
     out = {"what": "ns per record of 64 found keys in one wave's dependent chain (one row, one wave; median of reps; "
                    "difference of two ordered_apply launch times, so the launch's fixed part cancels): found_rec on "
-                   "the 1,024-entry register image (16 vs 4 records), found_small_rec on the 256-entry image (3 vs 1 "
-                   "records); insert: ns per new key (4 records x 64 new keys, the image growing n -> n + 256, launch "
+                   "the 1,024-entry register image (16 vs 4 records), found_small_rec on the 256-entry image (8 vs 2 "
+                   "records of 24 keys); insert: ns per new key (4 records x 64 new keys, the image growing n -> n + 256, launch "
                    "time / Incs).",
            "found_rec_ns": res["found_rec"], "found_small_rec_ns": res["found_small_rec"], "insert_ns": res["insert"]}
     print(json.dumps(out))

@@ -257,7 +257,7 @@ def c3_streams(rows=100_000, K=1024, B=8, per_batch=10_000, seed=1234, with_reco
 
 
 C3_LATENCY_JSON = os.path.join(ROOT, "profiles", "r02", "c3_inc_latency.json")
-C3_WAVES_PER_SIMD = {4: 5, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
+C3_WAVES_PER_SIMD = {4: 7, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
 
 
 def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20):
@@ -270,7 +270,7 @@ def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20):
     for the timed steps: the bench repeats the same batches, so the value of (row, col)
     before its k-th Inc of step s is s x S + P_k (S its net per step, P_k the partial sum
     before the Inc in message order), and the Inc inserts iff that is 0.  Rows are
-    independent waves, w of them resident per SIMD (5 for the 256-entry image, 3 for the
+    independent waves, w of them resident per SIMD (7 for the 256-entry image, 3 for the
     1,024-entry one), 1,024 SIMDs:
         T >= max( max_r t_r ,  sum_r t_r / (w_r x 1024) )
     (critical path vs latency-interleave throughput; optimistic: no issue contention)."""

@@ -153,7 +153,7 @@ struct OrdArgs {
   int32_t *cnt;
   int32_t *off;
   int32_t *tsum;
-  int32_t *list;
+  uint64_t *list;         // records grouped by slot: (message << 56) | byte offset of the row id
   int32_t *touched;       // slots with >= 1 record this call (unordered)
   uint32_t *ntouched;     // its length (zeroed by decode_streams)
   void *dense;

@@ -81,6 +81,15 @@ __device__ __forceinline__ void locate(const OrdArgs &a, const RecSpace &rs, int
   off = rs.sparse[b] ? a.recoff[rs.first[b] + k] : (uint64_t)(rs.first[b] + k * a.stride);
 }
 
+// A record list entry: (message << 56) | byte offset of the record's row id.  Sorting
+// entries as integers orders the records as the reference applies them (message, then
+// position), and the apply reaches a record without the record-offset table.
+constexpr uint64_t kRefOffMask = (1ull << 56) - 1;
+__device__ __forceinline__ uint64_t rec_ref(int b, uint64_t off) { return ((uint64_t)b << 56) | off; }
+__device__ __forceinline__ const uint8_t *rec_ptr(const OrdArgs &a, uint64_t e) {
+  return a.ss.data[e >> 56] + (e & kRefOffMask);
+}
+
 // Does any column of the sparse record at p lie outside [0, lim)?  Eight loads in flight
 // per step, no early exit (the columns are one record's, a few cache lines).
 __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
@@ -168,7 +177,7 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
     const int64_t s = o_slot(o_ld32(a.ss.data[b] + off), a);
     if (s < 0) continue;
     const int32_t p = atomicSub(&a.cnt[s], 1) - 1;
-    a.list[a.off[s] + p] = (int32_t)r;
+    a.list[a.off[s] + p] = rec_ref(b, off);
   }
 }
 
@@ -264,17 +273,22 @@ template <typename V> struct Ent {
   static constexpr int VO = sizeof(V) == 4 ? 4 : 8;
 };
 
-// Sort the r-list of one slot (L <= 64) by value, one entry per lane: rank = number of
-// smaller entries (r values are distinct).
-__device__ __forceinline__ int32_t wave_rank_sort(int32_t r, int L, int lane, int32_t *scratch) {
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, int k) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, k, 64), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), k, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Sort the record list of one slot (L <= 64) by value, one entry per lane: rank = number
+// of smaller entries (entries are distinct).
+__device__ __forceinline__ uint64_t wave_rank_sort(uint64_t r, int L, int lane, uint64_t *scratch) {
   int rank = 0;
   for (int k = 0; k < L; ++k) {
-    const int32_t x = __shfl(r, k, 64);
+    const uint64_t x = shfl64(r, k);
     rank += (x < r) ? 1 : 0;
   }
   if (lane < L) scratch[rank] = r;
   wave_sync();
-  const int32_t out = lane < L ? scratch[lane] : 0;
+  const uint64_t out = lane < L ? scratch[lane] : 0;
   wave_sync();
   return out;
 }
@@ -293,10 +307,7 @@ __device__ __forceinline__ double sparse_importance(const uint8_t *vals, int32_t
 template <typename V, int KIND, bool DRY = false>
 __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
   extern __shared__ __align__(16) uint8_t dyn[];
-  __shared__ int32_t sort_scratch[4][64];
-  __shared__ RecSpace rs;
-  if (threadIdx.x == 0) build_space(a, rs);
-  __syncthreads();
+  __shared__ uint64_t sort_scratch[4][64];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   if (wib >= wpb) return;
@@ -316,25 +327,20 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
     {
       const int32_t beg = __builtin_amdgcn_readfirstlane(a.off[slot]);
       const int32_t L = __builtin_amdgcn_readfirstlane(a.off[slot + 1]) - beg;
-      int32_t *lst = a.list + beg;
+      uint64_t *lst = a.list + beg;
       if constexpr (DRY) {
         int32_t grow = 0;
-        for (int32_t q = lane; q < L; q += 64) {
-          int b;
-          uint64_t roff;
-          locate(a, rs, lst[q], b, roff);
-          grow += o_ld32(a.ss.data[b] + roff + 4);
-        }
+        for (int32_t q = lane; q < L; q += 64) grow += o_ld32(rec_ptr(a, lst[q]) + 4);
         grow = wave_sum_i32(grow);
         if ((int64_t)a.nent[slot] + grow <= a.max_entries) continue;
       }
-      // order the slot's records by r = (message, position)
-      int32_t mine = 0;
+      // order the slot's records by (message, position)
+      uint64_t mine = 0;
       if (L <= 64) {
-        mine = wave_rank_sort(lane < L ? lst[lane] : 0x7fffffff, L, lane, sort_scratch[wib]);
+        mine = wave_rank_sort(lane < L ? lst[lane] : ~0ull, L, lane, sort_scratch[wib]);
       } else if (lane == 0) {
         for (int32_t i = 1; i < L; ++i) {   // rare: > 64 records for one row in one call
-          const int32_t x = lst[i];
+          const uint64_t x = lst[i];
           int32_t j = i - 1;
           while (j >= 0 && lst[j] > x) { lst[j + 1] = lst[j]; --j; }
           lst[j + 1] = x;
@@ -359,11 +365,8 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
 
       bool over = false;   // DRY: this row would exceed max_entries
       for (int32_t q = 0; q < L && !over; ++q) {
-        const int32_t r = L <= 64 ? __shfl(mine, q, 64) : lst[q];
-        int b;
-        uint64_t roff;
-        locate(a, rs, r, b, roff);
-        const uint8_t *rec = a.ss.data[b] + roff;
+        const uint64_t r = L <= 64 ? shfl64(mine, q) : lst[q];
+        const uint8_t *rec = rec_ptr(a, r);
         if (a.dense_records) {
           // duplicate-row replay of a dense record: row[e] += rec[e] (lane owns e)
           double p = 0.0;
@@ -638,8 +641,7 @@ __device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int
 // VGPR file's limit for J = 16.
 template <typename V, int KIND, int J, bool DRY = false>
 __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
-  __shared__ RecSpace rs;
-  __shared__ int32_t sort_scratch[4][64];
+  __shared__ uint64_t sort_scratch[4][64];
   // Key -> entry-index map of the wave's row (FindIndex in one LDS read instead of J
   // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
   // per row at load): int16 per key, -1 = absent.
@@ -651,7 +653,6 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   const bool go = o_gate(a) && (!DRY || *a.keyflag);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows)
   if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched) return;
-  if (threadIdx.x == 0) build_space(a, rs);
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
   __syncthreads();
@@ -672,14 +673,14 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
     {
       const int32_t beg = __builtin_amdgcn_readfirstlane(a.off[slot]);
       const int32_t L = __builtin_amdgcn_readfirstlane(a.off[slot + 1]) - beg;
-      int32_t *lst = a.list + beg;
-      int32_t mine = 0;
+      uint64_t *lst = a.list + beg;
+      uint64_t mine = 0;
       if (L <= 64) {
-        mine = wave_rank_sort(lane < L ? lst[lane] : 0x7fffffff, L, lane, sort_scratch[wib]);
+        mine = wave_rank_sort(lane < L ? lst[lane] : ~0ull, L, lane, sort_scratch[wib]);
       } else {
         if (lane == 0) {
           for (int32_t i = 1; i < L; ++i) {
-            const int32_t x = lst[i];
+            const uint64_t x = lst[i];
             int32_t j = i - 1;
             while (j >= 0 && lst[j] > x) { lst[j + 1] = lst[j]; --j; }
             lst[j + 1] = x;
@@ -691,12 +692,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       int32_t n = __builtin_amdgcn_readfirstlane(a.nent[slot]);
       if constexpr (DRY) {
         int32_t grow = 0;
-        for (int32_t q = lane; q < L; q += 64) {
-          int b;
-          uint64_t roff;
-          locate(a, rs, L <= 64 ? mine : lst[q], b, roff);
-          grow += o_ld32(a.ss.data[b] + roff + 4);
-        }
+        for (int32_t q = lane; q < L; q += 64) grow += o_ld32(rec_ptr(a, L <= 64 ? mine : lst[q]) + 4);
         if ((int64_t)n + wave_sum_i32(grow) <= (int64_t)cap) continue;
       }
       // load the row image
@@ -736,7 +732,8 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       uint64_t hoff = 0;
       int32_t hn = 0;
       if (L <= 64 && lane < L) {
-        locate(a, rs, mine, hb, hoff);
+        hb = (int)(mine >> 56);
+        hoff = mine & kRefOffMask;
         hn = o_ld32(a.ss.data[hb] + hoff + 4);
       }
       auto rec_at = [&](int32_t q, const uint8_t *&rec, int32_t &nn) {
@@ -748,10 +745,11 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
                 (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)hoff, q);
           nn = __builtin_amdgcn_readlane(hn, q);
         } else {
-          locate(a, rs, __builtin_amdgcn_readfirstlane(lst[q]), b, off);
-          b = __builtin_amdgcn_readfirstlane(b);
-          off = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(off >> 32)) << 32) |
-                (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)off);
+          const uint64_t e = lst[q];
+          const uint64_t eu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(e >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)e);
+          b = (int)(eu >> 56);
+          off = eu & kRefOffMask;
           nn = __builtin_amdgcn_readfirstlane(o_ld32(a.ss.data[b] + off + 4));
         }
         rec = a.ss.data[b] + off;

@@ -216,7 +216,7 @@ struct psx_ctx {
   uint8_t *d_zero = nullptr;
   uint8_t *d_staging = nullptr;
   size_t staging_cap = 0;
-  int32_t *d_list = nullptr;             // ordered path: record lists
+  uint64_t *d_list = nullptr;            // ordered path: record lists ((message << 56) | offset)
   size_t list_cap = 0;
   std::vector<PendingCall> pending;      // calls since the last psx_sync (duplicate-row replay)
   int64_t call_seq = 0;
@@ -482,7 +482,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       if (c->d_list) hipFree(c->d_list);
       c->d_list = nullptr;
       c->list_cap = 0;
-      HIP_TRY(c, hipMalloc(&c->d_list, list_need * sizeof(int32_t)));
+      HIP_TRY(c, hipMalloc(&c->d_list, list_need * sizeof(uint64_t)));
       c->list_cap = list_need;
     }
   }

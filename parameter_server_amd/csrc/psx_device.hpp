@@ -171,8 +171,10 @@ struct OrdArgs {
                           // (from then on every call runs the capacity dry run)
   int32_t *grow;          // split tables (256 < max_entries <= 1024): entries the call's records
                           // can add per slot (zero between calls); null otherwise
-  int32_t *split;         // [2][max_rows]: touched slots whose image fits 256 entries, the rest
+  int32_t *split;         // [2][max_rows] row descriptors {slot, list begin, list end, image
+                          // size} (int4): touched slots whose image fits 256 entries, the rest
   uint32_t *nsplit;       // the two lists' lengths
+  int32_t desc;           // 1: `touched` holds split-list row descriptors (the apply launches)
 };
 
 // A side stream and two events for launches that run beside the context stream.

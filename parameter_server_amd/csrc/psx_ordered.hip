@@ -184,6 +184,8 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
 // ordered_classify (split tables): a touched row whose image can outgrow 256 entries in
 // this call (entries now + its records' entries) goes to the 1,024-entry list, the rest
 // to the 256-entry list; the two apply launches then run concurrently.  grow returns to 0.
+// A list entry is the row's descriptor {slot, list begin, list end, image size}: the
+// apply starts a row with one load instead of a slot load and then three dependent ones.
 __global__ void __launch_bounds__(256) ordered_classify_kernel(OrdArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t nt = (int64_t)*a.ntouched;
@@ -191,12 +193,13 @@ __global__ void __launch_bounds__(256) ordered_classify_kernel(OrdArgs a) {
   const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
   for (int64_t i0 = base0; i0 < nt; i0 += G) {
     const int64_t i = i0 + lane;
-    int32_t s = 0;
+    int32_t s = 0, nen = 0;
     bool big = false;
     const bool have = i < nt;
     if (have) {
       s = a.touched[i];
-      big = (int64_t)a.nent[s] + a.grow[s] > 256;
+      nen = a.nent[s];
+      big = (int64_t)nen + a.grow[s] > 256;
       a.grow[s] = 0;
     }
 #pragma unroll
@@ -207,8 +210,10 @@ __global__ void __launch_bounds__(256) ordered_classify_kernel(OrdArgs a) {
       uint32_t base = 0;
       if (lane == leader) base = atomicAdd(&a.nsplit[k], (uint32_t)__builtin_popcountll(m));
       base = __builtin_amdgcn_readlane(base, leader);
-      if (have && big == (k == 1))
-        a.split[k * a.max_rows + base + __builtin_popcountll(m & ((1ull << lane) - 1))] = s;
+      if (have && big == (k == 1)) {
+        const int64_t at = k * a.max_rows + base + __builtin_popcountll(m & ((1ull << lane) - 1));
+        reinterpret_cast<int4 *>(a.split)[at] = int4{s, a.off[s], a.off[s + 1], nen};
+      }
     }
   }
 }
@@ -668,11 +673,22 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
     // per-row scalars are wave-uniform: readfirstlane keeps them in SGPRs so the row's
     // loops branch on SCC instead of running under exec masks
-    const int64_t slot = __builtin_amdgcn_readfirstlane(a.touched[ti]);
+    int64_t slot;
+    int32_t beg, L, n;
+    if (a.desc) {
+      const int4 d = reinterpret_cast<const int4 *>(a.touched)[ti];
+      slot = __builtin_amdgcn_readfirstlane(d.x);
+      beg = __builtin_amdgcn_readfirstlane(d.y);
+      L = __builtin_amdgcn_readfirstlane(d.z) - beg;
+      n = __builtin_amdgcn_readfirstlane(d.w);
+    } else {
+      slot = __builtin_amdgcn_readfirstlane(a.touched[ti]);
+      beg = __builtin_amdgcn_readfirstlane(a.off[slot]);
+      L = __builtin_amdgcn_readfirstlane(a.off[slot + 1]) - beg;
+      n = __builtin_amdgcn_readfirstlane(a.nent[slot]);
+    }
     if (!DRY && lane == 0) a.flags[slot] = 3;
     {
-      const int32_t beg = __builtin_amdgcn_readfirstlane(a.off[slot]);
-      const int32_t L = __builtin_amdgcn_readfirstlane(a.off[slot + 1]) - beg;
       uint64_t *lst = a.list + beg;
       uint64_t mine = 0;
       if (L <= 64) {
@@ -689,7 +705,6 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __builtin_amdgcn_wave_barrier();
       }
-      int32_t n = __builtin_amdgcn_readfirstlane(a.nent[slot]);
       if constexpr (DRY) {
         int32_t grow = 0;
         for (int32_t q = lane; q < L; q += 64) grow += o_ld32(rec_ptr(a, L <= 64 ? mine : lst[q]) + 4);
@@ -1073,8 +1088,9 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
       hipLaunchKernelGGL(ordered_classify_kernel, dim3(row_blocks(a.max_rows, 4)), dim3(256), 0, st, a);
       small.touched = a.split;
       small.ntouched = a.nsplit;
-      big.touched = a.split + a.max_rows;
+      big.touched = a.split + 4 * a.max_rows;
       big.ntouched = a.nsplit + 1;
+      small.desc = big.desc = 1;
       hipError_t e = hipEventRecord(fk.fork, st);
       if (e == hipSuccess) e = hipStreamWaitEvent(fk.aux, fk.fork, 0);
       if (e != hipSuccess) return e;

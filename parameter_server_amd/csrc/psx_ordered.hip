@@ -660,6 +660,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched) return;
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
+  for (int32_t k = lane; k < 1024; k += 64) s_pos[wib][k] = -1;
   __syncthreads();
   const bool pos_ok = a.keyflag && !*a.keyflag && a.max_entries <= 1024;
   int16_t *pos = s_pos[wib];
@@ -729,9 +730,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
           out = out || (j * 64 + lane < n && (key[j] < 0 || key[j] >= (int32_t)a.max_entries));
         use_pos = __ballot(out) == 0;
       }
-      if (use_pos) {
-        for (int32_t k = lane; k < (int32_t)a.max_entries; k += 64) pos[k] = -1;
-        wave_sync();
+      if (use_pos) {   // the map is all -1 between rows (cleared once, then per row below)
 #pragma unroll
         for (int j = 0; j < J; ++j)
           if (j * 64 + lane < n) pos[key[j]] = (int16_t)(j * 64 + lane);
@@ -984,6 +983,15 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
             }
           }
         }
+      }
+      if (use_pos) {
+        // back to all -1: every key the row ever mapped is in the final image or was
+        // unmapped when it left
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (j * 64 < n && j * 64 + lane < n) pos[key[j]] = -1;
+        wave_sync();
       }
       if (DRY) continue;
       // write the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)

@@ -410,14 +410,14 @@ bool has_sparse_serialized(const psx_ctx *c) {
   return false;
 }
 
-// Window-parallel decode (psx_walk.hip): 32 KiB windows; a call runs it when its messages
+// Window-parallel decode (psx_walk.hip): 48 KiB windows; a call runs it when its messages
 // have at most kWalkMaxItems (message, window) items (B x the largest message's windows:
-// 4 GiB of windows), on 1,024-thread blocks (147 KB of LDS: one per CU) on half the CUs.
+// 6 GiB of windows), on 1,024-thread blocks (149 KB of LDS: one per CU) on half the CUs.
 // The walk is bound by its window-to-window hand-offs (~1.7 us each), which ~100 blocks
 // keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
 // work takes ~15-20 us); the other half of the chip stays free for the previous call's
 // apply when the decode is pipelined (psx_ctx_set_pipeline).
-constexpr uint64_t kWalkWindowBytes = 32768;
+constexpr uint64_t kWalkWindowBytes = 49152;   // == psx_walk.hip kWBytes
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
 unsigned walk_blocks(psx_ctx *c) {

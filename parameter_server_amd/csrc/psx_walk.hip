@@ -12,7 +12,7 @@
 //               window range, the walker state at that table's first record.
 //   walk        persistent blocks of 1,024 threads take (window, message) tickets in
 //               window-major order.  Per window, speculatively for EVERY word q as a record
-//               start: the 1/2/4/8/16-record jump tables, then pointer jumping to the LAST
+//               start: the 1- and 16-record jump tables, then pointer jumping to the LAST
 //               record start on q's chain inside the window and the record count up to it
 //               (the window's exit map).  Then one wave waits for the predecessor window's
 //               walker state (8-byte {tag, value} granules written by atomics: the data is
@@ -33,17 +33,16 @@
 namespace psx {
 
 constexpr int kWalkThreads = 1024;
-constexpr int kWW = 8192;                       // words per window (32 KiB)
+constexpr int kWW = 12288;                      // words per window (48 KiB)
 constexpr uint64_t kWBytes = (uint64_t)kWW * 4;
-constexpr int kWLevels = 5;                     // jump tables: 1, 2, 4, 8, 16 records
 constexpr uint16_t kNo = 0xFFFFu;               // next record outside the window / bad header
 constexpr int kGran = 14;                       // granules per published walker state
 constexpr int kMaxSegs = kMaxTables;            // sparse tables with records in one window
 
 typedef unsigned long long __attribute__((address_space(1))) gu64;
 
-// Workspace of one call slot: [WalkCtl][WalkHead][granules: kGran per window item].  Only
-// the WalkCtl (16 bytes) is zeroed per call; the granules carry the call's epoch as tag.
+// Workspace of one call slot: [WalkCtl][WalkHead][granules: kGran per window item].
+// walk_head resets the ticket for its call; the granules carry the call's epoch as tag.
 constexpr size_t kWalkHeadOff = 256;
 
 // Walker state between windows.  mode 0: the next table header is at pos; 1: inside sparse
@@ -53,15 +52,14 @@ struct WalkState {
   int32_t k, t, mode, ntab;           // seen: bit t = table t met in this message (duplicate check)
 };
 
-struct WalkCtl {      // zeroed (hipMemsetAsync, 16 bytes) before every call
+struct WalkCtl {      // reset by walk_head for the walk of the same call
   uint32_t ticket;
-  uint32_t maxwin;    // max over messages of their window count
-  uint32_t pad[2];
+  uint32_t pad[3];
 };
 
 struct WalkHead {     // written by walk_head, read by the first window of each message
   WalkState st[kMaxFused];
-  uint32_t wfirst[kMaxFused];   // the message's first window (32 KiB grid from byte 0)
+  uint32_t wfirst[kMaxFused];   // the message's first window (48 KiB grid from byte 0)
   uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
 };
 constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
@@ -135,6 +133,7 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
     counters[t * kMaxFused + b] = 0;
     if (b == 0) ntouched[t] = 0;
   }
+  if (b == 0 && threadIdx.x == 0) ctl->ticket = 0;
   __syncthreads();
   if (threadIdx.x != 0) return;
   const uint8_t *p = ss.data[b];
@@ -161,7 +160,6 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
   if (s.mode == 1) {
     wf = (uint32_t)(s.pos / kWBytes);
     nwin = (uint32_t)((size + kWBytes - 1) / kWBytes) - wf;
-    atomicMax(&ctl->maxwin, nwin);
   }
   head->st[b] = s;
   head->wfirst[b] = wf;
@@ -193,17 +191,23 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                                                             uint32_t epoch) {
   gu64 *gran = (gu64 *)gran_p;
   __shared__ uint32_t win[kWW + 1];                 // + 1 halo word
-  __shared__ uint16_t jt[kWLevels][kWW];            // jt[l][q]: the record 2^l on from q, kNo if outside
-  __shared__ uint16_t xp[kWW];                      // exit map: last record start on q's chain in the window
-  __shared__ uint16_t xc[kWW];                      //           records from q up to it (exclusive)
+  __shared__ uint16_t jt0[kWW];                     // the next record from q, kNo if outside
+  // Exit map, packed: low 16 bits the last record start on q's chain inside the window, high
+  // 16 the records from q up to it (exclusive).  After the hand-off the same words hold the
+  // 16-record jump table jt4 (and its 2/8-record stage) for the expansion.
+  __shared__ uint32_t xm[kWW];
+  uint16_t *const tmp16 = reinterpret_cast<uint16_t *>(xm);
+  uint16_t *const jt4 = tmp16 + kWW;
   __shared__ uint16_t seg_q[kMaxSegs];
   __shared__ uint16_t seg_n[kMaxSegs];
   __shared__ uint64_t seg_rk[kMaxSegs];
-  __shared__ uint16_t a16[kWW / 16 + 1], a4[4], a1[4];
-  __shared__ uint32_t sh_nseg, sh_n16, sh_n4, sh_n1, sh_ticket;
+  __shared__ uint16_t a16[kWW / 32 + 1], a1[16];
+  __shared__ uint32_t sh_nseg, sh_n16, sh_n1, sh_ticket;
   const int tid = threadIdx.x;
   const int B = ss.n;
-  const uint32_t items = (uint32_t)B * ctl->maxwin;
+  uint32_t maxwin = 0;
+  for (int i = 0; i < B; ++i) maxwin = head->nwin[i] > maxwin ? head->nwin[i] : maxwin;
+  const uint32_t items = (uint32_t)B * maxwin;
 
   for (;;) {
     if (tid == 0) sh_ticket = atomicAdd(&ctl->ticket, 1u);
@@ -249,39 +253,27 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           if (nxt < nw && W0 + nxt * 4 <= size) v = (uint16_t)nxt;
         }
       }
-      jt[0][q] = v;
-      xp[q] = v == kNo ? (uint16_t)q : v;
-      xc[q] = v == kNo ? 0 : 1;
+      jt0[q] = v;
+      xm[q] = v == kNo ? q : ((uint32_t)v | (1u << 16));
     }
     __syncthreads();
-#pragma unroll
-    for (int lv = 1; lv < kWLevels; ++lv) {
-      for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
-        const uint16_t a = jt[lv - 1][q];
-        jt[lv][q] = a != kNo ? jt[lv - 1][a] : kNo;
-      }
-      __syncthreads();
-    }
-    // 3) exit map by pointer jumping (terminal records point to themselves with count 0)
+    // 3) exit map by pointer jumping (terminal records point to themselves with count 0):
+    //    one packed LDS word per lookup
     for (;;) {
       constexpr int PER = kWW / kWalkThreads;
-      uint16_t np[PER], nc[PER];
+      uint32_t nv[PER];
       bool changed = false;
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
-        const uint16_t a = xp[q];
-        np[k] = xp[a];
-        nc[k] = (uint16_t)(xc[q] + xc[a]);
-        changed |= np[k] != a;
+        const uint32_t v = xm[q];
+        const uint32_t t = xm[v & 0xFFFFu];
+        nv[k] = (t & 0xFFFFu) | (((v >> 16) + (t >> 16)) << 16);
+        changed |= (t & 0xFFFFu) != (v & 0xFFFFu);
       }
       const int any = __syncthreads_or(changed);
 #pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
-        xp[q] = np[k];
-        xc[q] = nc[k];
-      }
+      for (int k = 0; k < PER; ++k) xm[(uint32_t)tid + (uint32_t)k * kWalkThreads] = nv[k];
       __syncthreads();
       if (!any) break;
     }
@@ -332,8 +324,8 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           // sparse records from s.pos: one exit-map lookup
           const uint64_t q = (s.pos - W0) / 4;
           if (q >= nw) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }   // header past the end
-          const uint32_t T = xp[q];
-          const uint64_t c = (uint64_t)xc[q] + 1;                                    // records q .. T
+          const uint32_t T = xm[q] & 0xFFFFu;
+          const uint64_t c = (uint64_t)(xm[q] >> 16) + 1;                           // records q .. T
           const uint64_t take = s.left < c ? s.left : c;
           uint64_t endT = 0;
           if (take == c) {
@@ -359,8 +351,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
             // the table ends inside the chain: the record `take` on from q (binary lifting)
             uint32_t w = (uint32_t)q;
             uint64_t r = take;
-            for (int lv = kWLevels - 1; lv >= 0; --lv)
-              while (r >= (1ull << lv)) { w = jt[lv][w]; r -= 1ull << lv; }
+            for (; r; --r) w = jt0[w];   // once per table: its last window
             s.pos = W0 + (uint64_t)w * 4;
           }
           if (s.left == 0) {
@@ -384,61 +375,63 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       }
     }
     __syncthreads();
-    // 5) expand the window's record offsets (thread 0 collects hop starts, all threads fill)
+    // 5) expand the window's record offsets: the 16-record jump table by four squarings
+    //    (into the exit map's words, no longer needed), thread 0 collects hop starts, all
+    //    threads fill
     const uint32_t nseg = sh_nseg;
+    if (nseg) {
+      const uint16_t *src[4] = {jt0, tmp16, jt4, tmp16};
+      uint16_t *dst[4] = {tmp16, jt4, tmp16, jt4};
+#pragma unroll
+      for (int lv = 0; lv < 4; ++lv) {
+        uint16_t r[kWW / kWalkThreads];
+#pragma unroll
+        for (int k = 0; k < kWW / kWalkThreads; ++k) {
+          const uint16_t a = src[lv][tid + k * kWalkThreads];
+          r[k] = a != kNo ? src[lv][a] : kNo;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kWW / kWalkThreads; ++k) dst[lv][tid + k * kWalkThreads] = r[k];
+        __syncthreads();
+      }
+    }
     for (uint32_t si = 0; si < nseg; ++si) {
       if (tid == 0) {
         uint32_t w = seg_q[si];
         uint32_t rem = seg_n[si];
-        uint32_t n16 = 0, n4 = 0, n1 = 0;
+        uint32_t n16 = 0, n1 = 0;
         while (rem >= 16) {
           a16[n16++] = (uint16_t)w;
           rem -= 16;
-          if (rem) w = jt[4][w];
-        }
-        while (rem >= 4) {
-          a4[n4++] = (uint16_t)w;
-          rem -= 4;
-          if (rem) w = jt[2][w];
+          if (rem) w = jt4[w];
         }
         while (rem) {
           a1[n1++] = (uint16_t)w;
-          if (--rem) w = jt[0][w];
+          if (--rem) w = jt0[w];
         }
         sh_n16 = n16;
-        sh_n4 = n4;
         sh_n1 = n1;
       }
       __syncthreads();
-      const uint32_t n16 = sh_n16, n4 = sh_n4, n1 = sh_n1;
+      const uint32_t n16 = sh_n16, n1 = sh_n1;
       const uint64_t rk = seg_rk[si];
-      for (uint32_t i = tid; i < n16 * 4; i += kWalkThreads) {   // 4 threads per 16-record hop
-        uint32_t q = a16[i >> 2];
-        const uint32_t sub = i & 3;
-        for (uint32_t k = 0; k < sub; ++k) q = jt[2][q];
+      for (uint32_t i = tid; i < n16; i += kWalkThreads) {   // one thread per 16-record hop
+        uint32_t q = a16[i];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          recoff[rk + 16 * (uint64_t)(i >> 2) + 4 * sub + k] = W0 + (uint64_t)q * 4;
-          if (k < 3) q = jt[0][q];
+        for (int k = 0; k < 16; ++k) {
+          recoff[rk + 16 * (uint64_t)i + k] = W0 + (uint64_t)q * 4;
+          if (k < 15) q = jt0[q];
         }
       }
-      const uint64_t r4 = rk + 16 * (uint64_t)n16;
-      if (tid < n4) {
-        uint32_t q = a4[tid];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          recoff[r4 + 4 * (uint64_t)tid + k] = W0 + (uint64_t)q * 4;
-          if (k < 3) q = jt[0][q];
-        }
-      }
-      const uint64_t r1 = r4 + 4 * (uint64_t)n4;
+      const uint64_t r1 = rk + 16 * (uint64_t)n16;
       if (tid < n1) recoff[r1 + tid] = W0 + (uint64_t)a1[tid] * 4;
       __syncthreads();
     }
   }
 }
 
-// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 32 KiB window count);
+// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 48 KiB window count);
 // epoch: nonzero, different from the previous call's on this workspace (granule tags).
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
@@ -446,11 +439,9 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
-  hipError_t e = hipMemsetAsync(ws, 0, sizeof(WalkCtl), st);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(walk_head_kernel, dim3(ss.n), dim3(256), 0, st, ss, dir, segs, call_status, counters, ntouched,
                      ctl, head);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
                      head, gran, spec_wpr, epoch);

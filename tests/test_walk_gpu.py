@@ -1,6 +1,6 @@
 """The window-parallel decode (psx_walk.hip) against the one-workgroup-per-message decode
 (decode_streams) and the CPU oracle, on the record-chain shapes that stress it: records
-spanning several 32 KiB windows, windows holding 4,096 records, tables ending mid-window and
+spanning several 48 KiB windows, windows holding 6,144 records, tables ending mid-window and
 exactly on a window boundary, several sparse and dense tables in one message, empty sparse
 tables, messages of different lengths in one call, and malformed chains (the same error and
 nothing applied).  Reference: SerializedOpLogReader (serialized_oplog_reader.hpp:30-133)."""
@@ -15,6 +15,7 @@ from oracle.oracle import OracleServer, DENSE, SORTED_MAP, MAP, F32, F64, I32, I
 
 pytestmark = pytest.mark.gpu
 DECODE, WALK_CALLS = 7, 8
+WINDOW = 49152   # psx_walk.hip kWBytes: the walk's window grid from byte 0 of a message
 NP = {F32: np.float32, F64: np.float64, I32: np.int32, I64: np.int64}
 VS = {F32: 4, F64: 8, I32: 4, I64: 8}
 
@@ -103,7 +104,7 @@ def _run_both(tables, streams):
 
 
 def test_c3_shaped_messages_every_window():
-    """Zipf rows, nnz 1..32, 8 messages of ~46 windows each into sorted-map rows."""
+    """Zipf rows, nnz 1..32, 8 messages of ~30 windows each into sorted-map rows."""
     rng = np.random.RandomState(5)
     rows, K = 20_000, 1024
     p = 1.0 / np.arange(1, rows + 1)
@@ -117,8 +118,8 @@ def test_c3_shaped_messages_every_window():
 
 @pytest.mark.parametrize("dt", [F32, F64])
 def test_records_spanning_windows_and_tiny_records(dt):
-    """Records of 8,000-24,000 (col, val) pairs (up to 6 windows each) between runs of
-    one-pair records (2,048 per window), then a table of zero-pair records (4,096 per
+    """Records of 8,000-24,000 (col, val) pairs (up to 4 windows each) between runs of
+    one-pair records (3,072 per window), then a table of zero-pair records (6,144 per
     window) and one-pair records."""
     rng = np.random.RandomState(9)
     RA, KA, RB, KB = 1024, 24_000, 8192, 16
@@ -156,15 +157,15 @@ def test_several_tables_per_message_ending_anywhere():
                  (6, 4, []),
                  (7, 4, _rows(rng, ids[5], K, I32, rng.randint(0, 200, size=n)))]
         if b == 4:
-            # table 2's records end exactly on the first 32 KiB boundary of the message
+            # table 2's records end exactly on the first window boundary of the message
             parts[0] = (1, "dense", ids[0][:1], rng.normal(0, 1, (1, CAP)).astype(np.float32))
             head = 4 + 16 + 1 * (4 + 4 * CAP) + 16
             recs, used = [], head
-            while used + 8 + 8 * 64 < 32768:
+            while used + 8 + 8 * 64 < WINDOW:
                 recs += _rows(rng, [len(recs)], K, I32, [64])
                 used += 8 + 8 * 64
-            assert (32768 - used - 8) % 8 == 0
-            recs += _rows(rng, [len(recs)], K, I32, [(32768 - used - 8) // 8])
+            assert (WINDOW - used - 8) % 8 == 0
+            recs += _rows(rng, [len(recs)], K, I32, [(WINDOW - used - 8) // 8])
             parts[1] = (2, 4, recs)
         streams.append(_message(parts))
     assert any(s.size > 65536 for s in streams) and len({s.size for s in streams}) > 8

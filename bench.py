@@ -21,9 +21,9 @@ client splits oplogs by owning server (abstract_bg_worker.cpp:590-649): no colle
 weak scaling.
 
 After the timed region the bare run (no variant flags) also records the PCIe-inclusive
-rate and C3 walked/indexed (N = 1), or the exchange-bearing step (N > 1: each rank's batch
-spans every shard, one RCCL all-to-all over xGMI, then the owners' fused applies) —
-`--no-extras` leaves them out.
+rate and C3 walked / pipelined / indexed (N = 1, child processes), or the exchange-bearing
+step (N > 1: each rank's batch spans every shard, one RCCL all-to-all over xGMI, then the
+owners' fused applies) — `--no-extras` leaves them out.
 
 cpu_baseline: the CPU oracle (restated Server::ApplyOpLogUpdateVersion loop, one
 thread = one reference server thread) on a bounded sample of the same workload.
@@ -107,6 +107,19 @@ def parse():
                    help="exercise only the multi-rank harness (rank launch, barriers, max-over-ranks timing, "
                         "the JSON line) over gloo with a no-op step: the CPU test of --gpus N")
     return p.parse_args()
+
+
+def run_child(flags, timeout=300):
+    """One bench.py run as a child process (this process keeps its GPU context; the child
+    starts its own): returns the child's JSON line."""
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.abspath(__file__)] + flags, capture_output=True, text=True,
+                         timeout=timeout, env={k: v for k, v in os.environ.items()
+                                               if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    if out.returncode != 0 or not lines:
+        raise RuntimeError(f"child rc={out.returncode}: {out.stderr[-300:]}")
+    return json.loads(lines[-1])
 
 
 def launch_ranks(args):
@@ -881,13 +894,17 @@ def main():
         except Exception as e:   # reported, never allowed to drop the headline line
             exchange = {"error": repr(e)[:400]}
     if extras and world == 1:
+        # C3 in child processes (`bench.py --workload c3`), so its device memory and state
+        # start fresh rather than where C2 and the PCIe pass left them (a C3 run right after
+        # them in this process measured its apply 3x slower)
         other = {}
-        for name, ix, pl in (("C3_walked", False, False), ("C3_walked_pipelined", False, True),
-                             ("C3_indexed", True, False)):
+        for name, flags in (("C3_walked", ["--cpu-seconds", str(min(args.cpu_seconds, 6.0))]),
+                            ("C3_indexed", ["--indexed", "--cpu-seconds", "0"])):
             try:
-                m = c3_measure(args, ix, 20, 3, min(args.cpu_seconds, 6.0) if not (ix or pl) else 0.0, pipeline=pl)
-                other[name] = {k: m[k] for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step",
-                                                 "kernel_ms_per_step_breakdown_pass", "cpu_baseline")}
+                m = run_child(["--workload", "c3", "--steps", "20", "--warmup", "3"] + flags)
+                other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step",
+                                                     "kernel_ms_per_step_breakdown_pass", "cpu_baseline",
+                                                     "pipelined")}
                 other[name]["config"] = m["config"]["workload"]
                 lm = m.get("latency_model") or {}
                 other[name]["ordered_apply_frac_of_latency_bound"] = lm.get("frac_of_bound")

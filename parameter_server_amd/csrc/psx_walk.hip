@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           if (lane < kGran) x = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           v = (uint32_t)x;
           if (__all((uint32_t)(x >> 32) == epoch)) { ok = true; break; }
-          if (spins > (1u << 24)) break;        // bounded: a lost hand-off fails the call
+          if (spins > (1u << 20)) break;        // bounded (~1 s; a call takes ~0.1 ms): a lost hand-off fails the call
           __builtin_amdgcn_s_sleep(1);
         }
         auto lo_hi = [&](int i) { return (uint64_t)(uint32_t)__shfl((int)v, i) | ((uint64_t)(uint32_t)__shfl((int)v, i + 1) << 32); };

@@ -333,7 +333,14 @@ def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20):
     tput = float((t_r[~big].sum() / C3_WAVES_PER_SIMD[4] + t_r[big].sum() / C3_WAVES_PER_SIMD[16]) / 1024)
     bound = max(chain, tput)
     hot = int(np.argmax(t_r))
+    # measured row throughput: every row's share of the chip at full occupancy (its setup,
+    # one record) — the 256-entry launch cannot finish faster than its rows' shares
+    share = js.get("row_share_ns")
+    rows_bound = float((~big & (R_r > 0)).sum() * share * 1e-6) if share else None
+    if rows_bound is not None:
+        bound = max(bound, rows_bound)
     return {"bound_ms": round(bound, 4), "critical_path_ms": round(chain, 4), "interleave_ms": round(tput, 4),
+            "row_throughput_ms": round(rows_bound, 4) if rows_bound is not None else None,
             "ordered_apply_ms": round(apply_ms, 4), "frac_of_bound": round(bound / apply_ms, 3) if apply_ms else None,
             "rows_touched": int((R_r > 0).sum()), "rows_1024_image": int(big.sum()),
             "inserts_per_step": round(float(I_r.sum()), 1),

@@ -80,12 +80,44 @@ def main():
         t = [one_call(n, 4, "insert", rep) for rep in range(args.reps)]
         res["insert"][n] = round(float(np.median([a / b for a, b in t])), 1)
         print("insert", n, res["insert"][n], "ns/Inc", flush=True)
+    # Per ROW at full occupancy of the 256-entry kernel (the throughput side of the model):
+    # R rows, each with an image of 32 entries, get one record of one existing key; the
+    # difference of the launch times for R2 and R1 rows / (R2 - R1) is one row's share of
+    # the chip: its setup (descriptor, record references, header, image load, key map,
+    # write-back) with 7 waves per SIMD interleaved.
+    def rows_call(R, rep):
+        rng = np.random.RandomState(77 + rep)
+        srv = psa.Server(0, 1, [1, 99])
+        srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
+                                         oplog_dense_serialized=False, max_rows=R, max_entries=K))
+        have = np.arange(32, dtype=np.int32)
+        fill = wire.sparse_stream_np(3, 4, [(r, have, np.full(32, 5, np.int32)) for r in range(R)])
+        srv.ApplyOpLogUpdateVersion(fill.tobytes(), fill.size, 99, 0)
+        one = wire.sparse_stream_np(3, 4, [(int(r), np.array([int(rng.randint(32))], np.int32),
+                                            np.ones(1, np.int32)) for r in rng.permutation(R)])
+        d = torch.from_numpy(one).cuda()
+        torch.cuda.synchronize()
+        srv.timing(2)
+        srv.timing_reset()
+        srv.apply_device([(d.data_ptr(), d.numel(), 1, 0)])
+        srv.sync()
+        ms, _ = srv.timing_read("ordered_apply")
+        srv.close()
+        return ms * 1e6
+    r1, r2 = 7168 * 2, 7168 * 8
+    t1 = float(np.median([rows_call(r1, rep) for rep in range(args.reps)]))
+    t2 = float(np.median([rows_call(r2, rep) for rep in range(args.reps)]))
+    res["row_share"] = round((t2 - t1) / (r2 - r1), 2)
+    print("row_share", res["row_share"], "ns per row at full occupancy", flush=True)
     out = {"what": "ns per record of 64 found keys in one wave's dependent chain (one row, one wave; median of reps; "
                    "difference of two ordered_apply launch times, so the launch's fixed part cancels): found_rec on "
                    "the 1,024-entry register image (16 vs 4 records), found_small_rec on the 256-entry image (8 vs 2 "
                    "records of 24 keys); insert: ns per new key (4 records x 64 new keys, the image growing n -> n + 256, launch "
                    "time / Incs).",
-           "found_rec_ns": res["found_rec"], "found_small_rec_ns": res["found_small_rec"], "insert_ns": res["insert"]}
+           "found_rec_ns": res["found_rec"], "found_small_rec_ns": res["found_small_rec"], "insert_ns": res["insert"],
+           "row_share_ns": res["row_share"],
+           "row_share_what": "one row's share of the chip at full occupancy of the 256-entry kernel: launch time "
+                             "difference of 57,344 and 14,336 one-record rows (images of 32 entries) per row"}
     print(json.dumps(out))
     if args.out:
         json.dump(out, open(args.out, "w"), indent=1)

@@ -22,6 +22,7 @@
 //                  find / bubble / compact, reproducing the reference's entry ORDER
 //                  byte for byte (it is history dependent: found keys are not re-sorted).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include "psx_device.hpp"
 #include "psx_scan.hpp"
@@ -112,6 +113,10 @@ __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
+  if (a.grow && blockIdx.x == 0 && threadIdx.x < 3) {   // ordered_offsets' counters
+    if (threadIdx.x < 2) a.nsplit[threadIdx.x] = 0;
+    else a.tsum[0] = 0;
+  }
   // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
   if (!o_gate(a)) return;
   if (threadIdx.x == 0) build_space(a, rs);
@@ -168,7 +173,6 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
-  if (a.nsplit && blockIdx.x == 0 && threadIdx.x < 2) a.nsplit[threadIdx.x] = 0;
   if (!o_gate(a)) return;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
     int b;
@@ -181,39 +185,56 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
   }
 }
 
-// ordered_classify (split tables): a touched row whose image can outgrow 256 entries in
-// this call (entries now + its records' entries) goes to the 1,024-entry list, the rest
-// to the 256-entry list; the two apply launches then run concurrently.  grow returns to 0.
-// A list entry is the row's descriptor {slot, list begin, list end, image size}: the
-// apply starts a row with one load instead of a slot load and then three dependent ones.
-__global__ void __launch_bounds__(256) ordered_classify_kernel(OrdArgs a) {
+// ordered_offsets (split tables, instead of the exclusive scan): every touched row gets
+// its record-list range by one wave-aggregated atomic on a call counter (the ranges need
+// not follow slot order), and its descriptor {slot, list begin, list end, image size} goes
+// to three lists: the 256-entry and the 1,024-entry apply lists (a row whose image can
+// outgrow 256 entries in this call: entries now + its records' entries) and, in touched
+// order, the list the capacity dry run walks.  grow returns to 0.  One launch replaces the
+// three scan launches and the separate classification pass.
+__global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
+  if (!o_gate(a)) return;
   const int lane = threadIdx.x & 63;
   const int64_t nt = (int64_t)*a.ntouched;
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
   const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+  int4 *const desc = reinterpret_cast<int4 *>(a.split);
   for (int64_t i0 = base0; i0 < nt; i0 += G) {
     const int64_t i = i0 + lane;
-    int32_t s = 0, nen = 0;
-    bool big = false;
     const bool have = i < nt;
+    int32_t s = 0, c = 0, nen = 0;
+    bool big = false;
     if (have) {
       s = a.touched[i];
+      c = a.cnt[s];
       nen = a.nent[s];
       big = (int64_t)nen + a.grow[s] > 256;
       a.grow[s] = 0;
+    }
+    int32_t incl = c;   // wave-inclusive prefix of the rows' record counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    int32_t base = 0;
+    if (lane == 63) base = atomicAdd(&a.tsum[0], incl);
+    base = __shfl(base, 63, 64);
+    const int32_t beg = base + incl - c;
+    if (have) {
+      a.off[s] = beg;
+      desc[2 * a.max_rows + i] = int4{s, beg, beg + c, nen};
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const uint64_t m = __ballot(have && big == (k == 1));
       if (!m) continue;
       const int leader = __builtin_ctzll(m);
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(&a.nsplit[k], (uint32_t)__builtin_popcountll(m));
-      base = __builtin_amdgcn_readlane(base, leader);
-      if (have && big == (k == 1)) {
-        const int64_t at = k * a.max_rows + base + __builtin_popcountll(m & ((1ull << lane) - 1));
-        reinterpret_cast<int4 *>(a.split)[at] = int4{s, a.off[s], a.off[s + 1], nen};
-      }
+      uint32_t pos = 0;
+      if (lane == leader) pos = atomicAdd(&a.nsplit[k], (uint32_t)__builtin_popcountll(m));
+      pos = __builtin_amdgcn_readlane(pos, leader);
+      if (have && big == (k == 1))
+        desc[k * a.max_rows + pos + __builtin_popcountll(m & ((1ull << lane) - 1))] = int4{s, beg, beg + c, nen};
     }
   }
 }
@@ -638,7 +659,7 @@ __device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int
 }
 
 // Split tables run two launches of this kernel concurrently, over the touched rows
-// ordered_classify put in the 256- and the 1,024-entry list (a.touched / a.ntouched point
+// ordered_offsets put in the 256- and the 1,024-entry list (a.touched / a.ntouched point
 // at one list each).
 // DRY: the capacity dry run (see ordered_apply_kernel); J must hold max_entries.
 // Occupancy targets: 7 waves/SIMD for the 256-entry image (its rows are bound by their
@@ -1049,7 +1070,12 @@ static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
 }
 
 template <typename V, int KIND>
-static void launch_dry(const OrdArgs &a, int dtype, hipStream_t st) {
+static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
+  OrdArgs a = a0;
+  if (a.grow) {   // split tables: list ranges are not in slot order, walk the descriptors
+    a.touched = a.split + 2 * 4 * a.max_rows;
+    a.desc = 1;
+  }
   const unsigned blocks = row_blocks(a.max_rows, 4);
   if (a.max_entries <= 64)
     hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, true>), dim3(blocks), dim3(256), 0, st, a);
@@ -1070,7 +1096,10 @@ static void launch_dry(const OrdArgs &a, int dtype, hipStream_t st) {
 // slot, every validation, and the capacity dry run of sorted/map tables.
 hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
-  launch_exclusive_scan<int32_t>(a.cnt, a.max_rows, a.off, a.tsum, st);
+  if (a.grow)
+    hipLaunchKernelGGL(ordered_offsets_kernel, dim3(std::min(row_blocks(a.max_rows, 256), 256u)), dim3(256), 0, st, a);
+  else
+    launch_exclusive_scan<int32_t>(a.cnt, a.max_rows, a.off, a.tsum, st);
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
   if (a.kind != 0 && !a.dense_records && a.keyflag) {
 #define PSX_DRY(V) do { if (a.kind == 1) launch_dry<V, 1>(a, dtype, st); else launch_dry<V, 2>(a, dtype, st); } while (0)
@@ -1086,14 +1115,13 @@ hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st) {
 }
 
 // Stage 2: the apply (after every table's stage 1 and the duplicate-row gate).  Split
-// tables (a.grow set): ordered_classify, then the 1,024-entry launch on `aux` (its long
+// tables (a.grow set): the 1,024-entry launch on `aux` (its long
 // per-row chains start first) beside the 256-entry launch on `st`; `st` joins `aux`.
 hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk) {
   if (a.kind != 0 && a.max_entries <= 1024) {
     const unsigned blocks = row_blocks(a.max_rows, 4);
     OrdArgs small = a, big = a;
-    if (a.grow) {
-      hipLaunchKernelGGL(ordered_classify_kernel, dim3(row_blocks(a.max_rows, 4)), dim3(256), 0, st, a);
+    if (a.grow) {   // ordered_offsets wrote the two descriptor lists
       small.touched = a.split;
       small.ntouched = a.nsplit;
       big.touched = a.split + 4 * a.max_rows;

@@ -149,7 +149,10 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
           if (cols_outside(p, a.max_entries)) atomicOr(a.keyflag, 1u);
         }
         if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
-        first = atomicAdd(&a.cnt[s], 1) == 0;
+        if (a.grow)   // split tables: ordered_offsets finds the touched rows from the counts
+          atomicAdd(&a.cnt[s], 1);
+        else
+          first = atomicAdd(&a.cnt[s], 1) == 0;
       }
     }
     // append first-touched slots to the touched list, one atomic per wave
@@ -185,57 +188,100 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
   }
 }
 
-// ordered_offsets (split tables, instead of the exclusive scan): every touched row gets
-// its record-list range by one wave-aggregated atomic on a call counter (the ranges need
-// not follow slot order), and its descriptor {slot, list begin, list end, image size} goes
-// to three lists: the 256-entry and the 1,024-entry apply lists (a row whose image can
-// outgrow 256 entries in this call: entries now + its records' entries) and, in touched
-// order, the list the capacity dry run walks.  grow returns to 0.  One launch replaces the
-// three scan launches and the separate classification pass.
+// ordered_offsets (split tables, instead of the exclusive scan): each block takes a
+// contiguous range of slots and, over its touched ones (count > 0), gives every row its
+// record-list range and its descriptor {slot, list begin, list end, image size} in three
+// lists: the 256-entry and the 1,024-entry apply lists (a row whose image can outgrow 256
+// entries in this call: entries now + its records' entries) and, in slot order, the list
+// the capacity dry run walks (its length is the table's touched count).  A block adds its
+// four totals to the call counters once (ranges need not follow slot order), so the
+// counters see a few hundred atomics instead of one per wave of touched rows; the count
+// kernel then needs no first-touch atomics.  grow returns to 0.
+__device__ __forceinline__ int32_t block_excl_sum(int32_t v, int32_t *sh, int32_t &total) {
+  // 256 threads: exclusive prefix of v in thread order; sh holds 4 ints (one per wave)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  int32_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < w) pre += sh[k];
+    total += sh[k];
+  }
+  __syncthreads();
+  return pre + incl - v;
+}
+
 __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
+  __shared__ int32_t sh[4][4];
+  __shared__ int32_t base[4];   // touched, records, 256-entry list, 1,024-entry list
   if (!o_gate(a)) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t nt = (int64_t)*a.ntouched;
-  const int64_t G = (int64_t)gridDim.x * blockDim.x;
-  const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+  const int64_t R = a.max_rows;
+  const int64_t per = (R + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = (int64_t)blockIdx.x * per;
+  const int64_t c1 = c0 + per < R ? c0 + per : R;
+  // pass 1: the block's totals, one atomic per counter
+  int32_t nt = 0, nr = 0, ns = 0, nb = 0;
+  for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
+    const int32_t c = a.cnt[s];
+    if (c > 0) {
+      ++nt;
+      nr += c;
+      if ((int64_t)a.nent[s] + a.grow[s] > 256) ++nb; else ++ns;
+    }
+  }
+  int32_t tt, tr, ts, tb;
+  block_excl_sum(nt, sh[0], tt);
+  block_excl_sum(nr, sh[1], tr);
+  block_excl_sum(ns, sh[2], ts);
+  block_excl_sum(nb, sh[3], tb);
+  if (threadIdx.x == 0) {
+    base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
+    base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
+    base[2] = ts ? (int32_t)atomicAdd(&a.nsplit[0], (uint32_t)ts) : 0;
+    base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tb) : 0;
+  }
+  __syncthreads();
+  // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row
   int4 *const desc = reinterpret_cast<int4 *>(a.split);
-  for (int64_t i0 = base0; i0 < nt; i0 += G) {
-    const int64_t i = i0 + lane;
-    const bool have = i < nt;
-    int32_t s = 0, c = 0, nen = 0;
+  int32_t at = base[0], ar = base[1], as = base[2], ab = base[3];
+  for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
+    const int64_t s = t0 + threadIdx.x;
+    int32_t c = 0, nen = 0;
     bool big = false;
-    if (have) {
-      s = a.touched[i];
+    if (s < c1) {
       c = a.cnt[s];
-      nen = a.nent[s];
-      big = (int64_t)nen + a.grow[s] > 256;
-      a.grow[s] = 0;
+      if (c > 0) {
+        nen = a.nent[s];
+        big = (int64_t)nen + a.grow[s] > 256;
+        a.grow[s] = 0;
+      }
     }
-    int32_t incl = c;   // wave-inclusive prefix of the rows' record counts
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    int32_t base = 0;
-    if (lane == 63) base = atomicAdd(&a.tsum[0], incl);
-    base = __shfl(base, 63, 64);
-    const int32_t beg = base + incl - c;
-    if (have) {
+    const bool t = c > 0;
+    int32_t st, sr, ss2, sb;
+    const int32_t pt = block_excl_sum(t ? 1 : 0, sh[0], st);
+    const int32_t pr = block_excl_sum(c, sh[1], sr);
+    const int32_t ps = block_excl_sum(t && !big ? 1 : 0, sh[2], ss2);
+    const int32_t pb = block_excl_sum(t && big ? 1 : 0, sh[3], sb);
+    if (t) {
+      const int32_t beg = ar + pr;
+      const int4 d = int4{(int32_t)s, beg, beg + c, nen};
       a.off[s] = beg;
-      desc[2 * a.max_rows + i] = int4{s, beg, beg + c, nen};
+      desc[2 * R + at + pt] = d;
+      if (big) desc[R + ab + pb] = d;
+      else desc[as + ps] = d;
     }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const uint64_t m = __ballot(have && big == (k == 1));
-      if (!m) continue;
-      const int leader = __builtin_ctzll(m);
-      uint32_t pos = 0;
-      if (lane == leader) pos = atomicAdd(&a.nsplit[k], (uint32_t)__builtin_popcountll(m));
-      pos = __builtin_amdgcn_readlane(pos, leader);
-      if (have && big == (k == 1))
-        desc[k * a.max_rows + pos + __builtin_popcountll(m & ((1ull << lane) - 1))] = int4{s, beg, beg + c, nen};
-    }
+    at += st;
+    ar += sr;
+    as += ss2;
+    ab += sb;
   }
 }
 

@@ -404,6 +404,10 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
     import parameter_server_amd as psa
     rows, K, B = 100_000, 1024, args.batches
     streams, nupd, batches = c3_streams(rows, K, B, with_records=True)
+    # the window-parallel walk (psx_walk.hip) is opt-in (include/psx_debug.h); this is a
+    # single-context run, where it is exercised by its parity tests
+    from parameter_server_amd import _abi as _ab
+    _ab.load().psx_debug_set_variant(7, 0 if os.environ.get("PSX_DECODE_WALK") == "0" else 1)
     dev = [torch.from_numpy(s).cuda() for s in streams]
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(0, 1, bgs)

@@ -28,7 +28,10 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
                        uint32_t epoch, hipStream_t st);
 size_t walk_ws_bytes(uint64_t items);
-int g_decode_walk = 1;   // PSX_VARIANT_DECODE
+// PSX_VARIANT_DECODE.  Off by default: with two contexts walking concurrently on one GPU
+// the walk faulted intermittently (tests/test_indexed_rows_gpu.py, profiles/r02/s69, s71;
+// DESIGN.md §5); single-context runs (its parity tests, the C3 bench) opt in.
+int g_decode_walk = 0;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride,

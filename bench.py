@@ -75,9 +75,11 @@ def parse():
                         "(tools/pmc_summary.py); used for roofline.traffic on the default C2 configuration")
     p.add_argument("--f16-records", action="store_true",
                    help="C2 with kDenseRowOpLogFloat16 records (binary16 payloads, row_oplog_type 3)")
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c4shard", "c5"],
                    help="c2: dense f32 headline (default); c3: LDA-style sparse int sorted-map rows; "
-                        "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange")
+                        "c4: 10M x 1K dense table sharded over ranks with an all-to-all exchange; "
+                        "c4shard: one GPU's 1.25M-row shard of C4 with its 8 worker messages; "
+                        "c5: mixed dense + sparse clocks under SSPPush")
     p.add_argument("--c4-rows", type=int, default=10_000_000, help="C4 total rows (all shards)")
     p.add_argument("--adarevision", action="store_true",
                    help="C2 through the AdaRevision server-table logic (adarevision_server_table_logic.cpp): "
@@ -166,7 +168,15 @@ def selftest_launch(args):
         dist.destroy_process_group()
 
 
-def cpu_baseline(args):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        return None
+
+
+def cpu_baseline(args, rows=None, cap=None):
     """Oracle (CPU restatement of the reference apply loop) on a bounded sample, run as T
     server threads: rows are sharded row_id % T (the reference's comm-channel placement,
     context.hpp:291-304) and each thread applies its own shard's messages, as T reference
@@ -177,7 +187,7 @@ def cpu_baseline(args):
     from concurrent.futures import ThreadPoolExecutor
     from oracle.oracle import OracleServer, DENSE, F32
     from parameter_server_amd import wire
-    rows, cap, B = args.cpu_rows, args.cols, args.batches
+    rows, cap, B = rows or args.cpu_rows, cap or args.cols, args.batches
     T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     rng = np.random.default_rng(1234)
     init = rng.standard_normal((rows, cap), dtype=np.float32) * np.float32(0.1)
@@ -222,13 +232,7 @@ def cpu_baseline(args):
 
     v1, n1, e1 = timed_run(1, args.cpu_seconds / 3)
     vt, nt, et = timed_run(T, args.cpu_seconds * 2 / 3) if T > 1 else (v1, n1, e1)
-    model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
-    except OSError:
-        pass
-    return {"value": round(vt, 3), "unit": "GB/s", "cores": T, "kind": "port", "cpu_model": model,
+    return {"value": round(vt, 3), "unit": "GB/s", "cores": T, "kind": "port", "cpu_model": cpu_model(),
             "single_thread_GBps": round(v1, 3),
             "sample": f"{rows} rows x {cap} f32, {B} batches/step; {T} threads (rows % {T} shards): {nt} steps in "
                       f"{et:.1f} s; 1 thread: {n1} steps in {e1:.1f} s (oracle/psx_oracle.c restatement of "
@@ -404,10 +408,12 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
     import parameter_server_amd as psa
     rows, K, B = 100_000, 1024, args.batches
     streams, nupd, batches = c3_streams(rows, K, B, with_records=True)
-    # the window-parallel walk (psx_walk.hip) is opt-in (include/psx_debug.h); this is a
-    # single-context run, where it is exercised by its parity tests
+    # the product's decode (include/psx_debug.h PSX_VARIANT_DECODE; PSX_DECODE_WALK=0|1 in
+    # the environment overrides it at load); the JSON line names the path that ran
     from parameter_server_amd import _abi as _ab
-    _ab.load().psx_debug_set_variant(7, 0 if os.environ.get("PSX_DECODE_WALK") == "0" else 1)
+    L = _ab.load()
+    decode_variant = L.psx_debug_get_variant(7)
+    L.psx_debug_set_variant(8, 0)
     dev = [torch.from_numpy(s).cuda() for s in streams]
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(0, 1, bgs)
@@ -453,6 +459,13 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
     kern = {k: srv.timing_read(k) for k in ("decode_streams", "ordered_prep", "ordered_apply", "finish_call")}
     srv.timing(False)
     srv.close()
+    walk_calls = L.psx_debug_get_variant(8)
+    if indexed:
+        decode = "producer record offsets checked in parallel (decode_streams with offsets)"
+    elif walk_calls > 0:
+        decode = "window-parallel walk (psx_walk.hip)"
+    else:
+        decode = "one workgroup per message (decode_streams)"
     stream_bytes = sum(s.size for s in streams)
     model = c3_model(batches, rows, K, apply_ms / max(apply_n, 1))
     cpu = c3_cpu_baseline(args, batches, nupd, bgs, cpu_seconds) if cpu_seconds > 0 else None
@@ -468,6 +481,7 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
                                + (", decode overlapped with the previous call's apply (PSX_PIPELINE_ALL)"
                                   if pipeline else ""),
                    "updates_per_step": nupd, "stream_bytes_per_step": stream_bytes},
+        "decode": decode, "decode_variant": decode_variant, "walk_calls": walk_calls,
         "ordered_apply_ms_per_step": round(apply_ms / max(apply_n, 1), 4),
         "kernel_ms_per_step_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
         "latency_model": model,
@@ -477,7 +491,7 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
 def run_c3(args):
     m = c3_measure(args, args.indexed, args.steps, args.warmup, args.cpu_seconds)
     p = c3_measure(args, args.indexed, args.steps, args.warmup, 0.0, pipeline=True)
-    m["pipelined"] = {k: p[k] for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step")}
+    m["pipelined"] = {k: p[k] for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step", "decode")}
     m["pipelined"]["what"] = p["config"]["workload"]
     print(json.dumps(m), flush=True)
 
@@ -595,6 +609,81 @@ def run_c4(args):
         dist.destroy_process_group()
 
 
+def run_c4shard(args):
+    """SURVEY §8(d) C4, one GPU's shard: the 10M x 1024 f32 table row-range sharded over 8
+    GPUs gives each GPU 1.25M rows; per step its owner receives one full-coverage message
+    from each of the 8 workers (their per-owner sub-streams, rows in random order: 5.1 GB
+    each, 41 GB per step), applied in one fused, order-preserving call through the
+    reference-shaped psx_apply_streams_device (row ids read from the stream; each call's
+    index stage beside the previous call's apply).  The 8-GPU run adds the all-to-all that
+    delivers those messages (`--workload c4 --gpus 8`, driver-run).  cpu_baseline: the oracle
+    on a 2^15-row shard of the same shape, extrapolated to the full shard (labelled)."""
+    import torch
+    import parameter_server_amd as psa
+    from parameter_server_amd import wire
+    W, cap = 8, 1024
+    rows = args.c4_rows // W
+    g = torch.Generator(device="cuda").manual_seed(4242)
+    table0 = torch.randn(rows, cap, device="cuda", generator=g) * 0.1
+    streams = []
+    for w in range(W):
+        perm = torch.randperm(rows, device="cuda", generator=g).to(torch.int32)
+        upd = torch.randn(rows, cap, device="cuda", generator=g) * 0.01
+        streams.append(wire.dense_stream_torch(1, perm, upd))
+        del upd, perm
+    torch.cuda.synchronize()
+    bgs = [100 + w for w in range(W)]
+    srv = psa.Server(device=0, server_id=1, bg_ids=bgs)
+    srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    srv.set_pipeline(2)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows))
+    srv.load_rows(1, 0, None, on_device_ptr=table0.data_ptr(), num_rows=rows)
+    del table0
+    torch.cuda.empty_cache()
+    ver = [0]
+
+    def step():
+        srv.apply_device([(x.data_ptr(), x.numel(), bgs[w], ver[0]) for w, x in enumerate(streams)])
+        ver[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    srv.sync()
+    srv.timing(2)
+    srv.timing_reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    srv.sync()
+    apply_ms, apply_n = srv.timing_read("dense_apply")
+    srv.timing(False)
+    srv.close()
+    step_bytes = sum(x.numel() for x in streams) + 2 * rows * cap * 4
+    del streams
+    torch.cuda.empty_cache()
+    apply_s = apply_ms / max(apply_n, 1) / 1e3
+    cpu = None
+    if args.cpu_seconds > 0:
+        cpu = cpu_baseline(args, rows=1 << 15, cap=cap)
+        cpu["extrapolated_ms_per_step_full_shard"] = round(step_bytes / (cpu["value"] * 1e9) * 1e3, 1)
+        cpu["sample"] = "EXTRAPOLATED from a 2^15-row shard sample: " + cpu["sample"]
+    print(json.dumps({
+        "metric": "C4 one GPU's shard: dense gradient apply GB/s (device-resident)",
+        "value": round(step_bytes * args.steps / el / 1e9, 2), "unit": "GB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "dtype": "f32", "data": "synthetic (GPU-generated, full coverage, random order)",
+        "config": {"workload": f"C4 shard: {rows} rows x {cap} f32 (10M x 1K over 8 GPUs), {W} worker messages "
+                               f"per step, psx_apply_streams_device, PSX_PIPELINE_ALL",
+                   "algorithmic_bytes_per_step": step_bytes},
+        "roofline": {"bound": "hbm", "kernel": "dense_apply", "achieved": round(step_bytes / apply_s / 1e9, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_bytes / apply_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "avg_launch_ms": round(apply_s * 1e3, 3)},
+        "cpu_baseline": cpu}), flush=True)
+
+
 def run_pcie(args, srv, streams, rows, cap, bgs, ver):
     """Host-resident form of C2: messages start in pinned host memory (worker socket
     buffers) and every dirty row is served back to host memory each step."""
@@ -629,6 +718,99 @@ def run_pcie(args, srv, streams, rows, cap, bgs, ver):
             "what": "pinned H2D of all messages + fused apply + D2H of every row (served back), per step"}
 
 
+PCIE_PEAK_GBS = 63.0   # PCIe Gen5 x16 spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def c5_workload(rng_seed=77):
+    """C5's per-clock messages (one per worker) and each client's subscriptions."""
+    import numpy as np
+    from parameter_server_amd import wire
+    rows_d, cap, rows_s, K, B = 1 << 18, 256, 100_000, 1024, 8
+    rng = np.random.RandomState(rng_seed)
+    p = 1.0 / np.arange(1, rows_s + 1)
+    p /= p.sum()
+    parts, subs = [], []
+    for b in range(B):
+        ids_d = rng.permutation(rows_d)[: rows_d // 2].astype(np.int32)
+        upd = rng.normal(0, 0.01, size=(ids_d.size, cap)).astype(np.float32)
+        ids_s = rng.choice(rows_s, size=1250, replace=False, p=p).astype(np.int32)
+        cnt = np.zeros((ids_s.size, K), np.int32)
+        for r in range(ids_s.size):
+            c = rng.choice(K, size=rng.randint(1, 33), replace=False)
+            cnt[r, c] = rng.choice([-1, 1, 2], size=c.size)
+        parts.append((ids_d, upd, ids_s, cnt))
+        subs.append((ids_d, ids_s))
+    msgs = [wire.pack_np([dict(table_id=1, dense_serialized=True, row_ids=a, oplogs=u),
+                          dict(table_id=3, dense_serialized=False, row_ids=c, oplogs=n)]) for a, u, c, n in parts]
+    return dict(rows_d=rows_d, cap=cap, rows_s=rows_s, K=K, B=B, parts=parts, msgs=msgs, subs=subs)
+
+
+def c5_cpu_baseline(args, wl, seconds):
+    """The oracle running C5's clocks as T server threads (rows sharded row % T,
+    context.hpp:291-304; each worker's message split per server, abstract_bg_worker.cpp:
+    590-649): per clock every shard applies its 8 sub-messages, advances each sender's clock
+    (ClockUntil) and, when the min clock moves, serializes one push body per client from its
+    subscriptions (CreateSendServerPushRowMsgs) — the same work the GPU clock does."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.oracle import OracleServer, DENSE, SORTED_MAP, F32, I32
+    from parameter_server_amd import wire
+    T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    B, bgs = wl["B"], [100 + b for b in range(wl["B"])]
+
+    def build(nthreads):
+        shards = []
+        for t in range(nthreads):
+            o = OracleServer(bgs)
+            o.create_table(1, DENSE, F32, wl["cap"])
+            o.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+            msgs = []
+            for ids_d, upd, ids_s, cnt in wl["parts"]:
+                md, ms = ids_d % nthreads == t, ids_s % nthreads == t
+                msgs.append(wire.pack_np([dict(table_id=1, dense_serialized=True, row_ids=ids_d[md], oplogs=upd[md]),
+                                          dict(table_id=3, dense_serialized=False, row_ids=ids_s[ms],
+                                               oplogs=cnt[ms])]))
+            for b, (ids_d, ids_s) in enumerate(wl["subs"]):
+                for r in ids_d[ids_d % nthreads == t]:
+                    o.subscribe(1, int(r), b)
+                for r in ids_s[ids_s % nthreads == t]:
+                    o.subscribe(3, int(r), b)
+            shards.append([o, msgs, 0])
+        return shards
+
+    def clock(sh):
+        o, msgs, ver = sh
+        for b, m in enumerate(msgs):
+            assert o.apply_stream(m, bgs[b], ver) == 0
+        changed = 0
+        for bg in bgs:
+            changed = o.clock_until(bg, ver + 1) or changed
+        n = sum(len(x) for x in o.serialize_push([1, 3], B)) if changed else 0
+        sh[2] = ver + 1
+        return n
+
+    def timed_run(nthreads, secs):
+        shards = build(nthreads)
+        with ThreadPoolExecutor(nthreads) as ex:
+            list(ex.map(clock, shards))      # untimed warm-up clock
+            n, el = 0, 0.0
+            while el < secs or n == 0:
+                t0 = time.perf_counter()
+                list(ex.map(clock, shards))
+                el += time.perf_counter() - t0
+                n += 1
+        for sh in shards:
+            sh[0].close()
+        return n / el, n, el
+
+    v1, n1, e1 = timed_run(1, seconds / 3)
+    vt, nt, et = timed_run(T, seconds * 2 / 3) if T > 1 else (v1, n1, e1)
+    return {"value": round(vt, 3), "unit": "clocks/s", "cores": T, "kind": "port", "cpu_model": cpu_model(),
+            "single_thread": round(v1, 3),
+            "sample": f"the same C5 workload; {T} threads (rows % {T} shards): {nt} clocks in {et:.1f} s; "
+                      f"1 thread: {n1} clocks in {e1:.1f} s (oracle: apply + ClockUntil + per-client push bodies)"}
+
+
 def run_c5(args):
     """mixed dense + sparse tables, a continuous stream with clocks under
     SSPPush.  8 workers (= 8 clients) each send one message per clock carrying both tables
@@ -640,28 +822,13 @@ def run_c5(args):
     (server_thread.cpp:262-288), builds one push body per client from its subscriptions
     (CreateSendServerPushRowMsgs, server.cpp:189-309) into host memory.  Staleness 4 is the
     client's Get gate (ssp_push_consistency_controller.cpp:70-88): workers may run up to 4
-    clocks ahead, and the server sees the same stream.  Reports clocks/s and the split."""
-    import numpy as np
+    clocks ahead, and the server sees the same stream.  Reports clocks/s, the split, the
+    bound (device share at HBM peak + push bodies at the PCIe spec) and the CPU port."""
     import torch
     import parameter_server_amd as psa
-    from parameter_server_amd import wire
-    rows_d, cap, rows_s, K, B = 1 << 18, 256, 100_000, 1024, 8
-    rng = np.random.RandomState(77)
-    p = 1.0 / np.arange(1, rows_s + 1)
-    p /= p.sum()
-    msgs, subs = [], []
-    for b in range(B):
-        ids_d = rng.permutation(rows_d)[: rows_d // 2].astype(np.int32)
-        upd = rng.normal(0, 0.01, size=(ids_d.size, cap)).astype(np.float32)
-        ids_s = rng.choice(rows_s, size=1250, replace=False, p=p).astype(np.int32)
-        cnt = np.zeros((ids_s.size, K), np.int32)
-        for r in range(ids_s.size):
-            c = rng.choice(K, size=rng.randint(1, 33), replace=False)
-            cnt[r, c] = rng.choice([-1, 1, 2], size=c.size)
-        msgs.append(wire.pack_np([
-            dict(table_id=1, dense_serialized=True, row_ids=ids_d, oplogs=upd),
-            dict(table_id=3, dense_serialized=False, row_ids=ids_s, oplogs=cnt)]))
-        subs.append((ids_d, ids_s))
+    wl = c5_workload()
+    rows_d, cap, rows_s, K, B = wl["rows_d"], wl["cap"], wl["rows_s"], wl["K"], wl["B"]
+    msgs, subs = wl["msgs"], wl["subs"]
     dev = [torch.from_numpy(m).cuda() for m in msgs]
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(0, 1, bgs)
@@ -702,22 +869,36 @@ def run_c5(args):
         clock()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    srv.close()
+    del dev
     msg_bytes = sum(m.size for m in msgs)
-    step_bytes = msg_bytes + 2 * rows_d * cap * 4 + pushed[0] / args.steps
-    print(json.dumps({
+    push_per_clock = pushed[0] / args.steps
+    touched_d = len(set().union(*[set(a.tolist()) for a, _ in subs]))
+    device_bytes = msg_bytes + 2 * touched_d * cap * 4
+    step_bytes = device_bytes + push_per_clock
+    bound_ms = (device_bytes / (HBM_PEAK_GBS * 1e9) + push_per_clock / (PCIE_PEAK_GBS * 1e9)) * 1e3
+    ms = el / args.steps * 1e3
+    cpu = c5_cpu_baseline(args, wl, min(args.cpu_seconds, 12.0)) if args.cpu_seconds > 0 else None
+    line = {
         "metric": "C5 mixed dense+sparse clock under SSPPush (apply + ClockUntil + per-client push to host)",
         "value": round(args.steps / el, 2), "unit": "clocks/s",
         "GBps_algorithmic": round(step_bytes * args.steps / el / 1e9, 2),
-        "ms_per_clock": round(el / args.steps * 1e3, 3),
+        "ms_per_clock": round(ms, 3),
         "apply_ms_per_clock": round(t_apply[0] / args.steps * 1e3, 3),
         "clock_and_push_ms_per_clock": round(t_clock[0] / args.steps * 1e3, 3),
-        "pushes": pushes[0], "pushed_bytes_per_clock": int(pushed[0] / args.steps),
+        "pushes": pushes[0], "pushed_bytes_per_clock": int(push_per_clock),
         "message_bytes_per_clock": msg_bytes,
+        "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
+                  "device_ms_at_hbm_peak": round(device_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 3),
+                  "push_ms_at_pcie_spec": round(push_per_clock / (PCIE_PEAK_GBS * 1e9) * 1e3, 3),
+                  "what": "messages + dense row read/write at 8 TB/s, plus every client's push body to host "
+                          "memory at the PCIe Gen5 x16 spec (63 GB/s); the push is the path's end in host memory"},
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "dtype": "f32+int32",
         "data": "synthetic", "config": {"workload": "C5: dense 2^18x256 f32 + sorted-map 100Kx1024 int32, "
                                                     "8 clients x 1 msg/clock, SSPPush, staleness 4 (client gate)"},
-    }), flush=True)
-    srv.close()
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def main():
@@ -732,6 +913,8 @@ def main():
         return run_c3(args)
     if args.workload == "c4":
         return run_c4(args)
+    if args.workload == "c4shard":
+        return run_c4shard(args)
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -830,7 +1013,9 @@ def main():
     # the same way, reported beside `value`.
     walked = None
     if use_rows and not args.skip_walked:
-        srv.set_pipeline(0)
+        # the reference-shaped call at its best: the messages are resident before each call,
+        # so its decode/index stage may run beside the previous call's apply
+        srv.set_pipeline(2)
         for _ in range(2):
             step(walked=True)
         srv.sync()
@@ -866,8 +1051,10 @@ def main():
         wb = step_bytes - list_bytes
         walked = {"value": round(wb * args.steps * world / el_w / 1e9, 2), "unit": "GB/s",
                   "ms_per_step": round(el_w / args.steps * 1e3, 4),
-                  "what": "the same messages through psx_apply_streams_device: row ids read from the stream "
-                          "(dense_index), no index/apply overlap; algorithmic bytes without the lists"}
+                  "what": "the same messages through psx_apply_streams_device (the reference-shaped "
+                          "ApplyOpLogUpdateVersion call): row ids read from the stream (dense_index), the index "
+                          "stage beside the previous call's apply (PSX_PIPELINE_ALL); algorithmic bytes without "
+                          "the lists"}
 
     apply_avg_s = apply_ms / max(apply_n, 1) / 1e3
     achieved = step_bytes / apply_avg_s / 1e9 if apply_avg_s > 0 else None
@@ -909,16 +1096,27 @@ def main():
         # start fresh rather than where C2 and the PCIe pass left them (a C3 run right after
         # them in this process measured its apply 3x slower)
         other = {}
-        for name, flags in (("C3_walked", ["--cpu-seconds", str(min(args.cpu_seconds, 6.0))]),
+        cs = str(min(args.cpu_seconds, 6.0))
+        for name, flags in (("C3_walked", ["--cpu-seconds", cs]),
                             ("C3_indexed", ["--indexed", "--cpu-seconds", "0"])):
             try:
                 m = run_child(["--workload", "c3", "--steps", "20", "--warmup", "3"] + flags)
-                other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "ordered_apply_ms_per_step",
+                other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "decode",
+                                                     "ordered_apply_ms_per_step",
                                                      "kernel_ms_per_step_breakdown_pass", "cpu_baseline",
                                                      "pipelined")}
                 other[name]["config"] = m["config"]["workload"]
                 lm = m.get("latency_model") or {}
                 other[name]["ordered_apply_frac_of_latency_bound"] = lm.get("frac_of_bound")
+            except Exception as e:
+                other[name] = {"error": repr(e)[:400]}
+        for name, flags in (("C4_shard_1gpu", ["--workload", "c4shard", "--steps", "5", "--warmup", "2",
+                                               "--cpu-seconds", cs]),
+                            ("C5", ["--workload", "c5", "--steps", "10", "--warmup", "2", "--cpu-seconds", cs])):
+            try:
+                m = run_child(flags, timeout=400)
+                m.pop("metric", None)
+                other[name] = m
             except Exception as e:
                 other[name] = {"error": repr(e)[:400]}
     if rank == 0:

@@ -19,8 +19,8 @@ enum {
                                    classified into a 256- and a 1,024-entry image launch that
                                    run concurrently (default), 0: one 1,024-entry launch */,
   PSX_VARIANT_DECODE = 7        /* 1: walked messages with sparse tables decode window-parallel
-                                   (psx_walk.hip, where eligible; opt-in), 0: one workgroup per
-                                   message (decode_streams, the default) */,
+                                   (psx_walk.hip, where eligible; the default), 0: one workgroup
+                                   per message (decode_streams) */,
   PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */
 };
 

@@ -28,9 +28,12 @@ enum : uint32_t {
   kStState = 1u << 6,          // AdaRevision: a record names a (row, version) with no snapshot
   kStRowsMismatch = 1u << 7,   // a producer record-row list disagrees with its stream (found by the
                                // apply; not fatal to the rest of the call: see psx_apply_indexed_rows)
+  kStWalkLost = 1u << 8,       // window-parallel decode: a predecessor window's state never arrived
+  kStWalkBound = 1u << 9,      // window-parallel decode: a walker state outside its message's
+                               // record-offset range (internal error; nothing applied)
 };
 constexpr uint32_t kStFatal = kStMalformed | kStUnknownTable | kStRowRange | kStCapacity |
-                              kStUnsupported | kStState;
+                              kStUnsupported | kStState | kStWalkLost | kStWalkBound;
 constexpr int kAdaMaxS = 8;     // AdaRevision snapshot slots per row (psx_adarevision_config)
 
 // Table directory passed by value to the decoder.

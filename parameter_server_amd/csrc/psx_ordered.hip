@@ -176,7 +176,17 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
-  if (!o_gate(a)) return;
+  if (!o_gate(a)) {
+    // A failed call: ordered_count may have counted some records before a block of it set
+    // a fatal bit (and blocks that started after that counted none), and ordered_offsets
+    // skipped.  Restore the invariant (cnt and grow zero between calls) over every slot;
+    // O(max_rows), failed calls only.
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < a.max_rows; s += G) {
+      a.cnt[s] = 0;
+      if (a.grow) a.grow[s] = 0;
+    }
+    return;
+  }
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
     int b;
     uint64_t off;

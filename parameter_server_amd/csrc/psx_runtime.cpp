@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,11 +29,23 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
                        uint32_t epoch, hipStream_t st);
 size_t walk_ws_bytes(uint64_t items);
-// PSX_VARIANT_DECODE.  Off by default: with two contexts walking concurrently on one GPU
-// the walk faulted intermittently (tests/test_indexed_rows_gpu.py, profiles/r02/s69, s71;
-// DESIGN.md §5); single-context runs (its parity tests, the C3 bench) opt in.
-int g_decode_walk = 0;
+// PSX_VARIANT_DECODE: 1 (default) walked messages with sparse tables decode window-parallel
+// where eligible, 0 one workgroup per message.
+int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
+// Granule tags of the window-parallel decode: unique per call across every context of the
+// process, so a granule left in a recycled allocation by another context (or an earlier
+// call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
+// restarted at 1 per context and the workspace was zeroed by a null-stream hipMemset that
+// the context's non-blocking streams do not wait for, so a new context's walk could take a
+// freed context's granule as its predecessor's state, or have its own published granule
+// zeroed under it: an out-of-range recoff write, or a lost hand-off.)
+std::atomic<uint32_t> g_walk_epoch{0};
+uint32_t next_walk_epoch() {
+  uint32_t e;
+  do e = g_walk_epoch.fetch_add(1, std::memory_order_relaxed) + 1; while (e == 0);
+  return e;
+}
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride,
                               int64_t row_offset, int64_t row_stride, int64_t max_rows, int32_t *inv,
@@ -563,11 +576,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       c->d_walk[slot] = nullptr;
       c->walk_cap[slot] = 0;
       HIP_TRY(c, hipMalloc(&c->d_walk[slot], need));
-      HIP_TRY(c, hipMemset(c->d_walk[slot], 0, need));   // no stale granule tag can match
+      // ordered before the walk on the stream that runs it (the context's streams are
+      // non-blocking: the null stream does not order against them)
+      HIP_TRY(c, hipMemsetAsync(c->d_walk[slot], 0, need, prep));
       c->walk_cap[slot] = need;
-      c->walk_epoch[slot] = 0;
     }
-    if (++c->walk_epoch[slot] == 0) c->walk_epoch[slot] = 1;
+    c->walk_epoch[slot] = psx::next_walk_epoch();
     ++psx::g_walk_calls;
   }
   psx_status st = timed(
@@ -811,7 +825,23 @@ psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
   if (sticky & psx::kStState)
     return fail(c, PSX_ERR_STATE, "AdaRevision: a record names a (row, version) without a snapshot");
   if (sticky & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "row capacity exceeded (column >= row_capacity or sorted/map row over max_entries)");
-  if (sticky & psx::kStUnsupported) return fail(c, PSX_ERR_UNSUPPORTED, "table repeated within one message");
+  if (sticky & psx::kStWalkBound)
+    return fail(c, PSX_ERR_DEVICE, "window-parallel decode: a walker state outside its message (internal error; "
+                                   "nothing applied)");
+  if (sticky & psx::kStWalkLost) {
+    char m[256];
+    uint32_t d[2][8] = {};
+    for (int k = 0; k < 2; ++k)
+      if (c->d_walk[k]) (void)hipMemcpy(d[k], c->d_walk[k], sizeof(d[k]), hipMemcpyDeviceToHost);
+    const int k = d[0][1] ? 0 : 1;
+    snprintf(m, sizeof m,
+             "window-parallel decode: a window's predecessor state never arrived (nothing applied; ticket %u "
+             "message %u window %u epoch %u tag seen %u lanes tagged 0x%x)",
+             d[k][2], d[k][3], d[k][4], d[k][5], d[k][6], d[k][7]);
+    return fail(c, PSX_ERR_DEVICE, m);
+  }
+  if (sticky & psx::kStUnsupported)
+    return fail(c, PSX_ERR_UNSUPPORTED, "table repeated within one message (or a sparse table at an unaligned offset)");
   return PSX_OK;
 }
 

@@ -54,7 +54,8 @@ struct WalkState {
 
 struct WalkCtl {      // reset by walk_head for the walk of the same call
   uint32_t ticket;
-  uint32_t pad[3];
+  uint32_t lost;      // 1 once a hand-off timed out; dbg then holds the first one:
+  uint32_t dbg[6];    // {ticket, message, window, epoch expected, tag seen (lane 0), lanes tagged}
 };
 
 struct WalkHead {     // written by walk_head, read by the first window of each message
@@ -133,7 +134,10 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
     counters[t * kMaxFused + b] = 0;
     if (b == 0) ntouched[t] = 0;
   }
-  if (b == 0 && threadIdx.x == 0) ctl->ticket = 0;
+  if (b == 0 && threadIdx.x == 0) {
+    ctl->ticket = 0;
+    ctl->lost = 0;
+  }
   __syncthreads();
   if (threadIdx.x != 0) return;
   const uint8_t *p = ss.data[b];
@@ -285,15 +289,32 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         s = head->st[b];
       } else {
         const gu64 *g = gran + (uint64_t)(tk - (uint32_t)B) * kGran;
-        uint32_t v = 0;
+        uint32_t v = 0, tag = 0;
         bool ok = false;
         for (uint32_t spins = 0;; ++spins) {
           uint64_t x = (uint64_t)epoch << 32;
           if (lane < kGran) x = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           v = (uint32_t)x;
-          if (__all((uint32_t)(x >> 32) == epoch)) { ok = true; break; }
+          tag = (uint32_t)(x >> 32);
+          if (__all(tag == epoch)) { ok = true; break; }
           if (spins > (1u << 20)) break;        // bounded (~1 s; a call takes ~0.1 ms): a lost hand-off fails the call
           __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok) {
+          // record the first lost hand-off of the call (psx_last_error reports it)
+          const uint64_t tagged = __ballot(lane < kGran && tag == epoch);
+          const uint32_t tag0 = (uint32_t)__shfl((int)tag, 0);
+          if (lane == 0) {
+            atomicOr(call_status, kStWalkLost);
+            if (atomicCAS(&ctl->lost, 0u, 1u) == 0u) {
+              ctl->dbg[0] = tk;
+              ctl->dbg[1] = (uint32_t)b;
+              ctl->dbg[2] = j;
+              ctl->dbg[3] = epoch;
+              ctl->dbg[4] = tag0;
+              ctl->dbg[5] = (uint32_t)tagged;
+            }
+          }
         }
         auto lo_hi = [&](int i) { return (uint64_t)(uint32_t)__shfl((int)v, i) | ((uint64_t)(uint32_t)__shfl((int)v, i + 1) << 32); };
         s.pos = lo_hi(0);
@@ -305,17 +326,22 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         s.t = __shfl((int)v, 11);
         s.mode = __shfl((int)v, 12);
         s.ntab = __shfl((int)v, 13);
-        if (!ok) {
-          if (lane == 0) atomicOr(call_status, kStUnsupported);
-          s.mode = 2;
-        }
+        if (!ok) s.mode = 2;
       }
       if (lane == 0) {
         const uint64_t Wend = W0 + kWBytes;
+        // this message's record-offset range (psx_runtime.cpp sizes it size / 8 + 1)
+        const uint64_t rk_lo = ss.recoff_base[b], rk_hi = rk_lo + size / 8 + 1;
         uint32_t nseg = 0;
         Seg *segs_b = segs + b * kMaxTables;
         for (;;) {
           if (s.mode == 2) break;
+          if (s.mode == 1 && (s.pos < W0 || s.rk < rk_lo || s.rk + s.left > rk_hi)) {
+            // a state no walk of this message can reach: never expand from it
+            atomicOr(call_status, kStWalkBound);
+            s.mode = 2;
+            break;
+          }
           if (s.pos >= Wend && !last) break;          // the walk continues in a later window
           if (s.mode == 0) {
             walk_header(p, size, dir, segs_b, s, call_status);

@@ -10,7 +10,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 import parameter_server_amd as psa
-from parameter_server_amd import wire, PsxError
+from parameter_server_amd import wire, PsxError, _abi
 from oracle.oracle import OracleServer, pack_stream, DENSE, SORTED_MAP, MAP, F32, F64, I32, I64
 
 pytestmark = pytest.mark.gpu
@@ -165,6 +165,45 @@ def test_sparse_column_out_of_range_applies_nothing():
     assert not srv.read_rows(3, 0, 10).any()
 
 
+@pytest.mark.parametrize("kind,max_entries,err", [(SORTED_MAP, 96, "row"), (SORTED_MAP, 512, "row"),
+                                                   (SORTED_MAP, 512, "col"), (MAP, 96, "row"), (DENSE, None, "col")],
+                         ids=["sorted-row", "sorted-split-row", "sorted-split-col", "map-row", "dense-col"])
+def test_failed_call_then_valid_call_matches_oracle(kind, max_entries, err):
+    """A call that ordered_count rejects part-way (a row outside the shard, or a column
+    outside a dense row / a sorted map's key range), then a valid call on the same context:
+    the failed call applies nothing and leaves no per-slot counts behind, so the next call
+    equals the oracle applying only it (stale counts dropped updates)."""
+    rng = np.random.RandomState(41)
+    rows, K = 600, 96
+    srv, orc = _pair(kind, I32, rows, K, max_entries=max_entries, bgs=[100])
+    recs = _sparse_rows(rng, rows, K, 500, I32, positive=True)
+    if err == "row":
+        recs.insert(250, (rows + 7, np.array([1], np.int32), np.ones(1, np.int32)))
+    elif kind == DENSE:
+        recs.insert(250, (3, np.array([K], np.int32), np.ones(1, np.int32)))
+    else:
+        # a key outside [0, max_entries) of a row already holding max_entries entries
+        recs = [(5, np.arange(max_entries, dtype=np.int32), np.ones(max_entries, np.int32))] + recs[1:]
+        recs.insert(250, (5, np.array([max_entries + 3], np.int32), np.ones(1, np.int32)))
+    bad = torch.from_numpy(wire.sparse_stream_np(3, 4, recs)).cuda()
+    torch.cuda.synchronize()
+    srv.apply_device([(bad.data_ptr(), bad.numel(), 100, 0)])
+    with pytest.raises(PsxError) as e:
+        srv.sync()
+    assert e.value.status in (5, 6)
+    assert orc.apply_stream(np.zeros(0, np.uint8), 100, 0) == 0     # the version is consumed
+    good = wire.sparse_stream_np(3, 4, _sparse_rows(rng, rows, K, 500, I32, positive=True))
+    _apply(srv, orc, [good], [100], [1])
+    if kind == DENSE:
+        assert np.array_equal(srv.read_rows(3, 0, rows), orc.read_dense_rows(3, 0, rows))
+    elif kind == SORTED_MAP:
+        assert srv.serialize_rows(3, list(range(rows))) == orc.serialize_records(3, list(range(rows)))
+    else:
+        for r in range(rows):
+            g, w = srv.serialize_rows(3, [r]), orc.serialize_records(3, [r])
+            assert len(g) == len(w) and (not g or _as_map(g[12:], I32, True) == _as_map(w[12:], I32, True))
+
+
 def test_sorted_map_capacity_overflow_reported():
     srv, _ = _pair(SORTED_MAP, I32, 4, 8, max_entries=4, bgs=[100])
     recs = [(1, np.arange(6, dtype=np.int32), np.ones(6, np.int32))]
@@ -244,10 +283,23 @@ def test_duplicate_dense_rows_replayed_in_order():
     assert np.array_equal(srv.read_rows(1, 0, rows).view(np.uint32), orc.read_dense_rows(1, 0, rows).view(np.uint32))
 
 
-def test_c3_lda_config_parity():
+@pytest.mark.parametrize("decode", [1, 0], ids=["walk", "block"])
+def test_c3_lda_config_parity(decode):
     """SURVEY §8(d) C3 at full size: 100K SortedVectorMapRow<int32> rows, K = 1024, 8
     batches of 10K distinct Zipf-chosen rows, nnz uniform [1, 32], values +-{1..3}
-    (first batch positive).  Every touched row's bytes match the oracle."""
+    (first batch positive).  Every touched row's bytes match the oracle, through the
+    window-parallel decode (the default) and through decode_streams."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(7, decode)
+    L.psx_debug_set_variant(8, 0)
+    try:
+        _c3_full(walk_expected=decode == 1)
+    finally:
+        L.psx_debug_set_variant(7, old)
+
+
+def _c3_full(walk_expected):
+    L = _abi.load()
     rng = np.random.RandomState(1234)
     rows, K, B = 100_000, 1024, 8
     bgs = list(range(100, 100 + B))
@@ -267,8 +319,10 @@ def test_c3_lda_config_parity():
         touched.update(int(x) for x in ids)
         streams.append(wire.sparse_stream_np(3, 4, recs))
     _apply(srv, orc, streams, bgs)
+    assert (L.psx_debug_get_variant(8) > 0) == walk_expected
     ids = sorted(touched)
     assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids)
+    srv.close()
 
 
 @pytest.mark.parametrize("dt", [I32, F64])

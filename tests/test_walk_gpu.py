@@ -181,12 +181,61 @@ def test_mixed_value_sizes_fall_back_to_block_decode():
     tabs = [(2, SORTED_MAP, I32, K, False, R), (3, MAP, F64, K, False, R)]
     s = _message([(2, 4, _rows(rng, rng.permutation(R)[:300], K, I32, rng.randint(1, 20, size=300))),
                   (3, 8, _rows(rng, rng.permutation(R)[:300], K, F64, rng.randint(1, 20, size=300)))])
-    L.psx_debug_set_variant(WALK_CALLS, 0)
-    st = _Setup(tabs, [100])
-    st.apply([s], 0)
-    assert st.snapshot() == st.oracle_snapshot()
-    assert L.psx_debug_get_variant(WALK_CALLS) == 0
-    st.close()
+    old = L.psx_debug_set_variant(DECODE, 1)
+    try:
+        L.psx_debug_set_variant(WALK_CALLS, 0)
+        st = _Setup(tabs, [100])
+        st.apply([s], 0)
+        assert st.snapshot() == st.oracle_snapshot()
+        assert L.psx_debug_get_variant(WALK_CALLS) == 0
+        st.close()
+    finally:
+        L.psx_debug_set_variant(DECODE, old)
+
+
+def test_walk_is_the_default():
+    assert _abi.load().psx_debug_get_variant(DECODE) == 1
+
+
+def test_concurrent_contexts_on_recycled_workspaces():
+    """Round 2's fault: two contexts walking at once, created right after contexts that
+    walked and were closed (so their walk workspaces can be the freed ones, holding granules
+    of earlier calls).  Each round closes both contexts and opens two new ones; every call
+    of both is enqueued before either syncs; both must equal the oracle every round."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(DECODE, 1)
+    try:
+        rng = np.random.RandomState(29)
+        rows, K = 3000, 256
+        tabs = [(3, SORTED_MAP, I32, K, False, rows)]
+        for rnd in range(4):
+            L.psx_debug_set_variant(WALK_CALLS, 0)
+            pair = [_Setup(tabs, [100, 101, 102]) for _ in range(2)]
+            calls = []
+            for ver in range(3):
+                per = []
+                for st in pair:
+                    streams = [wire.sparse_stream_np(3, 4, _rows(rng, rng.permutation(rows)[:2500], K, I32,
+                                                                 rng.randint(1, 40, size=2500)))
+                               for _ in range(3)]
+                    dev = [torch.from_numpy(np.array(x, copy=True)).cuda() for x in streams]
+                    per.append((st, streams, dev))
+                torch.cuda.synchronize()
+                for st, streams, dev in per:
+                    st.srv.apply_device([(d.data_ptr(), d.numel(), bg, ver) for d, bg in zip(dev, st.bgs)])
+                calls.append(per)
+            for st in pair:
+                st.srv.sync()
+            for ver, per in enumerate(calls):
+                for st, streams, _ in per:
+                    for x, bg in zip(streams, st.bgs):
+                        assert st.orc.apply_stream(x, bg, ver) == 0
+            assert L.psx_debug_get_variant(WALK_CALLS) == 6
+            for st in pair:
+                assert st.snapshot() == st.oracle_snapshot(), f"round {rnd}"
+                st.close()
+    finally:
+        L.psx_debug_set_variant(DECODE, old)
 
 
 def _malformed_cases():

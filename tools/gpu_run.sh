@@ -9,6 +9,7 @@
 #           summarised with the kernel signature into $O/pmc_dense_apply.json
 #   c3 | c3idx | c4 | c5 | ada | f16 | d125 | imp   the other workloads' bench lines
 #   probe   tools/probe_ceiling (the C2 access pattern's hardware ceiling; build it first)
+#   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -30,7 +31,7 @@ for s in "$@"; do
   case $s in
     tests) run tests 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run bench 300 python -u bench.py --steps 20 --warmup 5 --pmc-json "$PMC_JSON" ;;
+    bench) run bench 600 python -u bench.py --steps 20 --warmup 5 --pmc-json "$PMC_JSON" ;;
     walked) run walked 300 python -u bench.py --walked --steps 20 --warmup 5 --cpu-seconds 0 ;;
     stats) run stats 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o c2 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --skip-walked --no-extras
            python3 tools/kernel_stats.py "$(find "$O/stats" -name '*.db' | head -1)" "$O/c2_kernel_stats.csv" && head -4 "$O/c2_kernel_stats.csv" | cut -c1-160 ;;
@@ -55,6 +56,7 @@ for s in "$@"; do
     d125) run d125 300 python -u bench.py --density 0.125 --steps 20 --warmup 3 --cpu-seconds 0 ;;
     imp) run imp 300 python -u bench.py --importance --steps 20 --warmup 3 --cpu-seconds 0 ;;
     probe) run probe 300 tools/probe_ceiling 10 ;;
+    hbm) run hbm 400 tools/probe_hbm 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

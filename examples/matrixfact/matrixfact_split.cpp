@@ -11,6 +11,12 @@
 // The data file is the data_split binary format (data_split.cpp:200-217), partition
 // suffix ".<client_id>": size_t nnz, rows, cols; int rows[nnz]; int cols[nnz];
 // float vals[nnz], nonzeros grouped by row.
+//
+// Built with -DMF_ADAREVISION this is matrixfact_adarevision
+// (apps/matrixfact/src/matrixfact_adarevision.cpp): R's table registers
+// AdaRevisionServerTableLogic as server_table_logic 1 with version_maintain and
+// no_oplog_replay (run_matrixfact_adarevision.sh:113-116), R's rows are initialised by the
+// logic on the server, L steps with per-coordinate AdaGrad and R receives raw gradients.
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -25,6 +31,9 @@
 #include <vector>
 
 #include <petuum_ps_common/include/petuum_ps.hpp>
+#ifdef MF_ADAREVISION
+#include <petuum_ps/server/adarevision_server_table_logic.hpp>
+#endif
 
 namespace {
 
@@ -125,6 +134,34 @@ void ReadR(petuum::Table<float> &R, int j, std::vector<float> *cache) {
   row.CopyToVector(cache);
 }
 
+#ifdef MF_ADAREVISION
+// matrixfact_adarevision.cpp:194-276: L steps by AdaGrad (history starts at 1), R gets the
+// raw gradient and the server's AdaRevision logic turns it into a step
+void SgdElement(int64_t a, float step_size, std::vector<std::vector<float>> &L, std::vector<std::vector<float>> &Lh,
+                size_t L_off, petuum::Table<float> &R, std::vector<float> *Rj_cache) {
+  const int i = X_row[a], j = X_col[a];
+  const float Xij = X_val[a];
+  ReadR(R, j, Rj_cache);
+  auto &Rj = *Rj_cache;
+  auto &Li = L[i - L_off];
+  auto &Lhi = Lh[i - L_off];
+  float LiRj = 0.0f;
+  for (int k = 0; k < K; ++k) LiRj += Li[k] * Rj[k];
+  petuum::DenseUpdateBatch<float> upd(0, K);
+  const float grad_coeff = -(Xij - LiRj);
+  const float reg = (float)lambda_;
+  for (int k = 0; k < K; ++k) upd[k] = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float Lg = 2 * (grad_coeff * Rj[k] + reg / float(nnz_per_row) * Li[k]);
+    const float Rg = 2 * (grad_coeff * Li[k] + reg / float(nnz_per_col) * Rj[k]);
+    Lhi[k] += Lg * Lg;
+    Li[k] -= step_size / std::sqrt(Lhi[k]) * Lg;
+    upd[k] += Rg;
+  }
+  R.DenseBatchInc(j, upd);
+}
+#else
+
 void SgdElement(int64_t a, float step_size, std::vector<std::vector<float>> &L, size_t L_off,
                 petuum::Table<float> &R, std::vector<float> *Rj_cache) {
   const int i = X_row[a], j = X_col[a];
@@ -145,8 +182,20 @@ void SgdElement(int64_t a, float step_size, std::vector<std::vector<float>> &L, 
   }
   R.DenseBatchInc(j, upd);
 }
+#endif
 
 void InitMF(std::vector<std::vector<float>> &L, petuum::Table<float> &R, int col_begin, int col_end) {
+#ifdef MF_ADAREVISION
+  // matrixfact_adarevision.cpp:278-291: L only (seed 12345); R's rows are drawn by the
+  // server logic when they are created (ServerRowCreated)
+  std::mt19937 gen(12345);
+  std::normal_distribution<float> dist(0, 0.1);
+  for (auto &row : L)
+    for (int k = 0; k < K; ++k) row[k] = dist(gen);
+  (void)R;
+  (void)col_begin;
+  (void)col_end;
+#else
   std::mt19937 gen(1234);
   std::normal_distribution<float> dist(0, 0.1);
   for (auto &row : L)
@@ -156,6 +205,7 @@ void InitMF(std::vector<std::vector<float>> &L, petuum::Table<float> &R, int col
     for (int k = 0; k < K; ++k) u[k] = dist(gen);
     R.DenseBatchInc(j, u);
   }
+#endif
 }
 
 void RecordLoss(int eval, int iter, int clock, std::vector<std::vector<float>> &L, size_t L_off,
@@ -195,6 +245,9 @@ void SolveMF(int tid, Barrier *process_barrier) {
   const int row_end = tid == (int)X_partition_starts.size() - 1 ? X_row.back()
                                                                  : X_row[X_partition_starts[tid + 1] - 1];
   std::vector<std::vector<float>> L(row_end - row_st + 1, std::vector<float>(K, 0.f));
+#ifdef MF_ADAREVISION
+  std::vector<std::vector<float>> Lh(L.size(), std::vector<float>(K, 1.f));   // InitLTable :186
+#endif
   const size_t L_off = row_st;
 
   const int total_workers = num_clients * num_worker_threads;
@@ -224,11 +277,19 @@ void SolveMF(int tid, Barrier *process_barrier) {
   double total_eval = 0.;
   int clock = 0, eval = 0;
   for (int iter = 0; iter < num_iterations; ++iter) {
+#ifdef MF_ADAREVISION
+    const float step = (float)init_step_size;   // :507
+#else
     const float step = use_step_dec ? (float)(init_step_size * std::pow(step_dec, iter))
                                     : (float)(init_step_size * std::pow(100.0 + iter, -0.5));
+#endif
     int64_t counter = 0;
     for (int64_t a = eb; a < ee; ++a) {
+#ifdef MF_ADAREVISION
+      SgdElement(a, step, L, Lh, L_off, R, &Rj_cache);
+#else
       SgdElement(a, step, L, L_off, R, &Rj_cache);
+#endif
       ++counter;
       if ((counter % work_per_clock == 0 && clock < (iter + 1) * num_clocks_per_iter - 1) || counter == ee - eb) {
         petuum::PSTableGroup::Clock();
@@ -297,6 +358,12 @@ int main(int argc, char **argv) {
   tg.num_total_clients = num_clients;
   tg.client_id = client_id;
   tg.num_local_app_threads = num_worker_threads + 1;
+#ifdef MF_ADAREVISION
+  // matrixfact_adarevision.cpp:633-635; its flag (DECLARE_double(init_step_size)) is the logic's
+  FLAGS_init_step_size = init_step_size;
+  petuum::ClassRegistry<petuum::AbstractServerTableLogic>::GetRegistry().AddCreator(
+      1, petuum::CreateObj<petuum::AbstractServerTableLogic, petuum::AdaRevisionServerTableLogic>);
+#endif
   petuum::PSTableGroup::RegisterRow<petuum::DenseRow<float>>(0);
   petuum::PSTableGroup::RegisterRow<petuum::DenseRow<int64_t>>(1);
   petuum::PSTableGroup::Init(tg, false);   // the init thread does not access tables
@@ -315,7 +382,15 @@ int main(int argc, char **argv) {
   tc.no_oplog_replay = flag_b("no_oplog_replay", false);
   tc.process_cache_capacity = (size_t)flag_i("M_cache_size", (int)X_num_cols);
   tc.oplog_capacity = tc.process_cache_capacity;
+#ifdef MF_ADAREVISION
+  // run_matrixfact_adarevision.sh:113-116
+  tc.table_info.server_table_logic = flag_i("server_table_logic", 1);
+  tc.table_info.version_maintain = flag_b("version_maintain", true);
+  tc.no_oplog_replay = flag_b("no_oplog_replay", true);
+#endif
   petuum::PSTableGroup::CreateTable(1, tc);
+  tc.table_info.server_table_logic = -1;
+  tc.table_info.version_maintain = false;
 
   tc.table_info.oplog_dense_serialized = true;
   tc.no_oplog_replay = false;

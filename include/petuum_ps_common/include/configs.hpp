@@ -11,11 +11,10 @@
 #include <string>
 #include <vector>
 
+#include <petuum_ps_common/include/constants.hpp>
 #include <petuum_ps_common/include/host_info.hpp>
 
 namespace petuum {
-
-constexpr size_t k1_Mi = 1024 * 1024;
 
 enum ConsistencyModel { SSP = 0, SSPPush = 1, SSPAggr = 2, LocalOOC = 6 };
 

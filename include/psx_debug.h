@@ -21,7 +21,8 @@ enum {
   PSX_VARIANT_DECODE = 7        /* 1: walked messages with sparse tables decode window-parallel
                                    (psx_walk.hip, where eligible; the default), 0: one workgroup
                                    per message (decode_streams) */,
-  PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */
+  PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */,
+  PSX_VARIANT_DENSE_STORE = 9   /* 1: dense table rows stored non-temporally (default), 0: plain stores */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -39,6 +39,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include <petuum_ps_common/include/abstract_server_table_logic.hpp>
 #include <petuum_ps_common/include/ps_table_group.hpp>
 
 #include "psx.h"
@@ -97,6 +98,7 @@ class ClientTableImpl : public AbstractClientTable {
     oplog_cap_ = cfg_.table_info.dense_row_oplog_capacity ? cfg_.table_info.dense_row_oplog_capacity
                                                           : cfg_.table_info.row_capacity;
     dense_oplog_ = cfg_.table_info.row_oplog_type == RowOpLogType::kDenseRowOpLog;
+    version_ = cfg_.table_info.version_maintain;
   }
 
   void RegisterThread() override {}
@@ -128,10 +130,14 @@ class ClientTableImpl : public AbstractClientTable {
     return it == cache_.end() ? nullptr : it->second;
   }
   void Insert(int32_t row_id, const uint8_t *data, size_t size);
-  void Reset(int32_t row_id, const uint8_t *data, size_t size);
+  void Reset(int32_t row_id, const uint8_t *data, size_t size, int ch);
   void ReplayOplogLocked(int32_t row_id, AbstractRow *r);
   // RowOpLogSerializer::AppendRowOpLog for the rows of shard ch (r % C == ch), then clears them
   size_t SerializeOplog(int ch, int C, std::vector<uint8_t> *out, int32_t *num_rows);
+  // Version tables: the end-of-version records a push produced for shard ch (taken)
+  int32_t TakeEndOfVersion(int ch, std::vector<uint8_t> *out);
+  bool version_maintain() const { return version_; }
+  void set_logic(std::unique_ptr<AbstractServerTableLogic> l) { logic_ = std::move(l); }
 
   int32_t id() const { return id_; }
   int kind() const { return kind_; }
@@ -147,10 +153,21 @@ class ClientTableImpl : public AbstractClientTable {
   int kind_ = 0, dtype_ = 0, vsize_ = 4;
   int64_t oplog_cap_ = 0;
   bool dense_oplog_ = true;
+  bool version_ = false;                                           // TableInfo.version_maintain
+  std::unique_ptr<AbstractServerTableLogic> logic_;                // server_table_logic (runs on the device)
   std::mutex mtx_;                                                 // cache_ + oplogs
   std::unordered_map<int32_t, std::shared_ptr<AbstractRow>> cache_;   // process storage
   std::map<int32_t, std::vector<uint8_t>> dense_oplog_rows_;        // DenseRowOpLog V[cap]
   std::map<int32_t, std::map<int32_t, uint64_t>> sparse_oplog_rows_;   // SparseRowOpLog col -> V bits
+  // Version tables (VersionDenseRowOpLog, version_dense_row_oplog.hpp:20-180): a row's oplog
+  // lives on after it is sent (Reset zeroes it) and carries the version of the row the
+  // server last pushed; rows touched since the last send (the oplog index).
+  std::map<int32_t, uint64_t> oplog_version_;
+  std::map<int32_t, bool> oplog_index_;
+  std::map<int, std::vector<uint8_t>> eov_;                        // shard -> end-of-version records
+  std::map<int, int32_t> eov_rows_;
+  void AppendVersionRecord(std::vector<uint8_t> *out, int32_t row_id, const std::vector<uint8_t> &op,
+                           uint64_t version, bool end_of_version);
 };
 
 class Runtime {
@@ -159,6 +176,12 @@ class Runtime {
     C_ = std::max(1, cfg.num_comm_channels_per_client);
     if (cfg.consistency_model != SSPPush && cfg.consistency_model != SSP)
       die("consistency models other than SSP/SSPPush are not provided by this runtime");
+    // Every client's bg sender is registered on this process's shards, but only this
+    // process's bg ever clocks them: with more clients the min clock would never advance
+    // and the first Get after a Clock would wait forever.  Cross-process clients are not
+    // provided (the reference reaches them over ZeroMQ tcp, out of scope).
+    if (cfg.num_total_clients > 1)
+      die("num_total_clients > 1 (clients in other processes) is not provided by this runtime");
     int32_t device = 0;
     if (const char *d = std::getenv("PSX_DEVICE")) device = std::atoi(d);
     shards_.resize(C_);
@@ -196,6 +219,32 @@ class Runtime {
     if (rot == RowOpLogType::kSparseRowOpLog && c.table_info.oplog_dense_serialized &&
         sample->psx_row_kind() == PSX_ROW_DENSE)   // sparse_row_oplog.hpp:156-159
       die("Sparse OpLog does not support dense serialize");
+    const bool version = c.table_info.version_maintain;
+    if (version && (sample->psx_row_kind() != PSX_ROW_DENSE || rot != RowOpLogType::kDenseRowOpLog ||
+                    !c.table_info.oplog_dense_serialized))
+      die("version_maintain needs DenseRow tables with dense-serialized kDenseRowOpLog oplogs "
+          "(VersionDenseRowOpLog, version_dense_row_oplog.hpp)");
+    if (version && !c.no_oplog_replay)   // CHECK(no_oplog_replay), abstract_bg_worker.cpp:809-811
+      die("version_maintain needs no_oplog_replay");
+    // TableInfo.server_table_logic: the registered logic (ServerTable::ServerTable,
+    // server_table.cpp:83-93) selects one of libpsx's device logics
+    std::unique_ptr<AbstractServerTableLogic> logic;
+    DeviceTableLogic dl;
+    if (c.table_info.server_table_logic >= 0) {
+      logic.reset(ClassRegistry<AbstractServerTableLogic>::GetRegistry().CreateObject(c.table_info.server_table_logic));
+      if (!logic)
+        die("server table logic " + std::to_string(c.table_info.server_table_logic) +
+            " not registered (ClassRegistry<AbstractServerTableLogic>::AddCreator)");
+      logic->Init(c.table_info, nullptr);
+      dl = logic->GetDeviceLogic();
+      if (dl.kind == DeviceTableLogicKind::kNone)
+        die("server table logic " + std::to_string(c.table_info.server_table_logic) +
+            " has no device implementation in libpsx (built in: AdaRevision)");
+      if (dl.kind == DeviceTableLogicKind::kAdaRevision &&
+          (sample->psx_row_kind() != PSX_ROW_DENSE || sample->psx_dtype() != PSX_F32 || rot != RowOpLogType::kDenseRowOpLog ||
+           !c.table_info.oplog_dense_serialized))
+        die("the AdaRevision logic runs on DenseRow<float> tables with dense-serialized kDenseRowOpLog oplogs");
+    }
     auto t = std::make_unique<ClientTableImpl>(this, id, c, std::move(sample));
     const int64_t rows = (int64_t)c.process_cache_capacity;
     for (int ch = 0; ch < C_; ++ch) {
@@ -212,8 +261,19 @@ class Runtime {
       if (pc.max_rows < 1) pc.max_rows = 1;
       pc.max_entries = t->kind() == PSX_ROW_DENSE ? 0 : std::max<int64_t>(pc.row_capacity, 64);
       pc.server_push_row_upper_bound = (int64_t)c.table_info.server_push_row_upper_bound;
+      pc.version_maintain = version ? 1 : 0;
       check(shards_[ch].ctx, psx_table_create(shards_[ch].ctx, &pc), "psx_table_create");
+      if (dl.kind == DeviceTableLogicKind::kAdaRevision) {
+        psx_adarevision_config ac{};
+        ac.init_step_size = dl.init_step_size;
+        ac.gaussian_init = dl.gaussian_init ? 1 : 0;
+        ac.old_grad_upper_bound = dl.old_grad_upper_bound;
+        ac.push_clients = std::max(1, cfg_.num_total_clients);
+        ac.max_snapshots_per_row = dl.max_snapshots_per_row;
+        check(shards_[ch].ctx, psx_table_set_adarevision(shards_[ch].ctx, id, &ac), "AdaRevision logic");
+      }
     }
+    t->set_logic(std::move(logic));
     staleness_ = std::max(staleness_, c.table_info.table_staleness);
     table_order_.push_back(id);
     tables_[id] = std::move(t);
@@ -401,12 +461,53 @@ class Runtime {
     std::vector<uint8_t> &mine = bodies[cfg_.client_id % C];
     mine.resize(used[cfg_.client_id % C]);
     Trace("push", ch, push_seq_++, mine.data(), mine.size());
-    ApplyPushBody(mine);
+    ApplyPushBody(mine, ch);
     s.pushed_clock = min_clock;
+    SendEndOfVersionLocked(ch);
+  }
+
+  // The end-of-version records a push produced (version tables): the reference appends
+  // them to the shard's serializer for the next message; they go out here as their own
+  // message (is_clock false) ahead of it, which the server applies in the same order.
+  void SendEndOfVersionLocked(int ch) {
+    Shard &s = shards_[ch];
+    std::vector<int32_t> ids(table_order_);
+    std::sort(ids.begin(), ids.end());
+    std::vector<uint8_t> payload(4, 0);
+    int32_t ntab = 0;
+    for (int32_t id : ids) {
+      ClientTableImpl *t = tables_[id].get();
+      if (!t->version_maintain()) continue;
+      std::vector<uint8_t> recs;
+      const int32_t nrows = t->TakeEndOfVersion(ch, &recs);
+      if (!nrows) continue;
+      ++ntab;
+      uint8_t head[16];
+      const uint64_t usz = (uint64_t)vsize_of(t->dtype());
+      std::memcpy(head, &id, 4);
+      std::memcpy(head + 4, &usz, 8);
+      std::memcpy(head + 12, &nrows, 4);
+      payload.insert(payload.end(), head, head + 16);
+      payload.insert(payload.end(), recs.begin(), recs.end());
+    }
+    if (!ntab) return;
+    std::memcpy(payload.data(), &ntab, 4);
+    psx_oplog_msg_header h{};
+    h.avai_size = payload.size();
+    h.is_clock = 0;
+    h.client_id = cfg_.client_id;
+    h.version = s.version++;
+    h.bg_clock = process_clock_;
+    std::vector<uint8_t> msg(PSX_OPLOG_MSG_HEADER_BYTES + payload.size());
+    psx_encode_oplog_header(&h, msg.data());
+    std::memcpy(msg.data() + PSX_OPLOG_MSG_HEADER_BYTES, payload.data(), payload.size());
+    Trace("msg", ch, msg_seq_++, msg.data(), msg.size());
+    int32_t changed = 0;
+    check(s.ctx, psx_handle_oplog_msg(s.ctx, msg.data(), msg.size(), s.bg_id, &changed), "HandleOpLogMsg (end of version)");
   }
 
   // SerializedRowReader walk (serialized_row_reader.hpp:30-100) over the host body
-  void ApplyPushBody(const std::vector<uint8_t> &b) {
+  void ApplyPushBody(const std::vector<uint8_t> &b, int ch) {
     if (b.size() < 4) return;
     size_t off = 0;
     int32_t table_id;
@@ -428,7 +529,7 @@ class Runtime {
       off += 8;
       auto it = tables_.find(table_id);
       if (it == tables_.end()) die("push for unknown table " + std::to_string(table_id));
-      it->second->Reset(rid, b.data() + off, (size_t)size);
+      it->second->Reset(rid, b.data() + off, (size_t)size, ch);
       off += size;
     }
   }
@@ -501,6 +602,12 @@ void ClientTableImpl::BatchInc(int32_t row_id, const int32_t *cols, const void *
     auto &op = sparse_oplog_rows_[row_id];
     for (int32_t i = 0; i < n; ++i) add_value(dtype_, (uint8_t *)&op[cols[i]], up + (size_t)i * vsize_);
   }
+  // a version table's updates reach the cache only through the server
+  // (SSPConsistencyController::BatchInc, ssp_consistency_controller.cpp:117-125)
+  if (version_) {
+    oplog_index_[row_id] = true;
+    return;
+  }
   auto it = cache_.find(row_id);   // the process cache sees the thread's own updates
   if (it != cache_.end()) it->second->ApplyBatchInc(cols, u, n);
 }
@@ -517,6 +624,10 @@ void ClientTableImpl::DenseBatchInc(int32_t row_id, const void *u, int32_t index
   } else {
     auto &op = sparse_oplog_rows_[row_id];
     for (int32_t i = 0; i < n; ++i) add_value(dtype_, (uint8_t *)&op[index_st + i], up + (size_t)i * vsize_);
+  }
+  if (version_) {
+    oplog_index_[row_id] = true;
+    return;
   }
   auto it = cache_.find(row_id);
   if (it != cache_.end()) it->second->ApplyDenseBatchInc(u, index_st, n);
@@ -535,6 +646,13 @@ void ClientTableImpl::ReplayOplogLocked(int32_t row_id, AbstractRow *r) {
 }
 
 void ClientTableImpl::Insert(int32_t row_id, const uint8_t *data, size_t size) {
+  // version tables: the row bytes end with the row's uint64 version (ExtractRowVersion,
+  // abstract_bg_worker.cpp:1032-1040); an inserted row leaves the oplog's version alone
+  // (InsertNonexistentRow, :852-880)
+  if (version_) {
+    if (size < 8) die("version row reply without its version");
+    size -= 8;
+  }
   std::shared_ptr<AbstractRow> r(ClassRegistry<AbstractRow>::GetRegistry().CreateObject(cfg_.table_info.row_type));
   r->Init(cfg_.table_info.row_capacity);
   r->Deserialize(data, size);
@@ -545,15 +663,54 @@ void ClientTableImpl::Insert(int32_t row_id, const uint8_t *data, size_t size) {
   cache_[row_id] = r;
 }
 
-void ClientTableImpl::Reset(int32_t row_id, const uint8_t *data, size_t size) {
+void ClientTableImpl::Reset(int32_t row_id, const uint8_t *data, size_t size, int ch) {
   std::lock_guard<std::mutex> g(mtx_);
+  uint64_t row_version = 0;
+  if (version_) {
+    if (size < 8) die("version row push without its version");
+    size -= 8;
+    std::memcpy(&row_version, data + size, 8);
+  }
   auto it = cache_.find(row_id);
   if (it == cache_.end()) return;   // not cached: the reference drops it too
   AbstractRow *r = it->second.get();
   r->GetWriteLock();
   r->ResetRowData(data, size);
   ReplayOplogLocked(row_id, r);
+  // UpdateExistingRow with version_maintain (abstract_bg_worker.cpp:807-823): a row that has
+  // an oplog sends it now as the end of its version, then the oplog restarts empty at the
+  // pushed row's version
+  auto op = dense_oplog_rows_.find(row_id);
+  if (version_ && op != dense_oplog_rows_.end()) {
+    AppendVersionRecord(&eov_[ch], row_id, op->second, oplog_version_[row_id], true);
+    ++eov_rows_[ch];
+    std::fill(op->second.begin(), op->second.end(), 0);
+    oplog_version_[row_id] = row_version;
+  }
   r->ReleaseWriteLock();
+}
+
+// VersionDenseRowOpLog::SerializeDense: int32 row_id; V[cap]; uint64 version; bool
+// end_of_version (version_dense_row_oplog.hpp:128-180)
+void ClientTableImpl::AppendVersionRecord(std::vector<uint8_t> *out, int32_t row_id, const std::vector<uint8_t> &op,
+                                          uint64_t version, bool end_of_version) {
+  const size_t at = out->size();
+  out->resize(at + 4 + op.size() + 9);
+  std::memcpy(out->data() + at, &row_id, 4);
+  std::memcpy(out->data() + at + 4, op.data(), op.size());
+  std::memcpy(out->data() + at + 4 + op.size(), &version, 8);
+  (*out)[at + 4 + op.size() + 8] = end_of_version ? 1 : 0;
+}
+
+int32_t ClientTableImpl::TakeEndOfVersion(int ch, std::vector<uint8_t> *out) {
+  std::lock_guard<std::mutex> g(mtx_);
+  auto it = eov_.find(ch);
+  if (it == eov_.end() || it->second.empty()) return 0;
+  out->insert(out->end(), it->second.begin(), it->second.end());
+  it->second.clear();
+  const int32_t n = eov_rows_[ch];
+  eov_rows_[ch] = 0;
+  return n;
 }
 
 size_t ClientTableImpl::SerializeOplog(int ch, int C, std::vector<uint8_t> *out, int32_t *num_rows) {
@@ -573,6 +730,19 @@ size_t ClientTableImpl::SerializeOplog(int ch, int C, std::vector<uint8_t> *out,
     }
     ++*num_rows;
   };
+  if (version_) {
+    // PrepareOpLogsNormalNoReplay (ssp_bg_worker.cpp:169-213): the rows in the oplog index,
+    // each sent with its version and then Reset (zeroed, kept)
+    for (auto it = oplog_index_.begin(); it != oplog_index_.end();) {
+      if (it->first % C != ch) { ++it; continue; }
+      auto &op = dense_oplog_rows_[it->first];
+      AppendVersionRecord(out, it->first, op, oplog_version_[it->first], false);
+      std::fill(op.begin(), op.end(), 0);
+      ++*num_rows;
+      it = oplog_index_.erase(it);
+    }
+    return out->size();
+  }
   for (auto it = dense_oplog_rows_.begin(); it != dense_oplog_rows_.end();) {
     if (it->first % C != ch) { ++it; continue; }
     if (dense_ser) {   // SerializeDense: int32 row_id; V[cap] (dense_row_oplog.hpp:133-136)

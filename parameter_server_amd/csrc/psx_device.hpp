@@ -94,6 +94,7 @@ struct DenseArgs {
   uint32_t rows_mask;          // bit b: message b was placed from the producer's record rows, so
                                // every record's row id is checked against its slot in the apply
   int64_t row_offset, row_stride;   // shard geometry (expected row id of a slot)
+  int32_t store_nt;                 // 1: table rows stored non-temporally (PSX_VARIANT_DENSE_STORE)
 };
 
 // AdaRevision server-table logic on one f32 dense table (psx_ada.hip).

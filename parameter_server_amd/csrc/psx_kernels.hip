@@ -423,7 +423,16 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p) {
     return v;
   }
 }
-__device__ __forceinline__ void store16(uint8_t *p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
+// Table-row stores.  Non-temporal (the default): the row leaves the XCD's L2 as a streaming
+// write instead of sitting there dirty until evicted amid the record gathers — the C2
+// apply's 1.07 GB of row writes cost ~0.8 ms of a 2.4 ms launch as plain stores and ~0.2 ms
+// less as nt stores (tools/probe_apply.hip, profiles/r03/s4).  Rows are 4-byte aligned.
+__device__ __forceinline__ void store16(uint8_t *p, u32x4 v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4_a4, v), reinterpret_cast<u32x4_a4 *>(p));
+  else
+    __builtin_memcpy(p, &v, 16);
+}
 
 // Four binary16 record values (8 bytes, 2-byte aligned) -> four f32 bit patterns, by the
 // hardware conversion (NaN payloads kept and quieted; every value then goes through
@@ -633,7 +642,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
               }
               acc = Vec<V>::add(acc, u[q][b]);
             }
-          if (full && has[q]) store16(trow[q] + e0 * VS, acc);
+          if (full && has[q]) store16(trow[q] + e0 * VS, acc, a.store_nt);
         }
       }
       // ragged tail (cap % EPV elements): element-wise on the first lanes
@@ -882,7 +891,7 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
               }
               acc = Vec<V>::add(acc, u[q][b]);
             }
-          if (full && has[q] && ((okq >> q) & 1u)) store16(trow[q] + e0 * VS, acc);
+          if (full && has[q] && ((okq >> q) & 1u)) store16(trow[q] + e0 * VS, acc, a.store_nt);
         }
       }
       if (!verified) verify();
@@ -1034,7 +1043,7 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
 #pragma unroll
             for (int j = 0; j < M; ++j)
               if (j >= beg[q] && j < beg[q + 1]) acc = Vec<V>::add(acc, u[j]);
-            if (full) store16(table + (s0 + ks[q]) * row_bytes + e0 * VS, acc);
+            if (full) store16(table + (s0 + ks[q]) * row_bytes + e0 * VS, acc, a.store_nt);
           }
         }
       }

@@ -33,6 +33,7 @@ size_t walk_ws_bytes(uint64_t items);
 // where eligible, 0 one workgroup per message.
 int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
+int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -740,6 +741,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.rows_mask = rows_mask[ti];
     a.row_offset = t.cfg.row_offset;
     a.row_stride = t.cfg.row_stride;
+    a.store_nt = psx::g_dense_store_nt;
     st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream, t.rec_f16()); });
     if (st) return st;
   }
@@ -2304,6 +2306,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_ORD_SPLIT: return &psx::g_ord_split;
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
+    case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     default: return nullptr;
   }
 }

@@ -11,8 +11,13 @@ class OracleBackend:
         self.num_clients = num_clients
         self.tables = []
 
-    def create(self, tid, kind, dt, cap, dense_serialized=True):
-        self.o.create_table(tid, kind, dt, cap if kind == DENSE else 0, oplog_dense_serialized=dense_serialized)
+    def create(self, tid, kind, dt, cap, dense_serialized=True, version_maintain=False, adarevision=None):
+        """adarevision: dict(init_step_size, gaussian_init, old_grad_upper_bound) attaches
+        AdaRevisionServerTableLogic (push_clients = this backend's clients)."""
+        self.o.create_table(tid, kind, dt, cap if kind == DENSE else 0, oplog_dense_serialized=dense_serialized,
+                            version_maintain=version_maintain)
+        if adarevision is not None:
+            assert self.o.set_adarevision(tid, push_clients=self.num_clients, **adarevision) == 0
         self.tables.append(tid)
 
     def ApplyOpLogUpdateVersion(self, payload, size, bg, version):

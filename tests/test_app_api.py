@@ -90,3 +90,53 @@ def test_client_rows_match_server_row_bytes(tmp_path, built_lib):
     m["c"], m["v"] = [4, 10], [-1.0, 2.5]
     assert out["map"] == _hex(m)
     assert out["batch"] == "2 1 2"
+
+
+LOGIC_PROGRAM = r"""
+#include <petuum_ps_common/include/petuum_ps.hpp>
+#include <petuum_ps_common/include/constants.hpp>
+#include <petuum_ps_common/include/abstract_server_table_logic.hpp>
+#include <petuum_ps/server/adarevision_server_table_logic.hpp>
+#include <cstdio>
+// an app's own logic without a device implementation compiles against the interface
+class MyLogic : public petuum::AbstractServerTableLogic {
+ public:
+  void Init(const petuum::TableInfo &, petuum::ApplyRowBatchIncFunc) override {}
+  void ServerRowCreated(int32_t, petuum::ServerRow *) override {}
+  void ApplyRowOpLog(int32_t, const int32_t *, const void *, int32_t, petuum::ServerRow *, uint64_t, bool) override {}
+  void ServerRowSent(int32_t, uint64_t, size_t) override {}
+  bool AllowSend() override { return true; }
+};
+int main() {
+  auto &reg = petuum::ClassRegistry<petuum::AbstractServerTableLogic>::GetRegistry();
+  reg.AddCreator(1, petuum::CreateObj<petuum::AbstractServerTableLogic, petuum::AdaRevisionServerTableLogic>);
+  reg.AddCreator(2, petuum::CreateObj<petuum::AbstractServerTableLogic, MyLogic>);
+  FLAGS_init_step_size = 0.25;
+  petuum::TableInfo ti;
+  ti.server_table_logic = 1;
+  petuum::AbstractServerTableLogic *a = reg.CreateObject(1), *m = reg.CreateObject(2);
+  a->Init(ti, nullptr);
+  m->Init(ti, nullptr);
+  const petuum::DeviceTableLogic d = a->GetDeviceLogic();
+  std::printf("%d %g %d %llu %d %zu %llu\n", (int)d.kind, d.init_step_size, (int)d.gaussian_init,
+              (unsigned long long)d.old_grad_upper_bound, (int)m->GetDeviceLogic().kind,
+              petuum::k1_Mi, (unsigned long long)petuum::kMaxPendingMsgs);
+  delete a;
+  delete m;
+  return 0;
+}
+"""
+
+
+def test_server_table_logic_seam_compiles_and_selects_adarevision(tmp_path, built_lib):
+    """abstract_server_table_logic.hpp (the reference's interface, :13-32), constants.hpp and
+    adarevision_server_table_logic.hpp: an app registers logics through ClassRegistry as
+    matrixfact_adarevision.cpp:633-635 does; AdaRevision maps to libpsx's device logic with
+    its flags, an app-defined logic to none (CreateTable then refuses it)."""
+    src = tmp_path / "logic.cpp"
+    src.write_text(LOGIC_PROGRAM)
+    exe = tmp_path / "logic"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert out == ["1", "0.25", "1", "10000", "0", str(1024 * 1024), "200"]

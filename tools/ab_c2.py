@@ -3,8 +3,9 @@ rule 24): the headline workload of bench.py, then R rounds; each round runs ever
 configuration for K steps and records the per-kernel HIP-event times.  Prints JSON with
 the median ms of every kernel per configuration.
 Usage: python tools/ab_c2.py --configs 0,0:1,2 [--rounds 5 --steps 5]
-       (apply_variant[:rows], include/psx_debug.h; rows = 1 applies through
-       psx_apply_indexed_rows with the batches' record-row lists)"""
+       (apply_variant[:rows[:store_nt]], include/psx_debug.h; rows = 1 applies through
+       psx_apply_indexed_rows with the batches' record-row lists; store_nt selects
+       PSX_VARIANT_DENSE_STORE, default 1)"""
 import argparse
 import json
 import os
@@ -47,11 +48,15 @@ def main():
     del table0
     ver = [0]
     kernels = ("decode_streams", "dense_index", "dense_verify", "dense_apply", "finish_call")
-    configs = [tuple(int(x) for x in (c + ":0").split(":")[:2]) for c in args.configs.split(",")]
+    configs = []
+    for c in args.configs.split(","):
+        f = [int(x) for x in c.split(":")]
+        configs.append(tuple(f + [0, 1][len(f) - 1:]) if len(f) < 3 else tuple(f[:3]))
     res = {c: {k: [] for k in kernels + ("step",)} for c in configs}
 
     def run(c, steps):
         L.psx_debug_set_variant(1, c[0])
+        L.psx_debug_set_variant(9, c[2])
         srv.timing(True)
         srv.timing_reset()
         torch.cuda.synchronize()
@@ -79,7 +84,7 @@ def main():
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))
             res[c]["step"].append(step_ms)
-    out = {f"apply{c[0]}" + ("_rows" if c[1] else ""): {k: round(statistics.median(v), 4) for k, v in res[c].items()}
+    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + ("_ntstore" if c[2] else "_plainstore"): {k: round(statistics.median(v), 4) for k, v in res[c].items()}
            for c in configs}
     print(json.dumps(out, indent=1))
     srv.close()

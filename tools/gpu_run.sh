@@ -16,6 +16,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${TAG:-run}
 mkdir -p "$O"
 export TMPDIR=/tmp
+# raw profiler output (SQLite databases, hundreds of MB) stays on the box; $O gets summaries
+R=/tmp/gr_${TAG:-run}
+mkdir -p "$R"
 PMC_JSON=$O/pmc_dense_apply.json
 [ -f "$PMC_JSON" ] || PMC_JSON=profiles/r02/pmc_dense_apply.json
 say() { echo "== $(date +%T) $*"; }
@@ -33,20 +36,32 @@ for s in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 5 --pmc-json "$PMC_JSON" ;;
     walked) run walked 300 python -u bench.py --walked --steps 20 --warmup 5 --cpu-seconds 0 ;;
-    stats) run stats 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o c2 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --skip-walked --no-extras
-           python3 tools/kernel_stats.py "$(find "$O/stats" -name '*.db' | head -1)" "$O/c2_kernel_stats.csv" && head -4 "$O/c2_kernel_stats.csv" | cut -c1-160 ;;
-    stats3) run stats3 300 rocprofv3 --kernel-trace --stats -d "$O/stats3" -o c3 -- python3 bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0
-           python3 tools/kernel_stats.py "$(find "$O/stats3" -name '*.db' | head -1)" "$O/c3_kernel_stats.csv" && head -6 "$O/c3_kernel_stats.csv" | cut -c1-160 ;;
+    stats) run stats 300 rocprofv3 --kernel-trace --stats -d "$R/stats" -o c2 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --skip-walked --no-extras
+           python3 tools/kernel_stats.py "$(find "$R/stats" -name '*.db' | head -1)" "$O/c2_kernel_stats.csv" && head -4 "$O/c2_kernel_stats.csv" | cut -c1-160 ;;
+    stats3) run stats3 300 rocprofv3 --kernel-trace --stats -d "$R/stats3" -o c3 -- python3 bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0
+           python3 tools/kernel_stats.py "$(find "$R/stats3" -name '*.db' | head -1)" "$O/c3_kernel_stats.csv" && head -6 "$O/c3_kernel_stats.csv" | cut -c1-160 ;;
     pmc)
       P=1
       for ctrs in "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" "FETCH_SIZE" "WRITE_SIZE"; do
         say "pmc pass $P: $ctrs"
-        timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$O/pmc/p$P" -o pmc -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --skip-walked --no-extras \
+        timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$R/pmc/p$P" -o pmc -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --skip-walked --no-extras \
           > "$O/pmc_p$P.log" 2>&1 || { echo "!! pmc pass $P"; tail -5 "$O/pmc_p$P.log"; exit 1; }
         P=$((P+1))
       done
-      python3 tools/pmc_summary.py "$O/pmc" "$O/pmc_dense_apply.json" || exit 1
+      python3 tools/pmc_summary.py "$R/pmc" "$O/pmc_dense_apply.json" || exit 1
       PMC_JSON=$O/pmc_dense_apply.json ;;
+    listpmc) timeout -s KILL 60 rocprofv3 -L > "$R/counters.txt" 2>&1; echo "listpmc rc=$?"; grep -o "SQ_[A-Z_0-9]*\|TCC_[A-Z_0-9]*\|TCP_[A-Z_0-9]*\|TA_[A-Z_0-9]*\|TD_[A-Z_0-9]*" "$R/counters.txt" | sort -u > "$O/counter_names.txt"; wc -l < "$O/counter_names.txt" ;;
+    pmc3)
+      P=1
+      for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+                  "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
+                  "TCC_HIT_sum TCC_MISS_sum SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH"; do
+        say "pmc3 pass $P: $ctrs"
+        timeout -s KILL 90 rocprofv3 --pmc $ctrs -d "$R/pmc3/p$P" -o pmc -- python3 bench.py --workload c3 --steps 3 --warmup 1 --cpu-seconds 0 \
+          > "$O/pmc3_p$P.log" 2>&1 || { echo "!! pmc3 pass $P"; tail -5 "$O/pmc3_p$P.log"; exit 1; }
+        P=$((P+1))
+      done
+      python3 tools/pmc_db.py $(find "$R/pmc3" -name '*.db' | sort) > "$O/pmc3.json" && echo "pmc3 summarised" ;;
     c3) run c3 300 python -u bench.py --workload c3 --steps 20 --warmup 3 ;;
     c3idx) run c3idx 300 python -u bench.py --workload c3 --indexed --steps 20 --warmup 3 ;;
     c4) run c4 600 python -u bench.py --workload c4 --steps 3 --warmup 1 ;;
@@ -57,6 +72,9 @@ for s in "$@"; do
     imp) run imp 300 python -u bench.py --importance --steps 20 --warmup 3 --cpu-seconds 0 ;;
     probe) run probe 300 tools/probe_ceiling 10 ;;
     hbm) run hbm 400 tools/probe_hbm 10 ;;
+    abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:0:0,0:0:1 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -40 ;;
+    pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
+    papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -94,7 +94,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 5
+#define PSX_ABI_VERSION 6
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -489,6 +489,46 @@ psx_status psx_pack_stream(psx_ctx *ctx, const psx_pack_table *tables, int32_t n
  * every record in message order, for psx_apply_indexed_rows. */
 psx_status psx_pack_stream_indexed(psx_ctx *ctx, const psx_pack_table *tables, int32_t n, void *out,
                                    size_t cap, size_t *used, uint64_t *record_offsets, int32_t *record_rows);
+
+/* ---- multi-GPU: the per-server split and the exchange ------------------------------ */
+/* The client's per-server split (AbstractBgWorker::CreateOpLogMsgs, abstract_bg_worker.cpp:
+ * 590-649, routing each row by GetPartitionServerID, row_oplog_serializer.hpp:100-124) of
+ * one packed message resident on this context's GPU: owner o (0 <= o < nowners) owns rows
+ * [row_begin[o], row_begin[o + 1]) (row-range shards; row_begin has nowners + 1 entries).
+ * out receives the owners' sub-streams back to back in owner order (device, 4-byte
+ * aligned), each a complete Appendix-A message: its tables in the message's order, tables
+ * without records for the owner omitted, records in message order; out_sizes[o] (host)
+ * its bytes — 0 (an empty message, abstract_bg_worker.cpp:670-682) for an owner with no
+ * records.  The tables are this context's (record formats); record_offsets as in
+ * psx_apply_indexed (NULL: sparse tables are walked).  A row outside every owner's range
+ * is PSX_ERR_ROW_RANGE.  out == NULL or out_cap too small: PSX_ERR_BUFFER_TOO_SMALL with
+ * out_sizes filled; size + nowners * (4 + 16 * tables in the message) always suffices.
+ * Synchronous on the context stream. */
+#define PSX_MAX_SPLIT_OWNERS 64
+psx_status psx_split_stream(psx_ctx *ctx, const void *stream, size_t size, const uint64_t *record_offsets,
+                            int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
+                            uint64_t *out_sizes);
+
+/* The exchange (RCCL over xGMI, one process per GPU): replaces the reference's ZeroMQ
+ * transport of per-server messages (SendOpLogMsgs, abstract_bg_worker.cpp:651-689 ->
+ * ServerThread receive, server_thread.cpp:419-426) for batches already on the GPUs.
+ * psx_comm_unique_id on one rank; every rank passes the same id to psx_comm_create.
+ * psx_exchange_sizes then psx_exchange_streams are collectives: send holds nranks
+ * sub-streams back to back in owner order (send_sizes[p] bytes for rank p, multiples of
+ * 4); recv receives the sub-streams addressed to this rank back to back in source-rank
+ * order (recv_sizes[p] from rank p, as psx_exchange_sizes returned them) — the order
+ * psx_apply_streams_device then applies them in.  hip_stream: the stream both run on
+ * (NULL: the null stream); psx_exchange_sizes synchronizes it, psx_exchange_streams does
+ * not. */
+#define PSX_COMM_ID_BYTES 128
+typedef struct psx_comm psx_comm;
+psx_status psx_comm_unique_id(void *id);
+psx_status psx_comm_create(const void *id, int32_t nranks, int32_t rank, int32_t device, psx_comm **out);
+psx_status psx_comm_destroy(psx_comm *comm);
+const char *psx_comm_last_error(psx_comm *comm);
+psx_status psx_exchange_sizes(psx_comm *comm, const uint64_t *send_sizes, uint64_t *recv_sizes, void *hip_stream);
+psx_status psx_exchange_streams(psx_comm *comm, const void *send, const uint64_t *send_sizes, void *recv,
+                                const uint64_t *recv_sizes, void *hip_stream);
 
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);

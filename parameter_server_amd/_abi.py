@@ -182,6 +182,13 @@ def load():
         "psx_timing_enable": ([vp, i32], ctypes.c_int),
         "psx_timing_read": ([vp, ctypes.c_char_p, P(ctypes.c_double), P(i64)], ctypes.c_int),
         "psx_timing_reset": ([vp], ctypes.c_int),
+        "psx_split_stream": ([vp, vp, sz, vp, i32, vp, vp, sz, vp], ctypes.c_int),
+        "psx_comm_unique_id": ([vp], ctypes.c_int),
+        "psx_comm_create": ([vp, i32, i32, i32, P(vp)], ctypes.c_int),
+        "psx_comm_destroy": ([vp], ctypes.c_int),
+        "psx_comm_last_error": ([vp], ctypes.c_char_p),
+        "psx_exchange_sizes": ([vp, vp, vp, vp], ctypes.c_int),
+        "psx_exchange_streams": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "psx_debug_set_variant": ([i32, i32], i32),
         "psx_debug_get_variant": ([i32], i32),
     }

@@ -158,6 +158,8 @@ struct OrdArgs {
   int32_t *off;
   int32_t *tsum;
   uint64_t *list;         // records grouped by slot: (message << 56) | byte offset of the row id
+  int32_t *list_n;        // beside list (sparse records): each record's column count n, so the
+                          // apply has a record's size without loading its header
   int32_t *touched;       // slots with >= 1 record this call (unordered)
   uint32_t *ntouched;     // its length (zeroed by decode_streams)
   void *dense;
@@ -314,6 +316,33 @@ struct ClientTable {
   int32_t *nent;
   uint64_t *ver;     // version tables: the pushed row version
   int32_t *claim;    // per slot, zero between calls
+};
+
+// psx_split_stream (psx_split.hip): one table of the message being split, stream order.
+struct SplitTab {
+  int64_t k0;        // flattened index of its first record
+  int64_t rec0;      // dense: byte offset of record 0; sparse: index into recoff
+  int64_t stride;    // dense record stride
+  int32_t sparse;
+  int32_t vsize;     // sparse value size
+};
+
+constexpr int kMaxSplitOwners = 64;   // == PSX_MAX_SPLIT_OWNERS
+
+struct SplitArgs {
+  const uint8_t *msg;
+  const uint64_t *recoff;
+  const SplitTab *tabs;
+  int32_t ntab;
+  int32_t nowners;
+  int64_t nrec, ntiles;                     // records; tiles of 64 records
+  int64_t row_begin[kMaxSplitOwners + 1];   // owner o: rows [row_begin[o], row_begin[o+1])
+  uint64_t *src_off, *meta;                 // per record: byte offset; owner << 48 | table << 40 | size
+  int64_t *tile_bytes, *tile_pre, *scan_tmp;   // [nowners][ntiles] bytes, its exclusive scan (+1)
+  int64_t *ot_count, *ot_bytes;             // [nowners][ntab]
+  const int64_t *owner_base, *hdr_shift;    // [nowners], [nowners][ntab]
+  uint8_t *out;
+  uint32_t *status;
 };
 
 // Write a few 4-byte words (table ids and separators) into the body.

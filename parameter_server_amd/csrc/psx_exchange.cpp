@@ -1,0 +1,138 @@
+// psx_exchange.cpp — the exchange step of the multi-GPU path, over RCCL (xGMI on one node).
+//
+// The reference moves a worker's per-server messages over ZeroMQ: the client splits its
+// oplog by owning server while packing (AbstractBgWorker::CreateOpLogMsgs,
+// abstract_bg_worker.cpp:590-649) and sends each server its message (SendOpLogMsgs,
+// :651-689); each server thread receives and applies (server_thread.cpp:419-426).  On one
+// MI355X node, when a worker's batch sits on one GPU and spans the row-range shards of
+// several, the per-owner sub-streams (psx_split_stream) travel in one all-to-all-v of
+// grouped ncclSend/ncclRecv: every GPU sends each owner its sub-stream and receives one
+// from every worker, in source-rank order, which psx_apply_streams_device then applies in
+// that order (bit-exact to the reference applying the same messages one by one).
+//
+// Why not reduce-scatter: the same bytes to 0.1% at full coverage, but it
+// would sum the workers' updates before the table add (a different rounding) and needs
+// dense full-width batches.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/psx.h"
+
+struct psx_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  uint64_t *d_sizes = nullptr;   // [2][nranks]: send sizes, received sizes
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string t_err;
+
+psx_status comm_fail(psx_comm *c, const std::string &m, psx_status st = PSX_ERR_DEVICE) {
+  if (c) c->err = m;
+  t_err = m;
+  return st;
+}
+
+#define NCCL_TRY(c, x)                                                                     \
+  do {                                                                                     \
+    ncclResult_t r_ = (x);                                                                 \
+    if (r_ != ncclSuccess) return comm_fail(c, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+#define HIPX_TRY(c, x)                                                                     \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return comm_fail(c, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+psx_status psx_comm_unique_id(void *id) {
+  static_assert(sizeof(ncclUniqueId) <= PSX_COMM_ID_BYTES, "ncclUniqueId size");
+  if (!id) return PSX_ERR_INVALID_ARG;
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return comm_fail(nullptr, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memset(id, 0, PSX_COMM_ID_BYTES);
+  std::memcpy(id, &u, sizeof(u));
+  return PSX_OK;
+}
+
+psx_status psx_comm_create(const void *id, int32_t nranks, int32_t rank, int32_t device, psx_comm **out) {
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return PSX_ERR_INVALID_ARG;
+  *out = nullptr;
+  auto *c = new psx_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  auto cleanup = [&](psx_status st) {
+    if (c->d_sizes) hipFree(c->d_sizes);
+    delete c;
+    return st;
+  };
+  if (hipSetDevice(device) != hipSuccess) return cleanup(comm_fail(nullptr, "hipSetDevice", PSX_ERR_NO_DEVICE));
+  if (hipMalloc(&c->d_sizes, sizeof(uint64_t) * 2 * (size_t)nranks) != hipSuccess)
+    return cleanup(comm_fail(nullptr, "hipMalloc", PSX_ERR_OOM));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) return cleanup(comm_fail(nullptr, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
+  *out = c;
+  return PSX_OK;
+}
+
+psx_status psx_comm_destroy(psx_comm *c) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->d_sizes) hipFree(c->d_sizes);
+  delete c;
+  return PSX_OK;
+}
+
+const char *psx_comm_last_error(psx_comm *c) { return c ? c->err.c_str() : t_err.c_str(); }
+
+psx_status psx_exchange_sizes(psx_comm *c, const uint64_t *send_sizes, uint64_t *recv_sizes, void *hip_stream) {
+  if (!c || !send_sizes || !recv_sizes) return PSX_ERR_INVALID_ARG;
+  for (int i = 0; i < c->nranks; ++i)
+    if (send_sizes[i] % 4) return comm_fail(c, "sub-stream sizes are multiples of 4 bytes", PSX_ERR_INVALID_ARG);
+  hipStream_t st = (hipStream_t)hip_stream;
+  HIPX_TRY(c, hipSetDevice(c->device));
+  const size_t n = (size_t)c->nranks;
+  HIPX_TRY(c, hipMemcpyAsync(c->d_sizes, send_sizes, sizeof(uint64_t) * n, hipMemcpyHostToDevice, st));
+  NCCL_TRY(c, ncclGroupStart());
+  for (int p = 0; p < c->nranks; ++p) {
+    NCCL_TRY(c, ncclSend(c->d_sizes + p, 1, ncclUint64, p, c->comm, st));
+    NCCL_TRY(c, ncclRecv(c->d_sizes + n + p, 1, ncclUint64, p, c->comm, st));
+  }
+  NCCL_TRY(c, ncclGroupEnd());
+  HIPX_TRY(c, hipMemcpyAsync(recv_sizes, c->d_sizes + n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
+  HIPX_TRY(c, hipStreamSynchronize(st));
+  return PSX_OK;
+}
+
+psx_status psx_exchange_streams(psx_comm *c, const void *send, const uint64_t *send_sizes, void *recv,
+                                const uint64_t *recv_sizes, void *hip_stream) {
+  if (!c || !send_sizes || !recv_sizes) return PSX_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)hip_stream;
+  HIPX_TRY(c, hipSetDevice(c->device));
+  uint64_t so = 0, ro = 0;
+  NCCL_TRY(c, ncclGroupStart());
+  for (int p = 0; p < c->nranks; ++p) {
+    if (send_sizes[p]) NCCL_TRY(c, ncclSend((const uint8_t *)send + so, send_sizes[p], ncclUint8, p, c->comm, st));
+    if (recv_sizes[p]) NCCL_TRY(c, ncclRecv((uint8_t *)recv + ro, recv_sizes[p], ncclUint8, p, c->comm, st));
+    so += send_sizes[p];
+    ro += recv_sizes[p];
+  }
+  NCCL_TRY(c, ncclGroupEnd());
+  return PSX_OK;
+}
+
+}  // extern "C"

@@ -25,6 +25,9 @@ hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t 
                          uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
                          hipStream_t st);
 bool dense_apply_checks_rows(const DenseArgs &a, bool rec_f16);
+hipError_t launch_split_count(const SplitArgs &a, hipStream_t st);
+hipError_t launch_split_scatter(const SplitArgs &a, const int64_t *pos, const uint32_t *val, int32_t nwords,
+                                hipStream_t st);
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
                        uint32_t epoch, hipStream_t st);
@@ -34,6 +37,7 @@ size_t walk_ws_bytes(uint64_t items);
 int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
+int g_ord_pipeline = 1;     // PSX_VARIANT_ORD_PIPELINE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -233,7 +237,10 @@ struct psx_ctx {
   uint8_t *d_zero = nullptr;
   uint8_t *d_staging = nullptr;
   size_t staging_cap = 0;
+  void *d_split_fixed = nullptr, *d_split_recoff = nullptr, *d_split_scratch = nullptr;   // psx_split_stream
+  size_t split_fixed_cap = 0, split_recoff_cap = 0, split_scratch_cap = 0;
   uint64_t *d_list = nullptr;            // ordered path: record lists ((message << 56) | offset)
+  int32_t *d_list_n = nullptr;           // beside d_list: each sparse record's column count
   size_t list_cap = 0;
   std::vector<PendingCall> pending;      // calls since the last psx_sync (duplicate-row replay)
   int64_t call_seq = 0;
@@ -497,9 +504,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     }
     if (any_ordered && list_need > c->list_cap) {
       if (c->d_list) hipFree(c->d_list);
+      if (c->d_list_n) hipFree(c->d_list_n);
       c->d_list = nullptr;
+      c->d_list_n = nullptr;
       c->list_cap = 0;
       HIP_TRY(c, hipMalloc(&c->d_list, list_need * sizeof(uint64_t)));
+      HIP_TRY(c, hipMalloc(&c->d_list_n, list_need * sizeof(int32_t)));
       c->list_cap = list_need;
     }
   }
@@ -650,7 +660,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.cnt = t.d_cnt;
     a.off = t.d_off;
     a.tsum = t.d_tsum;
-    a.list = c->d_list + list_region * ord_k++;
+    a.list = c->d_list + list_region * ord_k;
+    a.list_n = psx::g_ord_pipeline ? c->d_list_n + list_region * ord_k : nullptr;
+    ++ord_k;
     a.touched = t.d_touched;
     a.ntouched = c->d_ntouched[slot] + ti;
     a.dense = t.d_data;
@@ -1012,6 +1024,10 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (auto &t : c->tables) free_table(t);
   if (c->d_list) hipFree(c->d_list);
+  if (c->d_list_n) hipFree(c->d_list_n);
+  if (c->d_split_fixed) hipFree(c->d_split_fixed);
+  if (c->d_split_recoff) hipFree(c->d_split_recoff);
+  if (c->d_split_scratch) hipFree(c->d_split_scratch);
   for (auto &p : c->pending_ev) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -1814,6 +1830,181 @@ psx_status psx_adarevision_state(psx_ctx *c, int32_t table_id, int64_t first_row
   return PSX_OK;
 }
 
+// psx_split_stream (psx_split.hip): the client's per-server split of one packed message.
+psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const uint64_t *record_offsets,
+                            int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
+                            uint64_t *out_sizes) {
+  if (!c || !out_sizes || !row_begin || nowners < 1 || nowners > PSX_MAX_SPLIT_OWNERS || (size && !stream))
+    return PSX_ERR_INVALID_ARG;
+  for (int32_t o = 0; o < nowners; ++o) {
+    out_sizes[o] = 0;
+    if (row_begin[o + 1] < row_begin[o]) return fail(c, PSX_ERR_INVALID_ARG, "row_begin must be non-decreasing");
+  }
+  if (((uintptr_t)stream & 3) || (size & 3) || (out && ((uintptr_t)out & 3)))
+    return fail(c, PSX_ERR_INVALID_ARG, "split streams are 4-byte aligned");
+  if (size == 0) return PSX_OK;   // an empty message splits into empty messages
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  const size_t nrecoff = size / 8 + 1;
+  auto grow = [&](void *&p, size_t &cap, size_t need) -> psx_status {
+    if (need <= cap) return PSX_OK;
+    HIP_TRY(c, hipStreamSynchronize(st));
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(c, hipMalloc(&p, need));
+    cap = need;
+    return PSX_OK;
+  };
+  // 1) decode the message (tables, sparse record offsets) into the split's own buffers
+  psx_status e = grow(c->d_split_fixed, c->split_fixed_cap,
+                      sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables + 4096);
+  if (e) return e;
+  if ((e = grow(c->d_split_recoff, c->split_recoff_cap, nrecoff * sizeof(uint64_t)))) return e;
+  psx::Seg *segs = reinterpret_cast<psx::Seg *>(c->d_split_fixed);
+  uint32_t *words = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(c->d_split_fixed) +
+                                                 sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables);
+  uint32_t *status = words, *counters = words + 16, *ntouched = words + 16 + psx::kMaxFused * psx::kMaxTables;
+  HIP_TRY(c, hipMemsetAsync(status, 0, sizeof(uint32_t), st));
+  psx::StreamSet ss{};
+  ss.n = 1;
+  ss.data[0] = (const uint8_t *)stream;
+  ss.size[0] = size;
+  psx::TableDir dir{};
+  dir.n = (int32_t)c->tables.size();
+  for (size_t i = 0; i < c->tables.size(); ++i) {
+    dir.table_id[i] = c->tables[i].cfg.table_id;
+    dir.vsize[i] = c->tables[i].vsize;
+    dir.dense_serialized[i] = c->tables[i].cfg.oplog_dense_serialized;
+    dir.dense_body[i] = c->tables[i].dense_body();
+  }
+  psx::IdxSet ix{};
+  ix.p[0] = record_offsets;
+  uint64_t *recoff = reinterpret_cast<uint64_t *>(c->d_split_recoff);
+  HIP_TRY(c, psx::launch_decode(ss, dir, segs, recoff, status, counters, ntouched, ix, st));
+  std::vector<psx::Seg> hs(psx::kMaxTables);
+  uint32_t hst = 0;
+  HIP_TRY(c, hipMemcpyAsync(hs.data(), segs, sizeof(psx::Seg) * psx::kMaxTables, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(&hst, status, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  if (hst & psx::kStFatal) return sticky_error(c, hst);
+  // 2) the message's tables with records, in stream order
+  struct T { int ti; uint64_t first; };
+  std::vector<T> order;
+  for (int ti = 0; ti < dir.n; ++ti) {
+    const psx::Seg &g = hs[ti];
+    if (g.rec0 < 0 || g.num_rows <= 0) continue;
+    uint64_t first = (uint64_t)g.rec0;
+    if (g.sparse) HIP_TRY(c, hipMemcpy(&first, recoff + g.rec0, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    order.push_back({ti, first});
+  }
+  std::sort(order.begin(), order.end(), [](const T &a, const T &b) { return a.first < b.first; });
+  const int ntab = (int)order.size();
+  if (ntab == 0) return PSX_OK;
+  std::vector<psx::SplitTab> tabs(ntab);
+  int64_t nrec = 0;
+  for (int j = 0; j < ntab; ++j) {
+    const TableState &t = c->tables[order[j].ti];
+    const psx::Seg &g = hs[order[j].ti];
+    tabs[j].k0 = nrec;
+    tabs[j].rec0 = g.rec0;
+    tabs[j].sparse = g.sparse;
+    tabs[j].stride = t.dense_stride();
+    tabs[j].vsize = t.vsize;
+    nrec += g.num_rows;
+  }
+  const int64_t ntiles = (nrec + 63) / 64;
+  const int64_t nb = (int64_t)nowners * ntiles;
+  // scratch: tabs | src_off[nrec] meta[nrec] | tile_bytes[nb] tile_pre[nb+1] scan_tmp | ot_count ot_bytes |
+  //          owner_base hdr_shift | words pos/val
+  const size_t nscan = (size_t)((nb + 1023) / 1024) + 1;
+  const size_t nwmax = (size_t)nowners * (1 + 4 * ntab);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t at = off; off += (bytes + 255) / 256 * 256; return at; };
+  const size_t o_tabs = take(sizeof(psx::SplitTab) * ntab), o_src = take(8 * nrec), o_meta = take(8 * nrec),
+               o_tb = take(8 * nb), o_tp = take(8 * (nb + 1)), o_st = take(8 * nscan),
+               o_oc = take(8 * (size_t)nowners * ntab), o_ob = take(8 * (size_t)nowners * ntab),
+               o_base = take(8 * (size_t)nowners), o_hs = take(8 * (size_t)nowners * ntab), o_wp = take(8 * nwmax),
+               o_wv = take(4 * nwmax);
+  if ((e = grow(c->d_split_scratch, c->split_scratch_cap, off))) return e;
+  uint8_t *sc = reinterpret_cast<uint8_t *>(c->d_split_scratch);
+  psx::SplitArgs a{};
+  a.msg = (const uint8_t *)stream;
+  a.recoff = recoff;
+  a.tabs = reinterpret_cast<const psx::SplitTab *>(sc + o_tabs);
+  a.ntab = ntab;
+  a.nowners = nowners;
+  a.nrec = nrec;
+  a.ntiles = ntiles;
+  for (int o = 0; o <= nowners; ++o) a.row_begin[o] = row_begin[o];
+  a.src_off = reinterpret_cast<uint64_t *>(sc + o_src);
+  a.meta = reinterpret_cast<uint64_t *>(sc + o_meta);
+  a.tile_bytes = reinterpret_cast<int64_t *>(sc + o_tb);
+  a.tile_pre = reinterpret_cast<int64_t *>(sc + o_tp);
+  a.scan_tmp = reinterpret_cast<int64_t *>(sc + o_st);
+  a.ot_count = reinterpret_cast<int64_t *>(sc + o_oc);
+  a.ot_bytes = reinterpret_cast<int64_t *>(sc + o_ob);
+  a.owner_base = reinterpret_cast<const int64_t *>(sc + o_base);
+  a.hdr_shift = reinterpret_cast<const int64_t *>(sc + o_hs);
+  a.out = (uint8_t *)out;
+  a.status = status;
+  HIP_TRY(c, hipMemcpyAsync(sc + o_tabs, tabs.data(), sizeof(psx::SplitTab) * ntab, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemsetAsync(a.tile_bytes, 0, 8 * nb, st));
+  HIP_TRY(c, hipMemsetAsync(a.ot_count, 0, 16 * (size_t)nowners * ntab + 256, st));   // ot_count and ot_bytes
+  HIP_TRY(c, hipMemsetAsync(a.ot_bytes, 0, 8 * (size_t)nowners * ntab, st));
+  // 3) owners and sizes; per owner the tile bytes scanned
+  HIP_TRY(c, psx::launch_split_count(a, st));
+  std::vector<int64_t> cnt((size_t)nowners * ntab), byt((size_t)nowners * ntab);
+  HIP_TRY(c, hipMemcpyAsync(cnt.data(), a.ot_count, 8 * cnt.size(), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(byt.data(), a.ot_bytes, 8 * byt.size(), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(&hst, status, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  if (hst & psx::kStFatal) return sticky_error(c, hst);
+  // 4) every owner's message: int32 num_tables; per table {id, size_t update_size, num_rows}, records
+  std::vector<int64_t> base(nowners), shift((size_t)nowners * ntab, 0);
+  std::vector<int64_t> wpos;
+  std::vector<uint32_t> wval;
+  uint64_t total = 0;
+  for (int o = 0; o < nowners; ++o) {
+    int nt_o = 0;
+    uint64_t rb = 0;
+    for (int j = 0; j < ntab; ++j)
+      if (cnt[(size_t)o * ntab + j]) ++nt_o, rb += (uint64_t)byt[(size_t)o * ntab + j];
+    out_sizes[o] = nt_o ? 4 + 16 * (uint64_t)nt_o + rb : 0;
+    base[o] = (int64_t)total;
+    if (nt_o) {
+      wpos.push_back(base[o]);
+      wval.push_back((uint32_t)nt_o);
+      int r = 0;
+      uint64_t before = 0;
+      for (int j = 0; j < ntab; ++j) {
+        const int64_t n_oj = cnt[(size_t)o * ntab + j];
+        if (!n_oj) continue;
+        const int64_t hpos = base[o] + 4 + 16 * r + (int64_t)before;
+        const TableState &t = c->tables[order[j].ti];
+        const uint64_t usz = (uint64_t)t.vsize;
+        wpos.insert(wpos.end(), {hpos, hpos + 4, hpos + 8, hpos + 12});
+        wval.insert(wval.end(), {(uint32_t)t.cfg.table_id, (uint32_t)usz, (uint32_t)(usz >> 32), (uint32_t)n_oj});
+        ++r;
+        shift[(size_t)o * ntab + j] = 4 + 16 * (int64_t)r;
+        before += (uint64_t)byt[(size_t)o * ntab + j];
+      }
+    }
+    total += out_sizes[o];
+  }
+  if (!out || out_cap < total)
+    return fail(c, PSX_ERR_BUFFER_TOO_SMALL, "split output needs " + std::to_string(total) + " bytes");
+  HIP_TRY(c, hipMemcpyAsync(sc + o_base, base.data(), 8 * base.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(sc + o_hs, shift.data(), 8 * shift.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(sc + o_wp, wpos.data(), 8 * wpos.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(sc + o_wv, wval.data(), 4 * wval.size(), hipMemcpyHostToDevice, st));
+  // 5) records to their owners' messages, then the headers
+  HIP_TRY(c, psx::launch_split_scatter(a, reinterpret_cast<const int64_t *>(sc + o_wp),
+                                       reinterpret_cast<const uint32_t *>(sc + o_wv), (int32_t)wpos.size(), st));
+  HIP_TRY(c, hipStreamSynchronize(st));   // the host vectors above are pageable
+  return PSX_OK;
+}
+
 psx_status psx_pack_stream(psx_ctx *c, const psx_pack_table *tables, int32_t n, void *out, size_t cap,
                            size_t *used, uint64_t *record_offsets) {
   return psx_pack_stream_indexed(c, tables, n, out, cap, used, record_offsets, nullptr);
@@ -2307,6 +2498,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
+    case PSX_VARIANT_ORD_PIPELINE: return &psx::g_ord_pipeline;
     default: return nullptr;
   }
 }
@@ -2332,6 +2524,8 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
+    if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
+    if (const char *v = getenv("PSX_ORD_PIPELINE")) psx::g_ord_pipeline = atoi(v);
   }
 } variant_env;
 }  // namespace

@@ -393,6 +393,26 @@ class Server:
             res += (rws[:nrec],)
         return res if len(res) > 1 else out
 
+    def split_stream(self, msg, row_begin, record_offsets=None):
+        """psx_split_stream: the per-server split of one device message (CUDA uint8 tensor)
+        over row-range owners (row_begin: nowners + 1 ascending row ids).  Returns (out, sizes):
+        a CUDA uint8 tensor with the owners' sub-streams back to back and their byte counts."""
+        import torch
+        torch.cuda.current_stream(self.device).synchronize()
+        rb = (ctypes.c_int64 * len(row_begin))(*[int(x) for x in row_begin])
+        nown = len(row_begin) - 1
+        sizes = (ctypes.c_uint64 * nown)()
+        n = msg.numel()
+        ntab = len(self.tables)
+        cap = n + nown * (4 + 16 * max(ntab, 1))
+        out = torch.empty((cap + 3) // 4, dtype=torch.int32, device=msg.device).view(torch.uint8)
+        _check(self._L, self._ctx, self._L.psx_split_stream(
+            self._ctx, msg.data_ptr() if n else None, n,
+            record_offsets.data_ptr() if record_offsets is not None else None, nown, rb,
+            out.data_ptr(), out.numel(), sizes))
+        sz = [int(x) for x in sizes]
+        return out[:sum(sz)], sz
+
     # -- timing ------------------------------------------------------------------------
     def timing(self, on=True):
         """on: False/0 off, True/1 every pipeline kernel, 2 the apply kernels only."""

@@ -85,7 +85,8 @@ def test_mlr_weight_rows_match_oracle_every_clock(tmp_path, channels, staleness)
     assert counts["push"] > 0
     rows = [list(map(float, ln.split()[1:])) for ln in out.splitlines() if ln.startswith("LOSS ")]
     assert len(rows) == epochs
-    assert rows[-1][0] < rows[0][0] and rows[-1][1] > 2.0 / L, rows
+    # rows: {epoch, mean loss, accuracy}
+    assert rows[-1][1] < rows[0][1] and rows[-1][2] > 2.0 / L, rows
 
 
 def _write_split(prefix, rows=600, cols=300, nnz=4000, seed=77):

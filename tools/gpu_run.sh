@@ -62,6 +62,10 @@ for s in "$@"; do
         P=$((P+1))
       done
       python3 tools/pmc_db.py $(find "$R/pmc3" -name '*.db' | sort) > "$O/pmc3.json" && echo "pmc3 summarised" ;;
+    c3ab) run c3ab_off 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 &&
+          run c3ab_on 300 env PSX_ORD_PIPELINE=1 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 &&
+          run c3ab_off2 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 ;;
+    c2only) run c2only 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras ;;
     c3) run c3 300 python -u bench.py --workload c3 --steps 20 --warmup 3 ;;
     c3idx) run c3idx 300 python -u bench.py --workload c3 --indexed --steps 20 --warmup 3 ;;
     c4) run c4 600 python -u bench.py --workload c4 --steps 3 --warmup 1 ;;

@@ -192,6 +192,8 @@ typedef struct psx_ctx psx_ctx;
 
 /* ---- lifecycle ---------------------------------------------------------- */
 int32_t psx_abi_version(void);
+/* Visible HIP devices (hipGetDeviceCount); PSX_ERR_NO_DEVICE with *n = 0 when none. */
+psx_status psx_device_count(int32_t *n);
 psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out);
 psx_status psx_ctx_destroy(psx_ctx *ctx);
 /* Use an external hipStream_t (e.g. the caller's compute stream); NULL restores the

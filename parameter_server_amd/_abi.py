@@ -136,6 +136,7 @@ def load():
     P = ctypes.POINTER
     sigs = {
         "psx_abi_version": ([], i32),
+        "psx_device_count": ([P(i32)], ctypes.c_int),
         "psx_ctx_create": ([i32, i32, P(vp)], ctypes.c_int),
         "psx_ctx_destroy": ([vp], ctypes.c_int),
         "psx_ctx_set_stream": ([vp, vp], ctypes.c_int),

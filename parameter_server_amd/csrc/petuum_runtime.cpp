@@ -36,6 +36,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -81,6 +82,7 @@ bool is_zero(int dt, const uint8_t *p) {
 
 struct Shard {
   psx_ctx *ctx = nullptr;
+  int32_t device = 0;
   int32_t bg_id = 0;
   uint32_t version = 0;      // the bg thread's message version (ssp_bg_worker.cpp:250-257)
   int32_t pushed_clock = 0;  // the clock of its last push (ServerPushRowMsg clock)
@@ -182,12 +184,27 @@ class Runtime {
     // provided (the reference reaches them over ZeroMQ tcp, out of scope).
     if (cfg.num_total_clients > 1)
       die("num_total_clients > 1 (clients in other processes) is not provided by this runtime");
-    int32_t device = 0;
-    if (const char *d = std::getenv("PSX_DEVICE")) device = std::atoi(d);
+    // Shard (comm channel) ch lives on devices_[ch % devices_.size()]: every visible GPU by
+    // default, PSX_DEVICES="0,2,..." to choose them, PSX_DEVICE=<d> for one
+    if (const char *d = std::getenv("PSX_DEVICES")) {
+      for (const char *p = d; *p;) {
+        devices_.push_back(std::atoi(p));
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+      }
+    } else if (const char *d1 = std::getenv("PSX_DEVICE")) {
+      devices_.push_back(std::atoi(d1));
+    } else {
+      int32_t nd = 0;
+      check(nullptr, psx_device_count(&nd), "psx_device_count");
+      for (int32_t i = 0; i < nd; ++i) devices_.push_back(i);
+    }
+    if (devices_.empty()) die("no devices for the server shards");
     shards_.resize(C_);
     for (int ch = 0; ch < C_; ++ch) {
       Shard &s = shards_[ch];
-      check(nullptr, psx_ctx_create(device, cfg.client_id * 1000 + 1 + ch, &s.ctx), "psx_ctx_create");
+      s.device = devices_[ch % devices_.size()];
+      check(nullptr, psx_ctx_create(s.device, cfg.client_id * 1000 + 1 + ch, &s.ctx), "psx_ctx_create");
       // thread ids: client * 1000 + 100 + channel for bg threads (context.hpp:410-414)
       for (int32_t client = 0; client < std::max(1, cfg.num_total_clients); ++client)
         check(s.ctx, psx_register_sender(s.ctx, client * 1000 + 100 + ch), "register sender");
@@ -381,6 +398,7 @@ class Runtime {
 
   void Trace(const std::string &kind, int ch, int64_t seq, const void *p, size_t n) {
     if (trace_dir_.empty()) return;
+    std::lock_guard<std::mutex> g(trace_mtx_);
     if (!trace_index_) trace_index_ = std::fopen((trace_dir_ + "/index.txt").c_str(), "w");
     const std::string name = kind + "_" + std::to_string(seq) + "_ch" + std::to_string(ch) + ".bin";
     FILE *f = std::fopen((trace_dir_ + "/" + name).c_str(), "wb");
@@ -394,8 +412,39 @@ class Runtime {
     }
   }
 
+  // BgWorkers::ClockAllTables: every shard gets this client's message for the clock.  The
+  // reference's server threads run concurrently; here the shards on distinct GPUs do (one
+  // host thread per shard for the clock: a psx context is driven by one thread at a time),
+  // shards sharing a GPU take their turn.
   void ClockAllTablesLocked(int32_t clock) {
+    std::vector<std::vector<int>> by_dev;
     for (int ch = 0; ch < C_; ++ch) {
+      size_t k = 0;
+      while (k < by_dev.size() && shards_[by_dev[k][0]].device != shards_[ch].device) ++k;
+      if (k == by_dev.size()) by_dev.emplace_back();
+      by_dev[k].push_back(ch);
+    }
+    if (by_dev.size() == 1) {
+      for (int ch = 0; ch < C_; ++ch) ClockShardLocked(ch, clock);
+    } else {
+      std::vector<std::thread> th;
+      for (auto &chs : by_dev)
+        th.emplace_back([this, chs, clock] {
+          for (int ch : chs) ClockShardLocked(ch, clock);
+        });
+      for (auto &t : th) t.join();
+    }
+    int32_t sys = INT32_MAX;
+    for (auto &s : shards_) sys = std::min(sys, s.pushed_clock);
+    {
+      std::lock_guard<std::mutex> g(clock_mtx_);
+      system_clock_ = sys;
+    }
+    clock_cv_.notify_all();
+  }
+
+  void ClockShardLocked(int ch, int32_t clock) {
+    {
       Shard &s = shards_[ch];
       // OpLogSerializer: tables in ascending id, empty ones omitted (oplog_serializer.hpp:12-37)
       std::vector<int32_t> ids(table_order_);
@@ -434,13 +483,6 @@ class Runtime {
       check(s.ctx, psx_handle_oplog_msg(s.ctx, msg.data(), msg.size(), s.bg_id, &changed), "HandleOpLogMsg");
       if (changed) PushLocked(ch, changed);
     }
-    int32_t sys = INT32_MAX;
-    for (auto &s : shards_) sys = std::min(sys, s.pushed_clock);
-    {
-      std::lock_guard<std::mutex> g(clock_mtx_);
-      system_clock_ = sys;
-    }
-    clock_cv_.notify_all();
   }
 
   // SSPPushServerThread::ServerPushRow + SSPPushBgWorker::ApplyServerPushedRow for this client
@@ -536,6 +578,7 @@ class Runtime {
 
   TableGroupConfig cfg_;
   int C_ = 1;
+  std::vector<int32_t> devices_;
   std::vector<Shard> shards_;
   std::map<int32_t, std::unique_ptr<ClientTableImpl>> tables_;
   std::vector<int32_t> table_order_;
@@ -555,7 +598,8 @@ class Runtime {
   int64_t reg_gen_ = 0;
   std::string trace_dir_;
   FILE *trace_index_ = nullptr;
-  int64_t msg_seq_ = 0, push_seq_ = 0, req_seq_ = 0;
+  std::mutex trace_mtx_;
+  std::atomic<int64_t> msg_seq_{0}, push_seq_{0}, req_seq_{0};
 
  public:
   static thread_local int32_t tls_thread_id_;

@@ -973,6 +973,17 @@ const char *psx_status_string(psx_status s) {
   return "?";
 }
 
+psx_status psx_device_count(int32_t *n) {
+  if (!n) return PSX_ERR_INVALID_ARG;
+  int d = 0;
+  if (hipGetDeviceCount(&d) != hipSuccess || d <= 0) {
+    *n = 0;
+    return PSX_ERR_NO_DEVICE;
+  }
+  *n = d;
+  return PSX_OK;
+}
+
 psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   if (!out) return PSX_ERR_INVALID_ARG;
   *out = nullptr;

@@ -497,54 +497,62 @@ def run_c3(args):
 
 
 def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242):
-    """The exchange-bearing step (SURVEY §8(d) C4 shape): a dense f32 table of rows_total x
-    cap, row-range sharded over the ranks.  Per step every rank (one worker) holds a
-    full-coverage batch, packed per owner shard (rows in random order) as the reference
-    client does (abstract_bg_worker.cpp:590-649); one all-to-all (RCCL over xGMI) delivers
-    each owner its world_size messages, which one fused, order-preserving apply adds to the
-    shard (bit-exact vs sequential application).  The process group is already up.
-    Returns the measurement (max over ranks) as a dict."""
+    """The exchange-bearing step (SURVEY §8(d) C4 shape), through the product path: a dense
+    f32 table of rows_total x cap, row-range sharded over the ranks.  Per step every rank (one
+    worker) holds ONE full-coverage message over all rows_total rows in random order; it is
+    split per owner on the device (psx_split_stream: the client's per-server split,
+    abstract_bg_worker.cpp:590-649), the sub-streams cross GPUs in one all-to-all-v over
+    libpsx's own RCCL communicator (psx_exchange_*: grouped ncclSend/ncclRecv over xGMI),
+    and each owner applies the world_size messages it received in source-rank order in one
+    fused, order-preserving call (bit-exact vs sequential application).  The process group
+    (already up) only carries the communicator id.  Returns the measurement (max over ranks)."""
     import torch
     import torch.distributed as dist
     import parameter_server_amd as psa
     from parameter_server_amd import wire
-    from parameter_server_amd.exchange import alltoall_streams, split
+    from parameter_server_amd.exchange import Exchange, split
     shard = rows_total // world
     g = torch.Generator(device="cuda").manual_seed(seed + rank)
-    parts = []
-    for owner in range(world):
-        perm = torch.randperm(shard, device="cuda", generator=g).to(torch.int32) + owner * shard
-        upd = torch.randn(shard, cap, device="cuda", generator=g) * 0.01
-        parts.append(wire.dense_stream_torch(1, perm, upd))
-        del upd, perm
-    sizes = [p_.numel() for p_ in parts]
-    send = torch.cat(parts)
-    del parts
+    perm = torch.randperm(shard * world, device="cuda", generator=g).to(torch.int32)
+    upd = torch.randn(shard * world, cap, device="cuda", generator=g) * 0.01
+    msg = wire.dense_stream_torch(1, perm, upd)
+    del upd, perm
     torch.cuda.empty_cache()
     bgs = [100 + w for w in range(world)]
+    bounds = [w * shard for w in range(world + 1)]
     srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
                                      row_offset=rank * shard, max_rows=shard))
+    # the splitter: a context with the same table over every row (record formats only)
+    spl = psa.Server(device=local, server_id=900 + rank, bg_ids=[1])
+    spl.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
+                                     max_rows=shard * world))
+    xc = Exchange(local) if world > 1 else None
     ver = [0]
-    t_x = [0.0]
+    t_split, t_x = [0.0], [0.0]
 
     def step():
         t0 = time.perf_counter()
-        if world > 1:
-            recv, rs = alltoall_streams(send, sizes)
+        parts, sizes = spl.split_stream(msg, bounds)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if xc is not None:
+            recv, rs = xc.alltoall(parts, sizes)
+            torch.cuda.synchronize()
             msgs = split(recv, rs)
         else:
-            msgs = [send]
-        torch.cuda.synchronize()
-        t_x[0] += time.perf_counter() - t0
+            msgs = [parts]
+        t2 = time.perf_counter()
+        t_split[0] += t1 - t0
+        t_x[0] += t2 - t1
         srv.apply_device([(m.data_ptr(), m.numel(), bgs[w], ver[0]) for w, m in enumerate(msgs)])
         srv.sync()
         ver[0] += 1
 
     for _ in range(warmup):
         step()
-    t_x[0] = 0.0
+    t_split[0] = t_x[0] = 0.0
     srv.timing(True)
     srv.timing_reset()
     if world > 1:
@@ -559,20 +567,24 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
     el = time.perf_counter() - t0
     apply_ms, apply_n = srv.timing_read("dense_apply")
     idx_ms, _ = srv.timing_read("dense_index")
+    per_rank_stream = msg.numel()
     srv.close()
-    del send
+    spl.close()
+    if xc is not None:
+        xc.close()
+    del msg
     torch.cuda.empty_cache()
     if world > 1:
-        t = torch.tensor([el, t_x[0]], device="cuda", dtype=torch.float64)
+        t = torch.tensor([el, t_x[0], t_split[0]], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, t_x[0] = (float(x) for x in t.tolist())
-    per_rank_stream = sum(sizes)
+        el, t_x[0], t_split[0] = (float(x) for x in t.tolist())
     apply_bytes = per_rank_stream + 2 * shard * cap * 4    # per owner per step (same totals)
     sent = per_rank_stream * (world - 1) / world
     return {
         "value": round(apply_bytes * world * steps / el / 1e9, 2), "unit": "GB/s (algorithmic, all ranks)",
         "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": round(el / steps * 1e3, 3),
+        "split_ms_per_step": round(t_split[0] / steps * 1e3, 3),
         "exchange_ms_per_step": round(t_x[0] / steps * 1e3, 3),
         # nccl-tests all-to-all convention: algbw = bytes per rank / time, busbw =
         # algbw * (n-1)/n (the bytes that actually cross xGMI per rank)
@@ -582,7 +594,8 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
         "index_kernel_ms": round(idx_ms / max(apply_n, 1), 3),
         "config": {"workload": f"{rows_total} rows x {cap} f32, row-range shards x{world}",
                    "shard_rows": shard, "stream_bytes_per_rank": per_rank_stream,
-                   "parallelism": f"{world} shards, RCCL all-to-all of per-owner messages"},
+                   "parallelism": f"{world} shards; per step: device split per owner (psx_split_stream), "
+                                  f"libpsx RCCL all-to-all-v (psx_exchange_*), fused apply"},
     }
 
 

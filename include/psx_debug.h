@@ -22,10 +22,8 @@ enum {
                                    (psx_walk.hip, where eligible; the default), 0: one workgroup
                                    per message (decode_streams) */,
   PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */,
-  PSX_VARIANT_DENSE_STORE = 9   /* 1: dense table rows stored non-temporally (default), 0: plain stores */,
-  PSX_VARIANT_ORD_PIPELINE = 10 /* 1: the register sorted/map kernels pipeline each wave's row setup
-                                   (descriptors, record references and sizes loaded a row ahead;
-                                   default), 0: each row's setup loads in turn */
+  PSX_VARIANT_DENSE_STORE = 9   /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
+                                   (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

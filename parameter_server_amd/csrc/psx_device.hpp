@@ -94,7 +94,7 @@ struct DenseArgs {
   uint32_t rows_mask;          // bit b: message b was placed from the producer's record rows, so
                                // every record's row id is checked against its slot in the apply
   int64_t row_offset, row_stride;   // shard geometry (expected row id of a slot)
-  int32_t store_nt;                 // 1: table rows stored non-temporally (PSX_VARIANT_DENSE_STORE)
+  int32_t store_nt;                 // table-row policy (PSX_VARIANT_DENSE_STORE): bit0 nt store, bit1 nt load
 };
 
 // AdaRevision server-table logic on one f32 dense table (psx_ada.hip).
@@ -158,8 +158,6 @@ struct OrdArgs {
   int32_t *off;
   int32_t *tsum;
   uint64_t *list;         // records grouped by slot: (message << 56) | byte offset of the row id
-  int32_t *list_n;        // beside list (sparse records): each record's column count n, so the
-                          // apply has a record's size without loading its header
   int32_t *touched;       // slots with >= 1 record this call (unordered)
   uint32_t *ntouched;     // its length (zeroed by decode_streams)
   void *dense;

@@ -423,15 +423,20 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p) {
     return v;
   }
 }
-// Table-row stores.  Non-temporal (the default): the row leaves the XCD's L2 as a streaming
-// write instead of sitting there dirty until evicted amid the record gathers — the C2
-// apply's 1.07 GB of row writes cost ~0.8 ms of a 2.4 ms launch as plain stores and ~0.2 ms
-// less as nt stores (tools/probe_apply.hip, profiles/r03/s4).  Rows are 4-byte aligned.
-__device__ __forceinline__ void store16(uint8_t *p, u32x4 v, bool nt) {
-  if (nt)
+// Table-row loads and stores (DenseArgs.store_nt, PSX_VARIANT_DENSE_STORE): bit 0 stores
+// the row non-temporally (a streaming write instead of a dirty L2 line evicted later amid
+// the record gathers), bit 1 loads it non-temporally.  The C2 pattern's 1.07 GB of row
+// writes cost ~0.8 ms of a 2.4 ms launch as plain stores (reads alone: 1.57 ms); nt loads
+// + nt stores measured 2.19 ms, plain loads + plain stores 2.28, nt loads + plain stores
+// 2.41 (tools/probe_apply.hip, profiles/r03/s9).  Rows are 4-byte aligned.
+__device__ __forceinline__ void store16(uint8_t *p, u32x4 v, int mode) {
+  if (mode & 1)
     __builtin_nontemporal_store(__builtin_bit_cast(u32x4_a4, v), reinterpret_cast<u32x4_a4 *>(p));
   else
     __builtin_memcpy(p, &v, 16);
+}
+__device__ __forceinline__ u32x4 load_row16(const uint8_t *p, int mode) {
+  return (mode & 2) ? load16<true>(p) : load16<false>(p);
 }
 
 // Four binary16 record values (8 bytes, 2-byte aligned) -> four f32 bit patterns, by the
@@ -619,7 +624,7 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
         u32x4 u[PAIR][BMAX];
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
-          t[q] = (full && has[q]) ? load16<false>(trow[q] + e0 * VS) : u32x4{0, 0, 0, 0};
+          t[q] = (full && has[q]) ? load_row16(trow[q] + e0 * VS, a.store_nt) : u32x4{0, 0, 0, 0};
 #pragma unroll
           for (int b = 0; b < BMAX; ++b) {
             if constexpr (H16) {
@@ -868,7 +873,7 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
         u32x4 u[PAIR][BMAX];
 #pragma unroll
         for (int q = 0; q < PAIR; ++q) {
-          t[q] = load16<false>(trow[q] + te * VS);
+          t[q] = load_row16(trow[q] + te * VS, a.store_nt);
 #pragma unroll
           for (int b = 0; b < BMAX; ++b) {
             const bool pr = (presm >> (q * BMAX + b)) & 1u;
@@ -1032,7 +1037,7 @@ __global__ void __launch_bounds__(256) dense_apply_v4_kernel(DenseArgs a) {
         u32x4 t[PAIR], u[M];
 #pragma unroll
         for (int q = 0; q < PAIR; ++q)
-          if (q < nrows) t[q] = load16<false>(table + (s0 + ks[q]) * row_bytes + te * VS);
+          if (q < nrows) t[q] = load_row16(table + (s0 + ks[q]) * row_bytes + te * VS, a.store_nt);
 #pragma unroll
         for (int j = 0; j < M; ++j)
           if (j < nslot) u[j] = load16<NT>(s_rec[w][j] + te * VS);

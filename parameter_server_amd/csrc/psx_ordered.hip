@@ -195,7 +195,6 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
     if (s < 0) continue;
     const int32_t p = atomicSub(&a.cnt[s], 1) - 1;
     a.list[a.off[s] + p] = rec_ref(b, off);
-    if (a.list_n && !a.dense_records) a.list_n[a.off[s] + p] = o_ld32(a.ss.data[b] + off + 4);   // same line as the row id
   }
 }
 
@@ -372,26 +371,6 @@ __device__ __forceinline__ uint64_t wave_rank_sort(uint64_t r, int L, int lane, 
   if (lane < L) scratch[rank] = r;
   wave_sync();
   const uint64_t out = lane < L ? scratch[lane] : 0;
-  wave_sync();
-  return out;
-}
-
-// The same, carrying a 32-bit payload per entry (the record's column count).
-__device__ __forceinline__ uint64_t wave_rank_sort2(uint64_t r, int32_t pay, int L, int lane, uint64_t *scratch,
-                                                    int32_t *pay_out) {
-  int rank = 0;
-  for (int k = 0; k < L; ++k) {
-    const uint64_t x = shfl64(r, k);
-    rank += (x < r) ? 1 : 0;
-  }
-  int32_t *sp = reinterpret_cast<int32_t *>(scratch + 64);
-  if (lane < L) {
-    scratch[rank] = r;
-    sp[rank] = pay;
-  }
-  wave_sync();
-  const uint64_t out = lane < L ? scratch[lane] : 0;
-  *pay_out = lane < L ? sp[lane] : 0;
   wave_sync();
   return out;
 }
@@ -739,12 +718,12 @@ __device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int
 // ordered_offsets put in the 256- and the 1,024-entry list (a.touched / a.ntouched point
 // at one list each).
 // DRY: the capacity dry run (see ordered_apply_kernel); J must hold max_entries.
-// Occupancy targets: 6 waves/SIMD for the 256-entry image (7 before the row setup was
-// pipelined: rows bound by their setup's dependent loads wanted more rows in flight; the
-// pipeline's lookahead registers do not fit 7), the VGPR file's limit for J = 16.
+// Occupancy targets: 7 waves/SIMD for the 256-entry image (its rows are bound by their
+// setup's dependent loads, so more rows in flight pays: C3 apply 0.123 -> 0.114 ms), the
+// VGPR file's limit for J = 16.
 template <typename V, int KIND, int J, bool DRY = false>
-__global__ void __launch_bounds__(256, (J <= 4 ? 6 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
-  __shared__ uint64_t sort_scratch[4][96];   // 64 keys + 64 int32 payloads
+__global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
+  __shared__ uint64_t sort_scratch[4][64];
   // Key -> entry-index map of the wave's row (FindIndex in one LDS read instead of J
   // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
   // per row at load): int16 per key, -1 = absent.
@@ -769,66 +748,12 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 6 : (sizeof(V) == 4 ? 3 : 2))) 
 
   // one touched row per wave at a time (rows are independent; hot rows spread out)
   const int64_t nt = go ? (int64_t)*a.ntouched : 0;
-  // Row setup pipelined across the wave's rows (descriptor lists with record sizes): the
-  // descriptors of the next two rows (one VGPR: lanes 0-3 and 4-7) and the record
-  // references and sizes of the next row are loaded while this row runs, so a row starts
-  // with its references in registers and waits for one round trip (its row image and first
-  // record chunk, in parallel) instead of four dependent ones (descriptor -> references ->
-  // record header -> chunk).
-  const bool pf = a.desc && a.list_n && !a.dense_records;
-  const int32_t *dsc = reinterpret_cast<const int32_t *>(a.touched);
-  auto desc_to = [&](int32_t &dq, int64_t t, int lo) {
-    if (pf && t < nt && lane >= lo && lane < lo + 4) dq = dsc[t * 4 + lane - lo];
-  };
-  auto refs_of = [&](int32_t dq, uint64_t &r, int32_t &nn, int64_t t) {
-    const int32_t b0 = __builtin_amdgcn_readlane(dq, 1), l0 = __builtin_amdgcn_readlane(dq, 2) - b0;
-    r = ~0ull;
-    nn = 0;
-    if (t < nt && l0 <= 64 && lane < l0) {
-      r = a.list[b0 + lane];
-      nn = a.list_n[b0 + lane];
-    }
-  };
-  int32_t dq = 0;
-  int32_t c_slot = 0, c_beg = 0, c_end = 0, c_n = 0;   // this row's descriptor
-  uint64_t r_cur = ~0ull, r_nx = ~0ull;
-  int32_t n_cur = 0, n_nx = 0;
-  if (pf) {
-    desc_to(dq, wave_g, 0);
-    refs_of(dq, r_cur, n_cur, wave_g);
-    c_slot = __builtin_amdgcn_readlane(dq, 0);
-    c_beg = __builtin_amdgcn_readlane(dq, 1);
-    c_end = __builtin_amdgcn_readlane(dq, 2);
-    c_n = __builtin_amdgcn_readlane(dq, 3);
-    desc_to(dq, wave_g + nwaves, 0);
-    desc_to(dq, wave_g + 2 * nwaves, 4);
-  }
-  bool first = true;
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
-    if (pf) {
-      if (!first) {   // the loads the previous row issued become this row's
-        c_slot = __builtin_amdgcn_readlane(dq, 0);
-        c_beg = __builtin_amdgcn_readlane(dq, 1);
-        c_end = __builtin_amdgcn_readlane(dq, 2);
-        c_n = __builtin_amdgcn_readlane(dq, 3);
-        r_cur = r_nx;
-        n_cur = n_nx;
-        dq = __shfl(dq, lane + 4, 64);          // the row after next moves up
-        desc_to(dq, ti + 2 * nwaves, 4);
-      }
-      first = false;
-      refs_of(dq, r_nx, n_nx, ti + nwaves);
-    }
     // per-row scalars are wave-uniform: readfirstlane keeps them in SGPRs so the row's
     // loops branch on SCC instead of running under exec masks
     int64_t slot;
     int32_t beg, L, n;
-    if (pf) {
-      slot = c_slot;
-      beg = c_beg;
-      L = c_end - c_beg;
-      n = c_n;
-    } else if (a.desc) {
+    if (a.desc) {
       const int4 d = reinterpret_cast<const int4 *>(a.touched)[ti];
       slot = __builtin_amdgcn_readfirstlane(d.x);
       beg = __builtin_amdgcn_readfirstlane(d.y);
@@ -844,10 +769,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 6 : (sizeof(V) == 4 ? 3 : 2))) 
     {
       uint64_t *lst = a.list + beg;
       uint64_t mine = 0;
-      int32_t mine_n = 0;
-      if (L <= 64 && pf) {
-        mine = wave_rank_sort2(r_cur, n_cur, L, lane, sort_scratch[wib], &mine_n);
-      } else if (L <= 64) {
+      if (L <= 64) {
         mine = wave_rank_sort(lane < L ? lst[lane] : ~0ull, L, lane, sort_scratch[wib]);
       } else {
         if (lane == 0) {
@@ -863,10 +785,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 6 : (sizeof(V) == 4 ? 3 : 2))) 
       }
       if constexpr (DRY) {
         int32_t grow = 0;
-        if (L <= 64 && pf)
-          grow = mine_n;
-        else
-          for (int32_t q = lane; q < L; q += 64) grow += o_ld32(rec_ptr(a, L <= 64 ? mine : lst[q]) + 4);
+        for (int32_t q = lane; q < L; q += 64) grow += o_ld32(rec_ptr(a, L <= 64 ? mine : lst[q]) + 4);
         if ((int64_t)n + wave_sum_i32(grow) <= (int64_t)cap) continue;
       }
       // load the row image
@@ -906,7 +825,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 6 : (sizeof(V) == 4 ? 3 : 2))) 
       if (L <= 64 && lane < L) {
         hb = (int)(mine >> 56);
         hoff = mine & kRefOffMask;
-        hn = pf ? mine_n : o_ld32(a.ss.data[hb] + hoff + 4);
+        hn = o_ld32(a.ss.data[hb] + hoff + 4);
       }
       auto rec_at = [&](int32_t q, const uint8_t *&rec, int32_t &nn) {
         int b;

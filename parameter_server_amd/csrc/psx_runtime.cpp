@@ -37,7 +37,6 @@ size_t walk_ws_bytes(uint64_t items);
 int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
-int g_ord_pipeline = 1;     // PSX_VARIANT_ORD_PIPELINE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -240,7 +239,6 @@ struct psx_ctx {
   void *d_split_fixed = nullptr, *d_split_recoff = nullptr, *d_split_scratch = nullptr;   // psx_split_stream
   size_t split_fixed_cap = 0, split_recoff_cap = 0, split_scratch_cap = 0;
   uint64_t *d_list = nullptr;            // ordered path: record lists ((message << 56) | offset)
-  int32_t *d_list_n = nullptr;           // beside d_list: each sparse record's column count
   size_t list_cap = 0;
   std::vector<PendingCall> pending;      // calls since the last psx_sync (duplicate-row replay)
   int64_t call_seq = 0;
@@ -504,12 +502,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     }
     if (any_ordered && list_need > c->list_cap) {
       if (c->d_list) hipFree(c->d_list);
-      if (c->d_list_n) hipFree(c->d_list_n);
       c->d_list = nullptr;
-      c->d_list_n = nullptr;
       c->list_cap = 0;
       HIP_TRY(c, hipMalloc(&c->d_list, list_need * sizeof(uint64_t)));
-      HIP_TRY(c, hipMalloc(&c->d_list_n, list_need * sizeof(int32_t)));
       c->list_cap = list_need;
     }
   }
@@ -660,9 +655,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.cnt = t.d_cnt;
     a.off = t.d_off;
     a.tsum = t.d_tsum;
-    a.list = c->d_list + list_region * ord_k;
-    a.list_n = psx::g_ord_pipeline ? c->d_list_n + list_region * ord_k : nullptr;
-    ++ord_k;
+    a.list = c->d_list + list_region * ord_k++;
     a.touched = t.d_touched;
     a.ntouched = c->d_ntouched[slot] + ti;
     a.dense = t.d_data;
@@ -1035,7 +1028,6 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (auto &t : c->tables) free_table(t);
   if (c->d_list) hipFree(c->d_list);
-  if (c->d_list_n) hipFree(c->d_list_n);
   if (c->d_split_fixed) hipFree(c->d_split_fixed);
   if (c->d_split_recoff) hipFree(c->d_split_recoff);
   if (c->d_split_scratch) hipFree(c->d_split_scratch);
@@ -2509,7 +2501,6 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
-    case PSX_VARIANT_ORD_PIPELINE: return &psx::g_ord_pipeline;
     default: return nullptr;
   }
 }
@@ -2536,7 +2527,6 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
-    if (const char *v = getenv("PSX_ORD_PIPELINE")) psx::g_ord_pipeline = atoi(v);
   }
 } variant_env;
 }  // namespace

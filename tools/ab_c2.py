@@ -84,7 +84,7 @@ def main():
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))
             res[c]["step"].append(step_ms)
-    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + ("_ntstore" if c[2] else "_plainstore"): {k: round(statistics.median(v), 4) for k, v in res[c].items()}
+    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + f"_rowpolicy{c[2]}": {k: round(statistics.median(v), 4) for k, v in res[c].items()}
            for c in configs}
     print(json.dumps(out, indent=1))
     srv.close()

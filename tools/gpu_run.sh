@@ -76,7 +76,7 @@ for s in "$@"; do
     imp) run imp 300 python -u bench.py --importance --steps 20 --warmup 3 --cpu-seconds 0 ;;
     probe) run probe 300 tools/probe_ceiling 10 ;;
     hbm) run hbm 400 tools/probe_hbm 10 ;;
-    abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:0:0,0:0:1 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -40 ;;
+    abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
     *) echo "unknown step $s"; exit 2 ;;

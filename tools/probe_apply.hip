@@ -212,6 +212,7 @@ int main(int argc, char **argv) {
   run("sc1store", apply_kernel<8, 4, ST_SC1, true, false>, 4, 1);
   run("outplace", apply_kernel<8, 4, ST_PLAIN, true, true>, 4, 1);
   run("tabplain", apply_kernel<8, 4, ST_PLAIN, false, false>, 4, 1);
+  run("tabplain_ntstore", apply_kernel<8, 4, ST_NT, false, false>, 4, 1);
   run("base_x2grid", apply_kernel<8, 4, ST_PLAIN, true, false>, 4, 2);
   run("base_d2", apply_kernel<8, 2, ST_PLAIN, true, false>, 2, 1);
   run("base_d8", apply_kernel<8, 8, ST_PLAIN, true, false>, 8, 1);

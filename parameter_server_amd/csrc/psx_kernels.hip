@@ -425,10 +425,12 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p) {
 }
 // Table-row loads and stores (DenseArgs.store_nt, PSX_VARIANT_DENSE_STORE): bit 0 stores
 // the row non-temporally (a streaming write instead of a dirty L2 line evicted later amid
-// the record gathers), bit 1 loads it non-temporally.  The C2 pattern's 1.07 GB of row
-// writes cost ~0.8 ms of a 2.4 ms launch as plain stores (reads alone: 1.57 ms); nt loads
-// + nt stores measured 2.19 ms, plain loads + plain stores 2.28, nt loads + plain stores
-// 2.41 (tools/probe_apply.hip, profiles/r03/s9).  Rows are 4-byte aligned.
+// the record gathers), bit 1 loads it non-temporally.  In tools/probe_apply.hip (the C2
+// pattern alone) the 1.07 GB of row writes cost ~0.6-0.8 ms of a 2.2-2.4 ms launch (reads
+// alone: 1.60 ms) and the policy mattered there: nt store 2.20 ms, plain 2.38-2.41
+// (profiles/r03/s10).  In this kernel it does not: policies 0, 1 and 3 all measured
+// 2.290-2.293 ms walked and 2.316-2.320 ms with record rows on one box (s10, 5 rounds
+// each); 1 is the default.  Rows are 4-byte aligned.
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v, int mode) {
   if (mode & 1)
     __builtin_nontemporal_store(__builtin_bit_cast(u32x4_a4, v), reinterpret_cast<u32x4_a4 *>(p));

@@ -14,10 +14,17 @@ extern "C" {
 #endif
 
 enum {
-  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact */
+  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact,
+                                   3 / 4: v3 with 4- / 2-slot tiles, 5 / 6: v3 with 4 rows in
+                                   flight per wave and 4- / 16-slot tiles, 7 / 8 / 9: v5 (lean)
+                                   with 4 / 3 / 2 rows in flight per wave (2 < B <= 8) */
   PSX_VARIANT_ORD_SPLIT = 6     /* 1: rows of sorted/map tables with 256 < max_entries <= 1024
                                    classified into a 256- and a 1,024-entry image launch that
-                                   run concurrently (default), 0: one 1,024-entry launch */,
+                                   run concurrently (default), 2: spill mode (rows start on the
+                                   256-entry launch unless already 7/8 full; a row that outgrows
+                                   it is redone by a 1,024-entry launch that follows), 3: spill
+                                   mode with rows of >= 4 records taken first, 0: one
+                                   1,024-entry launch */,
   PSX_VARIANT_DECODE = 7        /* 1: walked messages with sparse tables decode window-parallel
                                    (psx_walk.hip, where eligible; the default), 0: one workgroup
                                    per message (decode_streams) */,

@@ -177,8 +177,16 @@ struct OrdArgs {
                           // can add per slot (zero between calls); null otherwise
   int32_t *split;         // [2][max_rows] row descriptors {slot, list begin, list end, image
                           // size} (int4): touched slots whose image fits 256 entries, the rest
-  uint32_t *nsplit;       // the two lists' lengths
+  uint32_t *nsplit;       // the lists' lengths: 256-entry, 1,024-entry, heavy
   int32_t desc;           // 1: `touched` holds split-list row descriptors (the apply launches)
+  int32_t spill;          // split tables, spill mode: ordered_offsets sends only rows already
+                          // near 256 entries to the 1,024-entry list; the 256-entry launch
+                          // hands a row that outgrows its image to that list (spill_list,
+                          // nspill) untouched, and the 1,024-entry launch runs after it
+  int32_t *spill_list;
+  uint32_t *nspill;
+  const int32_t *heavy_end;  // heavy-first (spill bit 1): heavy row descriptors end here,
+  const uint32_t *nheavy;    // listed backwards; the 256-entry launch takes them first
 };
 
 // A side stream and two events for launches that run beside the context stream.

@@ -113,8 +113,8 @@ __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
-  if (a.grow && blockIdx.x == 0 && threadIdx.x < 3) {   // ordered_offsets' counters
-    if (threadIdx.x < 2) a.nsplit[threadIdx.x] = 0;
+  if (a.grow && blockIdx.x == 0 && threadIdx.x < 4) {   // ordered_offsets' counters
+    if (threadIdx.x < 3) a.nsplit[threadIdx.x] = 0;
     else a.tsum[0] = 0;
   }
   // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
@@ -229,69 +229,92 @@ __device__ __forceinline__ int32_t block_excl_sum(int32_t v, int32_t *sh, int32_
   return pre + incl - v;
 }
 
+// Which apply launch a touched row starts on.  Default: the 1,024-entry one when its image
+// can outgrow 256 entries in this call (entries now + the call's Incs).  Spill mode: only
+// an image already 7/8 full; the rest start on the 256-entry launch and spill if they
+// outgrow it (rare).  Heavy-first (spill bit 1): 256-entry rows with >= kHeavyRecords
+// records are listed apart and taken first, so the longest chains start at time zero.
+constexpr int32_t kHeavyRecords = 4;
+__device__ __forceinline__ bool starts_big(const OrdArgs &a, int32_t nen, int32_t grow) {
+  return (int64_t)nen + grow > 256 && (!a.spill || nen > 224);
+}
+__device__ __forceinline__ bool starts_heavy(const OrdArgs &a, int32_t c) {
+  return (a.spill & 2) && c >= kHeavyRecords;
+}
+
 __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
-  __shared__ int32_t sh[4][4];
-  __shared__ int32_t base[4];   // touched, records, 256-entry list, 1,024-entry list
+  __shared__ int32_t sh[5][4];
+  __shared__ int32_t base[5];   // touched, records, 256-entry list, 1,024-entry list, heavy rows
   if (!o_gate(a)) return;
   const int64_t R = a.max_rows;
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * per;
   const int64_t c1 = c0 + per < R ? c0 + per : R;
   // pass 1: the block's totals, one atomic per counter
-  int32_t nt = 0, nr = 0, ns = 0, nb = 0;
+  int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0;
   for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
     const int32_t c = a.cnt[s];
     if (c > 0) {
       ++nt;
       nr += c;
-      if ((int64_t)a.nent[s] + a.grow[s] > 256) ++nb; else ++ns;
+      if (starts_big(a, a.nent[s], a.grow[s])) ++nb;
+      else if (starts_heavy(a, c)) ++nh;
+      else ++ns;
     }
   }
-  int32_t tt, tr, ts, tb;
+  int32_t tt, tr, ts, tb, th;
   block_excl_sum(nt, sh[0], tt);
   block_excl_sum(nr, sh[1], tr);
   block_excl_sum(ns, sh[2], ts);
   block_excl_sum(nb, sh[3], tb);
+  block_excl_sum(nh, sh[4], th);
   if (threadIdx.x == 0) {
     base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
     base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
     base[2] = ts ? (int32_t)atomicAdd(&a.nsplit[0], (uint32_t)ts) : 0;
     base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tb) : 0;
+    base[4] = th ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)th) : 0;
   }
   __syncthreads();
-  // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row
+  // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row.
+  // Heavy rows fill the 1,024-entry list's region from its end (big, spilled and heavy
+  // rows are distinct touched rows: they never meet).
   int4 *const desc = reinterpret_cast<int4 *>(a.split);
-  int32_t at = base[0], ar = base[1], as = base[2], ab = base[3];
+  int32_t at = base[0], ar = base[1], as = base[2], ab = base[3], ah = base[4];
   for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
     const int64_t s = t0 + threadIdx.x;
     int32_t c = 0, nen = 0;
-    bool big = false;
+    bool big = false, heavy = false;
     if (s < c1) {
       c = a.cnt[s];
       if (c > 0) {
         nen = a.nent[s];
-        big = (int64_t)nen + a.grow[s] > 256;
+        big = starts_big(a, nen, a.grow[s]);
+        heavy = !big && starts_heavy(a, c);
         a.grow[s] = 0;
       }
     }
     const bool t = c > 0;
-    int32_t st, sr, ss2, sb;
+    int32_t st, sr, ss2, sb, sh2;
     const int32_t pt = block_excl_sum(t ? 1 : 0, sh[0], st);
     const int32_t pr = block_excl_sum(c, sh[1], sr);
-    const int32_t ps = block_excl_sum(t && !big ? 1 : 0, sh[2], ss2);
+    const int32_t ps = block_excl_sum(t && !big && !heavy ? 1 : 0, sh[2], ss2);
     const int32_t pb = block_excl_sum(t && big ? 1 : 0, sh[3], sb);
+    const int32_t ph = block_excl_sum(t && heavy ? 1 : 0, sh[4], sh2);
     if (t) {
       const int32_t beg = ar + pr;
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
       a.off[s] = beg;
       desc[2 * R + at + pt] = d;
       if (big) desc[R + ab + pb] = d;
+      else if (heavy) desc[2 * R - 1 - (ah + ph)] = d;
       else desc[as + ps] = d;
     }
     at += st;
     ar += sr;
     as += ss2;
     ab += sb;
+    ah += sh2;
   }
 }
 
@@ -734,7 +757,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   const int wib = threadIdx.x >> 6;
   const bool go = o_gate(a) && (!DRY || *a.keyflag);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows)
-  if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched) return;
+  if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0)) return;
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
   for (int32_t k = lane; k < 1024; k += 64) s_pos[wib][k] = -1;
@@ -746,15 +769,18 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int32_t cap = (int32_t)a.max_entries;
 
-  // one touched row per wave at a time (rows are independent; hot rows spread out)
-  const int64_t nt = go ? (int64_t)*a.ntouched : 0;
+  // one touched row per wave at a time (rows are independent; hot rows spread out);
+  // heavy-first: the heavy rows' list (descending from heavy_end) before the rest
+  const int64_t nh = go && a.nheavy ? (int64_t)*a.nheavy : 0;
+  const int64_t nt = go ? nh + (int64_t)*a.ntouched : 0;
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
     // per-row scalars are wave-uniform: readfirstlane keeps them in SGPRs so the row's
     // loops branch on SCC instead of running under exec masks
     int64_t slot;
     int32_t beg, L, n;
     if (a.desc) {
-      const int4 d = reinterpret_cast<const int4 *>(a.touched)[ti];
+      const int4 d = ti < nh ? reinterpret_cast<const int4 *>(a.heavy_end)[-1 - ti]
+                             : reinterpret_cast<const int4 *>(a.touched)[ti - nh];
       slot = __builtin_amdgcn_readfirstlane(d.x);
       beg = __builtin_amdgcn_readfirstlane(d.y);
       L = __builtin_amdgcn_readfirstlane(d.z) - beg;
@@ -815,6 +841,8 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       }
       double impt = a.imp ? a.imp[slot] : 0.0;
       bool over = false;   // DRY: this row would exceed max_entries
+      bool spilled = false;
+      const int32_t n0 = n;
       // Record headers fetched for all of the row's records at once (lane q: record q in
       // message order; rows with <= 64 records in the call), and each record's first 64
       // (column, value) pairs loaded one record ahead, so the Inc chain does not wait on
@@ -928,6 +956,11 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
               }
             }
             if (idx < 0) {
+              if (!DRY && a.spill && n >= J * 64) {   // outgrows this image: hand the row on
+                spilled = true;
+                over = true;
+                continue;
+              }
               if (n >= cap) {
                 if (lane == 0) atomicOr(a.call_status, kStCapacity);
                 over = DRY;
@@ -1071,6 +1104,13 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         wave_sync();
       }
       if (DRY) continue;
+      if (spilled) {   // nothing of the row was written: the 1,024-entry launch redoes it
+        if (lane == 0) {
+          const uint32_t k = atomicAdd(a.nspill, 1u);
+          reinterpret_cast<int4 *>(a.spill_list)[k] = int4{(int32_t)slot, beg, beg + L, n0};
+        }
+        continue;
+      }
       // write the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)
       uint8_t *wrow = a.entries + slot * a.max_entries * ES;
 #pragma unroll
@@ -1106,6 +1146,7 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 
 // ---------------------------------------------------------------------------
 int g_ord_split = 1;  // rows of > 256-entry tables classified into a 256- and a 1,024-entry image launch
+                      // (1: concurrent launches, 2: spill mode, 0: one 1,024-entry launch)
 
 // One touched row per wave at a time: the grid is sized by rows (the touched count is on
 // the device), not by 64-row tiles — 100K rows as tiles gave 1,564 waves for ~35K touched
@@ -1183,9 +1224,17 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
       big.touched = a.split + 4 * a.max_rows;
       big.ntouched = a.nsplit + 1;
       small.desc = big.desc = 1;
-      hipError_t e = hipEventRecord(fk.fork, st);
-      if (e == hipSuccess) e = hipStreamWaitEvent(fk.aux, fk.fork, 0);
-      if (e != hipSuccess) return e;
+      small.spill_list = big.touched;
+      small.nspill = big.ntouched;
+      if (a.spill & 2) {   // heavy rows: from the end of the 1,024-entry list's region
+        small.heavy_end = a.split + 8 * a.max_rows;
+        small.nheavy = a.nsplit + 2;
+      }
+      if (!a.spill) {
+        hipError_t e = hipEventRecord(fk.fork, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(fk.aux, fk.fork, 0);
+        if (e != hipSuccess) return e;
+      }
     }
 #define PSX_REG(V, KIND)                                                                           \
   do {                                                                                             \
@@ -1193,7 +1242,10 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3(blocks), dim3(256), 0, st, a);   \
     else if (a.max_entries <= 256)                                                                 \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, a);   \
-    else if (a.grow) {                                                                             \
+    else if (a.grow && a.spill) {                                                                  \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, st, big); \
+    } else if (a.grow) {                                                                           \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, fk.aux, big); \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
     } else                                                                                         \
@@ -1208,7 +1260,7 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
     }
 #undef PSX_REGK
 #undef PSX_REG
-    if (a.grow) {
+    if (a.grow && !a.spill) {
       hipError_t e = hipEventRecord(fk.join, fk.aux);
       if (e == hipSuccess) e = hipStreamWaitEvent(st, fk.join, 0);
       if (e != hipSuccess) return e;

@@ -126,7 +126,7 @@ struct TableState {
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
   uint32_t *d_keyflag = nullptr;   // sorted/map: a key outside [0, max_entries) was seen
   int32_t *d_grow = nullptr;       // split sorted/map tables: per-slot entry growth of a call
-  int32_t *d_split = nullptr;      // split sorted/map tables: [2][max_rows] row lists
+  int32_t *d_split = nullptr;      // split sorted/map tables: [3][max_rows] row descriptor lists
   uint32_t *d_nsplit = nullptr;    // their lengths
   uint64_t *d_subs = nullptr;      // CallBackSubs::subscriptions_ per slot (bit c = client c), lazily
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
@@ -672,6 +672,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       a.grow = t.d_grow;
       a.split = t.d_split;
       a.nsplit = t.d_nsplit;
+      a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
     }
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
     if (st) return st;
@@ -1221,7 +1222,7 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     e = hipMalloc(&t.d_grow, R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, R * sizeof(int32_t), c->stream);
     if (e == hipSuccess) e = hipMalloc(&t.d_split, 3 * R * 4 * sizeof(int32_t));   // int4 descriptors x 3 lists
-    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 4 * sizeof(uint32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {

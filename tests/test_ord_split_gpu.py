@@ -1,0 +1,123 @@
+"""GPU parity of the split sorted/map apply (256 < max_entries <= 1,024) in each of its
+three launch forms (PSX_VARIANT_ORD_SPLIT, include/psx_debug.h): one 1,024-entry launch
+(0), the 256- and 1,024-entry launches run concurrently on rows classified by
+`entries + incs > 256` (1), and spill mode (2), where rows start on the 256-entry launch
+unless already 7/8 full and a row that outgrows 256 entries mid-call is handed, untouched,
+to a 1,024-entry launch that follows; (3) is spill mode with rows of >= 4 records listed
+apart and taken first.
+
+The rows are built to hit every branch of the spill: images that cross 256 entries inside
+one call (spilled after some of their records were processed in registers), images that
+start above 224 (classified big), rows that would be classified big by their Inc count
+but never outgrow 256 (they stay on the small launch in spill mode), and ordinary rows.
+Sorted-map rows byte-exact against the oracle (SortedVectorMapStore's entry order,
+sorted_vector_map_store.hpp:175-197,305-337), map rows as {col -> value}."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import parameter_server_amd as psa
+from parameter_server_amd import wire, _abi
+from oracle.oracle import OracleServer, SORTED_MAP, MAP, I32, F64, F32
+
+pytestmark = pytest.mark.gpu
+NP = {F32: np.float32, F64: np.float64, I32: np.int32}
+VS = {F32: 4, F64: 8, I32: 4}
+ORD_SPLIT = 6
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built_lib, oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _vals(rng, k, dt, sign=True):
+    if dt == I32:
+        v = rng.randint(1, 4, size=k) * (rng.choice([-1, 1], size=k) if sign else 1)
+    else:
+        v = rng.normal(0, 1, size=k)
+    return v.astype(NP[dt])
+
+
+def _calls(rng, dt, rows, K):
+    """Three calls of 4 messages.  Call 0 builds images of known sizes; calls 1-2 grow,
+    shrink and cross the 256-entry line."""
+    calls = []
+    # call 0: row r gets an image of size sizes[r] (one record per message, disjoint columns)
+    sizes = [0] * rows
+    for r in range(rows):
+        sizes[r] = [10, 60, 200, 240, 250, 300, 700, 200][r % 8]
+    msgs = []
+    for b in range(4):
+        recs = []
+        for r in range(rows):
+            n = sizes[r]
+            lo, hi = b * n // 4, (b + 1) * n // 4
+            if hi > lo:
+                cols = np.arange(lo, hi, dtype=np.int32)
+                recs.append((r, cols, _vals(rng, cols.size, dt, sign=False)))
+        msgs.append(recs)
+    calls.append(msgs)
+    for c in range(2):
+        msgs = []
+        for b in range(4):
+            recs = []
+            for r in rng.choice(rows, size=rows * 3 // 4, replace=False):
+                kind = int(r) % 8
+                if kind in (2, 3, 4):      # around 256: many new columns (inserts) + some found
+                    k = int(rng.randint(20, 40))
+                    cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+                elif kind == 7:            # entries + Incs > 256, but Incs on existing columns only
+                    cols = np.arange(0, 30, dtype=np.int32)
+                else:
+                    k = int(rng.randint(1, 33))
+                    cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+                recs.append((int(r), cols, _vals(rng, cols.size, dt)))
+            msgs.append(recs)
+        calls.append(msgs)
+    return calls
+
+
+def _as_map(raw, dt):
+    """A serialized map row's packed (int32 col, V value) entries as {col: value bytes}."""
+    es = 4 + VS[dt]
+    return {int(np.frombuffer(raw[k:k + 4], np.int32)[0]): bytes(raw[k + 4:k + es]) for k in range(0, len(raw), es)}
+
+
+@pytest.mark.parametrize("split", [3, 2, 1, 0], ids=["spill-heavy-first", "spill", "concurrent", "single"])
+@pytest.mark.parametrize("kind,dt", [(SORTED_MAP, I32), (SORTED_MAP, F64), (MAP, I32)],
+                         ids=["sorted-i32", "sorted-f64", "map-i32"])
+def test_split_forms_match_oracle(split, kind, dt):
+    L = _abi.load()
+    old = L.psx_debug_set_variant(ORD_SPLIT, split)
+    try:
+        rng = np.random.RandomState(100 + 10 * kind + dt)
+        rows, K = 512, 1024
+        bgs = [100, 101, 102, 103]
+        srv = psa.Server(0, 1, bgs)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=dt, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        orc = OracleServer(bgs)
+        orc.create_table(3, kind, dt, 0, oplog_dense_serialized=False)
+        for v, msgs in enumerate(_calls(rng, dt, rows, K)):
+            streams = [wire.sparse_stream_np(3, VS[dt], recs) for recs in msgs]
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+            srv.sync()
+            for s, bg in zip(streams, bgs):
+                assert orc.apply_stream(s, bg, v) == 0
+            ids = list(range(rows))
+            if kind == SORTED_MAP:
+                assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids), f"call {v}"
+            else:
+                for r in ids:
+                    g, w = srv.serialize_rows(3, [r]), orc.serialize_records(3, [r])
+                    assert len(g) == len(w), f"call {v} row {r}"
+                    if g:
+                        assert _as_map(g[12:], dt) == _as_map(w[12:], dt), f"call {v} row {r}"
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(ORD_SPLIT, old)

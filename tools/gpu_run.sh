@@ -2,13 +2,17 @@
 # One GPU session on the gpurun box: the steps named on the command line, in order, each
 # under its own time limit; the first failing step ends the session.
 #   tests   pytest -m gpu (the whole suite, one process)
+#   newtests  the dense / record-row / split-apply GPU test files only
+#   abdense tools/ab_c2.py over dense apply variants (ABCONF: its --configs)
 #   smoke   __graft_entry__.smoke()
 #   bench   the default C2 bench line (with the PMC JSON of this tree when present)
 #   stats   the default bench under rocprofv3 --kernel-trace --stats
 #   pmc     three PMC passes on the C2 bench (request counts, FETCH_SIZE, WRITE_SIZE),
 #           summarised with the kernel signature into $O/pmc_dense_apply.json
+#   c3split C3 with each split-apply form (PSX_ORD_SPLIT 1, 2, 3), twice, interleaved
 #   c3 | c3idx | c4 | c5 | ada | f16 | d125 | imp   the other workloads' bench lines
 #   probe   tools/probe_ceiling (the C2 access pattern's hardware ceiling; build it first)
+#   pmix    tools/probe_apply's mixing probe (records in random vs slot order; build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
 set -o pipefail
@@ -65,6 +69,8 @@ for s in "$@"; do
     c3ab) run c3ab_off 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 &&
           run c3ab_on 300 env PSX_ORD_PIPELINE=1 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 &&
           run c3ab_off2 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 ;;
+    c3split) i=0; for v in 1 2 3 1 2 3; do i=$((i+1)); run c3split_${i}_v$v 300 env PSX_ORD_SPLIT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+             grep -h '^{' $O/c3split_*.log | cut -c1-400 ;;
     c2only) run c2only 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras ;;
     c3) run c3 300 python -u bench.py --workload c3 --steps 20 --warmup 3 ;;
     c3idx) run c3idx 300 python -u bench.py --workload c3 --indexed --steps 20 --warmup 3 ;;
@@ -77,8 +83,11 @@ for s in "$@"; do
     probe) run probe 300 tools/probe_ceiling 10 ;;
     hbm) run hbm 400 tools/probe_hbm 10 ;;
     abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
+    abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,3:1:1,4:1:1,7:1:1,8:1:1,9:1:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
+    newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dense_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py ;;
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
+    pmix) run pmix 300 tools/probe_apply 10 1 && cat "$O/pmix.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -14,6 +14,8 @@
 //   tabplain  table rows loaded without nt
 //   pipe      the next D rows' loads issued before this D rows' stores
 //   blocked   each wave sweeps 16 consecutive rows (4 x D=4) before taking the next block
+// With a second argument 1 (mixing probe): table-plain variants with the records in random
+// order, then in slot order (every access a sequential sweep), then sequential and aligned.
 // Each line is one JSON object: ms per launch and algorithmic GB/s (the apply's bytes).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/probe_apply tools/probe_apply.hip
 #include <hip/hip_runtime.h>
@@ -62,6 +64,7 @@ struct Args {
   const uint8_t *stream;
   const int32_t *pos;   // [B][R]: record index of row r in message b
   int64_t R, stride, msg_bytes;
+  int64_t rec_off;   // payload offset of record 0 (24: the wire format's header + row id)
 };
 
 template <int B, int D>
@@ -73,7 +76,7 @@ __device__ __forceinline__ void load_rows(const Args &a, int64_t r0, int lane, b
     t[q] = tab_nt ? ld_nt(a.table + r * 1024 + lane * 16) : ld_plain(a.table + r * 1024 + lane * 16);
 #pragma unroll
     for (int b = 0; b < B; ++b)
-      u[q][b] = ld_nt(a.stream + b * a.msg_bytes + (int64_t)a.pos[b * a.R + r] * a.stride + 24 + lane * 16);
+      u[q][b] = ld_nt(a.stream + b * a.msg_bytes + (int64_t)a.pos[b * a.R + r] * a.stride + a.rec_off + lane * 16);
   }
 }
 
@@ -176,6 +179,7 @@ int main(int argc, char **argv) {
   Args a{};
   a.R = R;
   a.stride = 1028;
+  a.rec_off = 24;
   a.msg_bytes = 20 + R * 1028 + 64;
   uint8_t *stream;
   int32_t *pos;
@@ -205,6 +209,31 @@ int main(int argc, char **argv) {
            alg / ms / 1e6);
     fflush(stdout);
   };
+  const char *order = "random";
+  auto variants = [&] {
+    printf("{\"order\": \"%s\"}\n", order);
+    run("tabplain", apply_kernel<8, 4, ST_PLAIN, false, false>, 4, 1);
+    run("tabplain_nostore", apply_kernel<8, 4, ST_NONE, false, false>, 4, 1);
+    run("tabplain_outplace", apply_kernel<8, 4, ST_PLAIN, false, true>, 4, 1);
+    run("tabplain_ntstore", apply_kernel<8, 4, ST_NT, false, false>, 4, 1);
+    run("tabplain", apply_kernel<8, 4, ST_PLAIN, false, false>, 4, 1);
+  };
+  if (argc > 2 && atoi(argv[2]) == 1) {
+    // Mixing probe: the same variants with every message's records in slot order (record r
+    // of every message belongs to row r), so all reads and writes are sequential sweeps —
+    // the same bytes, read/write ratio and kernel; only the randomness is gone.
+    variants();
+    for (int64_t m = 0; m < B; ++m)
+      for (int64_t i = 0; i < R; ++i) h[m * R + i] = (int32_t)i;
+    CK(hipMemcpy(pos, h.data(), h.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    order = "sequential";
+    variants();
+    a.stride = 1024;   // sequential and line-aligned records (no 9th line per record)
+    a.rec_off = 0;
+    order = "sequential_aligned";
+    variants();
+    return 0;
+  }
   // the same variant twice, first and last, brackets the run's drift
   run("base", apply_kernel<8, 4, ST_PLAIN, true, false>, 4, 1);
   run("nostore", apply_kernel<8, 4, ST_NONE, true, false>, 4, 1);

@@ -277,7 +277,7 @@ C3_LATENCY_JSON = os.path.join(ROOT, "profiles", "r02", "c3_inc_latency.json")
 C3_WAVES_PER_SIMD = {4: 7, 16: 3}   # ordered_apply_reg_kernel<int32, sorted, J> occupancy (-Rpass-analysis)
 
 
-def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20):
+def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20, split=3):
     """The sorted-map apply's bound ("C3 bound").  A row's records are one
     dependent chain in one wave: each record's found keys (a chunk of <= 64 columns) are
     added at once (found_run), each new key is one LinearSearchAndMove insert.  So a row
@@ -327,7 +327,10 @@ def c3_model(batches, rows, K, apply_ms, warmup=3, steps=20):
     I_r = np.bincount(uniq[grp] // K, weights=ins, minlength=rows)
     net = np.add.reduceat(vs, start)
     n_r = np.bincount(uniq[net != 0] // K, minlength=rows).astype(np.float64)
-    big = n_r + k_r > 256                                      # the 1,024-entry launch
+    # the 1,024-entry launch: split form 1 classifies by entries + Incs; the spill forms (2, 3,
+    # the default) start a row there only when its image is already > 224 entries (a row that
+    # outgrows 256 mid-call spills to it; the timed steps' images stay below 256)
+    big = (n_r + k_r > 256) & ((n_r > 224) if split >= 2 else True)
     x16, y16 = curve("found_rec_ns")                           # 1,024-entry image
     x4, y4 = curve("found_small_rec_ns")                       # 256-entry image
     xi, yi = curve("insert_ns")
@@ -467,7 +470,7 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
     else:
         decode = "one workgroup per message (decode_streams)"
     stream_bytes = sum(s.size for s in streams)
-    model = c3_model(batches, rows, K, apply_ms / max(apply_n, 1))
+    model = c3_model(batches, rows, K, apply_ms / max(apply_n, 1), split=L.psx_debug_get_variant(6))
     cpu = c3_cpu_baseline(args, batches, nupd, bgs, cpu_seconds) if cpu_seconds > 0 else None
     return {
         "metric": "sparse int row-update apply (SortedVectorMapRow<int32>), C3",

@@ -18,19 +18,23 @@ enum {
                                    3 / 4: v3 with 4- / 2-slot tiles, 5 / 6: v3 with 4 rows in
                                    flight per wave and 4- / 16-slot tiles, 7 / 8 / 9: v5 (lean)
                                    with 4 / 3 / 2 rows in flight per wave (2 < B <= 8) */
-  PSX_VARIANT_ORD_SPLIT = 6     /* 1: rows of sorted/map tables with 256 < max_entries <= 1024
-                                   classified into a 256- and a 1,024-entry image launch that
-                                   run concurrently (default), 2: spill mode (rows start on the
-                                   256-entry launch unless already 7/8 full; a row that outgrows
-                                   it is redone by a 1,024-entry launch that follows), 3: spill
-                                   mode with rows of >= 4 records taken first, 0: one
-                                   1,024-entry launch */,
+  PSX_VARIANT_ORD_SPLIT = 6     /* rows of sorted/map tables with 256 < max_entries <= 1024:
+                                   3 (default): spill mode with rows of >= 4 records taken first;
+                                   2: spill mode (rows start on the 256-entry launch unless already
+                                   7/8 full; a row that outgrows it is redone, untouched, by a
+                                   1,024-entry launch that follows); 1: classified by entries + Incs
+                                   into a 256- and a 1,024-entry launch that run concurrently;
+                                   0: one 1,024-entry launch */,
   PSX_VARIANT_DECODE = 7        /* 1: walked messages with sparse tables decode window-parallel
                                    (psx_walk.hip, where eligible; the default), 0: one workgroup
                                    per message (decode_streams) */,
   PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */,
   PSX_VARIANT_DENSE_STORE = 9   /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
-                                   (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
+                                   (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */,
+  PSX_DEBUG_DENSE_KNOBS = 10    /* timing experiments on the v5 kernel only, NOT semantics-preserving
+                                   in general: bit0 skips the index reset (valid only while every call
+                                   rewrites the same index entries, e.g. bench.py's repeated C2
+                                   batches), bit1 skips the row flags; 0 (default) = the product */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -1004,7 +1004,7 @@ __global__ void __launch_bounds__(256) dense_apply_v5_kernel(DenseArgs a) {
     if (lane < D * BMAX && bj < B && sj < a.max_rows) {
       int32_t *p = a.inv + sj * a.inv_ss + (int64_t)bj * a.inv_sb;
       myidx = *p;
-      if (myidx >= 0) *p = -1;
+      if (myidx >= 0 && !(a.knobs & 1)) *p = -1;
     }
     if (skip) continue;
     const bool pres = myidx >= 0 && ((real >> bj) & 1u);
@@ -1049,7 +1049,7 @@ __global__ void __launch_bounds__(256) dense_apply_v5_kernel(DenseArgs a) {
           for (int q = 0; q < D; ++q)
             if ((badm >> (q * BMAX)) & 0xffull) okq &= ~(1u << q);
         }
-        if (lane < D && ((okq >> lane) & 1u)) {
+        if (lane < D && ((okq >> lane) & 1u) && !(a.knobs & 2)) {
           a.flags[s0 + lane] = 3;
           if (a.ver) a.ver[s0 + lane] += (uint64_t)__builtin_popcountll((presm >> (lane * BMAX)) & 0xffull);
         }
@@ -1427,8 +1427,12 @@ static void launch_v3(const DenseArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
 }
 
+int g_dense_knobs = 0;   // PSX_DEBUG_DENSE_KNOBS (v5 timing experiments only)
+
 template <typename V, int D>
-static void launch_v5(const DenseArgs &a, hipStream_t st) {
+static void launch_v5(const DenseArgs &a0, hipStream_t st) {
+  DenseArgs a = a0;
+  a.knobs = g_dense_knobs;
   auto k = dense_apply_v5_kernel<V, D>;
   const int64_t groups = (a.max_rows + D - 1) / D;
   const unsigned blocks = resident_blocks(k, (groups + 3) / 4);

@@ -1145,8 +1145,10 @@ __global__ void gather_entries_kernel(const int32_t *nent, const uint8_t *entrie
 }
 
 // ---------------------------------------------------------------------------
-int g_ord_split = 1;  // rows of > 256-entry tables classified into a 256- and a 1,024-entry image launch
-                      // (1: concurrent launches, 2: spill mode, 0: one 1,024-entry launch)
+int g_ord_split = 3;  // rows of > 256-entry tables: 3 spill mode with heavy rows first (default),
+                      // 2 spill mode, 1 classified into concurrent 256- / 1,024-entry launches,
+                      // 0 one 1,024-entry launch (C3 apply 0.088 / 0.059 / 0.051 ms for 1 / 2 / 3,
+                      // profiles/r03/s12)
 
 // One touched row per wave at a time: the grid is sized by rows (the touched count is on
 // the device), not by 64-row tiles — 100K rows as tiles gave 1,564 waves for ~35K touched

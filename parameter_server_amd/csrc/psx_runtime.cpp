@@ -2493,6 +2493,7 @@ psx_status psx_timing_reset(psx_ctx *c) {
 namespace psx {
 extern int g_apply_variant;
 extern int g_ord_split;
+extern int g_dense_knobs;
 }  // namespace psx
 
 static int *variant_slot(int32_t which) {
@@ -2502,6 +2503,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
+    case PSX_DEBUG_DENSE_KNOBS: return &psx::g_dense_knobs;
     default: return nullptr;
   }
 }

@@ -84,6 +84,7 @@ for s in "$@"; do
     hbm) run hbm 400 tools/probe_hbm 10 ;;
     abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
     abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,3:1:1,4:1:1,7:1:1,8:1:1,9:1:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
+    abzeros) run abzeros 400 python -u tools/ab_c2.py --zeros --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -30 "$O/abzeros.log" ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dense_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py ;;
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;

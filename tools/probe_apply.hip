@@ -147,6 +147,15 @@ __global__ void __launch_bounds__(256) blocked_kernel(Args a) {
   }
 }
 
+// Pseudo-random f32 data (|x| < 1, full mantissa entropy) for the data-dependence check.
+__global__ void fill_random(uint32_t *p, int64_t n, uint32_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 15; x *= 2246822519u; x ^= x >> 13; x *= 3266489917u; x ^= x >> 16;
+    p[i] = (x & 0x807fffffu) | 0x3e000000u;   // sign and mantissa random, exponent fixed: 0.125..0.25
+  }
+}
+
 template <typename K>
 static unsigned resident(K k) {
   int per = 0, cus = 0;
@@ -231,6 +240,23 @@ int main(int argc, char **argv) {
     a.stride = 1024;   // sequential and line-aligned records (no 9th line per record)
     a.rec_off = 0;
     order = "sequential_aligned";
+    variants();
+    // the same, random order, with random data in the table and every record (the runs
+    // above add zeros to zeros): does the data itself change the rate?
+    a.stride = 1028;
+    a.rec_off = 24;
+    std::mt19937 rng2(1234);
+    for (int64_t m = 0; m < B; ++m) {
+      std::vector<int32_t> perm(R);
+      for (int64_t i = 0; i < R; ++i) perm[i] = (int32_t)i;
+      std::shuffle(perm.begin(), perm.end(), rng2);
+      for (int64_t i = 0; i < R; ++i) h[m * R + perm[i]] = (int32_t)i;
+    }
+    CK(hipMemcpy(pos, h.data(), h.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    fill_random<<<4096, 256>>>(reinterpret_cast<uint32_t *>(a.table), R * 256, 17u);
+    fill_random<<<4096, 256>>>(reinterpret_cast<uint32_t *>(stream), B * a.msg_bytes / 4, 91u);
+    CK(hipDeviceSynchronize());
+    order = "random_data";
     variants();
     return 0;
   }

@@ -14,10 +14,7 @@ extern "C" {
 #endif
 
 enum {
-  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact,
-                                   3 / 4: v3 with 4- / 2-slot tiles, 5 / 6: v3 with 4 rows in
-                                   flight per wave and 4- / 16-slot tiles, 7 / 8 / 9: v5 (lean)
-                                   with 4 / 3 / 2 rows in flight per wave (2 < B <= 8) */
+  PSX_VARIANT_DENSE_APPLY = 1,  /* 0: auto (default), 1: force v2, 2: force v4 compact */
   PSX_VARIANT_ORD_SPLIT = 6     /* rows of sorted/map tables with 256 < max_entries <= 1024:
                                    3 (default): spill mode with rows of >= 4 records taken first;
                                    2: spill mode (rows start on the 256-entry launch unless already
@@ -29,17 +26,21 @@ enum {
                                    (psx_walk.hip, where eligible; the default), 0: one workgroup
                                    per message (decode_streams) */,
   PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */,
-  PSX_VARIANT_DENSE_STORE = 9   /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
-                                   (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */,
-  PSX_DEBUG_DENSE_KNOBS = 10    /* timing experiments on the v5 kernel only, NOT semantics-preserving
-                                   in general: bit0 skips the index reset (valid only while every call
-                                   rewrites the same index entries, e.g. bench.py's repeated C2
-                                   batches), bit1 skips the row flags; 0 (default) = the product */
+  PSX_VARIANT_DENSE_STORE = 9,  /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
+                                   (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
+  PSX_DEBUG_WALK_TRACE = 11     /* 1: walked calls record per-window timestamps (psx_debug_walk_trace) */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */
 int32_t psx_debug_set_variant(int32_t which, int32_t variant);
 int32_t psx_debug_get_variant(int32_t which);
+
+/* The last walked call's per-window timestamps (PSX_DEBUG_WALK_TRACE on): 6 uint64 per
+   (window, message) item in ticket order (item = window * B + message) — ticket taken,
+   window in LDS, exit map done, predecessor's state seen, own state published, records
+   expanded — in s_memrealtime ticks (100 MHz).  Copies min(items, max_items) items and
+   returns the call's item count, 0 when no call walked, -1 on error. */
+int64_t psx_debug_walk_trace(struct psx_ctx *ctx, uint64_t *out, int64_t max_items);
 
 #ifdef __cplusplus
 }

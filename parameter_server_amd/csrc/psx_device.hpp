@@ -95,7 +95,6 @@ struct DenseArgs {
                                // every record's row id is checked against its slot in the apply
   int64_t row_offset, row_stride;   // shard geometry (expected row id of a slot)
   int32_t store_nt;                 // table-row policy (PSX_VARIANT_DENSE_STORE): bit0 nt store, bit1 nt load
-  int32_t knobs;                    // PSX_DEBUG_DENSE_KNOBS (timing experiments; 0 in the product)
 };
 
 // AdaRevision server-table logic on one f32 dense table (psx_ada.hip).

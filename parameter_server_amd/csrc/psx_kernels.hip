@@ -941,163 +941,6 @@ __global__ void __launch_bounds__(256) dense_apply_v3_kernel(DenseArgs a) {
   }
 }
 
-// dense_apply_v5 (lean, D rows per wave at a time): the C2 access pattern with as few
-// instructions and registers around it as the semantics allow.  Rows are dealt in groups
-// of D consecutive slots, group g to wave g mod nwaves, so the chip's rows in flight (and
-// its row writes) form one front moving through the table.  Per group: lane j < 8D loads
-// the index entry of record (row j/8, message j%8) and resets it; one ballot gives the
-// presence mask; with record rows lane j also loads its record's row id (the first cache
-// line of the payload it gathers next: no added DRAM traffic); then every present
-// record's chunk and the D table rows are loaded back to back (absent ones are not loaded
-// at all: uniform branches on the mask), added in message order, and each row that has a
-// record (and whose record rows check) is stored once.  B <= 8, 32-bit stream offsets.
-template <typename V, int D>
-__global__ void __launch_bounds__(256) dense_apply_v5_kernel(DenseArgs a) {
-  constexpr int BMAX = 8;
-  static_assert(D * BMAX <= 64, "one lane per (row, message)");
-  constexpr int VS = (int)sizeof(V);
-  constexpr int EPV = 16 / VS;
-  constexpr int CHUNK = 64 * EPV;
-  const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
-  const int64_t wave_g = (int64_t)blockIdx.x * 4 + wib;
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
-  const int B = a.B;
-
-  bool skip = (*a.call_status & (kStFatal | kStDuplicateRow)) != 0 || (*a.sticky & kStDuplicateRow) != 0;
-  bool dup = false;
-  const uint8_t *pay0[BMAX];
-  uint32_t real = 0;   // bit b: message b holds this table
-#pragma unroll
-  for (int b = 0; b < BMAX; ++b) {
-    pay0[b] = a.zero_chunk;
-    if (b < B) {
-      const Seg sg = a.segs[b * kMaxTables + a.t];
-      if (sg.rec0 >= 0 && !sg.sparse) {
-        pay0[b] = a.ss.data[b] + sg.rec0 + 4;
-        real |= 1u << b;
-        if (a.counters[a.t * kMaxFused + b] != (uint32_t)sg.num_rows) dup = true;
-      }
-    }
-  }
-  if (dup && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.call_status, kStDuplicateRow);
-  skip = skip || dup;
-  __shared__ const uint8_t *s_pay0[BMAX];
-#pragma unroll
-  for (int b = 0; b < BMAX; ++b)
-    if (threadIdx.x == b) s_pay0[b] = pay0[b];
-  __syncthreads();
-
-  const bool rows_mode = a.rows_mask != 0;
-  const int64_t vec_elems = (a.cap / EPV) * EPV;
-  const int64_t row_bytes = a.row_cap * VS;
-  const uint32_t stride = (uint32_t)a.stride;
-  const uint32_t lane_off = (uint32_t)(lane * 16);
-  uint8_t *table = reinterpret_cast<uint8_t *>(a.table);
-  const int64_t ngroups = (a.max_rows + D - 1) / D;
-  const int qj = lane >> 3, bj = lane & 7;   // this lane's index entry: (row qj, message bj)
-
-  for (int64_t g = wave_g; g < ngroups; g += nwaves) {
-    const int64_t s0 = g * D;
-    const int64_t sj = s0 + qj;
-    int32_t myidx = -1;
-    if (lane < D * BMAX && bj < B && sj < a.max_rows) {
-      int32_t *p = a.inv + sj * a.inv_ss + (int64_t)bj * a.inv_sb;
-      myidx = *p;
-      if (myidx >= 0 && !(a.knobs & 1)) *p = -1;
-    }
-    if (skip) continue;
-    const bool pres = myidx >= 0 && ((real >> bj) & 1u);
-    const uint64_t presm = __ballot(pres);
-    if (!presm) continue;
-    bool bad = false;
-    if (rows_mode && pres && ((a.rows_mask >> bj) & 1u)) {
-      const int32_t rid = *reinterpret_cast<const int32_t *>(s_pay0[bj] + (uint32_t)myidx * stride - 4);
-      bad = rid != (int32_t)(a.row_offset + sj * a.row_stride);
-    }
-    uint32_t okq = 0;   // bit q: row q has a record and may be stored
-#pragma unroll
-    for (int q = 0; q < D; ++q)
-      if ((presm >> (q * BMAX)) & 0xffull) okq |= 1u << q;
-    bool verified = false;
-    for (int64_t c0 = 0; c0 < vec_elems; c0 += CHUNK) {
-      const int64_t e0 = c0 + (int64_t)lane * EPV;
-      const bool full = e0 < vec_elems;
-      const uint32_t coff = (uint32_t)(c0 * VS);
-      const int64_t te = full ? e0 : 0;
-      u32x4 t[D];
-      u32x4 u[D][BMAX];
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        const int64_t sq = s0 + q < a.max_rows ? s0 + q : a.max_rows - 1;
-        t[q] = load_row16(table + sq * row_bytes + te * VS, a.store_nt);
-#pragma unroll
-        for (int b = 0; b < BMAX; ++b) {
-          u[q][b] = u32x4{0, 0, 0, 0};
-          if ((presm >> (q * BMAX + b)) & 1ull) {
-            const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(myidx, q * BMAX + b);
-            u[q][b] = gload16<true>(pay0[b], full ? i * stride + coff + lane_off : i * stride);
-          }
-        }
-      }
-      if (!verified) {   // after the loads are issued: the row ids arrived with the first lines
-        verified = true;
-        const uint64_t badm = __ballot(bad);
-        if (badm) {
-          if (lane == 0) atomicOr(a.call_status, kStRowsMismatch);
-#pragma unroll
-          for (int q = 0; q < D; ++q)
-            if ((badm >> (q * BMAX)) & 0xffull) okq &= ~(1u << q);
-        }
-        if (lane < D && ((okq >> lane) & 1u) && !(a.knobs & 2)) {
-          a.flags[s0 + lane] = 3;
-          if (a.ver) a.ver[s0 + lane] += (uint64_t)__builtin_popcountll((presm >> (lane * BMAX)) & 0xffull);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        u32x4 acc = t[q];
-#pragma unroll
-        for (int b = 0; b < BMAX; ++b)
-          if ((presm >> (q * BMAX + b)) & 1ull) acc = Vec<V>::add(acc, u[q][b]);
-        if (((okq >> q) & 1u) && full) store16(table + (s0 + q) * row_bytes + e0 * VS, acc, a.store_nt);
-      }
-    }
-    if (!verified) {   // rows with no vector part (cap < 16 B / sizeof(V))
-      const uint64_t badm = __ballot(bad);
-      if (badm) {
-        if (lane == 0) atomicOr(a.call_status, kStRowsMismatch);
-#pragma unroll
-        for (int q = 0; q < D; ++q)
-          if ((badm >> (q * BMAX)) & 0xffull) okq &= ~(1u << q);
-      }
-      if (lane < D && ((okq >> lane) & 1u)) {
-        a.flags[s0 + lane] = 3;
-        if (a.ver) a.ver[s0 + lane] += (uint64_t)__builtin_popcountll((presm >> (lane * BMAX)) & 0xffull);
-      }
-    }
-    // ragged tail (cap % EPV elements): element-wise on the first lanes
-    const int64_t tail = a.cap - vec_elems;
-    if (tail) {
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        if (((okq >> q) & 1u) && lane < tail) {
-          const int64_t e = vec_elems + lane;
-          uint8_t *trow = table + (s0 + q) * row_bytes;
-          V acc = *reinterpret_cast<const V *>(trow + e * VS);
-#pragma unroll
-          for (int b = 0; b < BMAX; ++b)
-            if ((presm >> (q * BMAX + b)) & 1ull) {
-              const uint8_t *rec = pay0[b] + (int64_t)(uint32_t)__builtin_amdgcn_readlane(myidx, q * BMAX + b) * a.stride;
-              acc = Elem<V>::add(acc, Elem<V>::load_rec(rec + e * VS));
-            }
-          *reinterpret_cast<V *>(trow + e * VS) = acc;
-        }
-      }
-    }
-  }
-}
-
 // dense_apply_v4 (compact): for partially covered calls (a row present in few of the B
 // messages).  v2/v3 keep PAIR rows x BMAX record slots in flight, most of them empty when
 // coverage is sparse; v4 packs up to PAIR rows whose present records total <= M into a
@@ -1386,8 +1229,7 @@ static unsigned resident_blocks(K kernel, int64_t want) {
 // Run-time selectors (include/psx_debug.h): the defaults are the measured winners; the
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
-int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact), 3/4: v3 with 4-/2-slot tiles, 5/6: 4 rows in flight per wave (4-/16-slot tiles),
-                           // 7/8/9: v5 (lean) with 4/3/2 rows in flight per wave
+int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact)
 
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride, int64_t row_offset, int64_t row_stride, int64_t max_rows,
@@ -1427,18 +1269,6 @@ static void launch_v3(const DenseArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
 }
 
-int g_dense_knobs = 0;   // PSX_DEBUG_DENSE_KNOBS (v5 timing experiments only)
-
-template <typename V, int D>
-static void launch_v5(const DenseArgs &a0, hipStream_t st) {
-  DenseArgs a = a0;
-  a.knobs = g_dense_knobs;
-  auto k = dense_apply_v5_kernel<V, D>;
-  const int64_t groups = (a.max_rows + D - 1) / D;
-  const unsigned blocks = resident_blocks(k, (groups + 3) / 4);
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
-}
-
 // BMAX is the next power of two >= B and the rows in flight per wave grow as B shrinks,
 // so every wave keeps ~8-18 16-byte loads in flight whatever the batch width.
 template <typename V, bool IMP, int H16>
@@ -1446,20 +1276,8 @@ static void launch_adaptive_v3(const DenseArgs &a, hipStream_t st) {
   if (a.B <= 1) launch_v3<V, 1, 16, true, 8, IMP, H16>(a, st);
   else if (a.B <= 2) launch_v3<V, 2, 16, true, 4, IMP, H16>(a, st);
   else if (a.B <= 4) launch_v3<V, 4, 16, true, 3, IMP, H16>(a, st);
-  else if (a.B <= 8) {
-    // variants 3/4: 4- and 2-slot tiles (the chip's rows in flight, and its row writes,
-    // form one narrower front moving through the table); 5/6: four rows in flight per wave
-    if (g_apply_variant == 3) launch_v3<V, 8, 4, true, 2, IMP, H16>(a, st);
-    else if (g_apply_variant == 4) launch_v3<V, 8, 2, true, 2, IMP, H16>(a, st);
-    else if (g_apply_variant == 5) launch_v3<V, 8, 4, true, 4, IMP, H16>(a, st);
-    else if (g_apply_variant == 6) launch_v3<V, 8, 16, true, 4, IMP, H16>(a, st);
-    else if (!IMP && !H16 && g_apply_variant >= 7 && g_apply_variant <= 9) {
-      if (g_apply_variant == 7) launch_v5<V, 4>(a, st);
-      else if (g_apply_variant == 8) launch_v5<V, 3>(a, st);
-      else launch_v5<V, 2>(a, st);
-    }
-    else launch_v3<V, 8, 16, true, 2, IMP, H16>(a, st);
-  } else launch_v3<V, 16, 16, true, 1, IMP, H16>(a, st);
+  else if (a.B <= 8) launch_v3<V, 8, 16, true, 2, IMP, H16>(a, st);
+  else launch_v3<V, 16, 16, true, 1, IMP, H16>(a, st);
 }
 
 // v2 (64-bit record pointers): streams of >= 4 GiB, which v3's 32-bit offsets cannot reach.

@@ -30,12 +30,14 @@ hipError_t launch_split_scatter(const SplitArgs &a, const int64_t *pos, const ui
                                 hipStream_t st);
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, hipStream_t st);
+                       uint32_t epoch, uint64_t trace_items, hipStream_t st);
+size_t walk_trace_offset(uint64_t items);
 size_t walk_ws_bytes(uint64_t items);
 // PSX_VARIANT_DECODE: 1 (default) walked messages with sparse tables decode window-parallel
 // where eligible, 0 one workgroup per message.
 int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
+int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
@@ -212,6 +214,8 @@ struct psx_ctx {
   uint64_t *d_recoff[2] = {nullptr, nullptr};
   size_t recoff_cap[2] = {0, 0};                  // entries
   void *d_walk[2] = {nullptr, nullptr};           // window-parallel decode workspace (psx_walk.hip)
+  int walk_last_slot = 0;                         // the last walked call (psx_debug_walk_trace)
+  uint64_t walk_last_items = 0;
   size_t walk_cap[2] = {0, 0};                    // bytes
   uint32_t walk_epoch[2] = {0, 0};                // granule tag of the slot's last call
   hipStream_t side = nullptr;                     // decode/index/verify stage
@@ -439,7 +443,7 @@ bool has_sparse_serialized(const psx_ctx *c) {
 // keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
 // work takes ~15-20 us); the other half of the chip stays free for the previous call's
 // apply when the decode is pipelined (psx_ctx_set_pipeline).
-constexpr uint64_t kWalkWindowBytes = 49152;   // == psx_walk.hip kWBytes
+constexpr uint64_t kWalkWindowBytes = 98304;   // == psx_walk.hip kWBytes
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
 unsigned walk_blocks(psx_ctx *c) {
@@ -589,6 +593,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     }
     c->walk_epoch[slot] = psx::next_walk_epoch();
     ++psx::g_walk_calls;
+    c->walk_last_slot = slot;
+    c->walk_last_items = items;
   }
   psx_status st = timed(
       c, "decode_streams",
@@ -596,7 +602,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
         if (walk)
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
                                   c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
-                                  c->walk_epoch[slot], prep);
+                                  c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0, prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -2493,7 +2499,6 @@ psx_status psx_timing_reset(psx_ctx *c) {
 namespace psx {
 extern int g_apply_variant;
 extern int g_ord_split;
-extern int g_dense_knobs;
 }  // namespace psx
 
 static int *variant_slot(int32_t which) {
@@ -2503,7 +2508,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
-    case PSX_DEBUG_DENSE_KNOBS: return &psx::g_dense_knobs;
+    case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     default: return nullptr;
   }
 }
@@ -2519,6 +2524,19 @@ extern "C" int32_t psx_debug_set_variant(int32_t which, int32_t variant) {
 extern "C" int32_t psx_debug_get_variant(int32_t which) {
   int *v = variant_slot(which);
   return v ? *v : -1;
+}
+
+extern "C" int64_t psx_debug_walk_trace(psx_ctx *c, uint64_t *out, int64_t max_items) {
+  if (!c || !out || max_items < 0) return -1;
+  const int k = c->walk_last_slot;
+  const uint64_t items = c->walk_last_items;
+  if (!c->d_walk[k] || !items) return 0;
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess) return -1;
+  const uint64_t n = std::min<uint64_t>(items, (uint64_t)max_items);
+  if (hipMemcpy(out, reinterpret_cast<uint8_t *>(c->d_walk[k]) + psx::walk_trace_offset(items), n * 6 * sizeof(uint64_t),
+                hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return (int64_t)items;
 }
 
 namespace {

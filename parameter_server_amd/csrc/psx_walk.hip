@@ -3,7 +3,7 @@
 // The record chain of a sparse table (SerializedOpLogReader::Next,
 // src/petuum_ps/server/serialized_oplog_reader.hpp:50-85: each record's size comes from its
 // own n, so record k+1 starts where record k ends) is sequential.  decode_streams walks it
-// with one workgroup per message, one 32 KiB window after another.  Here every window of
+// with one workgroup per message, one 32 KiB window after another.  Here every 96 KiB window of
 // every message is its own work item, and the work that does not depend on where the chain
 // enters the window runs in parallel, before the chain arrives:
 //
@@ -33,9 +33,13 @@
 namespace psx {
 
 constexpr int kWalkThreads = 1024;
-constexpr int kWW = 12288;                      // words per window (48 KiB)
+constexpr int kWW = 24576;                      // words per window (96 KiB)
 constexpr uint64_t kWBytes = (uint64_t)kWW * 4;
 constexpr uint16_t kNo = 0xFFFFu;               // next record outside the window / bad header
+// n16: the record count word after q (q's n as a record start), clipped to 16 bits
+constexpr uint16_t kNBig = 0xFFFDu;             // n >= kNBig (read the word itself)
+constexpr uint16_t kNNeg = 0xFFFEu;             // n < 0
+constexpr uint16_t kNNone = 0xFFFFu;            // no such word (past the window and its halo)
 constexpr int kGran = 14;                       // granules per published walker state
 constexpr int kMaxSegs = kMaxTables;            // sparse tables with records in one window
 
@@ -60,12 +64,16 @@ struct WalkCtl {      // reset by walk_head for the walk of the same call
 
 struct WalkHead {     // written by walk_head, read by the first window of each message
   WalkState st[kMaxFused];
-  uint32_t wfirst[kMaxFused];   // the message's first window (48 KiB grid from byte 0)
+  uint32_t wfirst[kMaxFused];   // the message's first window (96 KiB grid from byte 0)
   uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
 };
 constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
 
-size_t walk_ws_bytes(uint64_t items) { return kWalkGranOff + items * kGran * 8; }
+// After the granules: a trace region of kTraceWords 64-bit timestamps per window item
+// (s_memrealtime, 100 MHz), written only when the launch asks for it (psx_debug_walk_trace).
+constexpr int kTraceWords = 6;   // ticket taken, window in LDS, exit map done, predecessor seen, published, expanded
+size_t walk_ws_bytes(uint64_t items) { return kWalkGranOff + items * kGran * 8 + items * kTraceWords * 8; }
+size_t walk_trace_offset(uint64_t items) { return kWalkGranOff + items * kGran * 8; }
 
 // One table header at s.pos (SerializedOpLogReader::StartNewTable, :87-121), read directly
 // from the message.  Returns false when the message is done or failed (s.mode = 2).
@@ -170,6 +178,15 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
   head->nwin[b] = nwin;
 }
 
+// The next record start after a speculative record at word q with count word c (n16), or
+// kNo when it lies outside the window or past the message (a count >= kNBig always does).
+__device__ __forceinline__ uint16_t next_of(uint32_t q, uint16_t c, uint32_t nw, uint64_t W0, uint64_t size,
+                                            uint32_t spec_wpr) {
+  if (q + 1 >= nw || c >= kNBig) return kNo;
+  const uint64_t nxt = (uint64_t)q + 2 + (uint64_t)c * spec_wpr;
+  return nxt < nw && W0 + nxt * 4 <= size ? (uint16_t)nxt : kNo;
+}
+
 __device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
   switch (i) {
     case 0: return (uint32_t)s.pos;
@@ -192,16 +209,21 @@ __device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
 __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
                                                             uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
-                                                            uint32_t epoch) {
+                                                            uint32_t epoch, unsigned long long *trace) {
   gu64 *gran = (gu64 *)gran_p;
-  __shared__ uint32_t win[kWW + 1];                 // + 1 halo word
-  __shared__ uint16_t jt0[kWW];                     // the next record from q, kNo if outside
+  // 96 KiB windows in 144 KiB of LDS: xm first holds the window's words; n16 (the clipped
+  // record count after each word) is all the resolve needs of them, and the next-record
+  // table jt0 is rebuilt from it in place once the hand-off is done.
   // Exit map, packed: low 16 bits the last record start on q's chain inside the window, high
   // 16 the records from q up to it (exclusive).  After the hand-off the same words hold the
   // 16-record jump table jt4 (and its 2/8-record stage) for the expansion.
   __shared__ uint32_t xm[kWW];
+  __shared__ uint16_t jt0[kWW];                     // n16 until the hand-off, then the next record from q (kNo: outside)
+  uint32_t *const win = xm;
+  uint16_t *const n16 = jt0;
   uint16_t *const tmp16 = reinterpret_cast<uint16_t *>(xm);
   uint16_t *const jt4 = tmp16 + kWW;
+  __shared__ uint32_t sh_halo;
   __shared__ uint16_t seg_q[kMaxSegs];
   __shared__ uint16_t seg_n[kMaxSegs];
   __shared__ uint64_t seg_rk[kMaxSegs];
@@ -225,6 +247,8 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       __syncthreads();   // sh_ticket is rewritten at the top
       continue;
     }
+    unsigned long long *tr = trace ? trace + (uint64_t)tk * kTraceWords : nullptr;
+    if (tr && tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
     const uint8_t *p = ss.data[b];
     const uint64_t size = ss.size[b];
     const uint64_t W0 = ((uint64_t)head->wfirst[b] + j) * kWBytes;
@@ -244,20 +268,23 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       }
 #pragma unroll
       for (int k = 0; k < PER; ++k) win[tid + k * kWalkThreads] = r[k];
-      if (tid == 0) win[nw] = halo ? src[nw] : 0u;
+      if (tid == 0) sh_halo = halo ? src[nw] : 0u;
     }
     __syncthreads();
-    // 2) jump tables (every word a speculative record start): next = q + 2 + n * wpr
+    if (tr && tid == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+    // 2) every word a speculative record start: n16 from the words, then the exit map's
+    //    first link (next = q + 2 + n * wpr) from n16, over the words (xm aliases them)
     for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
-      uint16_t v = kNo;
-      if (q + 1 < nw) {
-        const int32_t n = (int32_t)win[q + 1];
-        if (n >= 0) {
-          const uint64_t nxt = (uint64_t)q + 2 + (uint64_t)n * spec_wpr;
-          if (nxt < nw && W0 + nxt * 4 <= size) v = (uint16_t)nxt;
-        }
+      uint16_t c = kNNone;
+      if (q + 1 < nw || (q + 1 == nw && halo)) {
+        const int32_t n = (int32_t)(q + 1 < nw ? win[q + 1] : sh_halo);
+        c = n < 0 ? kNNeg : (n >= (int32_t)kNBig ? kNBig : (uint16_t)n);
       }
-      jt0[q] = v;
+      n16[q] = c;
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
+      const uint16_t v = next_of(q, n16[q], nw, W0, size, spec_wpr);
       xm[q] = v == kNo ? q : ((uint32_t)v | (1u << 16));
     }
     __syncthreads();
@@ -281,6 +308,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       __syncthreads();
       if (!any) break;
     }
+    if (tr && tid == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
     // 4) wave 0: wait for the predecessor's state, resolve this window, publish
     if (tid < 64) {
       const int lane = tid;
@@ -328,6 +356,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         s.ntab = __shfl((int)v, 13);
         if (!ok) s.mode = 2;
       }
+      if (tr && lane == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
       if (lane == 0) {
         const uint64_t Wend = W0 + kWBytes;
         // this message's record-offset range (psx_runtime.cpp sizes it size / 8 + 1)
@@ -359,8 +388,9 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
             // past the table's end the speculative chain may be garbage): its header inside
             // the message, n >= 0, its end inside the message
             if (T + 1 > nw || (T + 1 == nw && !halo)) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
-            const int32_t nT = (int32_t)win[T + 1];
-            if (nT < 0) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
+            const uint16_t cT = n16[T];
+            if (cT == kNNeg || cT == kNNone) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
+            const int32_t nT = cT == kNBig ? *reinterpret_cast<const int32_t *>(p + W0 + ((uint64_t)T + 1) * 4) : (int32_t)cT;
             endT = W0 + ((uint64_t)T + 2 + (uint64_t)nT * spec_wpr) * 4;
             if (endT > size) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
           }
@@ -375,9 +405,10 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
             s.pos = endT;
           } else {
             // the table ends inside the chain: the record `take` on from q (binary lifting)
+            // (every link before it is a checked in-window link: n16 holds its exact n)
             uint32_t w = (uint32_t)q;
             uint64_t r = take;
-            for (; r; --r) w = jt0[w];   // once per table: its last window
+            for (; r; --r) w = w + 2 + (uint32_t)n16[w] * spec_wpr;   // once per table: its last window
             s.pos = W0 + (uint64_t)w * 4;
           }
           if (s.left == 0) {
@@ -399,6 +430,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         __hip_atomic_store(g + lane, ((uint64_t)epoch << 32) | (uint64_t)mine, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (tr && lane == 0) tr[4] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     // 5) expand the window's record offsets: the 16-record jump table by four squarings
@@ -406,6 +438,9 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     //    threads fill
     const uint32_t nseg = sh_nseg;
     if (nseg) {
+      // the next-record table from n16, in place (the exit map is no longer needed)
+      for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) jt0[q] = next_of(q, n16[q], nw, W0, size, spec_wpr);
+      __syncthreads();
       const uint16_t *src[4] = {jt0, tmp16, jt4, tmp16};
       uint16_t *dst[4] = {tmp16, jt4, tmp16, jt4};
 #pragma unroll
@@ -454,14 +489,16 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       if (tid < n1) recoff[r1 + tid] = W0 + (uint64_t)a1[tid] * 4;
       __syncthreads();
     }
+    if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
-// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 48 KiB window count);
-// epoch: nonzero, different from the previous call's on this workspace (granule tags).
+// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 96 KiB window count);
+// epoch: nonzero, different from the previous call's on this workspace (granule tags);
+// trace_items: nonzero = write the per-item timestamps (the workspace's item count).
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, hipStream_t st) {
+                       uint32_t epoch, uint64_t trace_items, hipStream_t st) {
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
@@ -469,8 +506,11 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
                      ctl, head);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  unsigned long long *trace =
+      trace_items ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_trace_offset(trace_items))
+                  : nullptr;
   hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
-                     head, gran, spec_wpr, epoch);
+                     head, gran, spec_wpr, epoch, trace);
   return hipGetLastError();
 }
 

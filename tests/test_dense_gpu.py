@@ -243,13 +243,12 @@ def test_smoke_entry():
     __graft_entry__.smoke()
 
 
-@pytest.mark.parametrize("apply_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9],
-                         ids=["auto", "v2", "v4", "v3t4", "v3t2", "v3p4t4", "v3p4", "v5d4", "v5d3", "v5d2"])
+@pytest.mark.parametrize("apply_variant", [0, 1, 2], ids=["auto", "v2", "v4"])
 def test_every_kernel_variant_bit_exact(apply_variant):
     """Every dense kernel the product can launch (include/psx_debug.h: v3 default, v2 the
-    >= 4 GiB fallback, v4 the partial-coverage kernel, and the v3 tile / v5 forms for
-    2 < B <= 8) matches the oracle, including a ragged row tail (cap 301), rows narrower
-    than one 16-byte vector (cap 3), partial coverage and 8-byte values."""
+    >= 4 GiB fallback, v4 the partial-coverage kernel) matches the oracle, including a
+    ragged row tail (cap 301), rows narrower than one 16-byte vector (cap 3), partial
+    coverage and 8-byte values."""
     from parameter_server_amd import _abi
     L = _abi.load()
     old_a = L.psx_debug_set_variant(1, apply_variant)

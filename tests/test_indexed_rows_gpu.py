@@ -341,19 +341,3 @@ def test_pipelined_calls_bit_exact(mode):
     assert np.array_equal(srv.read_rows(1, 0, rows).view(np.uint32), orc.read_dense_rows(1, 0, rows).view(np.uint32))
     srv.close()
 
-
-@pytest.mark.parametrize("variant", [3, 4, 7, 8, 9], ids=["v3t4", "v3t2", "v5d4", "v5d3", "v5d2"])
-def test_dense_apply_forms_check_rows(variant):
-    """The v3 tile forms and the lean v5 kernel (PSX_VARIANT_DENSE_APPLY 3-9) on record
-    rows: parity with the checker and the walked path, and a list that disagrees with its
-    stream (those rows unchanged, the rest applied)."""
-    from parameter_server_amd import _abi
-    L = _abi.load()
-    old = L.psx_debug_set_variant(1, variant)
-    try:
-        test_rows_match_checker_and_walk(8, F32)
-        test_rows_match_checker_and_walk(3, F64)
-        test_rows_match_checker_and_walk(8, I64)
-        test_disagreeing_rows_leave_those_rows_unchanged()
-    finally:
-        L.psx_debug_set_variant(1, old)

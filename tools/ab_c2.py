@@ -3,10 +3,9 @@ rule 24): the headline workload of bench.py, then R rounds; each round runs ever
 configuration for K steps and records the per-kernel HIP-event times.  Prints JSON with
 the median ms of every kernel per configuration.
 Usage: python tools/ab_c2.py --configs 0,0:1,2 [--rounds 5 --steps 5]
-       (apply_variant[:rows[:store_nt[:knobs]]], include/psx_debug.h; rows = 1 applies
-       through psx_apply_indexed_rows with the batches' record-row lists; store_nt selects
-       PSX_VARIANT_DENSE_STORE, default 1; knobs PSX_DEBUG_DENSE_KNOBS, default 0 — valid
-       here because every step applies the same batches)"""
+       (apply_variant[:rows[:store_nt]], include/psx_debug.h; rows = 1 applies through
+       psx_apply_indexed_rows with the batches' record-row lists; store_nt selects
+       PSX_VARIANT_DENSE_STORE, default 1)"""
 import argparse
 import json
 import os
@@ -57,13 +56,12 @@ def main():
     configs = []
     for c in args.configs.split(","):
         f = [int(x) for x in c.split(":")]
-        configs.append(tuple((f + [0, 1, 0][len(f) - 1:])[:4]))
+        configs.append(tuple((f + [0, 1][len(f) - 1:])[:3]))
     res = {c: {k: [] for k in kernels + ("step",)} for c in configs}
 
     def run(c, steps):
         L.psx_debug_set_variant(1, c[0])
         L.psx_debug_set_variant(9, c[2])
-        L.psx_debug_set_variant(10, c[3])
         srv.timing(True)
         srv.timing_reset()
         torch.cuda.synchronize()
@@ -91,7 +89,7 @@ def main():
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))
             res[c]["step"].append(step_ms)
-    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + f"_rowpolicy{c[2]}" + (f"_knobs{c[3]}" if c[3] else ""):
+    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + f"_rowpolicy{c[2]}":
            {k: round(statistics.median(v), 4) for k, v in res[c].items()} for c in configs}
     print(json.dumps(out, indent=1))
     srv.close()

@@ -2,6 +2,7 @@
 # One GPU session on the gpurun box: the steps named on the command line, in order, each
 # under its own time limit; the first failing step ends the session.
 #   tests   pytest -m gpu (the whole suite, one process)
+#   walktests the walk / sparse / record-row / split / KAT GPU test files only
 #   newtests  the dense / record-row / split-apply GPU test files only
 #   abdense tools/ab_c2.py over dense apply variants (ABCONF: its --configs)
 #   smoke   __graft_entry__.smoke()
@@ -12,6 +13,7 @@
 #   c3split C3 with each split-apply form (PSX_ORD_SPLIT 1, 2, 3), twice, interleaved
 #   c3 | c3idx | c4 | c5 | ada | f16 | d125 | imp   the other workloads' bench lines
 #   probe   tools/probe_ceiling (the C2 access pattern's hardware ceiling; build it first)
+#   wtrace  tools/walk_trace.py: per-window timeline of the walk on the C3 batches
 #   pmix    tools/probe_apply's mixing probe (records in random vs slot order; build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
@@ -83,9 +85,11 @@ for s in "$@"; do
     probe) run probe 300 tools/probe_ceiling 10 ;;
     hbm) run hbm 400 tools/probe_hbm 10 ;;
     abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
-    abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,3:1:1,4:1:1,7:1:1,8:1:1,9:1:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
+    abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
     abzeros) run abzeros 400 python -u tools/ab_c2.py --zeros --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -30 "$O/abzeros.log" ;;
+    walktests) run walktests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dense_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py ;;
+    wtrace) run wtrace 200 python -u tools/walk_trace.py && head -c 3000 "$O/wtrace.log" ;;
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
     pmix) run pmix 300 tools/probe_apply 10 1 && cat "$O/pmix.log" ;;

@@ -46,10 +46,15 @@ def kernel_signature():
     kernels and their launch policy and of the compile flags.  A PMC JSON carries the
     signature it was measured on; traffic from another signature is not reported."""
     import hashlib
+    import re
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "parameter_server_amd", "csrc")
-    for f in ("psx_kernels.hip", "psx_device.hpp"):
-        h.update(open(os.path.join(csrc, f), "rb").read())
+    h.update(open(os.path.join(csrc, "psx_kernels.hip"), "rb").read())
+    # of psx_device.hpp only what the dense kernels take: the shared device constants and
+    # structs up to DenseArgs (the ordered path's and the walk's structs may change freely)
+    dev = open(os.path.join(csrc, "psx_device.hpp")).read()
+    m = re.search(r"^struct DenseArgs \{.*?^\};", dev, re.S | re.M)
+    h.update(dev[:m.end()].encode() if m else dev.encode())
     for line in open(os.path.join(csrc, "Makefile")):
         if line.startswith("HIPFLAGS") or line.startswith("           -"):
             h.update(line.encode())

@@ -28,7 +28,8 @@ enum {
   PSX_STAT_WALK_CALLS = 8       /* read: calls decoded window-parallel since load (set: reset) */,
   PSX_VARIANT_DENSE_STORE = 9,  /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
                                    (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
-  PSX_DEBUG_WALK_TRACE = 11     /* 1: walked calls record per-window timestamps (psx_debug_walk_trace) */
+  PSX_DEBUG_WALK_TRACE = 11,    /* 1: walked calls record per-window timestamps (psx_debug_walk_trace) */
+  PSX_VARIANT_WALK_CUS = 12     /* the walk's persistent grid: 0 half the CUs (default), 1 every CU */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

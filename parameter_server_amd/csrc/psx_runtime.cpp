@@ -38,6 +38,7 @@ size_t walk_ws_bytes(uint64_t items);
 int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
+int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: 1 = the walk's persistent grid on every CU (default: half)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
@@ -443,14 +444,14 @@ bool has_sparse_serialized(const psx_ctx *c) {
 // keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
 // work takes ~15-20 us); the other half of the chip stays free for the previous call's
 // apply when the decode is pipelined (psx_ctx_set_pipeline).
-constexpr uint64_t kWalkWindowBytes = 98304;   // == psx_walk.hip kWBytes
+constexpr uint64_t kWalkWindowBytes = 49152;   // == psx_walk.hip kWBytes
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
 unsigned walk_blocks(psx_ctx *c) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
     cus = 256;
-  return (unsigned)std::max(1, cus / 2);
+  return (unsigned)std::max(1, psx::g_walk_all_cus ? cus : cus / 2);
 }
 
 // Smallest record of any table in the context: bounds the records a message can hold
@@ -2509,6 +2510,7 @@ static int *variant_slot(int32_t which) {
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
+    case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
     default: return nullptr;
   }
 }
@@ -2548,6 +2550,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
+    if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);
   }
 } variant_env;
 }  // namespace

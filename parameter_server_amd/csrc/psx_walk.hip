@@ -3,7 +3,7 @@
 // The record chain of a sparse table (SerializedOpLogReader::Next,
 // src/petuum_ps/server/serialized_oplog_reader.hpp:50-85: each record's size comes from its
 // own n, so record k+1 starts where record k ends) is sequential.  decode_streams walks it
-// with one workgroup per message, one 32 KiB window after another.  Here every 96 KiB window of
+// with one workgroup per message, one 32 KiB window after another.  Here every 48 KiB window of
 // every message is its own work item, and the work that does not depend on where the chain
 // enters the window runs in parallel, before the chain arrives:
 //
@@ -33,7 +33,7 @@
 namespace psx {
 
 constexpr int kWalkThreads = 1024;
-constexpr int kWW = 24576;                      // words per window (96 KiB)
+constexpr int kWW = 12288;                      // words per window (48 KiB)
 constexpr uint64_t kWBytes = (uint64_t)kWW * 4;
 constexpr uint16_t kNo = 0xFFFFu;               // next record outside the window / bad header
 // n16: the record count word after q (q's n as a record start), clipped to 16 bits
@@ -64,7 +64,7 @@ struct WalkCtl {      // reset by walk_head for the walk of the same call
 
 struct WalkHead {     // written by walk_head, read by the first window of each message
   WalkState st[kMaxFused];
-  uint32_t wfirst[kMaxFused];   // the message's first window (96 KiB grid from byte 0)
+  uint32_t wfirst[kMaxFused];   // the message's first window (48 KiB grid from byte 0)
   uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
 };
 constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
@@ -77,11 +77,13 @@ size_t walk_trace_offset(uint64_t items) { return kWalkGranOff + items * kGran *
 
 // One table header at s.pos (SerializedOpLogReader::StartNewTable, :87-121), read directly
 // from the message.  Returns false when the message is done or failed (s.mode = 2).
+// Run by every lane of a wave on the same state (the state stays wave-uniform); only the
+// `writer` lane stores the segment and raises status bits.
 __device__ bool walk_header(const uint8_t *p, uint64_t size, const TableDir &dir, Seg *segs_b, WalkState &s,
-                            uint32_t *call_status) {
+                            uint32_t *call_status, bool writer = true) {
   if (s.k >= s.ntab) { s.mode = 2; return false; }
   uint64_t off = s.pos;
-  if (off + 16 > size) { atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
+  if (off + 16 > size) { if (writer) atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
   const int32_t tid = *reinterpret_cast<const int32_t *>(p + off);
   const uint64_t usz = (uint64_t) * reinterpret_cast<const uint32_t *>(p + off + 4) |
                        ((uint64_t) * reinterpret_cast<const uint32_t *>(p + off + 8) << 32);
@@ -90,33 +92,33 @@ __device__ bool walk_header(const uint8_t *p, uint64_t size, const TableDir &dir
   int t = -1;
   for (int i = 0; i < dir.n; ++i)
     if (dir.table_id[i] == tid) t = i;
-  if (t < 0) { atomicOr(call_status, kStUnknownTable); s.mode = 2; return false; }
-  if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
-  if ((s.seen >> t) & 1ull) { atomicOr(call_status, kStUnsupported); s.mode = 2; return false; }
+  if (t < 0) { if (writer) atomicOr(call_status, kStUnknownTable); s.mode = 2; return false; }
+  if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { if (writer) atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
+  if ((s.seen >> t) & 1ull) { if (writer) atomicOr(call_status, kStUnsupported); s.mode = 2; return false; }
   s.seen |= 1ull << t;
   Seg *sg = &segs_b[t];
   if (dir.dense_serialized[t]) {
     const uint64_t stride = 4 + (uint64_t)dir.dense_body[t];
     const uint64_t need = (uint64_t)nrows * stride;
-    if (off + need > size) { atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
+    if (off + need > size) { if (writer) atomicOr(call_status, kStMalformed); s.mode = 2; return false; }
     Seg v;
     v.rec0 = (int64_t)off;
     v.num_rows = nrows;
     v.sparse = 0;
     v.ord0 = (int64_t)s.kk;
-    *sg = v;
+    if (writer) *sg = v;
     s.pos = off + need;
     s.k += 1;
     s.kk += (uint64_t)nrows;
     return true;
   }
-  if (off & 3) { atomicOr(call_status, kStUnsupported); s.mode = 2; return false; }
+  if (off & 3) { if (writer) atomicOr(call_status, kStUnsupported); s.mode = 2; return false; }
   Seg v;
   v.rec0 = (int64_t)s.rk;
   v.num_rows = nrows;
   v.sparse = 1;
   v.ord0 = (int64_t)s.kk;
-  *sg = v;
+  if (writer) *sg = v;
   s.pos = off;
   if (nrows) {
     s.mode = 1;
@@ -211,18 +213,17 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace) {
   gu64 *gran = (gu64 *)gran_p;
-  // 96 KiB windows in 144 KiB of LDS: xm first holds the window's words; n16 (the clipped
-  // record count after each word) is all the resolve needs of them, and the next-record
-  // table jt0 is rebuilt from it in place once the hand-off is done.
-  // Exit map, packed: low 16 bits the last record start on q's chain inside the window, high
-  // 16 the records from q up to it (exclusive).  After the hand-off the same words hold the
-  // 16-record jump table jt4 (and its 2/8-record stage) for the expansion.
+  // 48 KiB windows in 144 KiB of LDS, everything but the hand-off done before it: xm first
+  // holds the window's words, then with xm2 the pointer-jumping rounds of the exit map
+  // (packed: low 16 bits the last record start on q's chain inside the window, high 16 the
+  // records from q up to it, exclusive); n16 keeps the clipped record count after each
+  // word (the resolve's one read of the words; single-record steps are computed from it,
+  // next_of); jt4, the 16-record jump table, falls out of the fourth round.
   __shared__ uint32_t xm[kWW];
-  __shared__ uint16_t jt0[kWW];                     // n16 until the hand-off, then the next record from q (kNo: outside)
+  __shared__ uint32_t xm2[kWW];
+  __shared__ uint16_t n16[kWW];
+  __shared__ uint16_t jt4[kWW];
   uint32_t *const win = xm;
-  uint16_t *const n16 = jt0;
-  uint16_t *const tmp16 = reinterpret_cast<uint16_t *>(xm);
-  uint16_t *const jt4 = tmp16 + kWW;
   __shared__ uint32_t sh_halo;
   __shared__ uint16_t seg_q[kMaxSegs];
   __shared__ uint16_t seg_n[kMaxSegs];
@@ -289,28 +290,44 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     }
     __syncthreads();
     // 3) exit map by pointer jumping (terminal records point to themselves with count 0):
-    //    one packed LDS word per lookup
-    for (;;) {
+    //    one packed LDS word per lookup, rounds ping-ponging between xm and xm2 (one
+    //    barrier per round).  After round r every word holds the node min(2^(r+1), to
+    //    the terminal) records on, so round 3's result is also the 16-record jump table
+    //    (its count is 16 exactly where 16 records follow inside the window).
+    uint32_t *xf = xm;
+    for (int r = 0;; ++r) {
       constexpr int PER = kWW / kWalkThreads;
-      uint32_t nv[PER];
+      const uint32_t *src = (r & 1) ? xm2 : xm;
+      uint32_t *dst = (r & 1) ? xm : xm2;
       bool changed = false;
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
-        const uint32_t v = xm[q];
-        const uint32_t t = xm[v & 0xFFFFu];
-        nv[k] = (t & 0xFFFFu) | (((v >> 16) + (t >> 16)) << 16);
+        const uint32_t v = src[q];
+        const uint32_t t = src[v & 0xFFFFu];
+        const uint32_t nv = (t & 0xFFFFu) | (((v >> 16) + (t >> 16)) << 16);
+        dst[q] = nv;
+        if (r == 3) jt4[q] = (nv >> 16) == 16 ? (uint16_t)(nv & 0xFFFFu) : kNo;
         changed |= (t & 0xFFFFu) != (v & 0xFFFFu);
       }
-      const int any = __syncthreads_or(changed);
-#pragma unroll
-      for (int k = 0; k < PER; ++k) xm[(uint32_t)tid + (uint32_t)k * kWalkThreads] = nv[k];
-      __syncthreads();
-      if (!any) break;
+      xf = dst;
+      if (!__syncthreads_or(changed)) {
+        // fewer than four rounds: no chain holds 16 records, the jump table is empty
+        if (r < 3)
+          for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) jt4[q] = kNo;
+        break;
+      }
     }
+    __syncthreads();
     if (tr && tid == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
-    // 4) wave 0: wait for the predecessor's state, resolve this window, publish
+    // 4) wave 0: wait for the predecessor's state, resolve this window (every lane on the
+    //    same state, lane 0 writing), publish (lane i its granule i)
     if (tid < 64) {
+      // read before the wait (a scalar-cache miss here would sit on the chain's critical
+      // path): this message's record-offset range (psx_runtime.cpp sizes it size / 8 + 1)
+      const uint64_t rk_lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)ss.recoff_base[b]) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ss.recoff_base[b] >> 32)) << 32);
+      const uint64_t rk_hi = rk_lo + size / 8 + 1;
       const int lane = tid;
       WalkState s;
       if (j == 0) {
@@ -344,59 +361,99 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
             }
           }
         }
-        auto lo_hi = [&](int i) { return (uint64_t)(uint32_t)__shfl((int)v, i) | ((uint64_t)(uint32_t)__shfl((int)v, i + 1) << 32); };
+        // readlane: the state lands in scalar registers, wave-uniform for the resolve
+        auto rl = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); };
+        auto lo_hi = [&](int i) { return (uint64_t)rl(i) | ((uint64_t)rl(i + 1) << 32); };
         s.pos = lo_hi(0);
         s.left = lo_hi(2);
         s.rk = lo_hi(4);
         s.kk = lo_hi(6);
         s.seen = lo_hi(8);
-        s.k = __shfl((int)v, 10);
-        s.t = __shfl((int)v, 11);
-        s.mode = __shfl((int)v, 12);
-        s.ntab = __shfl((int)v, 13);
+        s.k = (int32_t)rl(10);
+        s.t = (int32_t)rl(11);
+        s.mode = (int32_t)rl(12);
+        s.ntab = (int32_t)rl(13);
         if (!ok) s.mode = 2;
       }
-      if (tr && lane == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
-      if (lane == 0) {
+      // (stamps held in registers and stored together after the publish: a store here
+      // would put its own completion wait inside the resolve)
+      const uint64_t t_seen = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+      const bool w0 = lane == 0;
+      {
+        // Wave-uniform scalar code: every value read back through readfirstlane, so the
+        // loop branches on SCC; status bits gathered in `bad` and raised once.
         const uint64_t Wend = W0 + kWBytes;
-        // this message's record-offset range (psx_runtime.cpp sizes it size / 8 + 1)
-        const uint64_t rk_lo = ss.recoff_base[b], rk_hi = rk_lo + size / 8 + 1;
-        uint32_t nseg = 0;
+        uint32_t nseg = 0, bad = 0;
         Seg *segs_b = segs + b * kMaxTables;
-        for (;;) {
+        // Fast path (almost every window of a large sparse table): the table's records
+        // continue past this window — one exit-map lookup, the last record's count, done.
+        // Anything else (a table or the message ending here, a header, a bad state) takes
+        // the general loop below from the unchanged state.
+        bool done = false;
+        if (s.mode == 1 && !last && s.pos >= W0 && s.pos - W0 < (uint64_t)nw * 4 && s.rk >= rk_lo &&
+            s.rk + s.left <= rk_hi) {
+          const uint32_t q = (uint32_t)((s.pos - W0) / 4);
+          const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)xf[q]);
+          const uint32_t T = x & 0xFFFFu;
+          const uint64_t c = (uint64_t)(x >> 16) + 1;
+          if (s.left > c && T + 1 < nw) {
+            const uint32_t cT = (uint32_t)__builtin_amdgcn_readfirstlane((int)n16[T]);
+            if (cT < kNBig) {
+              const uint64_t endT = W0 + ((uint64_t)T + 2 + (uint64_t)cT * spec_wpr) * 4;
+              if (endT >= Wend && endT <= size) {
+                if (w0) {
+                  seg_q[0] = (uint16_t)q;
+                  seg_n[0] = (uint16_t)c;
+                  seg_rk[0] = s.rk;
+                }
+                nseg = 1;
+                s.rk += c;
+                s.kk += c;
+                s.left -= c;
+                s.pos = endT;
+                done = true;
+              }
+            }
+          }
+        }
+        for (; !done;) {
           if (s.mode == 2) break;
           if (s.mode == 1 && (s.pos < W0 || s.rk < rk_lo || s.rk + s.left > rk_hi)) {
             // a state no walk of this message can reach: never expand from it
-            atomicOr(call_status, kStWalkBound);
+            bad |= kStWalkBound;
             s.mode = 2;
             break;
           }
           if (s.pos >= Wend && !last) break;          // the walk continues in a later window
           if (s.mode == 0) {
-            walk_header(p, size, dir, segs_b, s, call_status);
+            walk_header(p, size, dir, segs_b, s, call_status, w0);
             continue;
           }
           // sparse records from s.pos: one exit-map lookup
-          const uint64_t q = (s.pos - W0) / 4;
-          if (q >= nw) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }   // header past the end
-          const uint32_t T = xm[q] & 0xFFFFu;
-          const uint64_t c = (uint64_t)(xm[q] >> 16) + 1;                           // records q .. T
+          const uint32_t q = (uint32_t)((s.pos - W0) / 4);
+          if (s.pos - W0 >= (uint64_t)nw * 4) { bad |= kStMalformed; s.mode = 2; break; }   // header past the end
+          const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)xf[q]);
+          const uint32_t T = x & 0xFFFFu;
+          const uint64_t c = (uint64_t)(x >> 16) + 1;                                // records q .. T
           const uint64_t take = s.left < c ? s.left : c;
           uint64_t endT = 0;
           if (take == c) {
             // the table holds T's record (before T every link is a checked jump-table link;
             // past the table's end the speculative chain may be garbage): its header inside
             // the message, n >= 0, its end inside the message
-            if (T + 1 > nw || (T + 1 == nw && !halo)) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
-            const uint16_t cT = n16[T];
-            if (cT == kNNeg || cT == kNNone) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
-            const int32_t nT = cT == kNBig ? *reinterpret_cast<const int32_t *>(p + W0 + ((uint64_t)T + 1) * 4) : (int32_t)cT;
+            if (T + 1 > nw || (T + 1 == nw && !halo)) { bad |= kStMalformed; s.mode = 2; break; }
+            const uint32_t cT = (uint32_t)__builtin_amdgcn_readfirstlane((int)n16[T]);
+            if (cT == kNNeg || cT == kNNone) { bad |= kStMalformed; s.mode = 2; break; }
+            const int32_t nT = cT == kNBig ? __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t *>(p + W0 + ((uint64_t)T + 1) * 4))
+                                           : (int32_t)cT;
             endT = W0 + ((uint64_t)T + 2 + (uint64_t)nT * spec_wpr) * 4;
-            if (endT > size) { atomicOr(call_status, kStMalformed); s.mode = 2; break; }
+            if (endT > size) { bad |= kStMalformed; s.mode = 2; break; }
           }
-          seg_q[nseg] = (uint16_t)q;
-          seg_n[nseg] = (uint16_t)take;
-          seg_rk[nseg] = s.rk;
+          if (w0) {
+            seg_q[nseg] = (uint16_t)q;
+            seg_n[nseg] = (uint16_t)take;
+            seg_rk[nseg] = s.rk;
+          }
           ++nseg;
           s.rk += take;
           s.kk += take;
@@ -404,11 +461,13 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           if (take == c) {
             s.pos = endT;
           } else {
-            // the table ends inside the chain: the record `take` on from q (binary lifting)
-            // (every link before it is a checked in-window link: n16 holds its exact n)
-            uint32_t w = (uint32_t)q;
+            // the table ends inside the chain: the record `take` on from q — 16 records a
+            // step on jt4, then single records (every link before it is a checked
+            // in-window link: n16 holds its exact n)
+            uint32_t w = q;
             uint64_t r = take;
-            for (; r; --r) w = w + 2 + (uint32_t)n16[w] * spec_wpr;   // once per table: its last window
+            for (; r >= 16; r -= 16) w = (uint32_t)__builtin_amdgcn_readfirstlane((int)jt4[w]);
+            for (; r; --r) w = w + 2 + (uint32_t)__builtin_amdgcn_readfirstlane((int)n16[w]) * spec_wpr;
             s.pos = W0 + (uint64_t)w * 4;
           }
           if (s.left == 0) {
@@ -416,76 +475,60 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
             s.mode = 0;
           }
         }
-        sh_nseg = nseg;
+        if (bad && w0) atomicOr(call_status, bad);
+        if (w0) sh_nseg = nseg;
       }
-      // lane i publishes granule i of lane 0's state
+      // lane i publishes granule i of the (wave-uniform) state
+      // lane i's granule: a select chain over the wave-uniform state (no divergent switch)
       uint32_t mine = 0;
 #pragma unroll
-      for (int i = 0; i < kGran; ++i) {
-        const uint32_t w = (uint32_t)__shfl((int)gran_value(s, i), 0);
-        if (lane == i) mine = w;
-      }
+      for (int i = 0; i < kGran; ++i) mine = lane == i ? gran_value(s, i) : mine;
       if (!last && lane < kGran) {
         gu64 *g = gran + (uint64_t)tk * kGran;
         __hip_atomic_store(g + lane, ((uint64_t)epoch << 32) | (uint64_t)mine, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (tr && lane == 0) tr[4] = __builtin_amdgcn_s_memrealtime();
-    }
-    __syncthreads();
-    // 5) expand the window's record offsets: the 16-record jump table by four squarings
-    //    (into the exit map's words, no longer needed), thread 0 collects hop starts, all
-    //    threads fill
-    const uint32_t nseg = sh_nseg;
-    if (nseg) {
-      // the next-record table from n16, in place (the exit map is no longer needed)
-      for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) jt0[q] = next_of(q, n16[q], nw, W0, size, spec_wpr);
-      __syncthreads();
-      const uint16_t *src[4] = {jt0, tmp16, jt4, tmp16};
-      uint16_t *dst[4] = {tmp16, jt4, tmp16, jt4};
-#pragma unroll
-      for (int lv = 0; lv < 4; ++lv) {
-        uint16_t r[kWW / kWalkThreads];
-#pragma unroll
-        for (int k = 0; k < kWW / kWalkThreads; ++k) {
-          const uint16_t a = src[lv][tid + k * kWalkThreads];
-          r[k] = a != kNo ? src[lv][a] : kNo;
+      if (tr) {
+        const uint64_t t_pub = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+          tr[3] = t_seen;
+          tr[4] = t_pub;
         }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kWW / kWalkThreads; ++k) dst[lv][tid + k * kWalkThreads] = r[k];
-        __syncthreads();
       }
     }
+    __syncthreads();
+    // 5) expand the window's record offsets: thread 0 collects the 16-record hop starts,
+    //    all threads fill
+    const uint32_t nseg = sh_nseg;
     for (uint32_t si = 0; si < nseg; ++si) {
       if (tid == 0) {
         uint32_t w = seg_q[si];
         uint32_t rem = seg_n[si];
-        uint32_t n16 = 0, n1 = 0;
+        uint32_t nh = 0, n1 = 0;
         while (rem >= 16) {
-          a16[n16++] = (uint16_t)w;
+          a16[nh++] = (uint16_t)w;
           rem -= 16;
           if (rem) w = jt4[w];
         }
         while (rem) {
           a1[n1++] = (uint16_t)w;
-          if (--rem) w = jt0[w];
+          if (--rem) w = next_of(w, n16[w], nw, W0, size, spec_wpr);
         }
-        sh_n16 = n16;
+        sh_n16 = nh;
         sh_n1 = n1;
       }
       __syncthreads();
-      const uint32_t n16 = sh_n16, n1 = sh_n1;
+      const uint32_t nh = sh_n16, n1 = sh_n1;
       const uint64_t rk = seg_rk[si];
-      for (uint32_t i = tid; i < n16; i += kWalkThreads) {   // one thread per 16-record hop
+      for (uint32_t i = tid; i < nh; i += kWalkThreads) {   // one thread per 16-record hop
         uint32_t q = a16[i];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           recoff[rk + 16 * (uint64_t)i + k] = W0 + (uint64_t)q * 4;
-          if (k < 15) q = jt0[q];
+          if (k < 15) q = next_of(q, n16[q], nw, W0, size, spec_wpr);
         }
       }
-      const uint64_t r1 = rk + 16 * (uint64_t)n16;
+      const uint64_t r1 = rk + 16 * (uint64_t)nh;
       if (tid < n1) recoff[r1 + tid] = W0 + (uint64_t)a1[tid] * 4;
       __syncthreads();
     }
@@ -493,7 +536,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
   }
 }
 
-// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 96 KiB window count);
+// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 48 KiB window count);
 // epoch: nonzero, different from the previous call's on this workspace (granule tags);
 // trace_items: nonzero = write the per-item timestamps (the workspace's item count).
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,

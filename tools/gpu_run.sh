@@ -11,8 +11,10 @@
 #   pmc     three PMC passes on the C2 bench (request counts, FETCH_SIZE, WRITE_SIZE),
 #           summarised with the kernel signature into $O/pmc_dense_apply.json
 #   c3split C3 with each split-apply form (PSX_ORD_SPLIT 1, 2, 3), twice, interleaved
+#   c3walk  C3 with the walk on half / all CUs (PSX_WALK_CUS 0, 1), twice, interleaved
 #   c3 | c3idx | c4 | c5 | ada | f16 | d125 | imp   the other workloads' bench lines
 #   probe   tools/probe_ceiling (the C2 access pattern's hardware ceiling; build it first)
+#   mixab   the mixing probe and the C2 apply A/B interleaved, three times (same box)
 #   wtrace  tools/walk_trace.py: per-window timeline of the walk on the C3 batches
 #   pmix    tools/probe_apply's mixing probe (records in random vs slot order; build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
@@ -73,6 +75,9 @@ for s in "$@"; do
           run c3ab_off2 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 ;;
     c3split) i=0; for v in 1 2 3 1 2 3; do i=$((i+1)); run c3split_${i}_v$v 300 env PSX_ORD_SPLIT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
              grep -h '^{' $O/c3split_*.log | cut -c1-400 ;;
+    c3walk) i=0; for v in 0 1 0 1; do i=$((i+1)); run c3walk_${i}_cus$v 300 env PSX_WALK_CUS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+            for f in $O/c3walk_*.log; do echo "$f $(grep -h '^{' $f | cut -c1-120)"; done ;;
+    wtrace1) run wtrace1 200 env PSX_WALK_CUS=1 python -u tools/walk_trace.py && head -c 1500 "$O/wtrace1.log" ;;
     c2only) run c2only 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras ;;
     c3) run c3 300 python -u bench.py --workload c3 --steps 20 --warmup 3 ;;
     c3idx) run c3idx 300 python -u bench.py --workload c3 --indexed --steps 20 --warmup 3 ;;
@@ -89,6 +94,8 @@ for s in "$@"; do
     abzeros) run abzeros 400 python -u tools/ab_c2.py --zeros --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -30 "$O/abzeros.log" ;;
     walktests) run walktests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dense_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py ;;
+    mixab) for i in 1 2 3; do run pmix_$i 300 tools/probe_apply 10 1 && run abdense_$i 400 python -u tools/ab_c2.py --configs 0:1:1,0:0:1 --rounds 3 --steps 5 || exit 1; done
+           grep -h '"probe"' $O/pmix_*.log | head -3; grep -h -A2 '"apply0' $O/abdense_*.log | grep dense_apply ;;
     wtrace) run wtrace 200 python -u tools/walk_trace.py && head -c 3000 "$O/wtrace.log" ;;
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;

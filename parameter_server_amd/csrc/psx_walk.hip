@@ -189,6 +189,33 @@ __device__ __forceinline__ uint16_t next_of(uint32_t q, uint16_t c, uint32_t nw,
   return nxt < nw && W0 + nxt * 4 <= size ? (uint16_t)nxt : kNo;
 }
 
+constexpr int kCand = 1024;   // entry candidates per window (== kWalkThreads)
+
+// The exit map entry of word q: the last record start on q's chain inside the window and
+// the records from q up to it, packed (16 | 16 bits): 16 records a step on jt4, then
+// single records.
+__device__ __forceinline__ uint32_t exit_walk(uint32_t q, const uint16_t *jt4, const uint16_t *n16, uint32_t nw,
+                                              uint64_t W0, uint64_t size, uint32_t spec_wpr) {
+  uint32_t w = q, cnt = 0;
+  for (uint16_t j = jt4[w]; j != kNo; j = jt4[w]) {
+    w = j;
+    cnt += 16;
+  }
+  for (uint16_t j = next_of(w, n16[w], nw, W0, size, spec_wpr); j != kNo; j = next_of(w, n16[w], nw, W0, size, spec_wpr)) {
+    w = j;
+    cnt += 1;
+  }
+  return w | (cnt << 16);
+}
+
+// The resolve's (wave-uniform) lookup: the candidates' table, or the walk itself for a
+// later entry.
+__device__ __forceinline__ uint32_t exit_at(uint32_t q, const uint32_t *xc, const uint16_t *jt4, const uint16_t *n16,
+                                            uint32_t nw, uint64_t W0, uint64_t size, uint32_t spec_wpr) {
+  if (q < (uint32_t)kCand) return (uint32_t)__builtin_amdgcn_readfirstlane((int)xc[q]);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)exit_walk(q, jt4, n16, nw, W0, size, spec_wpr));
+}
+
 __device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
   switch (i) {
     case 0: return (uint32_t)s.pos;
@@ -213,16 +240,17 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace) {
   gu64 *gran = (gu64 *)gran_p;
-  // 48 KiB windows in 144 KiB of LDS, everything but the hand-off done before it: xm first
-  // holds the window's words, then with xm2 the pointer-jumping rounds of the exit map
-  // (packed: low 16 bits the last record start on q's chain inside the window, high 16 the
-  // records from q up to it, exclusive); n16 keeps the clipped record count after each
-  // word (the resolve's one read of the words; single-record steps are computed from it,
-  // next_of); jt4, the 16-record jump table, falls out of the fourth round.
+  // 48 KiB windows in 148 KiB of LDS, everything but the hand-off done before it: xm first
+  // holds the window's words, then with xm2 the pointer-jumping rounds that build jt4, the
+  // 16-record jump table; n16 keeps the clipped record count after each word (the
+  // resolve's one read of the words; single-record steps are computed from it, next_of);
+  // xc is the exit map of the entry candidates (packed: low 16 bits the last record start
+  // on q's chain inside the window, high 16 the records from q up to it, exclusive).
   __shared__ uint32_t xm[kWW];
   __shared__ uint32_t xm2[kWW];
   __shared__ uint16_t n16[kWW];
   __shared__ uint16_t jt4[kWW];
+  __shared__ uint32_t xc[kCand];   // exit map of the first kCand words (the entry candidates)
   uint32_t *const win = xm;
   __shared__ uint32_t sh_halo;
   __shared__ uint16_t seg_q[kMaxSegs];
@@ -289,35 +317,31 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       xm[q] = v == kNo ? q : ((uint32_t)v | (1u << 16));
     }
     __syncthreads();
-    // 3) exit map by pointer jumping (terminal records point to themselves with count 0):
-    //    one packed LDS word per lookup, rounds ping-ponging between xm and xm2 (one
-    //    barrier per round).  After round r every word holds the node min(2^(r+1), to
-    //    the terminal) records on, so round 3's result is also the 16-record jump table
-    //    (its count is 16 exactly where 16 records follow inside the window).
-    uint32_t *xf = xm;
-    for (int r = 0;; ++r) {
+    // 3) the 16-record jump table by four pointer-jumping rounds (terminal records point to
+    //    themselves with count 0; one packed LDS word per lookup, rounds ping-ponging
+    //    between xm and xm2, one barrier each): after round r every word holds the node
+    //    min(2^(r+1), to the terminal) records on, so round 3's count is 16 exactly where
+    //    16 records follow inside the window.
+    for (int r = 0; r < 4; ++r) {
       constexpr int PER = kWW / kWalkThreads;
       const uint32_t *src = (r & 1) ? xm2 : xm;
       uint32_t *dst = (r & 1) ? xm : xm2;
-      bool changed = false;
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
         const uint32_t v = src[q];
         const uint32_t t = src[v & 0xFFFFu];
         const uint32_t nv = (t & 0xFFFFu) | (((v >> 16) + (t >> 16)) << 16);
-        dst[q] = nv;
-        if (r == 3) jt4[q] = (nv >> 16) == 16 ? (uint16_t)(nv & 0xFFFFu) : kNo;
-        changed |= (t & 0xFFFFu) != (v & 0xFFFFu);
+        if (r < 3) dst[q] = nv;
+        else jt4[q] = (nv >> 16) == 16 ? (uint16_t)(nv & 0xFFFFu) : kNo;
       }
-      xf = dst;
-      if (!__syncthreads_or(changed)) {
-        // fewer than four rounds: no chain holds 16 records, the jump table is empty
-        if (r < 3)
-          for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) jt4[q] = kNo;
-        break;
-      }
+      __syncthreads();
     }
+    //    The exit map for the window's first kCand words only — the chain enters a window
+    //    inside the record that crosses its start, so in practice within its first few
+    //    hundred bytes (a later entry, a record longer than kCand words, is walked by the
+    //    resolve itself): thread q walks q's chain, 16 records a step, then single ones.
+    if ((uint32_t)tid < (uint32_t)kCand) xc[tid] = exit_walk((uint32_t)tid, jt4, n16, nw, W0, size, spec_wpr);
     __syncthreads();
     if (tr && tid == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
     // 4) wave 0: wait for the predecessor's state, resolve this window (every lane on the
@@ -393,7 +417,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         if (s.mode == 1 && !last && s.pos >= W0 && s.pos - W0 < (uint64_t)nw * 4 && s.rk >= rk_lo &&
             s.rk + s.left <= rk_hi) {
           const uint32_t q = (uint32_t)((s.pos - W0) / 4);
-          const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)xf[q]);
+          const uint32_t x = exit_at(q, xc, jt4, n16, nw, W0, size, spec_wpr);
           const uint32_t T = x & 0xFFFFu;
           const uint64_t c = (uint64_t)(x >> 16) + 1;
           if (s.left > c && T + 1 < nw) {
@@ -432,7 +456,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           // sparse records from s.pos: one exit-map lookup
           const uint32_t q = (uint32_t)((s.pos - W0) / 4);
           if (s.pos - W0 >= (uint64_t)nw * 4) { bad |= kStMalformed; s.mode = 2; break; }   // header past the end
-          const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)xf[q]);
+          const uint32_t x = exit_at(q, xc, jt4, n16, nw, W0, size, spec_wpr);
           const uint32_t T = x & 0xFFFFu;
           const uint64_t c = (uint64_t)(x >> 16) + 1;                                // records q .. T
           const uint64_t take = s.left < c ? s.left : c;

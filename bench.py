@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-PMC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_dense_apply.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "r03", "pmc_dense_apply.json")
 
 
 def kernel_signature():

@@ -37,6 +37,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+EXCHANGE_TIMEOUT_S = 180   # N > 1: the exchange extra is abandoned (headline kept) past this
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 PMC_JSON = os.path.join(ROOT, "profiles", "r03", "pmc_dense_apply.json")
 
@@ -1095,56 +1096,8 @@ def main():
     elif c2_dims:
         traffic_note = "no PMC JSON for this tree"
 
-    # The driver runs the bare `python bench.py [--gpus N]`: on the plain C2 configuration
-    # the same run also records, beside `value`, the PCIe-inclusive rate and C3 (N = 1), or
-    # the exchange-bearing step over xGMI (N > 1).  None of it is inside the timed region.
-    extras = args.extras and c2_dims and not args.adarevision and not args.walked
-    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie or (extras and world == 1) else None
-    srv.close()
-    del streams, record_rows
-    torch.cuda.empty_cache()
-    other, exchange = None, None
-    if extras and world > 1:
-        try:
-            exchange = exchange_measure(world * rows, cap, min(args.steps, 10), 2, world, rank, local)
-            exchange["what"] = ("a worker batch spanning every shard: per-owner sub-streams of each rank's full-coverage "
-                                "batch, one RCCL all-to-all over xGMI, then the owner's fused apply of the N messages "
-                                "in source-rank order (C4's step at C2's row width)")
-        except Exception as e:   # reported, never allowed to drop the headline line
-            exchange = {"error": repr(e)[:400]}
-    if extras and world == 1:
-        # C3 in child processes (`bench.py --workload c3`), so its device memory and state
-        # start fresh rather than where C2 and the PCIe pass left them (a C3 run right after
-        # them in this process measured its apply 3x slower)
-        other = {}
-        cs = str(min(args.cpu_seconds, 6.0))
-        for name, flags in (("C3_walked", ["--cpu-seconds", cs]),
-                            ("C3_indexed", ["--indexed", "--cpu-seconds", "0"])):
-            try:
-                m = run_child(["--workload", "c3", "--steps", "20", "--warmup", "3"] + flags)
-                other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "decode",
-                                                     "ordered_apply_ms_per_step",
-                                                     "kernel_ms_per_step_breakdown_pass", "cpu_baseline",
-                                                     "pipelined")}
-                other[name]["config"] = m["config"]["workload"]
-                lm = m.get("latency_model") or {}
-                other[name]["ordered_apply_frac_of_latency_bound"] = lm.get("frac_of_bound")
-            except Exception as e:
-                other[name] = {"error": repr(e)[:400]}
-        for name, flags in (("C4_shard_1gpu", ["--workload", "c4shard", "--steps", "5", "--warmup", "2",
-                                               "--cpu-seconds", cs]),
-                            ("C5", ["--workload", "c5", "--steps", "10", "--warmup", "2", "--cpu-seconds", cs])):
-            try:
-                m = run_child(flags, timeout=400)
-                m.pop("metric", None)
-                other[name] = m
-            except Exception as e:
-                other[name] = {"error": repr(e)[:400]}
-    if rank == 0:
-        cpu = None
-        if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(args)
-        line = {
+    def build_line(cpu):
+        return {
             "metric": "row-update apply GB/s (device-resident), dense float rows"
                       + (", float16 records" if args.f16_records else "")
                       + (", AdaRevision server logic" if args.adarevision else ""),
@@ -1192,6 +1145,76 @@ def main():
             "kernel_ms_per_launch_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},
             "cpu_baseline": cpu,
         }
+
+    # The driver runs the bare `python bench.py [--gpus N]`: on the plain C2 configuration
+    # the same run also records, beside `value`, the PCIe-inclusive rate and C3 (N = 1), or
+    # the exchange-bearing step over xGMI (N > 1).  None of it is inside the timed region.
+    extras = args.extras and c2_dims and not args.adarevision and not args.walked
+    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie or (extras and world == 1) else None
+    srv.close()
+    del streams, record_rows
+    torch.cuda.empty_cache()
+    other, exchange = None, None
+    if extras and world > 1:
+        # The exchange extra must never cost the headline: if it has not finished within
+        # EXCHANGE_TIMEOUT_S (a collective that never completes, say), rank 0 prints the
+        # line without it and every rank leaves.
+        import threading
+        done = threading.Event()
+
+        def watchdog():
+            if done.wait(EXCHANGE_TIMEOUT_S):
+                return
+            if rank == 0:
+                ln = build_line(None)
+                if walked:
+                    ln["walked"] = walked
+                ln["exchange"] = {"error": f"not finished within {EXCHANGE_TIMEOUT_S} s: abandoned"}
+                print(json.dumps(ln), flush=True)
+            sys.stdout.flush()
+            os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            exchange = exchange_measure(world * rows, cap, min(args.steps, 10), 2, world, rank, local)
+            exchange["what"] = ("a worker batch spanning every shard: per-owner sub-streams of each rank's full-coverage "
+                                "batch, one RCCL all-to-all over xGMI, then the owner's fused apply of the N messages "
+                                "in source-rank order (C4's step at C2's row width)")
+        except Exception as e:   # reported, never allowed to drop the headline line
+            exchange = {"error": repr(e)[:400]}
+        done.set()
+    if extras and world == 1:
+        # C3 in child processes (`bench.py --workload c3`), so its device memory and state
+        # start fresh rather than where C2 and the PCIe pass left them (a C3 run right after
+        # them in this process measured its apply 3x slower)
+        other = {}
+        cs = str(min(args.cpu_seconds, 6.0))
+        for name, flags in (("C3_walked", ["--cpu-seconds", cs]),
+                            ("C3_indexed", ["--indexed", "--cpu-seconds", "0"])):
+            try:
+                m = run_child(["--workload", "c3", "--steps", "20", "--warmup", "3"] + flags)
+                other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "decode",
+                                                     "ordered_apply_ms_per_step",
+                                                     "kernel_ms_per_step_breakdown_pass", "cpu_baseline",
+                                                     "pipelined")}
+                other[name]["config"] = m["config"]["workload"]
+                lm = m.get("latency_model") or {}
+                other[name]["ordered_apply_frac_of_latency_bound"] = lm.get("frac_of_bound")
+            except Exception as e:
+                other[name] = {"error": repr(e)[:400]}
+        for name, flags in (("C4_shard_1gpu", ["--workload", "c4shard", "--steps", "5", "--warmup", "2",
+                                               "--cpu-seconds", cs]),
+                            ("C5", ["--workload", "c5", "--steps", "10", "--warmup", "2", "--cpu-seconds", cs])):
+            try:
+                m = run_child(flags, timeout=400)
+                m.pop("metric", None)
+                other[name] = m
+            except Exception as e:
+                other[name] = {"error": repr(e)[:400]}
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(args)
+        line = build_line(cpu)
         if walked:
             line["walked"] = walked
         if pcie:

@@ -444,7 +444,7 @@ bool has_sparse_serialized(const psx_ctx *c) {
 // keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
 // work takes ~15-20 us); the other half of the chip stays free for the previous call's
 // apply when the decode is pipelined (psx_ctx_set_pipeline).
-constexpr uint64_t kWalkWindowBytes = 49152;   // == psx_walk.hip kWBytes
+constexpr uint64_t kWalkWindowBytes = 98304;   // == psx_walk.hip kWBytes
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
 unsigned walk_blocks(psx_ctx *c) {

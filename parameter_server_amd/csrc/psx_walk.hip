@@ -3,7 +3,7 @@
 // The record chain of a sparse table (SerializedOpLogReader::Next,
 // src/petuum_ps/server/serialized_oplog_reader.hpp:50-85: each record's size comes from its
 // own n, so record k+1 starts where record k ends) is sequential.  decode_streams walks it
-// with one workgroup per message, one 32 KiB window after another.  Here every 48 KiB window of
+// with one workgroup per message, one 32 KiB window after another.  Here every 96 KiB window of
 // every message is its own work item, and the work that does not depend on where the chain
 // enters the window runs in parallel, before the chain arrives:
 //
@@ -33,7 +33,7 @@
 namespace psx {
 
 constexpr int kWalkThreads = 1024;
-constexpr int kWW = 12288;                      // words per window (48 KiB)
+constexpr int kWW = 24576;                      // words per window (96 KiB)
 constexpr uint64_t kWBytes = (uint64_t)kWW * 4;
 constexpr uint16_t kNo = 0xFFFFu;               // next record outside the window / bad header
 // n16: the record count word after q (q's n as a record start), clipped to 16 bits
@@ -64,7 +64,7 @@ struct WalkCtl {      // reset by walk_head for the walk of the same call
 
 struct WalkHead {     // written by walk_head, read by the first window of each message
   WalkState st[kMaxFused];
-  uint32_t wfirst[kMaxFused];   // the message's first window (48 KiB grid from byte 0)
+  uint32_t wfirst[kMaxFused];   // the message's first window (96 KiB grid from byte 0)
   uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
 };
 constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
@@ -240,18 +240,20 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace) {
   gu64 *gran = (gu64 *)gran_p;
-  // 48 KiB windows in 148 KiB of LDS, everything but the hand-off done before it: xm first
-  // holds the window's words, then with xm2 the pointer-jumping rounds that build jt4, the
-  // 16-record jump table; n16 keeps the clipped record count after each word (the
-  // resolve's one read of the words; single-record steps are computed from it, next_of);
-  // xc is the exit map of the entry candidates (packed: low 16 bits the last record start
-  // on q's chain inside the window, high 16 the records from q up to it, exclusive).
-  __shared__ uint32_t xm[kWW];
-  __shared__ uint32_t xm2[kWW];
+  // 96 KiB windows in 150 KiB of LDS, everything but the hand-off done before it.  wbuf
+  // first holds the window's words; n16 keeps the clipped record count after each word
+  // (the resolve's one read of the words; single-record steps are computed from it,
+  // next_of); then wbuf's two halves (sa, sb) take the 16-bit squarings of the next-record
+  // link — 2, 4, 8, 16 records — and sb ends as jt4, the 16-record jump table; xc is the
+  // exit map of the entry candidates (packed: low 16 bits the last record start on q's
+  // chain inside the window, high 16 the records from q up to it, exclusive).
+  __shared__ uint32_t wbuf[kWW];
   __shared__ uint16_t n16[kWW];
-  __shared__ uint16_t jt4[kWW];
   __shared__ uint32_t xc[kCand];   // exit map of the first kCand words (the entry candidates)
-  uint32_t *const win = xm;
+  uint32_t *const win = wbuf;
+  uint16_t *const sa = reinterpret_cast<uint16_t *>(wbuf);
+  uint16_t *const sb = sa + kWW;
+  uint16_t *const jt4 = sb;
   __shared__ uint32_t sh_halo;
   __shared__ uint16_t seg_q[kMaxSegs];
   __shared__ uint16_t seg_n[kMaxSegs];
@@ -288,21 +290,23 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     // 1) the window (and its halo word) into LDS
     {
       const uint32_t *src = reinterpret_cast<const uint32_t *>(p + W0);
-      constexpr int PER = kWW / kWalkThreads;
-      uint32_t r[PER];
+      constexpr int PER = 12;   // loads in flight per thread (two passes over 96 KiB)
 #pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const uint32_t i = (uint32_t)tid + (uint32_t)k * kWalkThreads;
-        r[k] = i < nw ? src[i] : 0u;
+      for (int h = 0; h < kWW / (PER * kWalkThreads); ++h) {
+        uint32_t r[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          const uint32_t i = (uint32_t)tid + (uint32_t)(h * PER + k) * kWalkThreads;
+          r[k] = i < nw ? src[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) win[tid + (h * PER + k) * kWalkThreads] = r[k];
       }
-#pragma unroll
-      for (int k = 0; k < PER; ++k) win[tid + k * kWalkThreads] = r[k];
       if (tid == 0) sh_halo = halo ? src[nw] : 0u;
     }
     __syncthreads();
     if (tr && tid == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
-    // 2) every word a speculative record start: n16 from the words, then the exit map's
-    //    first link (next = q + 2 + n * wpr) from n16, over the words (xm aliases them)
+    // 2) every word a speculative record start: n16 from the words
     for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
       uint16_t c = kNNone;
       if (q + 1 < nw || (q + 1 == nw && halo)) {
@@ -312,30 +316,29 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       n16[q] = c;
     }
     __syncthreads();
-    for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
-      const uint16_t v = next_of(q, n16[q], nw, W0, size, spec_wpr);
-      xm[q] = v == kNo ? q : ((uint32_t)v | (1u << 16));
-    }
-    __syncthreads();
-    // 3) the 16-record jump table by four pointer-jumping rounds (terminal records point to
-    //    themselves with count 0; one packed LDS word per lookup, rounds ping-ponging
-    //    between xm and xm2, one barrier each): after round r every word holds the node
-    //    min(2^(r+1), to the terminal) records on, so round 3's count is 16 exactly where
-    //    16 records follow inside the window.
-    for (int r = 0; r < 4; ++r) {
+    // 3) the 16-record jump table by four squarings of the next-record link in 16 bits,
+    //    one barrier each (the words are no longer needed: sa and sb are their buffer)
+    {
       constexpr int PER = kWW / kWalkThreads;
-      const uint32_t *src = (r & 1) ? xm2 : xm;
-      uint32_t *dst = (r & 1) ? xm : xm2;
 #pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
-        const uint32_t v = src[q];
-        const uint32_t t = src[v & 0xFFFFu];
-        const uint32_t nv = (t & 0xFFFFu) | (((v >> 16) + (t >> 16)) << 16);
-        if (r < 3) dst[q] = nv;
-        else jt4[q] = (nv >> 16) == 16 ? (uint16_t)(nv & 0xFFFFu) : kNo;
+      for (int lv = 0; lv < 4; ++lv) {
+        const uint16_t *src = (lv & 1) ? sa : sb;   // lv 0 reads n16, not sb
+        uint16_t *dst = (lv & 1) ? sb : sa;
+#pragma unroll 8
+        for (int k = 0; k < PER; ++k) {
+          const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
+          uint16_t r;
+          if (lv == 0) {
+            const uint16_t a = next_of(q, n16[q], nw, W0, size, spec_wpr);
+            r = a != kNo ? next_of(a, n16[a], nw, W0, size, spec_wpr) : kNo;
+          } else {
+            const uint16_t a = src[q];
+            r = a != kNo ? src[a] : kNo;
+          }
+          dst[q] = r;
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
     //    The exit map for the window's first kCand words only — the chain enters a window
     //    inside the record that crosses its start, so in practice within its first few
@@ -560,7 +563,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
   }
 }
 
-// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 48 KiB window count);
+// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 96 KiB window count);
 // epoch: nonzero, different from the previous call's on this workspace (granule tags);
 // trace_items: nonzero = write the per-item timestamps (the workspace's item count).
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,

@@ -92,6 +92,7 @@ for s in "$@"; do
     abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
     abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
     abzeros) run abzeros 400 python -u tools/ab_c2.py --zeros --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -30 "$O/abzeros.log" ;;
+    mrtest) run mrtest 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_multi_rank_gpu.py tests/test_split_gpu.py ;;
     walktests) run walktests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dense_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py ;;
     mixab) for i in 1 2 3; do run pmix_$i 300 tools/probe_apply 10 1 && run abdense_$i 400 python -u tools/ab_c2.py --configs 0:1:1,0:0:1 --rounds 3 --steps 5 || exit 1; done

@@ -177,7 +177,7 @@ struct OrdArgs {
                           // can add per slot (zero between calls); null otherwise
   int32_t *split;         // [2][max_rows] row descriptors {slot, list begin, list end, image
                           // size} (int4): touched slots whose image fits 256 entries, the rest
-  uint32_t *nsplit;       // the lists' lengths: 256-entry, 1,024-entry, heavy
+  uint32_t *nsplit;       // the lists' lengths: 256-entry, 1,024-entry, heavy, capacity dry run
   int32_t desc;           // 1: `touched` holds split-list row descriptors (the apply launches)
   int32_t spill;          // split tables, spill mode: ordered_offsets sends only rows already
                           // near 256 entries to the 1,024-entry list; the 256-entry launch

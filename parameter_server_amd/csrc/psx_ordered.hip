@@ -113,8 +113,8 @@ __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   __shared__ RecSpace rs;
-  if (a.grow && blockIdx.x == 0 && threadIdx.x < 4) {   // ordered_offsets' counters
-    if (threadIdx.x < 3) a.nsplit[threadIdx.x] = 0;
+  if (a.grow && blockIdx.x == 0 && threadIdx.x < 5) {   // ordered_offsets' counters
+    if (threadIdx.x < 4) a.nsplit[threadIdx.x] = 0;
     else a.tsum[0] = 0;
   }
   // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
@@ -143,9 +143,11 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
         if (!a.dense_records && a.kind == 0) {
           // sparse record into a dense row: every column must lie inside the row
           if (cols_outside(p, a.row_cap)) atomicOr(a.call_status, kStCapacity);
-        } else if (a.kind != 0 && a.keyflag && !*a.keyflag) {
+        } else if (a.kind != 0 && a.keyflag && !*a.keyflag && !a.grow) {
           // sorted/map rows: while every key stays in [0, max_entries) no row can hold
-          // more than max_entries entries and the capacity dry run is skipped
+          // more than max_entries entries and the capacity dry run is skipped (split
+          // tables bound each row by its Incs instead, ordered_offsets, and check the
+          // key map's columns in the apply: no column scan here)
           if (cols_outside(p, a.max_entries)) atomicOr(a.keyflag, 1u);
         }
         if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
@@ -242,79 +244,92 @@ __device__ __forceinline__ bool starts_heavy(const OrdArgs &a, int32_t c) {
   return (a.spill & 2) && c >= kHeavyRecords;
 }
 
+// The capacity dry run's rows: those whose image can outgrow max_entries in this call
+// (entries now + the call's Incs).  Any other row cannot overflow, whatever its keys.
+__device__ __forceinline__ bool may_overflow(const OrdArgs &a, int32_t nen, int32_t grow) {
+  return (int64_t)nen + grow > a.max_entries;
+}
+
 __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
-  __shared__ int32_t sh[5][4];
-  __shared__ int32_t base[5];   // touched, records, 256-entry list, 1,024-entry list, heavy rows
+  __shared__ int32_t sh[6][4];
+  __shared__ int32_t base[6];   // touched, records, 256-entry list, 1,024-entry list, heavy rows, dry run
   if (!o_gate(a)) return;
   const int64_t R = a.max_rows;
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * per;
   const int64_t c1 = c0 + per < R ? c0 + per : R;
   // pass 1: the block's totals, one atomic per counter
-  int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0;
+  int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0, nd = 0;
   for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
     const int32_t c = a.cnt[s];
     if (c > 0) {
       ++nt;
       nr += c;
-      if (starts_big(a, a.nent[s], a.grow[s])) ++nb;
+      const int32_t nen = a.nent[s], g = a.grow[s];
+      if (starts_big(a, nen, g)) ++nb;
       else if (starts_heavy(a, c)) ++nh;
       else ++ns;
+      if (may_overflow(a, nen, g)) ++nd;
     }
   }
-  int32_t tt, tr, ts, tb, th;
+  int32_t tt, tr, ts, tb, th, td;
   block_excl_sum(nt, sh[0], tt);
   block_excl_sum(nr, sh[1], tr);
   block_excl_sum(ns, sh[2], ts);
   block_excl_sum(nb, sh[3], tb);
   block_excl_sum(nh, sh[4], th);
+  block_excl_sum(nd, sh[5], td);
   if (threadIdx.x == 0) {
     base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
     base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
     base[2] = ts ? (int32_t)atomicAdd(&a.nsplit[0], (uint32_t)ts) : 0;
     base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tb) : 0;
     base[4] = th ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)th) : 0;
+    base[5] = td ? (int32_t)atomicAdd(&a.nsplit[3], (uint32_t)td) : 0;
   }
   __syncthreads();
   // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row.
   // Heavy rows fill the 1,024-entry list's region from its end (big, spilled and heavy
   // rows are distinct touched rows: they never meet).
   int4 *const desc = reinterpret_cast<int4 *>(a.split);
-  int32_t at = base[0], ar = base[1], as = base[2], ab = base[3], ah = base[4];
+  int32_t ar = base[1], as = base[2], ab = base[3], ah = base[4], ad = base[5];
   for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
     const int64_t s = t0 + threadIdx.x;
     int32_t c = 0, nen = 0;
-    bool big = false, heavy = false;
+    bool big = false, heavy = false, risky = false;
     if (s < c1) {
       c = a.cnt[s];
       if (c > 0) {
         nen = a.nent[s];
-        big = starts_big(a, nen, a.grow[s]);
+        const int32_t g = a.grow[s];
+        big = starts_big(a, nen, g);
         heavy = !big && starts_heavy(a, c);
+        risky = may_overflow(a, nen, g);
         a.grow[s] = 0;
       }
     }
     const bool t = c > 0;
-    int32_t st, sr, ss2, sb, sh2;
-    const int32_t pt = block_excl_sum(t ? 1 : 0, sh[0], st);
+    int32_t st, sr, ss2, sb, sh2, sd;
+    (void)block_excl_sum(t ? 1 : 0, sh[0], st);
     const int32_t pr = block_excl_sum(c, sh[1], sr);
     const int32_t ps = block_excl_sum(t && !big && !heavy ? 1 : 0, sh[2], ss2);
     const int32_t pb = block_excl_sum(t && big ? 1 : 0, sh[3], sb);
     const int32_t ph = block_excl_sum(t && heavy ? 1 : 0, sh[4], sh2);
+    const int32_t pd = block_excl_sum(t && risky ? 1 : 0, sh[5], sd);
     if (t) {
       const int32_t beg = ar + pr;
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
       a.off[s] = beg;
-      desc[2 * R + at + pt] = d;
+      if (risky) desc[2 * R + ad + pd] = d;   // the capacity dry run's list
       if (big) desc[R + ab + pb] = d;
       else if (heavy) desc[2 * R - 1 - (ah + ph)] = d;
       else desc[as + ps] = d;
     }
-    at += st;
     ar += sr;
     as += ss2;
     ab += sb;
     ah += sh2;
+    ad += sd;
   }
 }
 
@@ -755,14 +770,15 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
-  const bool go = o_gate(a) && (!DRY || *a.keyflag);
+  const bool go = o_gate(a) && (!DRY || a.grow || *a.keyflag);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows)
   if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0)) return;
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
   for (int32_t k = lane; k < 1024; k += 64) s_pos[wib][k] = -1;
   __syncthreads();
-  const bool pos_ok = a.keyflag && !*a.keyflag && a.max_entries <= 1024;
+  // split tables check each record chunk's columns here instead (cols_checked below)
+  const bool pos_ok = a.keyflag && (a.grow || !*a.keyflag) && a.max_entries <= 1024;
   int16_t *pos = s_pos[wib];
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + wib;
@@ -899,6 +915,19 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
           const int32_t my_col = c0 == 0 ? col0 : (pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0);
           const V my_d = c0 == 0 ? d0 : (pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0));
           const int32_t cnt = nn - c0 < 64 ? nn - c0 : 64;
+          if (use_pos && a.grow &&
+              __ballot(lane < cnt && (uint32_t)my_col >= (uint32_t)a.max_entries)) {
+            // a column outside [0, max_entries) (split tables: no column scan before the
+            // apply): the key map cannot index it — clear it (every mapped key is in the
+            // image) and finish the row on ballots
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+              if (j * 64 < n && j * 64 + lane < n) pos[key[j]] = -1;
+            wave_sync();
+            use_pos = false;
+            pos_dirty = false;
+          }
           // With the key map, lane t looks up its own column once for the whole chunk
           // (a record's columns are distinct, so an Inc moves no other key except by an
           // insert/remove shift, after which the chunk's lookups are re-read).
@@ -1159,6 +1188,13 @@ static unsigned row_blocks(int64_t n, int wpb) {
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
 
+// Launches that usually find few rows or none — the capacity dry run (only when a key
+// lies outside [0, max_entries)) and the 1,024-entry launch of spill mode (rows already
+// 7/8 full, and spills) — take the J = 16 kernel's resident grid (3 waves per SIMD: 768
+// blocks of 4 waves on 256 CUs) and loop over their rows: an empty 4,096-block launch
+// cost 4.7-4.9 µs per C3 step (profiles/r03/s26/c3_kernel_stats.csv).
+static unsigned few_row_blocks(int64_t n) { return std::min(row_blocks(n, 4), 768u); }
+
 static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
   const int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
   const int64_t per_wave = a.kind == 0 ? 0 : a.max_entries * esz;
@@ -1171,11 +1207,12 @@ static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
 template <typename V, int KIND>
 static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
   OrdArgs a = a0;
-  if (a.grow) {   // split tables: list ranges are not in slot order, walk the descriptors
+  if (a.grow) {   // split tables: the rows that may overflow (ordered_offsets), as descriptors
     a.touched = a.split + 2 * 4 * a.max_rows;
+    a.ntouched = a.nsplit + 3;
     a.desc = 1;
   }
-  const unsigned blocks = row_blocks(a.max_rows, 4);
+  const unsigned blocks = few_row_blocks(a.max_rows);
   if (a.max_entries <= 64)
     hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.max_entries <= 256)
@@ -1246,7 +1283,7 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, a);   \
     else if (a.grow && a.spill) {                                                                  \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, st, big); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(few_row_blocks(a.max_rows)), dim3(256), 0, st, big); \
     } else if (a.grow) {                                                                           \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, fk.aux, big); \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \

@@ -1229,7 +1229,7 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     e = hipMalloc(&t.d_grow, R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, R * sizeof(int32_t), c->stream);
     if (e == hipSuccess) e = hipMalloc(&t.d_split, 3 * R * 4 * sizeof(int32_t));   // int4 descriptors x 3 lists
-    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 5 * sizeof(uint32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {

@@ -121,3 +121,60 @@ def test_split_forms_match_oracle(split, kind, dt):
         srv.close()
     finally:
         L.psx_debug_set_variant(ORD_SPLIT, old)
+
+
+@pytest.mark.parametrize("split", [3, 1], ids=["spill-heavy-first", "concurrent"])
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted", "map"])
+def test_keys_outside_the_key_map_range(split, kind):
+    """Split tables no longer scan every record's columns before the apply: the apply checks
+    each record chunk's columns and finishes a row whose columns fall outside
+    [0, max_entries) (negative keys, keys far past it) without the key map; the capacity dry
+    run takes only the rows whose entries + Incs exceed max_entries.  Byte-exact (sorted) /
+    {col -> value} (map) against the oracle over several calls, mixing such rows with rows
+    inside the range and rows whose Incs exceed max_entries without overflowing."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(ORD_SPLIT, split)
+    try:
+        rng = np.random.RandomState(7 + split + 10 * kind)
+        rows, cap = 300, 512
+        bgs = [100, 101, 102]
+        srv = psa.Server(0, 1, bgs)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=cap, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=cap))
+        orc = OracleServer(bgs)
+        orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+        for v in range(4):
+            msgs = []
+            for b in range(3):
+                recs = []
+                for r in rng.choice(rows, size=200, replace=False):
+                    r = int(r)
+                    if r % 3 == 0:     # keys outside the map's range, few per row
+                        cols = np.unique(rng.choice(np.r_[np.arange(-40, 0), np.arange(cap, cap + 80),
+                                                          np.arange(100000, 100040)], size=rng.randint(1, 12)))
+                    elif r % 3 == 1:   # many Incs on a few keys: entries + Incs > cap, no overflow
+                        cols = np.arange(0, 200, dtype=np.int64)
+                    else:
+                        cols = np.unique(rng.choice(cap, size=rng.randint(1, 33)))
+                    vals = rng.randint(1, 4, size=cols.size) * (1 if v == 0 else rng.choice([-1, 1], size=cols.size))
+                    recs.append((r, cols.astype(np.int32), vals.astype(np.int32)))
+                msgs.append(recs)
+            streams = [wire.sparse_stream_np(3, 4, recs) for recs in msgs]
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+            srv.sync()
+            for s, bg in zip(streams, bgs):
+                assert orc.apply_stream(s, bg, v) == 0
+        ids = list(range(rows))
+        if kind == SORTED_MAP:
+            assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids)
+        else:
+            for r in ids:
+                g, w = srv.serialize_rows(3, [r]), orc.serialize_records(3, [r])
+                assert len(g) == len(w), f"row {r}"
+                if g:
+                    assert _as_map(g[12:], I32) == _as_map(w[12:], I32), f"row {r}"
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(ORD_SPLIT, old)

@@ -3,9 +3,10 @@ rule 24): the headline workload of bench.py, then R rounds; each round runs ever
 configuration for K steps and records the per-kernel HIP-event times.  Prints JSON with
 the median ms of every kernel per configuration.
 Usage: python tools/ab_c2.py --configs 0,0:1,2 [--rounds 5 --steps 5]
-       (apply_variant[:rows[:store_nt]], include/psx_debug.h; rows = 1 applies through
-       psx_apply_indexed_rows with the batches' record-row lists; store_nt selects
-       PSX_VARIANT_DENSE_STORE, default 1)"""
+       (apply_variant[:rows[:store_nt[:layout]]], include/psx_debug.h; rows = 1 applies
+       through psx_apply_indexed_rows with the batches' record-row lists; store_nt selects
+       PSX_VARIANT_DENSE_STORE, default 1; layout 1 = the messages back to back in one
+       allocation instead of one allocation each)"""
 import argparse
 import json
 import os
@@ -45,6 +46,13 @@ def main():
         streams.append(wire.dense_stream_torch(1, perm, upd))
         lists.append(perm)
         del upd, perm
+    # layout 1: the same messages back to back in one allocation (a receive buffer)
+    contig = torch.empty(sum(x.numel() for x in streams), dtype=torch.uint8, device="cuda")
+    cstreams, o = [], 0
+    for x in streams:
+        contig[o:o + x.numel()].copy_(x)
+        cstreams.append(contig[o:o + x.numel()])
+        o += x.numel()
     bgs = [100 + b for b in range(B)]
     srv = psa.Server(device=0, server_id=1, bg_ids=bgs)
     srv.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -56,7 +64,7 @@ def main():
     configs = []
     for c in args.configs.split(","):
         f = [int(x) for x in c.split(":")]
-        configs.append(tuple((f + [0, 1][len(f) - 1:])[:3]))
+        configs.append(tuple((f + [0, 1, 0][len(f) - 1:])[:4]))
     res = {c: {k: [] for k in kernels + ("step",)} for c in configs}
 
     def run(c, steps):
@@ -67,7 +75,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            msgs = [(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(streams)]
+            msgs = [(s.data_ptr(), s.numel(), bgs[b], ver[0]) for b, s in enumerate(cstreams if c[3] else streams)]
             if c[1]:
                 srv.apply_indexed_rows(msgs, [r.data_ptr() for r in lists])
             else:
@@ -89,7 +97,7 @@ def main():
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))
             res[c]["step"].append(step_ms)
-    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + f"_rowpolicy{c[2]}":
+    out = {f"apply{c[0]}" + ("_rows" if c[1] else "") + f"_rowpolicy{c[2]}" + ("_contig" if c[3] else ""):
            {k: round(statistics.median(v), 4) for k, v in res[c].items()} for c in configs}
     print(json.dumps(out, indent=1))
     srv.close()

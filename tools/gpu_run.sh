@@ -78,6 +78,8 @@ for s in "$@"; do
     c3walk) i=0; for v in 0 1 0 1; do i=$((i+1)); run c3walk_${i}_cus$v 300 env PSX_WALK_CUS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
             for f in $O/c3walk_*.log; do echo "$f $(grep -h '^{' $f | cut -c1-120)"; done ;;
     wtrace1) run wtrace1 200 env PSX_WALK_CUS=1 python -u tools/walk_trace.py && head -c 1500 "$O/wtrace1.log" ;;
+    c2layout) for i in 1 2; do run c2sep_$i 300 env PSX_BENCH_SEPARATE=1 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras && run c2buf_$i 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras || exit 1; done
+              for f in $O/c2sep_* $O/c2buf_*; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["roofline"]["avg_launch_ms"], d["walked"]["value"])')"; done ;;
     c2only) run c2only 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras ;;
     c3) run c3 300 python -u bench.py --workload c3 --steps 20 --warmup 3 ;;
     c3idx) run c3idx 300 python -u bench.py --workload c3 --indexed --steps 20 --warmup 3 ;;

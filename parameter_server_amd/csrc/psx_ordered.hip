@@ -985,7 +985,9 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
               }
             }
             if (idx < 0) {
-              if (!DRY && a.spill && n >= J * 64) {   // outgrows this image: hand the row on
+              // outgrows this image: hand the row on (only the 256-entry launch of a split
+              // table spills; the 1,024-entry image holds every entry max_entries allows)
+              if (!DRY && a.spill && a.spill_list && J * 64 < a.max_entries && n >= J * 64) {
                 spilled = true;
                 over = true;
                 continue;

@@ -94,6 +94,7 @@ for s in "$@"; do
     abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
     abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
     abzeros) run abzeros 400 python -u tools/ab_c2.py --zeros --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -30 "$O/abzeros.log" ;;
+    pushtests) run pushtests 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_ssp_gpu.py tests/test_push_body_gpu.py tests/test_matrixfact_gpu.py tests/test_app_drivers_gpu.py tests/test_configs_gpu.py ;;
     mrtest) run mrtest 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_multi_rank_gpu.py tests/test_split_gpu.py ;;
     walktests) run walktests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dense_gpu.py tests/test_indexed_rows_gpu.py tests/test_ord_split_gpu.py ;;

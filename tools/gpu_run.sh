@@ -17,6 +17,7 @@
 #   mixab   the mixing probe and the C2 apply A/B interleaved, three times (same box)
 #   wtrace  tools/walk_trace.py: per-window timeline of the walk on the C3 batches
 #   pmix    tools/probe_apply's mixing probe (records in random vs slot order; build it first)
+#   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
 set -o pipefail
@@ -104,6 +105,7 @@ for s in "$@"; do
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
     pmix) run pmix 300 tools/probe_apply 10 1 && cat "$O/pmix.log" ;;
+    pcopy) run pcopy 300 tools/probe_copy 10 && cat "$O/pcopy.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

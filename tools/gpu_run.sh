@@ -105,7 +105,7 @@ for s in "$@"; do
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
     pmix) run pmix 300 tools/probe_apply 10 1 && cat "$O/pmix.log" ;;
-    pcopy) run pcopy 300 tools/probe_copy 10 && cat "$O/pcopy.log" ;;
+    pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

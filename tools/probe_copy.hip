@@ -7,6 +7,10 @@
 //   copy  persist   grid sized to residency x M, tiles handed out grid-stride (probe_hbm's form)
 //   write flat      16-B stores only (what the row stores alone can reach)
 //   read  flat      16-B loads only
+//   mixK  seq|split K 1-KiB reads per wave then one 1-KiB write, flat grid, one wave per
+//                   row: "seq" reads K consecutive KiB of one sweep (two streams in all),
+//                   "split" reads piece k from region k (K + 1 streams, the C2 apply's shape
+//                   with records in slot order) — the read/write ratio without the gather
 //   apply flat      the C2 pattern (8 records + table row read, row written), D rows per
 //                   wave, one tile per block, rows in slot order — against probe_hbm's
 //                   persistent apply of the same bytes
@@ -115,6 +119,71 @@ __global__ void __launch_bounds__(256) apply_flat(uint8_t *table, const uint8_t 
   }
 }
 
+// K reads of 1 KiB then 1 write of 1 KiB per wave (row w = one wave), plain loads, nt or plain store
+template <int K, bool SPLIT>
+__global__ void __launch_bounds__(256) mix_flat(const u32x4 *src, u32x4 *dst, int64_t rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  u32x4 v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    v[k] = ld<true>(src + (SPLIT ? (int64_t)k * rows * 64 + w * 64 : (w * K + k) * 64) + lane);
+  u32x4 acc = v[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) acc ^= v[k];
+  st<false>(dst + w * 64 + lane, acc);
+}
+
+// 9:1 variants (seq streams, 2^20 rows): MODE 0 = plain loads, 1 = nt store, 2 = store before
+// the loads (a constant), 3 = two rows per wave (18 loads, 2 stores), 4 = role split: of
+// every 10 waves, 9 read 10 KiB each... (wave w % 10 == 9 writes the ten rows' 10 KiB)
+template <int MODE>
+__global__ void __launch_bounds__(256) mix9_var(const u32x4 *src, u32x4 *dst, int64_t rows, uint32_t *sink) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if constexpr (MODE == 4) {
+    // 10 waves cover 9 rows' reads (81 KiB) and 9 rows' writes (9 KiB): waves 0..8 read
+    // 9 KiB each, wave 9 writes 9 KiB
+    const int64_t grp = w / 10, r = w % 10;
+    if (grp * 9 >= rows) return;
+    if (r < 9) {
+      if (grp * 9 + r >= rows) return;
+      u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc ^= ld<true>(src + ((grp * 9 + r) * 9 + k) * 64 + lane);
+      if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9e3779b9u) sink[0] = 1;
+    } else {
+      const u32x4 v = {(uint32_t)grp, 1u, 2u, 3u};
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+        if (grp * 9 + k < rows) st<false>(dst + (grp * 9 + k) * 64 + lane, v);
+    }
+    return;
+  }
+  constexpr int RW = MODE == 3 ? 2 : 1;
+  if (w * RW >= rows) return;
+  if constexpr (MODE == 2) st<false>(dst + w * 64 + lane, u32x4{(uint32_t)w, 0u, 0u, 0u});
+  u32x4 acc[RW];
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    acc[q] = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const u32x4 *p = src + ((w * RW + q) * 9 + k) * 64 + lane;
+      acc[q] ^= MODE == 0 ? ld<false>(p) : ld<true>(p);
+    }
+  }
+  if constexpr (MODE == 2) {
+    if ((acc[0][0] ^ acc[0][1]) == 0x9e3779b9u) sink[0] = 1;
+  } else {
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      if (MODE == 1) st<true>(dst + (w * RW + q) * 64 + lane, acc[q]);
+      else st<false>(dst + (w * RW + q) * 64 + lane, acc[q]);
+    }
+  }
+}
+
 template <typename K>
 static unsigned resident(K k) {
   int per = 0, cus = 0;
@@ -160,7 +229,9 @@ int main(int argc, char **argv) {
   CK(hipMemset(b, 0, BBYTES));
   char ex[256];
 
+  const bool only_mix = argc > 2 && argv[2][0] == 'm';   // "mix": the ratio and apply forms only
   for (int64_t gib : {1, 4}) {
+    if (only_mix) break;
     const int64_t bytes = gib << 30, n16 = bytes / 16;
 #define FLAT(U, NT)                                                                                   \
     {                                                                                                 \
@@ -197,6 +268,27 @@ int main(int argc, char **argv) {
       line("read", ex, (double)bytes, ms);                                                            \
     }
     READF(1, false) READF(4, false) READF(4, true)
+  }
+
+  // read/write ratio K:1 with sequential streams, 2^20 rows (1 GiB written)
+  {
+    const int64_t R = 1 << 20;
+#define MIX(K, SPLIT)                                                                                 \
+    {                                                                                                 \
+      const unsigned g = (unsigned)(R / 4);                                                          \
+      const float ms = time_ms([&] { mix_flat<K, SPLIT><<<g, 256>>>((const u32x4 *)a, (u32x4 *)b, R); }, reps); \
+      snprintf(ex, sizeof ex, "\"form\": \"%s\", \"K\": %d", SPLIT ? "split" : "seq", K);           \
+      line("mix", ex, (double)(K + 1) * R * 1024, ms);                                               \
+    }
+    MIX(1, false) MIX(2, false) MIX(4, false) MIX(9, false) MIX(9, true) MIX(4, true)
+#define MIXV(MODE, WAVES)                                                                             \
+    {                                                                                                 \
+      const unsigned g = (unsigned)((WAVES + 3) / 4);                                                \
+      const float ms = time_ms([&] { mix9_var<MODE><<<g, 256>>>((const u32x4 *)a, (u32x4 *)b, R, sink); }, reps); \
+      snprintf(ex, sizeof ex, "\"form\": \"seq9_mode%d\", \"K\": 9", MODE);                        \
+      line("mix", ex, 10.0 * R * 1024, ms);                                                          \
+    }
+    MIXV(0, R) MIXV(1, R) MIXV(2, R) MIXV(3, R / 2) MIXV(4, (R / 9 + 1) * 10) MIX(9, false)
   }
 
   // the C2 pattern, one tile per block (2^20 rows x 256 f32, 8 messages, 1,028-B records)

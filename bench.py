@@ -706,6 +706,24 @@ def run_c4shard(args):
         "cpu_baseline": cpu}), flush=True)
 
 
+def read_sweep_rate(bufs, reps=5):
+    """GB/s of psx_debug_read_sweep over the device buffers `bufs` (bytes / time summed over
+    all of them), or None when the hook fails."""
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    tot_b, tot_s = 0.0, 0.0
+    for t in bufs:
+        nb = (t.numel() * t.element_size()) // 16384 * 16384
+        if nb < 16384:
+            continue
+        g = L.psx_debug_read_sweep(t.data_ptr(), nb, reps)
+        if g <= 0:
+            return None
+        tot_b += nb
+        tot_s += nb / (g * 1e9)
+    return tot_b / tot_s / 1e9 if tot_s > 0 else None
+
+
 def run_pcie(args, srv, streams, rows, cap, bgs, ver):
     """Host-resident form of C2: messages start in pinned host memory (worker socket
     buffers) and every dirty row is served back to host memory each step."""
@@ -1031,6 +1049,9 @@ def main():
     kernels = {k: srv.timing_read(k) for k in ("decode_streams", "dense_index", "dense_verify",
                                                apply_kernel, "finish_call")}
     srv.timing(False)
+    # The box's own HBM read rate (north_star: "≥70 % of single-GPU HBM read bandwidth"): a
+    # read-only sweep over the resident message buffers, after the timed region.
+    read_sweep = read_sweep_rate(streams)
     # The walked path (row ids read from the stream, no overlap) on the same messages, timed
     # the same way, reported beside `value`.
     walked = None
@@ -1141,6 +1162,11 @@ def main():
                 "kernel_signature": kernel_signature(),
                 "dram_GBps": round(traffic / apply_avg_s / 1e9, 1) if traffic and apply_avg_s > 0 else None,
                 "avg_launch_ms": round(apply_avg_s * 1e3, 4),
+                "read_sweep_GBps": round(read_sweep, 1) if read_sweep else None,
+                "frac_of_read_sweep": round(achieved / read_sweep, 4) if achieved and read_sweep else None,
+                "read_sweep_note": "this GPU's HBM read rate in the same run (psx_debug_read_sweep: 16-B "
+                                   "non-temporal loads over the resident message buffers); north_star's target "
+                                   "is 0.70 of single-GPU HBM read bandwidth",
             },
             "kernel_ms_per_launch_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},
             "cpu_baseline": cpu,

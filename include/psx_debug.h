@@ -43,6 +43,12 @@ int32_t psx_debug_get_variant(int32_t which);
    returns the call's item count, 0 when no call walked, -1 on error. */
 int64_t psx_debug_walk_trace(struct psx_ctx *ctx, uint64_t *out, int64_t max_items);
 
+/* The box's HBM read rate: GB/s of a read-only sweep (16-B non-temporal loads) over the
+   device buffer [buf, buf + bytes), mean of reps launches after one warm-up, timed with HIP
+   events on a stream of its own.  buf 16-B aligned, bytes >= 16 KiB (the tail past the
+   last 16 KiB tile is not read).  Returns -1 on bad arguments or a HIP error. */
+double psx_debug_read_sweep(const void *buf, int64_t bytes, int32_t reps);
+
 #ifdef __cplusplus
 }
 #endif

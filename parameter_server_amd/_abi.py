@@ -193,6 +193,7 @@ def load():
         "psx_debug_set_variant": ([i32, i32], i32),
         "psx_debug_get_variant": ([i32], i32),
         "psx_debug_walk_trace": ([vp, vp, ctypes.c_int64], ctypes.c_int64),
+        "psx_debug_read_sweep": ([vp, ctypes.c_int64, i32], ctypes.c_double),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -270,3 +270,14 @@ def test_every_kernel_variant_bit_exact(apply_variant):
             srv.close()
     finally:
         L.psx_debug_set_variant(1, old_a)
+
+
+def test_read_sweep_hook_measures_a_rate():
+    """psx_debug_read_sweep (include/psx_debug.h): bench.py's same-run HBM read rate."""
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    buf = torch.ones(64 << 20, dtype=torch.uint8, device="cuda")
+    g = L.psx_debug_read_sweep(buf.data_ptr(), buf.numel(), 3)
+    assert 100.0 < g < 9000.0, g
+    assert L.psx_debug_read_sweep(buf.data_ptr() + 4, buf.numel() - 16, 1) == -1.0   # misaligned
+    assert L.psx_debug_read_sweep(buf.data_ptr(), 1024, 1) == -1.0                   # below one tile

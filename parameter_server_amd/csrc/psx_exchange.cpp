@@ -44,6 +44,16 @@ psx_status comm_fail(psx_comm *c, const std::string &m, psx_status st = PSX_ERR_
     ncclResult_t r_ = (x);                                                                 \
     if (r_ != ncclSuccess) return comm_fail(c, std::string(#x) + ": " + ncclGetErrorString(r_)); \
   } while (0)
+// inside ncclGroupStart/End: close the group before reporting, so the next call does not
+// nest into a half-built group
+#define NCCL_TRY_G(c, x)                                                                   \
+  do {                                                                                     \
+    ncclResult_t r_ = (x);                                                                 \
+    if (r_ != ncclSuccess) {                                                               \
+      ncclGroupEnd();                                                                      \
+      return comm_fail(c, std::string(#x) + ": " + ncclGetErrorString(r_));                \
+    }                                                                                      \
+  } while (0)
 #define HIPX_TRY(c, x)                                                                     \
   do {                                                                                     \
     hipError_t e_ = (x);                                                                   \
@@ -109,8 +119,8 @@ psx_status psx_exchange_sizes(psx_comm *c, const uint64_t *send_sizes, uint64_t 
   HIPX_TRY(c, hipMemcpyAsync(c->d_sizes, send_sizes, sizeof(uint64_t) * n, hipMemcpyHostToDevice, st));
   NCCL_TRY(c, ncclGroupStart());
   for (int p = 0; p < c->nranks; ++p) {
-    NCCL_TRY(c, ncclSend(c->d_sizes + p, 1, ncclUint64, p, c->comm, st));
-    NCCL_TRY(c, ncclRecv(c->d_sizes + n + p, 1, ncclUint64, p, c->comm, st));
+    NCCL_TRY_G(c, ncclSend(c->d_sizes + p, 1, ncclUint64, p, c->comm, st));
+    NCCL_TRY_G(c, ncclRecv(c->d_sizes + n + p, 1, ncclUint64, p, c->comm, st));
   }
   NCCL_TRY(c, ncclGroupEnd());
   HIPX_TRY(c, hipMemcpyAsync(recv_sizes, c->d_sizes + n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
@@ -121,13 +131,16 @@ psx_status psx_exchange_sizes(psx_comm *c, const uint64_t *send_sizes, uint64_t 
 psx_status psx_exchange_streams(psx_comm *c, const void *send, const uint64_t *send_sizes, void *recv,
                                 const uint64_t *recv_sizes, void *hip_stream) {
   if (!c || !send_sizes || !recv_sizes) return PSX_ERR_INVALID_ARG;
+  for (int p = 0; p < c->nranks; ++p)
+    if ((send_sizes[p] && !send) || (recv_sizes[p] && !recv))
+      return comm_fail(c, "exchange_streams: null buffer with a nonzero size", PSX_ERR_INVALID_ARG);
   hipStream_t st = (hipStream_t)hip_stream;
   HIPX_TRY(c, hipSetDevice(c->device));
   uint64_t so = 0, ro = 0;
   NCCL_TRY(c, ncclGroupStart());
   for (int p = 0; p < c->nranks; ++p) {
-    if (send_sizes[p]) NCCL_TRY(c, ncclSend((const uint8_t *)send + so, send_sizes[p], ncclUint8, p, c->comm, st));
-    if (recv_sizes[p]) NCCL_TRY(c, ncclRecv((uint8_t *)recv + ro, recv_sizes[p], ncclUint8, p, c->comm, st));
+    if (send_sizes[p]) NCCL_TRY_G(c, ncclSend((const uint8_t *)send + so, send_sizes[p], ncclUint8, p, c->comm, st));
+    if (recv_sizes[p]) NCCL_TRY_G(c, ncclRecv((uint8_t *)recv + ro, recv_sizes[p], ncclUint8, p, c->comm, st));
     so += send_sizes[p];
     ro += recv_sizes[p];
   }

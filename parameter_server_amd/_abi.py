@@ -8,7 +8,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpsx.so")
+# PSX_LIB: another in-tree build of the library (A/B runs of two builds on one box,
+# tools/gpu_run.sh c3lib); default the package's own libpsx.so
+LIB_PATH = os.environ.get("PSX_LIB") or os.path.join(_HERE, "libpsx.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psx.h")
 
 PSX_OK = 0

@@ -185,8 +185,9 @@ struct OrdArgs {
                           // nspill) untouched, and the 1,024-entry launch runs after it
   int32_t *spill_list;
   uint32_t *nspill;
-  const int32_t *heavy_end;  // heavy-first (spill bit 1): heavy row descriptors end here,
-  const uint32_t *nheavy;    // listed backwards; the 256-entry launch takes them first
+  const int32_t *heavy_end;  // heavy-first (spill bit 1): heavy row descriptors end here (the
+  const uint32_t *nheavy;    // 256-entry list's region), listed backwards; the 256-entry
+                             // launch takes them first
 };
 
 // A side stream and two events for launches that run beside the context stream.

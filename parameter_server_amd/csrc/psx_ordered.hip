@@ -289,8 +289,10 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   }
   __syncthreads();
   // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row.
-  // Heavy rows fill the 1,024-entry list's region from its end (big, spilled and heavy
-  // rows are distinct touched rows: they never meet).
+  // Heavy rows fill the 256-entry list's region [0, R) from its end: small and heavy rows
+  // are distinct touched rows, so the two never meet.  The 1,024-entry region [R, 2R) holds
+  // the big rows and, appended behind them by the 256-entry launch, the spilled rows (small
+  // or heavy, each at most once): at most the touched count in all.
   int4 *const desc = reinterpret_cast<int4 *>(a.split);
   int32_t ar = base[1], as = base[2], ab = base[3], ah = base[4], ad = base[5];
   for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
@@ -322,7 +324,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       a.off[s] = beg;
       if (risky) desc[2 * R + ad + pd] = d;   // the capacity dry run's list
       if (big) desc[R + ab + pb] = d;
-      else if (heavy) desc[2 * R - 1 - (ah + ph)] = d;
+      else if (heavy) desc[R - 1 - (ah + ph)] = d;
       else desc[as + ps] = d;
     }
     ar += sr;
@@ -789,14 +791,26 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   // heavy-first: the heavy rows' list (descending from heavy_end) before the rest
   const int64_t nh = go && a.nheavy ? (int64_t)*a.nheavy : 0;
   const int64_t nt = go ? nh + (int64_t)*a.ntouched : 0;
+  // Descriptor lists: the wave's next row's descriptor is loaded a row ahead (a scalar load:
+  // the index is wave-uniform), so a row's setup starts from its record list, not from its
+  // descriptor.
+  auto desc_at = [&](int64_t t) -> int4 {
+    t = (int64_t)__builtin_amdgcn_readfirstlane((int32_t)t);   // t < nt < 2^31
+    const int4 *p = t < nh ? reinterpret_cast<const int4 *>(a.heavy_end) - 1 - t
+                           : reinterpret_cast<const int4 *>(a.touched) + (t - nh);
+    const __attribute__((address_space(4))) int32_t *q = (const __attribute__((address_space(4))) int32_t *)p;
+    return int4{q[0], q[1], q[2], q[3]};
+  };
+  int4 d_next = int4{0, 0, 0, 0};
+  if (a.desc && wave_g < nt) d_next = desc_at(wave_g);
   for (int64_t ti = wave_g; ti < nt; ti += nwaves) {
     // per-row scalars are wave-uniform: readfirstlane keeps them in SGPRs so the row's
     // loops branch on SCC instead of running under exec masks
     int64_t slot;
     int32_t beg, L, n;
     if (a.desc) {
-      const int4 d = ti < nh ? reinterpret_cast<const int4 *>(a.heavy_end)[-1 - ti]
-                             : reinterpret_cast<const int4 *>(a.touched)[ti - nh];
+      const int4 d = d_next;
+      if (ti + nwaves < nt) d_next = desc_at(ti + nwaves);
       slot = __builtin_amdgcn_readfirstlane(d.x);
       beg = __builtin_amdgcn_readfirstlane(d.y);
       L = __builtin_amdgcn_readfirstlane(d.z) - beg;
@@ -830,6 +844,19 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         for (int32_t q = lane; q < L; q += 64) grow += o_ld32(rec_ptr(a, L <= 64 ? mine : lst[q]) + 4);
         if ((int64_t)n + wave_sum_i32(grow) <= (int64_t)cap) continue;
       }
+      // Record headers fetched for all of the row's records at once (lane q: record q in
+      // message order; rows with <= 64 records in the call), issued before the row image so
+      // that the first record's chunk loads below wait on the headers only (loads return in
+      // order); each record's first 64 (column, value) pairs are loaded one record ahead, so
+      // the Inc chain does not wait on a dependent global load per record.
+      int hb = 0;
+      uint64_t hoff = 0;
+      int32_t hn = 0;
+      if (L <= 64 && lane < L) {
+        hb = (int)(mine >> 56);
+        hoff = mine & kRefOffMask;
+        hn = o_ld32(a.ss.data[hb] + hoff + 4);
+      }
       // load the row image
       const uint8_t *row = a.entries + slot * a.max_entries * ES;
       int32_t key[J];
@@ -839,37 +866,6 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         const int32_t i = j * 64 + lane;
         key[j] = i < n ? o_ld32(row + (int64_t)i * ES) : 0;
         val[j] = i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
-      }
-      bool use_pos = pos_ok;
-      bool pos_dirty = false;   // sorted rows: inserts not yet written to the key map
-      if (use_pos) {
-        bool out = false;
-#pragma unroll
-        for (int j = 0; j < J; ++j)
-          out = out || (j * 64 + lane < n && (key[j] < 0 || key[j] >= (int32_t)a.max_entries));
-        use_pos = __ballot(out) == 0;
-      }
-      if (use_pos) {   // the map is all -1 between rows (cleared once, then per row below)
-#pragma unroll
-        for (int j = 0; j < J; ++j)
-          if (j * 64 + lane < n) pos[key[j]] = (int16_t)(j * 64 + lane);
-        wave_sync();
-      }
-      double impt = a.imp ? a.imp[slot] : 0.0;
-      bool over = false;   // DRY: this row would exceed max_entries
-      bool spilled = false;
-      const int32_t n0 = n;
-      // Record headers fetched for all of the row's records at once (lane q: record q in
-      // message order; rows with <= 64 records in the call), and each record's first 64
-      // (column, value) pairs loaded one record ahead, so the Inc chain does not wait on
-      // a dependent global load per record.
-      int hb = 0;
-      uint64_t hoff = 0;
-      int32_t hn = 0;
-      if (L <= 64 && lane < L) {
-        hb = (int)(mine >> 56);
-        hoff = mine & kRefOffMask;
-        hn = o_ld32(a.ss.data[hb] + hoff + 4);
       }
       auto rec_at = [&](int32_t q, const uint8_t *&rec, int32_t &nn) {
         int b;
@@ -897,6 +893,25 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         col_n = lane < nn_n ? o_ld32(rec_n + 8 + (int64_t)lane * 4) : 0;
         d_n = lane < nn_n ? ldv<V>(rec_n + 8 + (int64_t)nn_n * 4 + (int64_t)lane * sizeof(V)) : V(0);
       }
+      bool use_pos = pos_ok;
+      bool pos_dirty = false;   // sorted rows: inserts not yet written to the key map
+      if (use_pos) {
+        bool out = false;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          out = out || (j * 64 + lane < n && (key[j] < 0 || key[j] >= (int32_t)a.max_entries));
+        use_pos = __ballot(out) == 0;
+      }
+      if (use_pos) {   // the map is all -1 between rows (cleared once, then per row below)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (j * 64 + lane < n) pos[key[j]] = (int16_t)(j * 64 + lane);
+        wave_sync();
+      }
+      double impt = a.imp ? a.imp[slot] : 0.0;
+      bool over = false;   // DRY: this row would exceed max_entries
+      bool spilled = false;
+      const int32_t n0 = n;
       for (int32_t q = 0; q < L && !over; ++q) {
         const uint8_t *rec = rec_n;
         const int32_t nn = nn_n;
@@ -1267,8 +1282,8 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
       small.desc = big.desc = 1;
       small.spill_list = big.touched;
       small.nspill = big.ntouched;
-      if (a.spill & 2) {   // heavy rows: from the end of the 1,024-entry list's region
-        small.heavy_end = a.split + 8 * a.max_rows;
+      if (a.spill & 2) {   // heavy rows: listed backwards
+        small.heavy_end = a.split + 4 * a.max_rows;   // end of the 256-entry list's region
         small.nheavy = a.nsplit + 2;
       }
       if (!a.spill) {

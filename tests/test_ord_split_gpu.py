@@ -178,3 +178,41 @@ def test_keys_outside_the_key_map_range(split, kind):
         srv.close()
     finally:
         L.psx_debug_set_variant(ORD_SPLIT, old)
+
+
+def test_every_row_heavy_and_spilling():
+    """Spill mode with heavy rows first when every row of the table is touched, has >= 4
+    records in the call and outgrows 256 entries inside it: the heavy rows' descriptors and
+    the spilled rows' descriptors (appended by the 256-entry launch while it runs) must not
+    share list space.  R = 40,000 rows is more rows than waves resident at once, so late
+    rows read their descriptors after early rows have spilled.  Byte-exact vs the oracle."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(ORD_SPLIT, 3)
+    try:
+        rows, K, dt = 40_000, 1024, I32
+        bgs = [100, 101, 102, 103]
+        srv = psa.Server(0, 1, bgs)
+        srv.CreateTable(3, psa.TableInfo(row_kind=SORTED_MAP, dtype=dt, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        orc = OracleServer(bgs)
+        orc.create_table(3, SORTED_MAP, dt, 0, oplog_dense_serialized=False)
+        rng = np.random.RandomState(2024)
+        # call 0: 200 entries per row (50 columns per message, values 1..3: no zeros)
+        c0 = [[(r, np.arange(50 * b, 50 * b + 50, dtype=np.int32),
+                rng.randint(1, 4, size=50).astype(np.int32)) for r in range(rows)] for b in range(4)]
+        # call 1: every row 4 records of 20 new columns each (200 + 80 > 256: every row spills)
+        c1 = [[(r, np.arange(200 + 20 * b, 220 + 20 * b, dtype=np.int32),
+                rng.randint(1, 4, size=20).astype(np.int32)) for r in range(rows)] for b in range(4)]
+        for v, msgs in enumerate((c0, c1)):
+            streams = [wire.sparse_stream_np(3, VS[dt], recs) for recs in msgs]
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+            srv.sync()
+            for s, bg in zip(streams, bgs):
+                assert orc.apply_stream(s, bg, v) == 0
+        ids = list(range(rows))
+        assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids)
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(ORD_SPLIT, old)

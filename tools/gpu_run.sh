@@ -17,6 +17,9 @@
 #   mixab   the mixing probe and the C2 apply A/B interleaved, three times (same box)
 #   wtrace  tools/walk_trace.py: per-window timeline of the walk on the C3 batches
 #   pmix    tools/probe_apply's mixing probe (records in random vs slot order; build it first)
+#   c3lib   C3 with this tree's libpsx and ab_old/libpsx.so (PSX_LIB), interleaved twice
+#   oldheavy the all-rows-heavy-and-spilling test on ab_old/libpsx.so (reported, never fatal)
+#   splittests the split-apply / sparse / KAT GPU test files only
 #   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
@@ -105,6 +108,11 @@ for s in "$@"; do
     pphase) run pphase 120 tools/probe_phase 10 && cat "$O/pphase.log" ;;
     papply) run papply 300 tools/probe_apply 10 && cat "$O/papply.log" ;;
     pmix) run pmix 300 tools/probe_apply 10 1 && cat "$O/pmix.log" ;;
+    c3lib) i=0; for v in new old new old; do i=$((i+1)); L=; [ $v = old ] && L=ab_old/libpsx.so
+             run c3lib_${i}_$v 300 env PSX_LIB=$L python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+           for f in $O/c3lib_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"])')"; done ;;
+    oldheavy) say oldheavy; timeout -k 10 300 env PSX_LIB=ab_old/libpsx.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ord_split_gpu.py -k every_row_heavy > "$O/oldheavy.log" 2>&1; echo "oldheavy rc=$? (the pre-fix library: a failure here is the collision)"; tail -5 "$O/oldheavy.log" ;;
+    splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

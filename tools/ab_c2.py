@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--cols", type=int, default=256)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--zeros", action="store_true", help="zero table and updates (data-dependence check)")
+    ap.add_argument("--drift", action="store_true",
+                    help="print every round's dense_apply ms with its time since the first round (one line each)")
     args = ap.parse_args()
     import torch
     import parameter_server_amd as psa
@@ -90,9 +92,14 @@ def main():
 
     for c in configs:   # warm-up of every configuration
         run(c, 2)
-    for _ in range(args.rounds):
+    t_start = time.perf_counter()
+    for r in range(args.rounds):
         for c in configs:
             kt, step_ms = run(c, args.steps)
+            if args.drift:
+                ms, n = kt["dense_apply"]
+                print(json.dumps({"round": r, "t_s": round(time.perf_counter() - t_start, 3), "config": c,
+                                  "dense_apply": round(ms / max(n, 1), 4), "step": round(step_ms, 4)}), flush=True)
             for k in kernels:
                 ms, n = kt[k]
                 res[c][k].append(ms / max(n, 1))

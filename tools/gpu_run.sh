@@ -111,6 +111,11 @@ for s in "$@"; do
     c3lib) i=0; for v in new old new old; do i=$((i+1)); L=; [ $v = old ] && L=ab_old/libpsx.so
              run c3lib_${i}_$v 300 env PSX_LIB=$L python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
            for f in $O/c3lib_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"])')"; done ;;
+    c2lib) i=0; for v in new old new old; do i=$((i+1)); L=; [ $v = old ] && L=ab_old/libpsx.so
+             run c2lib_${i}_$v 300 env PSX_LIB=$L python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras --skip-walked || exit 1; done
+           for f in $O/c2lib_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["roofline"]["avg_launch_ms"], d["roofline"]["frac_of_read_sweep"])')"; done ;;
+    drift) for i in 1 2 3; do run drift_$i 300 python -u tools/ab_c2.py --configs 0:1:1 --rounds ${DRIFT_ROUNDS:-60} --steps 20 --drift || exit 1; done
+           for f in $O/drift_*.log; do echo "$f"; grep -h '"round"' $f | awk 'NR%6==1' | cut -c1-120; done ;;
     oldheavy) say oldheavy; timeout -k 10 300 env PSX_LIB=ab_old/libpsx.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ord_split_gpu.py -k every_row_heavy > "$O/oldheavy.log" 2>&1; echo "oldheavy rc=$? (the pre-fix library: a failure here is the collision)"; tail -5 "$O/oldheavy.log" ;;
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;

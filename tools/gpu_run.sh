@@ -116,6 +116,17 @@ for s in "$@"; do
            for f in $O/c2lib_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["roofline"]["avg_launch_ms"], d["roofline"]["frac_of_read_sweep"])')"; done ;;
     drift) for i in 1 2 3; do run drift_$i 300 python -u tools/ab_c2.py --configs 0:1:1 --rounds ${DRIFT_ROUNDS:-60} --steps 20 --drift || exit 1; done
            for f in $O/drift_*.log; do echo "$f"; grep -h '"round"' $f | awk 'NR%6==1' | cut -c1-120; done ;;
+    tlb) for i in 1 2 3 4; do
+           say "tlb pass $i"
+           timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum \
+             -d "$R/tlb/p$i" -o pmc -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 --skip-walked --no-extras > "$O/tlb_p$i.log" 2>&1 || { echo "!! tlb pass $i"; tail -5 "$O/tlb_p$i.log"; exit 1; }
+           grep -h '^{' "$O/tlb_p$i.log" | python3 -c 'import json,sys; d=json.load(sys.stdin); print("avg_launch_ms", d["roofline"]["avg_launch_ms"])'
+         done
+         python3 tools/pmc_db.py $(find "$R/tlb" -name '*.db' | sort) > "$O/tlb.json" && python3 -c "
+import json; d=json.load(open('$O/tlb.json'))
+for db, ks in d.items():
+    for k, v in ks.items():
+        if 'dense_apply' in k: print(db[-40:], {c: round(x) for c, x in v.items()})" ;;
     oldheavy) say oldheavy; timeout -k 10 300 env PSX_LIB=ab_old/libpsx.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ord_split_gpu.py -k every_row_heavy > "$O/oldheavy.log" 2>&1; echo "oldheavy rc=$? (the pre-fix library: a failure here is the collision)"; tail -5 "$O/oldheavy.log" ;;
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;

@@ -188,6 +188,23 @@ struct OrdArgs {
   const int32_t *heavy_end;  // heavy-first (spill bit 1): heavy row descriptors end here (the
   const uint32_t *nheavy;    // 256-entry list's region), listed backwards; the 256-entry
                              // launch takes them first
+  int32_t counted;           // split tables: the walk already counted this call's records
+                             // (WalkCount): ordered_count is not launched
+};
+
+// ordered_count's work for one split sorted/map table (grow set), done by the window-parallel
+// walk as it writes each record's offset (psx_walk.hip): per record cnt[slot] += 1 and
+// grow[slot] += its pairs, kStRowRange for a row outside the shard; walk_head zeroes
+// ordered_offsets' counters.  Only on calls whose decode is not pipelined (the walk then runs
+// after the previous call's ordered work on the same stream).
+struct WalkCount {
+  int64_t row_offset, row_stride, max_rows;
+  int32_t *cnt;
+  int32_t *grow;
+  uint32_t *nsplit;   // ordered_offsets' list counters [0..3]
+  int32_t *tsum;      // its record-range base [0]
+  int32_t on;
+  int32_t pad;
 };
 
 // A side stream and two events for launches that run beside the context stream.

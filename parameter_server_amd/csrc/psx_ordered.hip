@@ -1248,7 +1248,7 @@ static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
 // Stage 1 of the ordered path (before any table of the call is applied): record lists by
 // slot, every validation, and the capacity dry run of sorted/map tables.
 hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st) {
-  hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
+  if (!a.counted) hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
   if (a.grow)
     hipLaunchKernelGGL(ordered_offsets_kernel, dim3(std::min(row_blocks(a.max_rows, 256), 256u)), dim3(256), 0, st, a);
   else

@@ -30,7 +30,7 @@ hipError_t launch_split_scatter(const SplitArgs &a, const int64_t *pos, const ui
                                 hipStream_t st);
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, uint64_t trace_items, hipStream_t st);
+                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, hipStream_t st);
 size_t walk_trace_offset(uint64_t items);
 size_t walk_ws_bytes(uint64_t items);
 // PSX_VARIANT_DECODE: 1 (default) walked messages with sparse tables decode window-parallel
@@ -38,6 +38,7 @@ size_t walk_ws_bytes(uint64_t items);
 int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
+int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: 1 = the walk's persistent grid on every CU (default: half)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
@@ -219,6 +220,8 @@ struct psx_ctx {
   uint64_t walk_last_items = 0;
   size_t walk_cap[2] = {0, 0};                    // bytes
   uint32_t walk_epoch[2] = {0, 0};                // granule tag of the slot's last call
+  psx::WalkCount *d_wcount = nullptr;             // walk-counted split tables (kMaxTables entries)
+  std::vector<psx::WalkCount> h_wcount;           // what d_wcount holds
   hipStream_t side = nullptr;                     // decode/index/verify stage
   hipStream_t aux = nullptr;                      // launches beside the context stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -598,13 +601,45 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     c->walk_last_slot = slot;
     c->walk_last_items = items;
   }
+  // Split sorted/map tables on a walked call whose decode is not pipelined: the walk does
+  // ordered_count's work as it writes the record offsets (WalkCount), and the ordered prep
+  // skips that launch.  (A pipelined walk runs beside the previous call's ordered work,
+  // which still uses the tables' counts.)
+  bool wcount = false;
+  if (walk && !pipelined && psx::g_walk_count) {
+    std::vector<psx::WalkCount> w(c->tables.size());
+    for (size_t ti = 0; ti < c->tables.size(); ++ti) {
+      TableState &t = c->tables[ti];
+      psx::WalkCount &x = w[ti];
+      std::memset(&x, 0, sizeof x);
+      if ((t.fast() && !force_ordered) || !t.split() || !psx::g_ord_split) continue;
+      x.row_offset = t.cfg.row_offset;
+      x.row_stride = t.cfg.row_stride;
+      x.max_rows = t.cfg.max_rows;
+      x.cnt = t.d_cnt;
+      x.grow = t.d_grow;
+      x.nsplit = t.d_nsplit;
+      x.tsum = t.d_tsum;
+      x.on = 1;
+      wcount = true;
+    }
+    if (wcount) {
+      if (!c->d_wcount) HIP_TRY(c, hipMalloc(&c->d_wcount, sizeof(psx::WalkCount) * psx::kMaxTables));
+      if (w.size() != c->h_wcount.size() || std::memcmp(w.data(), c->h_wcount.data(), sizeof(psx::WalkCount) * w.size())) {
+        c->h_wcount = w;   // the copy reads the context's own (persistent) vector
+        HIP_TRY(c, hipMemcpyAsync(c->d_wcount, c->h_wcount.data(), sizeof(psx::WalkCount) * w.size(),
+                                  hipMemcpyHostToDevice, prep));
+      }
+    }
+  }
   psx_status st = timed(
       c, "decode_streams",
       [&] {
         if (walk)
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
                                   c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
-                                  c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0, prep);
+                                  c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
+                                  wcount ? c->d_wcount : nullptr, prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -681,6 +716,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       a.split = t.d_split;
       a.nsplit = t.d_nsplit;
       a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
+      a.counted = wcount && c->h_wcount[ti].on ? 1 : 0;
     }
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
     if (st) return st;
@@ -1071,6 +1107,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->d_client_tabs) hipFree(c->d_client_tabs);
   if (c->d_pack) hipFree(c->d_pack);
   if (c->d_staging) hipFree(c->d_staging);
+  if (c->d_wcount) hipFree(c->d_wcount);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
   return PSX_OK;
@@ -2531,6 +2568,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
+    case PSX_VARIANT_WALK_COUNT: return &psx::g_walk_count;
     default: return nullptr;
   }
 }
@@ -2571,6 +2609,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
     if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);
+    if (const char *v = getenv("PSX_WALK_COUNT")) psx::g_walk_count = atoi(v);
   }
 } variant_env;
 }  // namespace

@@ -132,7 +132,7 @@ __device__ bool walk_header(const uint8_t *p, uint64_t size, const TableDir &dir
 
 __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir dir, Seg *segs, uint32_t *call_status,
                                                         uint32_t *counters, uint32_t *ntouched, WalkCtl *ctl,
-                                                        WalkHead *head) {
+                                                        WalkHead *head, const WalkCount *wc) {
   const int b = blockIdx.x;
   for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
     Seg s;
@@ -143,6 +143,11 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
     segs[b * kMaxTables + t] = s;
     counters[t * kMaxFused + b] = 0;
     if (b == 0) ntouched[t] = 0;
+    if (b == 0 && wc && t < dir.n && wc[t].on) {   // ordered_count's reset of ordered_offsets' counters
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wc[t].nsplit[i] = 0;
+      wc[t].tsum[0] = 0;
+    }
   }
   if (b == 0 && threadIdx.x == 0) {
     ctl->ticket = 0;
@@ -235,10 +240,30 @@ __device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
   }
 }
 
+// ordered_count for one record of a walk-counted split table (WalkCount): the record's row
+// id and pair count at p (a record the walk accepted: its header lies inside the message).
+__device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w, uint32_t *call_status) {
+  const int32_t rid = *reinterpret_cast<const int32_t *>(p);
+  const int32_t n = *reinterpret_cast<const int32_t *>(p + 4);
+  int64_t d = (int64_t)rid - w.row_offset;
+  bool ok = d >= 0;
+  if (ok && w.row_stride != 1) {
+    ok = d % w.row_stride == 0;
+    d /= w.row_stride;
+  }
+  if (!ok || d >= w.max_rows) {
+    atomicOr(call_status, kStRowRange);
+    return;
+  }
+  atomicAdd(&w.grow[d], n);
+  atomicAdd(&w.cnt[d], 1);
+}
+
 __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
                                                             uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
-                                                            uint32_t epoch, unsigned long long *trace) {
+                                                            uint32_t epoch, unsigned long long *trace,
+                                                            const WalkCount *wc) {
   gu64 *gran = (gu64 *)gran_p;
   // 96 KiB windows in 150 KiB of LDS, everything but the hand-off done before it.  wbuf
   // first holds the window's words; n16 keeps the clipped record count after each word
@@ -258,6 +283,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
   __shared__ uint16_t seg_q[kMaxSegs];
   __shared__ uint16_t seg_n[kMaxSegs];
   __shared__ uint64_t seg_rk[kMaxSegs];
+  __shared__ uint8_t seg_t[kMaxSegs];   // the segment's table (walk-counted tables: WalkCount)
   __shared__ uint16_t a16[kWW / 32 + 1], a1[16];
   __shared__ uint32_t sh_nseg, sh_n16, sh_n1, sh_ticket;
   const int tid = threadIdx.x;
@@ -432,6 +458,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                   seg_q[0] = (uint16_t)q;
                   seg_n[0] = (uint16_t)c;
                   seg_rk[0] = s.rk;
+                  seg_t[0] = (uint8_t)s.t;
                 }
                 nseg = 1;
                 s.rk += c;
@@ -480,6 +507,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
             seg_q[nseg] = (uint16_t)q;
             seg_n[nseg] = (uint16_t)take;
             seg_rk[nseg] = s.rk;
+            seg_t[nseg] = (uint8_t)s.t;
           }
           ++nseg;
           s.rk += take;
@@ -558,6 +586,18 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       const uint64_t r1 = rk + 16 * (uint64_t)nh;
       if (tid < n1) recoff[r1 + tid] = W0 + (uint64_t)a1[tid] * 4;
       __syncthreads();
+      // walk-counted tables: ordered_count's per-record work, one record per thread from
+      // the offsets just written (the block's own stores: visible after the barrier)
+      if (wc) {
+        const int t = seg_t[si];
+        if (wc[t].on) {
+          const uint32_t nrec = 16 * nh + n1;
+          for (uint32_t r = (uint32_t)tid; r < nrec; r += kWalkThreads) {
+            const uint64_t off = recoff[rk + r];
+            if (off + 8 <= size) walk_count(p + off, wc[t], call_status);
+          }
+        }
+      }
     }
     if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memrealtime();
   }
@@ -565,22 +605,23 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
 
 // ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 96 KiB window count);
 // epoch: nonzero, different from the previous call's on this workspace (granule tags);
-// trace_items: nonzero = write the per-item timestamps (the workspace's item count).
+// trace_items: nonzero = write the per-item timestamps (the workspace's item count);
+// wc: null, or per table (TableDir index) the walk-counted split tables' WalkCount.
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, uint64_t trace_items, hipStream_t st) {
+                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, hipStream_t st) {
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
   hipLaunchKernelGGL(walk_head_kernel, dim3(ss.n), dim3(256), 0, st, ss, dir, segs, call_status, counters, ntouched,
-                     ctl, head);
+                     ctl, head, wc);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   unsigned long long *trace =
       trace_items ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_trace_offset(trace_items))
                   : nullptr;
   hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
-                     head, gran, spec_wpr, epoch, trace);
+                     head, gran, spec_wpr, epoch, trace, wc);
   return hipGetLastError();
 }
 

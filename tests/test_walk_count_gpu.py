@@ -1,0 +1,150 @@
+"""The window-parallel walk doing ordered_count's work for split sorted/map tables
+(PSX_VARIANT_WALK_COUNT, WalkCount in psx_device.hpp): on walked calls whose decode is not
+pipelined the walk adds each record to cnt/grow as it writes the record's offset and the
+ordered prep launches no ordered_count.  Every form — walk-counted, ordered_count, and the
+pipelined decode (never walk-counted) — must give the oracle's rows byte for byte
+(SortedVectorMapStore, sorted_vector_map_store.hpp:175-197,305-337) over several calls, and a
+call that names a row outside the shard must fail with nothing applied and leave the counts
+clean for the next call (the reference rejects such a row: server_table.hpp FindRow/CreateRow
+on an unowned id)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import parameter_server_amd as psa
+from parameter_server_amd import wire, PsxError, _abi
+from oracle.oracle import OracleServer, SORTED_MAP, MAP, I32
+
+pytestmark = pytest.mark.gpu
+DECODE, WALK_CALLS, ORD_SPLIT, WALK_COUNT = 7, 8, 6, 13
+PIPELINE_ALL = 2
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built_lib, oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _batches(rng, rows, K, calls, per_batch=6_000, B=4):
+    p = 1.0 / np.arange(1, rows + 1)
+    p /= p.sum()
+    out = []
+    for c in range(calls):
+        msgs = []
+        for b in range(B):
+            ids = rng.choice(rows, size=per_batch, replace=False, p=p)
+            recs = []
+            for rid in ids:
+                k = int(rng.randint(1, 33))
+                cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+                v = (rng.randint(1, 4, size=k) * rng.choice([-1, 1], size=k)).astype(np.int32)
+                if c == 0:
+                    v = np.abs(v)
+                recs.append((int(rid), cols, v))
+            msgs.append(wire.sparse_stream_np(3, 4, recs))
+        out.append(msgs)
+    return out
+
+
+def _run(kind, calls, rows, K, walk_count, pipeline, split):
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, walk_count), L.psx_debug_set_variant(ORD_SPLIT, split),
+           L.psx_debug_set_variant(DECODE, 1)]
+    try:
+        bgs = [100, 101, 102, 103]
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(pipeline)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        L.psx_debug_set_variant(WALK_CALLS, 0)
+        snaps = []
+        for v, msgs in enumerate(calls):
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs]
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+            srv.sync()
+            snaps.append(srv.serialize_rows(3, list(range(rows))))
+        walked = L.psx_debug_get_variant(WALK_CALLS)
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(ORD_SPLIT, old[1])
+        L.psx_debug_set_variant(DECODE, old[2])
+    assert walked == len(calls)
+    return snaps
+
+
+@pytest.mark.parametrize("walk_count,pipeline", [(1, 0), (0, 0), (1, PIPELINE_ALL)],
+                         ids=["walk-counted", "ordered_count", "pipelined"])
+@pytest.mark.parametrize("split", [3, 1], ids=["spill-heavy-first", "concurrent"])
+def test_split_tables_counted_by_the_walk(walk_count, pipeline, split):
+    rng = np.random.RandomState(31)
+    rows, K = 12_000, 1024
+    calls = _batches(rng, rows, K, 3)
+    snaps = _run(SORTED_MAP, calls, rows, K, walk_count, pipeline, split)
+    orc = OracleServer([100, 101, 102, 103])
+    orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, [100, 101, 102, 103]):
+            assert orc.apply_stream(s, bg, v) == 0
+        assert snaps[v] == orc.serialize_records(3, list(range(rows))), f"call {v}"
+    orc.close()
+
+
+def test_map_table_walk_counted_matches_ordered_count():
+    rng = np.random.RandomState(32)
+    rows, K = 8_000, 512
+    calls = _batches(rng, rows, K, 2, per_batch=4_000)
+    a = _run(MAP, calls, rows, K, 1, 0, 3)
+    b = _run(MAP, calls, rows, K, 0, 0, 3)
+    assert a == b
+
+
+@pytest.mark.parametrize("walk_count", [1, 0], ids=["walk-counted", "ordered_count"])
+def test_row_outside_the_shard_fails_and_leaves_counts_clean(walk_count):
+    """A call with one record naming a row past the shard: PSX_ERR_ROW_RANGE, nothing of the
+    call applied; the next call (valid) must equal the oracle, so no count of the failed call
+    may survive it."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, walk_count), L.psx_debug_set_variant(DECODE, 1)]
+    rng = np.random.RandomState(33)
+    rows, K = 6_000, 1024
+    good = _batches(rng, rows, K, 2, per_batch=3_000, B=2)
+    bad = [list(m) for m in _batches(rng, rows, K, 1, per_batch=3_000, B=2)][0]
+    # the second message of the bad call: its records plus one for row `rows` (outside)
+    recs = [(5, np.array([1, 2], np.int32), np.array([1, 1], np.int32)),
+            (rows, np.array([3], np.int32), np.array([1], np.int32)),
+            (7, np.array([4], np.int32), np.array([2], np.int32))]
+    bad[1] = wire.sparse_stream_np(3, 4, recs)
+    bgs = [100, 101]
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.CreateTable(3, psa.TableInfo(row_kind=SORTED_MAP, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        orc = OracleServer(bgs)
+        orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+
+        def apply(msgs, v):
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs]
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+            srv.sync()
+
+        apply(good[0], 0)
+        for s, bg in zip(good[0], bgs):
+            assert orc.apply_stream(s, bg, 0) == 0
+        before = srv.serialize_rows(3, list(range(rows)))
+        with pytest.raises(PsxError):
+            apply(bad, 1)
+        assert srv.serialize_rows(3, list(range(rows))) == before
+        apply(good[1], 2)   # the failed call used version 1 on the device
+        for s, bg in zip(good[1], bgs):
+            assert orc.apply_stream(s, bg, 1) == 0   # the oracle never saw version 1
+        assert srv.serialize_rows(3, list(range(rows))) == orc.serialize_records(3, list(range(rows)))
+        srv.close()
+        orc.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(DECODE, old[1])

@@ -30,9 +30,9 @@ enum {
                                    (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
   PSX_DEBUG_WALK_TRACE = 11,    /* 1: walked calls record per-window timestamps (psx_debug_walk_trace) */
   PSX_VARIANT_WALK_CUS = 12,    /* the walk's persistent grid: 0 half the CUs (default), 1 every CU */
-  PSX_VARIANT_WALK_COUNT = 13   /* 1 (default): on walked calls whose decode is not pipelined, the walk
-                                   counts the records of split sorted/map tables (no ordered_count
-                                   launch); 0: ordered_count counts them */
+  PSX_VARIANT_WALK_COUNT = 13   /* 1 (default): on walked calls the walk counts the records of split
+                                   sorted/map tables into the call slot's count state (no
+                                   ordered_count launch); 0: ordered_count counts them */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -195,8 +195,8 @@ struct OrdArgs {
 // ordered_count's work for one split sorted/map table (grow set), done by the window-parallel
 // walk as it writes each record's offset (psx_walk.hip): per record cnt[slot] += 1 and
 // grow[slot] += its pairs, kStRowRange for a row outside the shard; walk_head zeroes
-// ordered_offsets' counters.  Only on calls whose decode is not pipelined (the walk then runs
-// after the previous call's ordered work on the same stream).
+// ordered_offsets' counters.  The pointers are the call slot's count state (a pipelined walk
+// runs beside the previous call's ordered work, which uses the other slot's).
 struct WalkCount {
   int64_t row_offset, row_stride, max_rows;
   int32_t *cnt;

@@ -124,9 +124,10 @@ struct TableState {
   uint8_t *d_entries = nullptr;    // sorted/map: [max_rows][max_entries] Entry<V>
   uint8_t *d_flags = nullptr;
   int32_t *d_inv[2] = {nullptr, nullptr};   // fast dense path inverse index, one per call slot
-  int32_t *d_cnt = nullptr;        // ordered path: per-slot counts (zero between calls)
+  int32_t *d_cnt = nullptr;        // ordered path: per-slot counts (zero between calls), [2][R] by call slot
   int32_t *d_off = nullptr;        // ordered path: exclusive prefix (max_rows + 1)
-  int32_t *d_tsum = nullptr;       // ordered path: scan tile sums
+  int32_t *d_tsum = nullptr;       // ordered path: scan tile sums, [2][tsum_slot] by call slot
+  int64_t tsum_slot = 0;
   int32_t *d_touched = nullptr;    // ordered path: touched slots (max_rows)
   uint32_t *d_keyflag = nullptr;   // sorted/map: a key outside [0, max_entries) was seen
   int32_t *d_grow = nullptr;       // split sorted/map tables: per-slot entry growth of a call
@@ -220,8 +221,8 @@ struct psx_ctx {
   uint64_t walk_last_items = 0;
   size_t walk_cap[2] = {0, 0};                    // bytes
   uint32_t walk_epoch[2] = {0, 0};                // granule tag of the slot's last call
-  psx::WalkCount *d_wcount = nullptr;             // walk-counted split tables (kMaxTables entries)
-  std::vector<psx::WalkCount> h_wcount;           // what d_wcount holds
+  psx::WalkCount *d_wcount[2] = {nullptr, nullptr};   // walk-counted split tables per call slot (kMaxTables entries)
+  std::vector<psx::WalkCount> h_wcount[2];             // what d_wcount[slot] holds
   hipStream_t side = nullptr;                     // decode/index/verify stage
   hipStream_t aux = nullptr;                      // launches beside the context stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -601,12 +602,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     c->walk_last_slot = slot;
     c->walk_last_items = items;
   }
-  // Split sorted/map tables on a walked call whose decode is not pipelined: the walk does
-  // ordered_count's work as it writes the record offsets (WalkCount), and the ordered prep
-  // skips that launch.  (A pipelined walk runs beside the previous call's ordered work,
-  // which still uses the tables' counts.)
+  // Split sorted/map tables on a walked call: the walk does ordered_count's work as it
+  // writes the record offsets (WalkCount), into this call slot's count state (a pipelined
+  // walk runs beside the previous call's ordered work, which uses the other slot's), and
+  // the ordered prep skips that launch.
   bool wcount = false;
-  if (walk && !pipelined && psx::g_walk_count) {
+  if (walk && psx::g_walk_count) {
     std::vector<psx::WalkCount> w(c->tables.size());
     for (size_t ti = 0; ti < c->tables.size(); ++ti) {
       TableState &t = c->tables[ti];
@@ -616,18 +617,21 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       x.row_offset = t.cfg.row_offset;
       x.row_stride = t.cfg.row_stride;
       x.max_rows = t.cfg.max_rows;
-      x.cnt = t.d_cnt;
-      x.grow = t.d_grow;
-      x.nsplit = t.d_nsplit;
-      x.tsum = t.d_tsum;
+      x.cnt = t.d_cnt + (int64_t)slot * t.cfg.max_rows;
+      x.grow = t.d_grow + (int64_t)slot * t.cfg.max_rows;
+      x.nsplit = t.d_nsplit + 5 * slot;
+      x.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
       x.on = 1;
       wcount = true;
     }
     if (wcount) {
-      if (!c->d_wcount) HIP_TRY(c, hipMalloc(&c->d_wcount, sizeof(psx::WalkCount) * psx::kMaxTables));
-      if (w.size() != c->h_wcount.size() || std::memcmp(w.data(), c->h_wcount.data(), sizeof(psx::WalkCount) * w.size())) {
-        c->h_wcount = w;   // the copy reads the context's own (persistent) vector
-        HIP_TRY(c, hipMemcpyAsync(c->d_wcount, c->h_wcount.data(), sizeof(psx::WalkCount) * w.size(),
+      std::vector<psx::WalkCount> &hw = c->h_wcount[slot];
+      if (!c->d_wcount[slot]) HIP_TRY(c, hipMalloc(&c->d_wcount[slot], sizeof(psx::WalkCount) * psx::kMaxTables));
+      if (w.size() != hw.size() || std::memcmp(w.data(), hw.data(), sizeof(psx::WalkCount) * w.size())) {
+        // a slot's contents change only with the tables: the copy reads the context's own
+        // (persistent) vector, and the slot's previous walk has finished on this stream
+        hw = w;
+        HIP_TRY(c, hipMemcpyAsync(c->d_wcount[slot], hw.data(), sizeof(psx::WalkCount) * w.size(),
                                   hipMemcpyHostToDevice, prep));
       }
     }
@@ -639,7 +643,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
                                   c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
                                   c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
-                                  wcount ? c->d_wcount : nullptr, prep);
+                                  wcount ? c->d_wcount[slot] : nullptr, prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -695,9 +699,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.row_stride = t.cfg.row_stride;
     a.max_rows = t.cfg.max_rows;
     a.recoff = c->d_recoff[slot];
-    a.cnt = t.d_cnt;
+    a.cnt = t.d_cnt + (int64_t)slot * t.cfg.max_rows;
     a.off = t.d_off;
-    a.tsum = t.d_tsum;
+    a.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
     a.list = c->d_list + list_region * ord_k++;
     a.touched = t.d_touched;
     a.ntouched = c->d_ntouched[slot] + ti;
@@ -712,11 +716,11 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.imp = t.d_imp;
     a.keyflag = t.d_keyflag;
     if (t.split() && psx::g_ord_split) {
-      a.grow = t.d_grow;
+      a.grow = t.d_grow + (int64_t)slot * t.cfg.max_rows;
       a.split = t.d_split;
-      a.nsplit = t.d_nsplit;
+      a.nsplit = t.d_nsplit + 5 * slot;
       a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
-      a.counted = wcount && c->h_wcount[ti].on ? 1 : 0;
+      a.counted = wcount && c->h_wcount[slot][ti].on ? 1 : 0;
     }
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
     if (st) return st;
@@ -1107,7 +1111,8 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->d_client_tabs) hipFree(c->d_client_tabs);
   if (c->d_pack) hipFree(c->d_pack);
   if (c->d_staging) hipFree(c->d_staging);
-  if (c->d_wcount) hipFree(c->d_wcount);
+  for (int k = 0; k < 2; ++k)
+    if (c->d_wcount[k]) hipFree(c->d_wcount[k]);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
   return PSX_OK;
@@ -1258,20 +1263,23 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
       if (e == hipSuccess) e = hipMemsetAsync(t.d_inv[k], 0xff, inv_bytes, c->stream);
     }
   }
-  if (e == hipSuccess) e = hipMalloc(&t.d_cnt, R * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMemsetAsync(t.d_cnt, 0, R * sizeof(int32_t), c->stream);
+  // the per-call count state twice, one per call slot: a pipelined walk counts the next
+  // call's records while this call's ordered work still uses its own (WalkCount)
+  if (e == hipSuccess) e = hipMalloc(&t.d_cnt, 2 * R * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(t.d_cnt, 0, 2 * R * sizeof(int32_t), c->stream);
   if (e == hipSuccess) e = hipMalloc(&t.d_off, (R + 1) * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&t.d_tsum, ntiles * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&t.d_tsum, 2 * ntiles * sizeof(int32_t));
+  t.tsum_slot = (int64_t)ntiles;
   if (e == hipSuccess) e = hipMalloc(&t.d_touched, R * sizeof(int32_t));
   if (e == hipSuccess && cfg->row_kind != PSX_ROW_DENSE) {
     e = hipMalloc(&t.d_keyflag, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_keyflag, 0, sizeof(uint32_t), c->stream);
   }
   if (e == hipSuccess && t.split()) {
-    e = hipMalloc(&t.d_grow, R * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, R * sizeof(int32_t), c->stream);
+    e = hipMalloc(&t.d_grow, 2 * R * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, 2 * R * sizeof(int32_t), c->stream);
     if (e == hipSuccess) e = hipMalloc(&t.d_split, 3 * R * 4 * sizeof(int32_t));   // int4 descriptors x 3 lists
-    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 5 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * 5 * sizeof(uint32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {

@@ -1,8 +1,8 @@
 """The window-parallel walk doing ordered_count's work for split sorted/map tables
-(PSX_VARIANT_WALK_COUNT, WalkCount in psx_device.hpp): on walked calls whose decode is not
-pipelined the walk adds each record to cnt/grow as it writes the record's offset and the
-ordered prep launches no ordered_count.  Every form — walk-counted, ordered_count, and the
-pipelined decode (never walk-counted) — must give the oracle's rows byte for byte
+(PSX_VARIANT_WALK_COUNT, WalkCount in psx_device.hpp): on walked calls the walk adds each
+record to the call slot's cnt/grow as it writes the record's offset and the ordered prep
+launches no ordered_count.  Every form — walk-counted, ordered_count, and walk-counted with
+the decode pipelined beside the previous call's ordered work — must give the oracle's rows byte for byte
 (SortedVectorMapStore, sorted_vector_map_store.hpp:175-197,305-337) over several calls, and a
 call that names a row outside the shard must fail with nothing applied and leave the counts
 clean for the next call (the reference rejects such a row: server_table.hpp FindRow/CreateRow
@@ -76,8 +76,8 @@ def _run(kind, calls, rows, K, walk_count, pipeline, split):
     return snaps
 
 
-@pytest.mark.parametrize("walk_count,pipeline", [(1, 0), (0, 0), (1, PIPELINE_ALL)],
-                         ids=["walk-counted", "ordered_count", "pipelined"])
+@pytest.mark.parametrize("walk_count,pipeline", [(1, 0), (0, 0), (1, PIPELINE_ALL), (0, PIPELINE_ALL)],
+                         ids=["walk-counted", "ordered_count", "pipelined-walk-counted", "pipelined-ordered_count"])
 @pytest.mark.parametrize("split", [3, 1], ids=["spill-heavy-first", "concurrent"])
 def test_split_tables_counted_by_the_walk(walk_count, pipeline, split):
     rng = np.random.RandomState(31)

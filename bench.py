@@ -37,7 +37,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-EXCHANGE_TIMEOUT_S = 180   # N > 1: the exchange extra is abandoned (headline kept) past this
+EXCHANGE_TIMEOUT_S = 420   # N > 1: the exchange extras are abandoned (headline kept, exit 3) past this
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 PMC_JSON = os.path.join(ROOT, "profiles", "r03", "pmc_dense_apply.json")
 
@@ -111,6 +111,10 @@ def parse():
                         "after the timed region (profiler passes)")
     p.add_argument("--master-port", type=int, default=29531,
                    help="rendezvous port when bench.py launches its own ranks (--gpus N, WORLD_SIZE unset)")
+    p.add_argument("--selftest-exchange", action="store_true",
+                   help="run exchange_measure's orchestration and parity check over gloo on the CPU "
+                        "(CpuShardExchange in place of the device path): the CPU test of the N > 1 extras")
+    p.add_argument("--selftest-reverse", action="store_true", help=argparse.SUPPRESS)   # the check's negative test
     p.add_argument("--selftest-launch", action="store_true",
                    help="exercise only the multi-rank harness (rank launch, barriers, max-over-ranks timing, "
                         "the JSON line) over gloo with a no-op step: the CPU test of --gpus N")
@@ -505,112 +509,286 @@ def run_c3(args):
     print(json.dumps(m), flush=True)
 
 
-def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242):
-    """The exchange-bearing step (SURVEY §8(d) C4 shape), through the product path: a dense
-    f32 table of rows_total x cap, row-range sharded over the ranks.  Per step every rank (one
-    worker) holds ONE full-coverage message over all rows_total rows in random order; it is
-    split per owner on the device (psx_split_stream: the client's per-server split,
-    abstract_bg_worker.cpp:590-649), the sub-streams cross GPUs in one all-to-all-v over
-    libpsx's own RCCL communicator (psx_exchange_*: grouped ncclSend/ncclRecv over xGMI),
-    and each owner applies the world_size messages it received in source-rank order in one
-    fused, order-preserving call (bit-exact vs sequential application).  The process group
-    (already up) only carries the communicator id.  Returns the measurement (max over ranks)."""
+def progress(msg, rank=0):
+    """A progress line on stderr (long runs must keep writing: the GPU box takes 3 silent
+    minutes for a hang)."""
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+C4_CHUNK_BYTES = (1 << 31) - 4   # a worker batch travels as Appendix-A messages of < 2 GiB (the
+                                 # reference reader's int32 cursor, serialized_oplog_reader.hpp:137)
+
+
+def _gen(dev, *key):
+    import torch
+    h = 0
+    for k in key:
+        h = (h * 1000003 + int(k)) % (1 << 62)
+    return torch.Generator(device=dev).manual_seed(h)
+
+
+def batch_perm(seed, w, rows_total, dev):
+    """Worker w's batch order: every table row once, in a random order."""
+    import torch
+    return torch.randperm(rows_total, generator=_gen(dev, seed, 1, w), device=dev).to(torch.int32)
+
+
+def batch_updates(seed, w, c, n, cap, dev):
+    """The N(0, 0.01) f32 updates of worker w's chunk c (n records), from their own seed."""
+    import torch
+    return torch.randn(n, cap, generator=_gen(dev, seed, 2, w, c), device=dev) * 0.01
+
+
+def shard_init(seed, o, shard, cap, dev):
+    """Owner o's initial rows, N(0, 0.1) (matrixfact_split.cpp:234-235)."""
+    import torch
+    return torch.randn(shard, cap, generator=_gen(dev, seed, 3, o), device=dev) * 0.1
+
+
+def batch_chunks(seed, w, rows_total, cap, dev, max_bytes):
+    """Worker w's batch as Appendix-A messages of at most max_bytes each: records in the
+    batch order, rpc records per message (the last takes the rest)."""
+    from parameter_server_amd import wire
+    rpc = (max_bytes - 20) // (4 + 4 * cap)
+    perm = batch_perm(seed, w, rows_total, dev)
+    chunks = []
+    for c, st in enumerate(range(0, rows_total, rpc)):
+        rows = perm[st:st + rpc]
+        chunks.append(wire.dense_stream_torch(1, rows, batch_updates(seed, w, c, rows.numel(), cap, dev)))
+    return chunks, rpc
+
+
+def expected_shard(seed, world, o, bounds, cap, rpc, rounds, dev):
+    """Owner o's rows after `rounds` steps, recomputed from the seeds alone (independent of
+    every byte the split and the exchange moved): its initial rows, then per step, per chunk
+    round c, per worker w in rank order — the order the owner's fused calls apply them in —
+    w's chunk-c records that fall in [bounds[o], bounds[o+1]) added in place (one f32 add per
+    element, as Server::ApplyOpLogUpdateVersion, server.cpp:154-178)."""
+    lo, hi = bounds[o], bounds[o + 1]
+    rows_total = bounds[-1]
+    exp = shard_init(seed, o, hi - lo, cap, dev)
+    perms = [batch_perm(seed, w, rows_total, dev) for w in range(world)]
+    nch = (rows_total + rpc - 1) // rpc
+    for _ in range(rounds):
+        for c in range(nch):
+            for w in range(world):
+                rows = perms[w][c * rpc:(c + 1) * rpc]
+                m = (rows >= lo) & (rows < hi)
+                if not bool(m.any()):
+                    continue
+                upd = batch_updates(seed, w, c, rows.numel(), cap, dev)
+                idx = (rows[m] - lo).long()
+                exp[idx] += upd[m]
+                del upd
+    return exp
+
+
+class CpuShardExchange:
+    """Stand-in of parameter_server_amd.exchange.ShardExchange for the gloo CPU harness
+    (`--selftest-exchange`): the same chunk rounds, the split by owner, the all-to-all (gloo)
+    and the in-order apply done with torch on the CPU.  Not a product path: it lets the
+    orchestration, the routing and the parity check of exchange_measure run on the CPU."""
+
+    reverse = False   # --selftest-reverse: apply the sources in reverse rank order (parity must catch it)
+
+    def __init__(self, init, bounds, rank, world):
+        self.table, self.bounds, self.rank, self.world = init.clone(), bounds, rank, world
+        self.chunks = 0
+        self.sent_bytes = self.recv_bytes = 0
+        self.split_s = self.wait_s = self.sync_s = self.x_ms = 0.0
+
+    def reset_counters(self):
+        self.__init__(self.table, self.bounds, self.rank, self.world)
+
+    def _split(self, msg):
+        import torch
+        recs = msg[20:].view(torch.int32).view(-1, 1 + self.table.shape[1])
+        own = torch.bucketize(recs[:, 0].long(), torch.tensor(self.bounds[1:-1]), right=True)
+        parts, sizes = [], []
+        for o in range(self.world):
+            sub = recs[own == o]
+            if sub.shape[0] == 0:
+                sizes.append(0)
+                continue
+            hdr = torch.tensor([1, 1, 4, 0, sub.shape[0]], dtype=torch.int32)
+            parts.append(torch.cat([hdr, sub.reshape(-1)]).view(torch.uint8))
+            sizes.append(parts[-1].numel())
+        return (torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8)), sizes
+
+    def run(self, chunks, log=None):
+        import torch
+        from parameter_server_amd.exchange import alltoall_streams
+        lo = self.bounds[self.rank]
+        for msg in chunks:
+            send, sizes = self._split(msg)
+            recv, rs = alltoall_streams(send, sizes)
+            offs = [sum(rs[:w]) for w in range(self.world)]
+            for w in (reversed(range(self.world)) if self.reverse else range(self.world)):
+                if rs[w]:
+                    sub = recv[offs[w]:offs[w] + rs[w]]
+                    n = int(sub[16:20].view(torch.int32).item())
+                    recs = sub[20:].view(torch.int32).view(n, -1)
+                    idx = (recs[:, 0] - lo).long()
+                    self.table[idx] += recs[:, 1:].view(torch.float32)
+            self.chunks += 1
+            self.sent_bytes += sum(sizes)
+            self.recv_bytes += sum(rs)
+
+    def read_table(self):
+        return self.table
+
+    def close(self):
+        pass
+
+
+def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242, backend="psx",
+                     max_bytes=C4_CHUNK_BYTES):
+    """The exchange-bearing step, self-checked.  A dense f32 table of
+    rows_total x cap, row-range sharded over the ranks (initial rows N(0, 0.1)).  Every rank is
+    one worker whose batch covers every row once in a random order (updates N(0, 0.01)),
+    carried as Appendix-A messages of < 2 GiB.  Per step each rank pushes its batch through
+    ShardExchange (psx): per chunk, device split per owner (psx_split_stream_formats), sizes
+    and bytes over libpsx's RCCL communicator, the owner's fused in-order apply — chunk k's
+    exchange beside chunk k-1's apply.  After the timed steps every owner compares its shard
+    bit for bit with expected_shard(), recomputed from the seeds (never from the delivered
+    bytes): `parity` is "bit-exact" or the count of differing values over all ranks.
+    backend "cpu": the same orchestration with CpuShardExchange under gloo (CPU tests)."""
     import torch
     import torch.distributed as dist
-    import parameter_server_amd as psa
-    from parameter_server_amd import wire
-    from parameter_server_amd.exchange import Exchange, split
+    cpu = backend == "cpu"
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local)
+    assert rows_total % world == 0, "row-range shards of equal size"
     shard = rows_total // world
-    g = torch.Generator(device="cuda").manual_seed(seed + rank)
-    perm = torch.randperm(shard * world, device="cuda", generator=g).to(torch.int32)
-    upd = torch.randn(shard * world, cap, device="cuda", generator=g) * 0.01
-    msg = wire.dense_stream_torch(1, perm, upd)
-    del upd, perm
-    torch.cuda.empty_cache()
-    bgs = [100 + w for w in range(world)]
     bounds = [w * shard for w in range(world + 1)]
-    srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
-    srv.set_stream(torch.cuda.current_stream().cuda_stream)
-    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
-                                     row_offset=rank * shard, max_rows=shard))
-    # the splitter: a context with the same table over every row (record formats only)
-    spl = psa.Server(device=local, server_id=900 + rank, bg_ids=[1])
-    spl.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
-                                     max_rows=shard * world))
-    xc = Exchange(local) if world > 1 else None
-    ver = [0]
-    t_split, t_x = [0.0], [0.0]
-
-    def step():
-        t0 = time.perf_counter()
-        parts, sizes = spl.split_stream(msg, bounds)
+    lo = bounds[rank]
+    t_gen = time.perf_counter()
+    progress(f"exchange_measure {rows_total} x {cap}, world {world}: generating", rank)
+    chunks, rpc = batch_chunks(seed, rank, rows_total, cap, dev, max_bytes)
+    init = shard_init(seed, rank, shard, cap, dev)
+    bgs = [100 + w for w in range(world)]
+    xc = srv = None
+    if cpu:
+        ex = CpuShardExchange(init, bounds, rank, world)
+    else:
+        import parameter_server_amd as psa
+        from parameter_server_amd.exchange import Exchange, ShardExchange
+        srv = psa.Server(device=local, server_id=1 + rank, bg_ids=bgs)
+        info = psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, row_offset=lo, max_rows=shard)
+        srv.CreateTable(1, info)
+        srv.load_rows(1, lo, None, on_device_ptr=init.data_ptr(), num_rows=shard)
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if xc is not None:
-            recv, rs = xc.alltoall(parts, sizes)
-            torch.cuda.synchronize()
-            msgs = split(recv, rs)
-        else:
-            msgs = [parts]
-        t2 = time.perf_counter()
-        t_split[0] += t1 - t0
-        t_x[0] += t2 - t1
-        srv.apply_device([(m.data_ptr(), m.numel(), bgs[w], ver[0]) for w, m in enumerate(msgs)])
-        srv.sync()
-        ver[0] += 1
+        xc = Exchange(local)
+        ex = ShardExchange(srv, 1, info, bounds, bgs, xc, local)
+    del init
+    if not cpu:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    gen_s = time.perf_counter() - t_gen
 
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    progress(f"{len(chunks)} chunks of {rpc} records; warmup", rank)
+    verbose = (lambda m: progress(m, rank)) if os.environ.get("PSX_BENCH_VERBOSE") else None
     for _ in range(warmup):
-        step()
-    t_split[0] = t_x[0] = 0.0
-    srv.timing(True)
-    srv.timing_reset()
+        ex.run(chunks, log=verbose)
+        sync()
+        progress("warmup step done", rank)
+    ex.reset_counters()
+    if srv is not None:
+        srv.timing(2)
+        srv.timing_reset()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
+        ex.run(chunks)
+    sync()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    apply_ms, apply_n = srv.timing_read("dense_apply")
-    idx_ms, _ = srv.timing_read("dense_index")
-    per_rank_stream = msg.numel()
-    srv.close()
-    spl.close()
+    progress(f"{steps} timed steps in {el:.3f} s; checking parity", rank)
+    apply_ms, apply_n = srv.timing_read("dense_apply") if srv is not None else (0.0, 0)
+    hbm_used = None
+    if not cpu:
+        free, total = torch.cuda.mem_get_info(local)
+        hbm_used = total - free
+    msg_bytes = sum(c.numel() for c in chunks)
+    nchunks = len(chunks)
+    del chunks
+    # parity: the owner's shard against the seeds
+    t_chk = time.perf_counter()
+    if srv is not None:
+        got = torch.empty(shard, cap, dtype=torch.float32, device=dev)
+        srv.read_rows_device(1, lo, shard, got)
+    else:
+        got = ex.read_table()
+    exp = expected_shard(seed, world, rank, bounds, cap, rpc, warmup + steps, dev)
+    ndiff = int((got.view(torch.int32) != exp.view(torch.int32)).sum().item())
+    del got, exp
+    chk_s = time.perf_counter() - t_chk
+    st = dict(split_s=ex.split_s, wait_s=ex.wait_s, sync_s=ex.sync_s, x_ms=ex.x_ms, chunks=ex.chunks,
+              sent=ex.sent_bytes, recv=ex.recv_bytes)
+    ex.close()
+    if srv is not None:
+        srv.close()
     if xc is not None:
         xc.close()
-    del msg
-    torch.cuda.empty_cache()
+    if not cpu:
+        torch.cuda.empty_cache()
+    vals = [el, st["split_s"], st["wait_s"], st["sync_s"], st["x_ms"], apply_ms / max(apply_n, 1), gen_s, chk_s,
+            float(hbm_used or 0)]
+    sums = [float(ndiff), float(st["recv"])]
     if world > 1:
-        t = torch.tensor([el, t_x[0], t_split[0]], device="cuda", dtype=torch.float64)
+        t = torch.tensor(vals, dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, t_x[0], t_split[0] = (float(x) for x in t.tolist())
-    apply_bytes = per_rank_stream + 2 * shard * cap * 4    # per owner per step (same totals)
-    sent = per_rank_stream * (world - 1) / world
+        vals = t.tolist()
+        t = torch.tensor(sums, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        sums = t.tolist()
+    el, split_s, wait_s, sync_s, x_ms, apply_ms, gen_s, chk_s, hbm_used = vals
+    ndiff, recv_all = int(sums[0]), sums[1]
+    per_step = el / steps
+    # algorithmic bytes per step, all owners: the received records once + every row read and
+    # written once (SURVEY §8(d) C4 "reduced payload + 2 x RMW", with the payload the N
+    # workers' records — the all-to-all form, DESIGN.md §7)
+    apply_bytes = recv_all / steps + 2.0 * rows_total * cap * 4
+    xbytes = msg_bytes * (world - 1) / world          # per rank per step, crossing xGMI
     return {
-        "value": round(apply_bytes * world * steps / el / 1e9, 2), "unit": "GB/s (algorithmic, all ranks)",
+        "value": round(apply_bytes / per_step / 1e9, 2), "unit": "GB/s (algorithmic apply bytes, all ranks)",
         "n_gpus": world, "steps": steps, "warmup": warmup,
-        "ms_per_step": round(el / steps * 1e3, 3),
-        "split_ms_per_step": round(t_split[0] / steps * 1e3, 3),
-        "exchange_ms_per_step": round(t_x[0] / steps * 1e3, 3),
-        # nccl-tests all-to-all convention: algbw = bytes per rank / time, busbw =
-        # algbw * (n-1)/n (the bytes that actually cross xGMI per rank)
-        "exchange_algbw_GBps": round(per_rank_stream * steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
-        "exchange_busbw_GBps": round(sent * steps / t_x[0] / 1e9, 2) if world > 1 and t_x[0] > 0 else None,
-        "apply_kernel_ms": round(apply_ms / max(apply_n, 1), 3),
-        "index_kernel_ms": round(idx_ms / max(apply_n, 1), 3),
+        "ms_per_step": round(per_step * 1e3, 3),
+        "parity": "bit-exact" if ndiff == 0 else f"{ndiff} values differ",
+        "parity_check": "every owner's shard vs an in-order f32 sum recomputed from the seeds "
+                        "(expected_shard), bit for bit, after warmup + steps rounds",
+        "chunks_per_step": nchunks, "records_per_chunk": rpc,
+        "split_host_ms_per_step": round(split_s / steps * 1e3, 3),
+        "exchange_wait_ms_per_step": round(wait_s / steps * 1e3, 3),
+        "apply_wait_ms_per_step": round(sync_s / steps * 1e3, 3),
+        "exchange_kernel_ms_per_step": round(x_ms / steps, 3) if not cpu else None,
+        # nccl-tests all-to-all convention: algbw = bytes a rank sends / time, busbw = the
+        # share that crosses the links, (n-1)/n of it
+        "exchange_algbw_GBps": round(msg_bytes / (x_ms / steps / 1e3) / 1e9, 2) if x_ms > 0 else None,
+        "exchange_busbw_GBps": round(xbytes / (x_ms / steps / 1e3) / 1e9, 2) if x_ms > 0 and world > 1 else None,
+        "apply_kernel_ms_per_chunk": round(apply_ms, 3) if apply_ms else None,
+        "hbm_used_GB_max_rank": round(hbm_used / 1e9, 2) if hbm_used else None,
+        "setup_s": round(gen_s, 2), "check_s": round(chk_s, 2),
         "config": {"workload": f"{rows_total} rows x {cap} f32, row-range shards x{world}",
-                   "shard_rows": shard, "stream_bytes_per_rank": per_rank_stream,
-                   "parallelism": f"{world} shards; per step: device split per owner (psx_split_stream), "
-                                  f"libpsx RCCL all-to-all-v (psx_exchange_*), fused apply"},
+                   "shard_rows": shard, "batch_bytes_per_rank": msg_bytes,
+                   "parallelism": f"{world} shards; per chunk: device split per owner (psx_split_stream_formats), "
+                                  f"libpsx RCCL all-to-all-v (psx_exchange_sizes_async / psx_exchange_streams), "
+                                  f"fused in-order apply; chunk k's exchange beside chunk k-1's apply"
+                                  if not cpu else f"{world} shards over gloo (CPU stand-in)"},
     }
 
 
 def run_c4(args):
     """a dense f32 gradient table of c4_rows x 1024, row-range sharded
-    over the ranks, one all-to-all exchange per step (exchange_measure)."""
+    over the ranks; every rank's batch spans every shard (exchange_measure).  N = 1 is the
+    same pipeline with a one-rank (self) exchange."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -627,6 +805,25 @@ def run_c4(args):
         line.update({"higher_is_better": True, "scaling": "strong", "dtype": "f32",
                      "data": "synthetic (GPU-generated N(0,0.01) gradients, full coverage, random row order)"})
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def selftest_exchange(args):
+    """exchange_measure's orchestration and parity check under gloo on the CPU (world 2 in
+    tests/test_bench_launch.py), with CpuShardExchange in place of the device path and
+    messages small enough that a batch takes several chunks."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    CpuShardExchange.reverse = args.selftest_reverse
+    m = exchange_measure(4096 * world, 16, args.steps, args.warmup, world, rank, 0, backend="cpu",
+                         max_bytes=20 + 68 * 1000)
+    if rank == 0:
+        m["metric"] = "selftest-exchange"
+        print(json.dumps(m), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -988,6 +1185,8 @@ def main():
         sys.exit(launch_ranks(args))
     if args.selftest_launch:
         return selftest_launch(args)
+    if args.selftest_exchange:
+        return selftest_exchange(args)
     if args.workload == "c5":
         return run_c5(args)
     if args.workload == "c3":
@@ -1221,11 +1420,11 @@ def main():
     srv.close()
     del streams, record_rows
     torch.cuda.empty_cache()
-    other, exchange = None, None
+    other, exchange, c4 = None, None, None
     if extras and world > 1:
-        # The exchange extra must never cost the headline: if it has not finished within
-        # EXCHANGE_TIMEOUT_S (a collective that never completes, say), rank 0 prints the
-        # line without it and every rank leaves.
+        # The exchange extras must never cost the headline: if they have not finished within
+        # EXCHANGE_TIMEOUT_S (a collective that never completes, say), rank 0 prints the line
+        # without them and every rank exits with status 3, so the launcher sees the hang.
         import threading
         done = threading.Event()
 
@@ -1236,18 +1435,28 @@ def main():
                 ln = build_line(None)
                 if walked:
                     ln["walked"] = walked
-                ln["exchange"] = {"error": f"not finished within {EXCHANGE_TIMEOUT_S} s: abandoned"}
+                if exchange:
+                    ln["exchange"] = exchange
+                ln["c4" if exchange else "exchange"] = {"error": f"not finished within {EXCHANGE_TIMEOUT_S} s: abandoned"}
                 print(json.dumps(ln), flush=True)
             sys.stdout.flush()
-            os._exit(0)
+            sys.stderr.flush()
+            os._exit(3)
         threading.Thread(target=watchdog, daemon=True).start()
         try:
-            exchange = exchange_measure(world * rows, cap, min(args.steps, 10), 2, world, rank, local)
-            exchange["what"] = ("a worker batch spanning every shard: per-owner sub-streams of each rank's full-coverage "
-                                "batch, one RCCL all-to-all over xGMI, then the owner's fused apply of the N messages "
-                                "in source-rank order (C4's step at C2's row width)")
+            exchange = exchange_measure(world * rows, cap, 3, 1, world, rank, local)
+            exchange["what"] = ("a worker batch spanning every shard at C2's row width: per chunk, the device split "
+                                "per owner, one RCCL all-to-all over xGMI, the owner's fused in-order apply; "
+                                "parity against the seeds")
         except Exception as e:   # reported, never allowed to drop the headline line
             exchange = {"error": repr(e)[:400]}
+        try:
+            c4 = exchange_measure(args.c4_rows, 1024, 3, 1, world, rank, local)
+            c4["what"] = ("SURVEY C4: the 10M x 1024 f32 table row-range sharded over the ranks, every rank's batch "
+                          "spanning every shard (< 2 GiB messages), exchanged and applied per chunk; parity against "
+                          "the seeds")
+        except Exception as e:
+            c4 = {"error": repr(e)[:400]}
         done.set()
     if extras and world == 1:
         # C3 in child processes (`bench.py --workload c3`), so its device memory and state
@@ -1270,6 +1479,7 @@ def main():
                 other[name] = {"error": repr(e)[:400]}
         for name, flags in (("C4_shard_1gpu", ["--workload", "c4shard", "--steps", "5", "--warmup", "2",
                                                "--cpu-seconds", cs]),
+                            ("C4_pipeline_1gpu", ["--workload", "c4", "--steps", "3", "--warmup", "1"]),
                             ("C5", ["--workload", "c5", "--steps", "10", "--warmup", "2", "--cpu-seconds", cs])):
             try:
                 m = run_child(flags, timeout=400)
@@ -1288,6 +1498,8 @@ def main():
             line["pcie_inclusive"] = pcie
         if exchange:
             line["exchange"] = exchange
+        if c4:
+            line["c4"] = c4
         if other:
             line["other_configs"] = other
         print(json.dumps(line), flush=True)

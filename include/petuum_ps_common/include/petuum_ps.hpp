@@ -8,4 +8,6 @@
 #include <petuum_ps_common/storage/dense_row.hpp>
 #include <petuum_ps_common/storage/sorted_vector_map_row.hpp>
 #include <petuum_ps_common/storage/sparse_row.hpp>
+#include <petuum_ps_common/util/utils.hpp>
+#include <petuum_ps_common/util/stats.hpp>
 #include <petuum_ps_common/util/high_resolution_timer.hpp>

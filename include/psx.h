@@ -94,7 +94,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 6
+#define PSX_ABI_VERSION 7
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -510,6 +510,18 @@ psx_status psx_pack_stream_indexed(psx_ctx *ctx, const psx_pack_table *tables, i
 psx_status psx_split_stream(psx_ctx *ctx, const void *stream, size_t size, const uint64_t *record_offsets,
                             int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
                             uint64_t *out_sizes);
+/* ABI 7: psx_split_stream with the record formats given by the caller instead of the
+ * context's tables — the client side of the split needs only each table's record format
+ * (TableInfo's dtype, row kind, oplog_dense_serialized, dense_row_oplog_capacity,
+ * version_maintain, row_oplog_type; the reference client's sample row oplog,
+ * server_table.cpp:56-67), not a server table.  formats[i] is checked as psx_table_create
+ * checks those fields; the shard geometry (row_offset, row_stride, max_rows) is ignored and
+ * nothing is allocated for rows.  ctx supplies the device, the stream and the split's
+ * scratch.  A message whose tables are all dense-serialized needs no record-offset buffer. */
+psx_status psx_split_stream_formats(psx_ctx *ctx, const psx_table_config *formats, int32_t nformats,
+                                    const void *stream, size_t size, const uint64_t *record_offsets,
+                                    int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
+                                    uint64_t *out_sizes);
 
 /* The exchange (RCCL over xGMI, one process per GPU): replaces the reference's ZeroMQ
  * transport of per-server messages (SendOpLogMsgs, abstract_bg_worker.cpp:651-689 ->
@@ -531,6 +543,31 @@ const char *psx_comm_last_error(psx_comm *comm);
 psx_status psx_exchange_sizes(psx_comm *comm, const uint64_t *send_sizes, uint64_t *recv_sizes, void *hip_stream);
 psx_status psx_exchange_streams(psx_comm *comm, const void *send, const uint64_t *send_sizes, void *recv,
                                 const uint64_t *recv_sizes, void *hip_stream);
+/* ABI 7: psx_exchange_sizes without the synchronization, so that a pipelined caller can
+ * enqueue chunk k+1's sizes behind chunk k's bytes: send_sizes is copied before the call
+ * returns; recv_sizes (page-locked host memory, else PSX_ERR_INVALID_ARG) is written by
+ * hip_stream and valid once the stream has passed this call (an event recorded after it,
+ * or hipStreamSynchronize).  Same collective as psx_exchange_sizes (every rank calls it in
+ * the same order). */
+psx_status psx_exchange_sizes_async(psx_comm *comm, const uint64_t *send_sizes, uint64_t *recv_sizes,
+                                    void *hip_stream);
+
+/* ---- server statistics ------------------------------------------------------------ */
+/* ABI 7: what the reference server thread accumulates around each apply with
+ * STATS_SERVER_ACCUM_APPLY_OPLOG_BEGIN/END (server_thread.cpp:240-244 ->
+ * server_accum_apply_oplog_sec / server_accum_oplog_recv_mb, stats.cpp:1153-1162), per
+ * context, since its creation or the last reset.  Always on (two events per call). */
+typedef struct psx_apply_stats {
+  uint64_t calls;          /* apply calls accepted (psx_apply_stream and the device forms) */
+  uint64_t messages;       /* ClientSendOpLogMsg payloads in them */
+  uint64_t oplog_bytes;    /* their payload bytes (server_accum_oplog_recv_mb = oplog_bytes / 2^20) */
+  double apply_sec;        /* server_accum_apply_oplog_sec: per settled call, the device time from its
+                              first stage to its finish, summed (pipelined calls overlap: each counts
+                              its own span; a duplicate-row replay, run inside psx_sync, is not in it) */
+  uint64_t settled_calls;  /* calls whose span is in apply_sec (those settled by a psx_sync) */
+} psx_apply_stats;
+/* Copy the statistics into *out (may be NULL); reset != 0 zeroes them afterwards. */
+psx_status psx_ctx_stats(psx_ctx *ctx, psx_apply_stats *out, int32_t reset);
 
 /* ---- diagnostics ---------------------------------------------------------------- */
 const char *psx_last_error(psx_ctx *ctx);

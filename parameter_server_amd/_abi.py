@@ -108,6 +108,11 @@ PUSH_MSG_HEADER_BYTES = 37
 COMPAT_INT32_STREAM_OFFSETS = 1
 
 
+class psx_apply_stats(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("messages", ctypes.c_uint64), ("oplog_bytes", ctypes.c_uint64),
+                ("apply_sec", ctypes.c_double), ("settled_calls", ctypes.c_uint64)]
+
+
 class PsxError(RuntimeError):
     def __init__(self, status, msg):
         self.status = status
@@ -185,13 +190,16 @@ def load():
         "psx_timing_enable": ([vp, i32], ctypes.c_int),
         "psx_timing_read": ([vp, ctypes.c_char_p, P(ctypes.c_double), P(i64)], ctypes.c_int),
         "psx_timing_reset": ([vp], ctypes.c_int),
+        "psx_ctx_stats": ([vp, P(psx_apply_stats), i32], ctypes.c_int),
         "psx_split_stream": ([vp, vp, sz, vp, i32, vp, vp, sz, vp], ctypes.c_int),
+        "psx_split_stream_formats": ([vp, P(psx_table_config), i32, vp, sz, vp, i32, vp, vp, sz, vp], ctypes.c_int),
         "psx_comm_unique_id": ([vp], ctypes.c_int),
         "psx_comm_create": ([vp, i32, i32, i32, P(vp)], ctypes.c_int),
         "psx_comm_destroy": ([vp], ctypes.c_int),
         "psx_comm_last_error": ([vp], ctypes.c_char_p),
         "psx_exchange_sizes": ([vp, vp, vp, vp], ctypes.c_int),
         "psx_exchange_streams": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "psx_exchange_sizes_async": ([vp, vp, vp, vp], ctypes.c_int),
         "psx_debug_set_variant": ([i32, i32], i32),
         "psx_debug_get_variant": ([i32], i32),
         "psx_debug_walk_trace": ([vp, vp, ctypes.c_int64], ctypes.c_int64),

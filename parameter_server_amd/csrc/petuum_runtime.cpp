@@ -42,6 +42,7 @@
 
 #include <petuum_ps_common/include/abstract_server_table_logic.hpp>
 #include <petuum_ps_common/include/ps_table_group.hpp>
+#include <petuum_ps_common/util/stats.hpp>
 
 #include "psx.h"
 
@@ -578,6 +579,26 @@ class Runtime {
 
   TableGroupConfig cfg_;
   int C_ = 1;
+
+ public:
+  // STATS_SERVER_ACCUM_APPLY_OPLOG_* of every shard context (psx_ctx_stats), summed
+  ServerApplyStatsSum ServerApplyStats() {
+    std::lock_guard<std::mutex> g(mtx_);
+    ServerApplyStatsSum sum;
+    for (auto &s : shards_) {
+      psx_apply_stats st{};
+      if (s.ctx && psx_ctx_stats(s.ctx, &st, 0) == PSX_OK) {
+        sum.calls += st.calls;
+        sum.messages += st.messages;
+        sum.oplog_bytes += st.oplog_bytes;
+        sum.settled_calls += st.settled_calls;
+        sum.apply_sec += st.apply_sec;
+      }
+    }
+    return sum;
+  }
+
+ private:
   std::vector<int32_t> devices_;
   std::vector<Shard> shards_;
   std::map<int32_t, std::unique_ptr<ClientTableImpl>> tables_;
@@ -833,6 +854,7 @@ int32_t RegisterThread() { return g_rt->RegisterThread(); }
 void DeregisterThread() { g_rt->DeregisterThread(); }
 void Clock() { g_rt->Clock(); }
 void GlobalBarrier() { g_rt->GlobalBarrier(); }
+ServerApplyStatsSum ServerApplyStats() { return g_rt ? g_rt->ServerApplyStats() : ServerApplyStatsSum{}; }
 
 }  // namespace runtime
 }  // namespace petuum

@@ -22,10 +22,17 @@
 
 #include "../../include/psx.h"
 
+// psx_exchange_sizes_async stages the send sizes through a ring of page-locked slots, so a
+// call returns before its sizes have crossed: slot k is reused only after its event.
+constexpr int kSizeSlots = 8;
+
 struct psx_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0, device = 0;
-  uint64_t *d_sizes = nullptr;   // [2][nranks]: send sizes, received sizes
+  uint64_t *d_sizes = nullptr;   // [1 + kSizeSlots][2][nranks]: send sizes, received sizes
+  uint64_t *h_send = nullptr;    // [kSizeSlots][nranks], page-locked
+  hipEvent_t ev[kSizeSlots] = {};
+  int next_slot = 0;
   std::string err;
 };
 
@@ -84,12 +91,20 @@ psx_status psx_comm_create(const void *id, int32_t nranks, int32_t rank, int32_t
   c->device = device;
   auto cleanup = [&](psx_status st) {
     if (c->d_sizes) hipFree(c->d_sizes);
+    if (c->h_send) hipHostFree(c->h_send);
+    for (hipEvent_t &e : c->ev)
+      if (e) hipEventDestroy(e);
     delete c;
     return st;
   };
   if (hipSetDevice(device) != hipSuccess) return cleanup(comm_fail(nullptr, "hipSetDevice", PSX_ERR_NO_DEVICE));
-  if (hipMalloc(&c->d_sizes, sizeof(uint64_t) * 2 * (size_t)nranks) != hipSuccess)
+  if (hipMalloc(&c->d_sizes, sizeof(uint64_t) * 2 * (size_t)nranks * (1 + kSizeSlots)) != hipSuccess)
     return cleanup(comm_fail(nullptr, "hipMalloc", PSX_ERR_OOM));
+  if (hipHostMalloc(&c->h_send, sizeof(uint64_t) * (size_t)nranks * kSizeSlots, 0) != hipSuccess)
+    return cleanup(comm_fail(nullptr, "hipHostMalloc", PSX_ERR_OOM));
+  for (hipEvent_t &e : c->ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return cleanup(comm_fail(nullptr, "hipEventCreate", PSX_ERR_DEVICE));
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
@@ -102,7 +117,13 @@ psx_status psx_comm_destroy(psx_comm *c) {
   if (!c) return PSX_ERR_INVALID_ARG;
   hipSetDevice(c->device);
   if (c->comm) ncclCommDestroy(c->comm);
+  for (hipEvent_t &e : c->ev)
+    if (e) {
+      hipEventSynchronize(e);
+      hipEventDestroy(e);
+    }
   if (c->d_sizes) hipFree(c->d_sizes);
+  if (c->h_send) hipHostFree(c->h_send);
   delete c;
   return PSX_OK;
 }
@@ -125,6 +146,39 @@ psx_status psx_exchange_sizes(psx_comm *c, const uint64_t *send_sizes, uint64_t 
   NCCL_TRY(c, ncclGroupEnd());
   HIPX_TRY(c, hipMemcpyAsync(recv_sizes, c->d_sizes + n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
   HIPX_TRY(c, hipStreamSynchronize(st));
+  return PSX_OK;
+}
+
+psx_status psx_exchange_sizes_async(psx_comm *c, const uint64_t *send_sizes, uint64_t *recv_sizes,
+                                    void *hip_stream) {
+  if (!c || !send_sizes || !recv_sizes) return PSX_ERR_INVALID_ARG;
+  for (int i = 0; i < c->nranks; ++i)
+    if (send_sizes[i] % 4) return comm_fail(c, "sub-stream sizes are multiples of 4 bytes", PSX_ERR_INVALID_ARG);
+  HIPX_TRY(c, hipSetDevice(c->device));
+  // recv_sizes is written by the stream: it must be page-locked for the copy to stay
+  // asynchronous (a pageable destination would make the copy wait for the collective)
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, recv_sizes) != hipSuccess || at.type != hipMemoryTypeHost) {
+    (void)hipGetLastError();
+    return comm_fail(c, "exchange_sizes_async: recv_sizes must be page-locked host memory", PSX_ERR_INVALID_ARG);
+  }
+  hipStream_t st = (hipStream_t)hip_stream;
+  const size_t n = (size_t)c->nranks;
+  const int k = c->next_slot;
+  c->next_slot = (k + 1) % kSizeSlots;
+  HIPX_TRY(c, hipEventSynchronize(c->ev[k]));   // the slot's previous sizes have crossed
+  uint64_t *hs = c->h_send + (size_t)k * n;
+  std::memcpy(hs, send_sizes, sizeof(uint64_t) * n);
+  uint64_t *ds = c->d_sizes + 2 * n * (size_t)(1 + k);
+  HIPX_TRY(c, hipMemcpyAsync(ds, hs, sizeof(uint64_t) * n, hipMemcpyHostToDevice, st));
+  NCCL_TRY(c, ncclGroupStart());
+  for (int p = 0; p < c->nranks; ++p) {
+    NCCL_TRY_G(c, ncclSend(ds + p, 1, ncclUint64, p, c->comm, st));
+    NCCL_TRY_G(c, ncclRecv(ds + n + p, 1, ncclUint64, p, c->comm, st));
+  }
+  NCCL_TRY(c, ncclGroupEnd());
+  HIPX_TRY(c, hipMemcpyAsync(recv_sizes, ds + n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
+  HIPX_TRY(c, hipEventRecord(c->ev[k], st));
   return PSX_OK;
 }
 

@@ -188,6 +188,7 @@ void free_table(TableState &t) {
 struct PendingCall {
   std::vector<psx_stream> streams;
   int ring;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;   // the call's first stage / its finish (psx_ctx_stats)
 };
 
 struct EventPair {
@@ -223,6 +224,9 @@ struct psx_ctx {
   uint32_t walk_epoch[2] = {0, 0};                // granule tag of the slot's last call
   psx::WalkCount *d_wcount[2] = {nullptr, nullptr};   // walk-counted split tables per call slot (kMaxTables entries)
   std::vector<psx::WalkCount> h_wcount[2];             // what d_wcount[slot] holds
+  bool wcount_dirty[2] = {false, false};   // a walk counted into the slot and the call's ordered
+                                           // prep (whose ordered_fill zeroes the counts) was never
+                                           // enqueued: the next call on the slot clears them first
   hipStream_t side = nullptr;                     // decode/index/verify stage
   hipStream_t aux = nullptr;                      // launches beside the context stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -259,6 +263,7 @@ struct psx_ctx {
   std::vector<EventPair> pending_ev;
   std::vector<hipEvent_t> ev_pool;
   std::map<std::string, std::pair<double, int64_t>> times;
+  psx_apply_stats stats{};               // psx_ctx_stats (STATS_SERVER_ACCUM_APPLY_OPLOG_*)
 };
 
 namespace {
@@ -551,6 +556,15 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   // the main stream after it.
   const bool pipelined = c->pipeline == PSX_PIPELINE_ALL || (c->pipeline == PSX_PIPELINE_LISTED && light);
   hipStream_t prep = pipelined ? c->side : c->stream;
+  // psx_ctx_stats: the call's device time, from its first stage to its finish (replays of a
+  // counted call are not counted again); the event goes back to the pool on an early return
+  struct EventGuard {
+    psx_ctx *c;
+    hipEvent_t e;
+    ~EventGuard() {
+      if (e) c->ev_pool.push_back(e);
+    }
+  } call_ev{c, force_ordered ? nullptr : get_event(c)};
   psx::TableDir dir{};
   dir.n = (int32_t)c->tables.size();
   for (size_t i = 0; i < c->tables.size(); ++i) {
@@ -566,6 +580,20 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   psx::Seg *segs = c->d_segs[slot];
   uint32_t *counters = c->d_counters[slot];
   if (pipelined) HIP_TRY(c, hipStreamWaitEvent(prep, c->ev_free[slot], 0));
+  if (call_ev.e) HIP_TRY(c, hipEventRecord(call_ev.e, prep));
+  if (c->wcount_dirty[slot]) {
+    // the slot's last call failed between its counting walk and its ordered prep
+    for (auto &t : c->tables) {
+      if (!t.d_cnt || !t.split()) continue;
+      const size_t R = (size_t)t.cfg.max_rows;
+      HIP_TRY(c, hipMemsetAsync(t.d_cnt + slot * R, 0, R * sizeof(int32_t), prep));
+      if (t.d_grow) HIP_TRY(c, hipMemsetAsync(t.d_grow + slot * R, 0, R * sizeof(int32_t), prep));
+      if (t.d_nsplit) HIP_TRY(c, hipMemsetAsync(t.d_nsplit + 5 * slot, 0, 5 * sizeof(uint32_t), prep));
+      if (t.d_tsum) HIP_TRY(c, hipMemsetAsync(t.d_tsum + slot * (size_t)t.tsum_slot, 0,
+                                              (size_t)t.tsum_slot * sizeof(int32_t), prep));
+    }
+    c->wcount_dirty[slot] = false;
+  }
   // Walked messages with sparse tables: the window-parallel decode (psx_walk.hip) when every
   // sparse table of the context has one record pair size and the window items are bounded;
   // otherwise (and for producer record offsets) one workgroup per message.
@@ -628,14 +656,17 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       std::vector<psx::WalkCount> &hw = c->h_wcount[slot];
       if (!c->d_wcount[slot]) HIP_TRY(c, hipMalloc(&c->d_wcount[slot], sizeof(psx::WalkCount) * psx::kMaxTables));
       if (w.size() != hw.size() || std::memcmp(w.data(), hw.data(), sizeof(psx::WalkCount) * w.size())) {
-        // a slot's contents change only with the tables: the copy reads the context's own
-        // (persistent) vector, and the slot's previous walk has finished on this stream
+        // a slot's contents change only with the tables (rarely): wait for every copy still
+        // reading the context's persistent vector before it changes — the source is pageable,
+        // so stream order alone does not say when HIP has read it
+        HIP_TRY(c, hipStreamSynchronize(prep));
         hw = w;
         HIP_TRY(c, hipMemcpyAsync(c->d_wcount[slot], hw.data(), sizeof(psx::WalkCount) * w.size(),
                                   hipMemcpyHostToDevice, prep));
       }
     }
   }
+  if (wcount) c->wcount_dirty[slot] = true;
   psx_status st = timed(
       c, "decode_streams",
       [&] {
@@ -725,6 +756,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
     if (st) return st;
   }
+  c->wcount_dirty[slot] = false;   // every walk-counted table's ordered_fill is enqueued
   // 3) AdaRevision tables with version records: every record's snapshot must exist
   std::vector<psx::AdaArgs> ada(c->tables.size());
   for (int i = 0; i < fast.n; ++i) {
@@ -806,6 +838,21 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   PendingCall pc;
   pc.streams.assign(s, s + n);
   pc.ring = ring;
+  if (call_ev.e) {
+    hipEvent_t b = get_event(c);
+    if (b && hipEventRecord(b, c->stream) == hipSuccess) {
+      pc.ev_a = call_ev.e;
+      pc.ev_b = b;
+      call_ev.e = nullptr;
+    } else if (b) {
+      c->ev_pool.push_back(b);
+    }
+  }
+  if (!force_ordered) {
+    c->stats.calls++;
+    c->stats.messages += (uint64_t)n;
+    for (int i = 0; i < n; ++i) c->stats.oplog_bytes += s[i].size;
+  }
   c->pending.push_back(pc);
   c->call_seq++;
   c->pending_calls++;
@@ -911,6 +958,17 @@ psx_status sync_impl(psx_ctx *c) {
   std::vector<PendingCall> pending;
   pending.swap(c->pending);
   c->pending_calls = 0;
+  for (PendingCall &p : pending) {
+    if (!p.ev_a) continue;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.ev_a, p.ev_b) == hipSuccess) {
+      c->stats.apply_sec += ms * 1e-3;
+      c->stats.settled_calls++;
+    }
+    c->ev_pool.push_back(p.ev_a);
+    c->ev_pool.push_back(p.ev_b);
+    p.ev_a = p.ev_b = nullptr;
+  }
   if (sticky) {
     uint32_t zero = 0;
     HIP_TRY(c, hipMemcpy(c->d_status, &zero, sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1188,14 +1246,12 @@ psx_status psx_sender_version(psx_ctx *c, int32_t bg_id, int64_t *version) {
   return PSX_OK;
 }
 
-psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
-  if (!c || !cfg) return PSX_ERR_INVALID_ARG;
-  if (c->tables.size() >= (size_t)psx::kMaxTables) return fail(c, PSX_ERR_INVALID_ARG, "too many tables");
-  if (find_table(c, cfg->table_id)) return fail(c, PSX_ERR_INVALID_ARG, "table exists");
+// The record-format half of a table config — dtype, row kind, record variant, widths —
+// checked and copied into t (nothing allocated).  psx_table_create adds the shard geometry
+// and the storage; psx_split_stream_formats needs only this.
+static psx_status table_format(psx_ctx *c, const psx_table_config *cfg, TableState &t) {
   if (cfg->dtype < PSX_F32 || cfg->dtype > PSX_I64) return fail(c, PSX_ERR_INVALID_ARG, "bad dtype");
   if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
-  if (cfg->max_rows <= 0 || cfg->row_stride <= 0) return fail(c, PSX_ERR_INVALID_ARG, "bad shard geometry");
-  if (cfg->max_rows > ((int64_t)1 << 31) - 2) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
   if (cfg->reserved1 != 0 || cfg->server_push_row_upper_bound < 0 ||
       (cfg->accum_importance != 0 && cfg->accum_importance != 1) ||
       (cfg->version_maintain != 0 && cfg->version_maintain != 1) || cfg->row_oplog_type < 0 ||
@@ -1210,9 +1266,6 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     return fail(c, PSX_ERR_UNSUPPORTED, "version_maintain needs dense rows with dense-serialized kDenseRowOpLog records");
   if (f16 && cfg->dtype != PSX_F32)
     return fail(c, PSX_ERR_UNSUPPORTED, "float16 records need f32 rows (dense_row_oplog_float16.hpp:28)");
-  if (c->has_ada && !cfg->oplog_dense_serialized)
-    return fail(c, PSX_ERR_UNSUPPORTED, "contexts with an AdaRevision table take dense-serialized tables only");
-  TableState t;
   t.cfg = *cfg;
   if (!f16) t.cfg.row_oplog_type = 0;   // kSparse*RowOpLog: no server-side difference for sparse records
   if (t.cfg.server_push_row_upper_bound == 0) t.cfg.server_push_row_upper_bound = 100;   // table_gflags.cpp:21
@@ -1233,6 +1286,22 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     if (t.max_entries * t.es > 150 * 1024)
       return fail(c, PSX_ERR_UNSUPPORTED, "max_entries * sizeof(Entry) must fit one wave's LDS image (150 KiB)");
   }
+  return PSX_OK;
+}
+
+psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
+  if (!c || !cfg) return PSX_ERR_INVALID_ARG;
+  if (c->tables.size() >= (size_t)psx::kMaxTables) return fail(c, PSX_ERR_INVALID_ARG, "too many tables");
+  if (find_table(c, cfg->table_id)) return fail(c, PSX_ERR_INVALID_ARG, "table exists");
+  if (cfg->dtype < PSX_F32 || cfg->dtype > PSX_I64) return fail(c, PSX_ERR_INVALID_ARG, "bad dtype");
+  if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
+  if (cfg->max_rows <= 0 || cfg->row_stride <= 0) return fail(c, PSX_ERR_INVALID_ARG, "bad shard geometry");
+  if (cfg->max_rows > ((int64_t)1 << 31) - 2) return fail(c, PSX_ERR_INVALID_ARG, "max_rows exceeds int32 row ids");
+  if (c->has_ada && !cfg->oplog_dense_serialized)
+    return fail(c, PSX_ERR_UNSUPPORTED, "contexts with an AdaRevision table take dense-serialized tables only");
+  TableState t;
+  psx_status fe = table_format(c, cfg, t);
+  if (fe) return fe;
   HIP_TRY(c, hipSetDevice(c->device));
   const size_t R = (size_t)cfg->max_rows;
   const size_t ntiles = (R + 1023) / 1024;
@@ -1892,9 +1961,11 @@ psx_status psx_adarevision_state(psx_ctx *c, int32_t table_id, int64_t first_row
 }
 
 // psx_split_stream (psx_split.hip): the client's per-server split of one packed message.
-psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const uint64_t *record_offsets,
-                            int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
-                            uint64_t *out_sizes) {
+// fmts: the record formats of the tables a message may carry (the context's own tables for
+// psx_split_stream, the caller's configs for psx_split_stream_formats).
+static psx_status split_impl(psx_ctx *c, const std::vector<TableState> &fmts, const void *stream, size_t size,
+                             const uint64_t *record_offsets, int32_t nowners, const int64_t *row_begin, void *out,
+                             size_t out_cap, uint64_t *out_sizes) {
   if (!c || !out_sizes || !row_begin || nowners < 1 || nowners > PSX_MAX_SPLIT_OWNERS || (size && !stream))
     return PSX_ERR_INVALID_ARG;
   for (int32_t o = 0; o < nowners; ++o) {
@@ -1906,7 +1977,12 @@ psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const u
   if (size == 0) return PSX_OK;   // an empty message splits into empty messages
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
-  const size_t nrecoff = size / 8 + 1;
+  // sparse record offsets: at most one per 8 bytes of message; none when every table is
+  // dense-serialized (fixed stride: the decode writes no offsets), so a dense message of
+  // any size costs no offset buffer
+  bool any_sparse = false;
+  for (const TableState &t : fmts) any_sparse |= !t.cfg.oplog_dense_serialized;
+  const size_t nrecoff = any_sparse ? size / 8 + 1 : 1;
   auto grow = [&](void *&p, size_t &cap, size_t need) -> psx_status {
     if (need <= cap) return PSX_OK;
     HIP_TRY(c, hipStreamSynchronize(st));
@@ -1932,12 +2008,12 @@ psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const u
   ss.data[0] = (const uint8_t *)stream;
   ss.size[0] = size;
   psx::TableDir dir{};
-  dir.n = (int32_t)c->tables.size();
-  for (size_t i = 0; i < c->tables.size(); ++i) {
-    dir.table_id[i] = c->tables[i].cfg.table_id;
-    dir.vsize[i] = c->tables[i].vsize;
-    dir.dense_serialized[i] = c->tables[i].cfg.oplog_dense_serialized;
-    dir.dense_body[i] = c->tables[i].dense_body();
+  dir.n = (int32_t)fmts.size();
+  for (size_t i = 0; i < fmts.size(); ++i) {
+    dir.table_id[i] = fmts[i].cfg.table_id;
+    dir.vsize[i] = fmts[i].vsize;
+    dir.dense_serialized[i] = fmts[i].cfg.oplog_dense_serialized;
+    dir.dense_body[i] = fmts[i].dense_body();
   }
   psx::IdxSet ix{};
   ix.p[0] = record_offsets;
@@ -1965,7 +2041,7 @@ psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const u
   std::vector<psx::SplitTab> tabs(ntab);
   int64_t nrec = 0;
   for (int j = 0; j < ntab; ++j) {
-    const TableState &t = c->tables[order[j].ti];
+    const TableState &t = fmts[order[j].ti];
     const psx::Seg &g = hs[order[j].ti];
     tabs[j].k0 = nrec;
     tabs[j].rec0 = g.rec0;
@@ -2011,7 +2087,7 @@ psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const u
   a.status = status;
   HIP_TRY(c, hipMemcpyAsync(sc + o_tabs, tabs.data(), sizeof(psx::SplitTab) * ntab, hipMemcpyHostToDevice, st));
   HIP_TRY(c, hipMemsetAsync(a.tile_bytes, 0, 8 * nb, st));
-  HIP_TRY(c, hipMemsetAsync(a.ot_count, 0, 16 * (size_t)nowners * ntab + 256, st));   // ot_count and ot_bytes
+  HIP_TRY(c, hipMemsetAsync(a.ot_count, 0, 8 * (size_t)nowners * ntab, st));
   HIP_TRY(c, hipMemsetAsync(a.ot_bytes, 0, 8 * (size_t)nowners * ntab, st));
   // 3) owners and sizes; per owner the tile bytes scanned
   HIP_TRY(c, psx::launch_split_count(a, st));
@@ -2042,7 +2118,7 @@ psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const u
         const int64_t n_oj = cnt[(size_t)o * ntab + j];
         if (!n_oj) continue;
         const int64_t hpos = base[o] + 4 + 16 * r + (int64_t)before;
-        const TableState &t = c->tables[order[j].ti];
+        const TableState &t = fmts[order[j].ti];
         const uint64_t usz = (uint64_t)t.vsize;
         wpos.insert(wpos.end(), {hpos, hpos + 4, hpos + 8, hpos + 12});
         wval.insert(wval.end(), {(uint32_t)t.cfg.table_id, (uint32_t)usz, (uint32_t)(usz >> 32), (uint32_t)n_oj});
@@ -2064,6 +2140,28 @@ psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const u
                                        reinterpret_cast<const uint32_t *>(sc + o_wv), (int32_t)wpos.size(), st));
   HIP_TRY(c, hipStreamSynchronize(st));   // the host vectors above are pageable
   return PSX_OK;
+}
+
+psx_status psx_split_stream(psx_ctx *c, const void *stream, size_t size, const uint64_t *record_offsets,
+                            int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
+                            uint64_t *out_sizes) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  return split_impl(c, c->tables, stream, size, record_offsets, nowners, row_begin, out, out_cap, out_sizes);
+}
+
+psx_status psx_split_stream_formats(psx_ctx *c, const psx_table_config *formats, int32_t nformats,
+                                    const void *stream, size_t size, const uint64_t *record_offsets,
+                                    int32_t nowners, const int64_t *row_begin, void *out, size_t out_cap,
+                                    uint64_t *out_sizes) {
+  if (!c || nformats < 0 || nformats > psx::kMaxTables || (nformats && !formats)) return PSX_ERR_INVALID_ARG;
+  std::vector<TableState> fmts((size_t)nformats);
+  for (int32_t i = 0; i < nformats; ++i) {
+    for (int32_t j = 0; j < i; ++j)
+      if (formats[j].table_id == formats[i].table_id) return fail(c, PSX_ERR_INVALID_ARG, "table id twice in formats");
+    psx_status e = table_format(c, &formats[i], fmts[(size_t)i]);
+    if (e) return e;
+  }
+  return split_impl(c, fmts, stream, size, record_offsets, nowners, row_begin, out, out_cap, out_sizes);
 }
 
 psx_status psx_pack_stream(psx_ctx *c, const psx_pack_table *tables, int32_t n, void *out, size_t cap,
@@ -2546,6 +2644,13 @@ psx_status psx_timing_read(psx_ctx *c, const char *kernel, double *total_ms, int
   auto it = c->times.find(kernel);
   *total_ms = it == c->times.end() ? 0.0 : it->second.first;
   *launches = it == c->times.end() ? 0 : it->second.second;
+  return PSX_OK;
+}
+
+psx_status psx_ctx_stats(psx_ctx *c, psx_apply_stats *out, int32_t reset) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  if (out) *out = c->stats;
+  if (reset) c->stats = psx_apply_stats{};
   return PSX_OK;
 }
 

@@ -31,18 +31,20 @@ class Exchange:
 
     def __init__(self, device, group=None):
         L = self._L = _abi.load()
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        single = not dist.is_initialized()     # one rank without a process group: a self exchange
+        self.world = 1 if single else dist.get_world_size(group)
+        self.rank = 0 if single else dist.get_rank(group)
         uid = (ctypes.c_uint8 * 128)()
         if self.rank == 0:
             st = L.psx_comm_unique_id(uid)
             if st:
                 raise _abi.PsxError(st, L.psx_comm_last_error(None).decode())
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        if dist.get_backend(group) == "nccl":
-            t = t.cuda(device)
-        dist.broadcast(t, 0, group=group)
-        uid = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        if not single:
+            t = torch.tensor(list(uid), dtype=torch.uint8)
+            if dist.get_backend(group) == "nccl":
+                t = t.cuda(device)
+            dist.broadcast(t, 0, group=group)
+            uid = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
         self._c = ctypes.c_void_p()
         st = L.psx_comm_create(uid, self.world, self.rank, device, ctypes.byref(self._c))
         if st:
@@ -55,21 +57,193 @@ class Exchange:
 
     def alltoall(self, send, send_sizes, stream=None):
         """send: CUDA uint8 tensor with world sub-streams back to back (owner order).
-        Returns (recv, recv_sizes) in source-rank order."""
+        Returns (recv, recv_sizes) in source-rank order.  With a `stream` other than the
+        current one, both tensors are marked as used on it (record_stream), so the caching
+        allocator does not hand them out before RCCL is done with them."""
+        import torch
         L = self._L
         n = self.world
+        if len(send_sizes) != n:
+            raise ValueError(f"{len(send_sizes)} sub-stream sizes for {n} ranks")
+        if any(int(x) % 4 for x in send_sizes):
+            raise ValueError("sub-stream sizes are multiples of 4 bytes")
+        if send.numel() < sum(int(x) for x in send_sizes):
+            raise ValueError(f"send holds {send.numel()} bytes, the sizes name {sum(int(x) for x in send_sizes)}")
         ss = (ctypes.c_uint64 * n)(*[int(x) for x in send_sizes])
         rs = (ctypes.c_uint64 * n)()
-        hs = stream if stream is not None else torch.cuda.current_stream(send.device).cuda_stream
+        cur = torch.cuda.current_stream(send.device)
+        hs = stream if stream is not None else cur.cuda_stream
         st = L.psx_exchange_sizes(self._c, ss, rs, ctypes.c_void_p(hs))
         if st:
             raise _abi.PsxError(st, L.psx_comm_last_error(self._c).decode())
         rsz = [int(x) for x in rs]
         recv = torch.empty(max(sum(rsz), 4), dtype=torch.uint8, device=send.device)
+        if stream is not None and stream != cur.cuda_stream:
+            ext = torch.cuda.ExternalStream(stream, device=send.device)
+            recv.record_stream(ext)
+            send.record_stream(ext)
         st = L.psx_exchange_streams(self._c, send.data_ptr(), ss, recv.data_ptr(), rs, ctypes.c_void_p(hs))
         if st:
             raise _abi.PsxError(st, L.psx_comm_last_error(self._c).decode())
         return recv[:sum(rsz)], rsz
+
+    def sizes_async(self, send_sizes, recv_sizes, stream):
+        """psx_exchange_sizes_async: enqueue the sub-stream sizes on `stream` (a HIP stream
+        handle); recv_sizes is a page-locked int64 CPU tensor of world entries, valid once the
+        stream has passed this point."""
+        n = self.world
+        if any(int(x) % 4 for x in send_sizes):
+            raise ValueError("sub-stream sizes are multiples of 4 bytes")
+        assert recv_sizes.is_pinned() and recv_sizes.numel() >= n and recv_sizes.element_size() == 8
+        ss = (ctypes.c_uint64 * n)(*[int(x) for x in send_sizes])
+        st = self._L.psx_exchange_sizes_async(self._c, ss, ctypes.c_void_p(recv_sizes.data_ptr()),
+                                              ctypes.c_void_p(stream))
+        if st:
+            raise _abi.PsxError(st, self._L.psx_comm_last_error(self._c).decode())
+
+    def streams_into(self, send, send_sizes, recv, recv_sizes, stream):
+        """psx_exchange_streams into a caller-owned recv buffer on `stream` (HIP handle);
+        the caller keeps send and recv alive and unused until the stream has passed."""
+        n = self.world
+        if send.numel() < sum(send_sizes) or recv.numel() < sum(recv_sizes):
+            raise ValueError("exchange buffers smaller than the sizes they carry")
+        ss = (ctypes.c_uint64 * n)(*[int(x) for x in send_sizes])
+        rs = (ctypes.c_uint64 * n)(*[int(x) for x in recv_sizes])
+        st = self._L.psx_exchange_streams(self._c, send.data_ptr(), ss, recv.data_ptr(), rs, ctypes.c_void_p(stream))
+        if st:
+            raise _abi.PsxError(st, self._L.psx_comm_last_error(self._c).decode())
+
+
+class ShardExchange:
+    """One rank's side of the exchange-bearing step (SURVEY §8(e), C4's shape).
+
+    Every rank holds worker batches that span every row-range shard.  The reference client
+    splits each batch by owning server while packing and sends each server its message
+    (AbstractBgWorker::CreateOpLogMsgs / SendOpLogMsgs, abstract_bg_worker.cpp:590-689); each
+    server applies what it receives (Server::ApplyOpLogUpdateVersion, server.cpp:120-179).
+    Here a batch arrives as a sequence of Appendix-A messages of at most 2 GiB each (chunks:
+    the reference reader keeps its cursor in an int32, serialized_oplog_reader.hpp:137), and
+    per chunk:
+      1. split per owner on the device (psx_split_stream_formats: record formats only, no
+         table) into send slot k % 2, on the split stream;
+      2. the sub-stream sizes, then the bytes, to every owner (psx_exchange_sizes_async /
+         psx_exchange_streams: RCCL grouped send/recv over xGMI) into recv slot k % 2, on the
+         exchange stream;
+      3. the owner applies the world's sub-streams in source-rank order in one fused call
+         (psx_apply_streams_device on the owner context's stream), bit-exact to applying the
+         same messages one by one.
+    Chunk k's bytes cross while chunk k-1 applies and chunk k+1 splits; two slots of each
+    buffer bound the HBM the step needs beyond the batches and the table to about four
+    chunks.  Each sender's messages carry consecutive versions (one per chunk round; an
+    owner with no records from a sender gets an empty message, which only bumps it)."""
+
+    def __init__(self, server, table_id, info, row_begin, bg_ids, exchange, device, splitter_id=900):
+        import torch
+        from .server import Server
+        self.srv, self.xc, self.device = server, exchange, device
+        self.world = exchange.world
+        assert len(row_begin) == self.world + 1 and len(bg_ids) == self.world
+        self.bounds = [int(x) for x in row_begin]
+        self.bgs = list(bg_ids)
+        self.formats = {table_id: info}
+        self.splitter = Server(device=device, server_id=splitter_id + exchange.rank)   # no tables
+        self.s_split = torch.cuda.Stream(device)
+        self.s_x = torch.cuda.Stream(device)
+        self.s_apply = torch.cuda.Stream(device)
+        self.splitter.set_stream(self.s_split.cuda_stream)
+        server.set_stream(self.s_apply.cuda_stream)
+        self.send = [None, None]
+        self.recv = [None, None]
+        self.ev_sent = [torch.cuda.Event(), torch.cuda.Event()]     # a send slot's bytes have left
+        self.ev_recv = [torch.cuda.Event(), torch.cuda.Event()]     # a recv slot's bytes have arrived
+        self.ev_x0 = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+        self.ev_x1 = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+        self.rsz = torch.zeros((2, self.world), dtype=torch.int64).pin_memory()
+        self.version = 0
+        self.reset_counters()
+
+    def reset_counters(self):
+        self.split_s = self.wait_s = self.sync_s = 0.0
+        self.x_ms = 0.0
+        self.chunks = 0
+        self.sent_bytes = self.recv_bytes = 0
+        self._x_pending = []
+
+    def _grow(self, bufs, s, nbytes, ev=None):
+        import torch
+        if bufs[s] is None or bufs[s].numel() < nbytes:
+            if ev is not None:
+                ev.synchronize()
+            bufs[s] = None
+            bufs[s] = torch.empty((max(nbytes, 4) + 3) // 4, dtype=torch.int32,
+                                  device=torch.device("cuda", self.device)).view(torch.uint8)
+        return bufs[s]
+
+    def _collect_x(self, keep_last=1):
+        while len(self._x_pending) > keep_last:
+            a, b = self._x_pending.pop(0)
+            b.synchronize()
+            self.x_ms += a.elapsed_time(b)
+
+    def run(self, chunks, log=None):
+        """Apply one batch per rank (a list of <= 2 GiB device messages, this rank's worker
+        batch in record order) to the owners' shards.  Returns after every apply settled."""
+        import time
+        n = self.world
+        for k, msg in enumerate(chunks):
+            s = k % 2
+            ntab = len(self.formats)
+            send = self._grow(self.send, s, msg.numel() + n * (4 + 16 * ntab), self.ev_sent[s])
+            t0 = time.perf_counter()
+            self.s_split.wait_event(self.ev_sent[s])        # chunk k-2's bytes have left the slot
+            parts, sizes = self.splitter.split_stream(msg, self.bounds, formats=self.formats, out=send,
+                                                      sync_current=False)
+            t1 = time.perf_counter()
+            rs = self.rsz[s]
+            self.xc.sizes_async(sizes, rs, self.s_x.cuda_stream)
+            ev = self.ev_x1[s]
+            ev.record(self.s_x)
+            ev.synchronize()                                # sizes known = chunk k-1's bytes arrived
+            t2 = time.perf_counter()
+            rsz = [int(x) for x in rs.tolist()]
+            # recv slot s was last read by chunk k-2's apply, settled by the last srv.sync()
+            recv = self._grow(self.recv, s, sum(rsz))
+            a, b = torch_event_pair()
+            a.record(self.s_x)
+            self.xc.streams_into(parts, sizes, recv, rsz, self.s_x.cuda_stream)
+            b.record(self.s_x)
+            self.ev_sent[s].record(self.s_x)
+            self.ev_recv[s].record(self.s_x)
+            self._x_pending.append((a, b))
+            # chunk k-1's apply finishes beside chunk k's exchange; then chunk k's is enqueued
+            self.srv.sync()
+            t3 = time.perf_counter()
+            self.s_apply.wait_event(self.ev_recv[s])
+            msgs, off = [], 0
+            for w in range(n):
+                msgs.append((recv.data_ptr() + off, rsz[w], self.bgs[w], self.version))
+                off += rsz[w]
+            self.srv.apply_device(msgs)
+            self.version += 1
+            self.split_s += t1 - t0
+            self.wait_s += t2 - t1
+            self.sync_s += t3 - t2
+            self.chunks += 1
+            self.sent_bytes += sum(sizes)
+            self.recv_bytes += sum(rsz)
+            self._collect_x()
+            if log is not None:
+                log(f"chunk {k}: split {t1 - t0:.4f} s, sizes wait {t2 - t1:.4f} s, apply wait {t3 - t2:.4f} s")
+        self.srv.sync()
+        self._collect_x(0)
+
+    def close(self):
+        self.splitter.close()
+
+
+def torch_event_pair():
+    import torch
+    return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
 def alltoall_streams(send, send_sizes, group=None):

@@ -34,6 +34,19 @@ class TableInfo:
     row_oplog_type: int = 0                 # RowOpLogType (configs.hpp:35-40); 3 = float16 dense records
 
 
+def table_config(table_id, info: TableInfo):
+    """The psx_table_config of a TableInfo (psx_table_create / psx_split_stream_formats)."""
+    return psx_table_config(
+        table_id=table_id, row_kind=info.row_kind, dtype=info.dtype,
+        oplog_dense_serialized=1 if info.oplog_dense_serialized else 0,
+        row_capacity=info.row_capacity,
+        dense_row_oplog_capacity=info.dense_row_oplog_capacity or info.row_capacity,
+        row_offset=info.row_offset, row_stride=info.row_stride, max_rows=info.max_rows,
+        max_entries=info.max_entries, accum_importance=1 if info.accum_importance else 0,
+        server_push_row_upper_bound=info.server_push_row_upper_bound,
+        version_maintain=1 if info.version_maintain else 0, row_oplog_type=info.row_oplog_type)
+
+
 def _check(L, ctx, st):
     if st != _abi.PSX_OK:
         msg = L.psx_last_error(ctx).decode() if ctx else ""
@@ -88,15 +101,7 @@ class Server:
 
     # -- Server API (server.hpp) ----------------------------------------------
     def CreateTable(self, table_id, info: TableInfo):
-        cfg = psx_table_config(
-            table_id=table_id, row_kind=info.row_kind, dtype=info.dtype,
-            oplog_dense_serialized=1 if info.oplog_dense_serialized else 0,
-            row_capacity=info.row_capacity,
-            dense_row_oplog_capacity=info.dense_row_oplog_capacity or info.row_capacity,
-            row_offset=info.row_offset, row_stride=info.row_stride, max_rows=info.max_rows,
-            max_entries=info.max_entries, accum_importance=1 if info.accum_importance else 0,
-            server_push_row_upper_bound=info.server_push_row_upper_bound,
-            version_maintain=1 if info.version_maintain else 0, row_oplog_type=info.row_oplog_type)
+        cfg = table_config(table_id, info)
         _check(self._L, self._ctx, self._L.psx_table_create(self._ctx, ctypes.byref(cfg)))
         self.tables[table_id] = info
 
@@ -169,6 +174,19 @@ class Server:
         a = np.ascontiguousarray(rows, dtype=self._np(table_id)).reshape(-1, info.row_capacity)
         _check(self._L, self._ctx, self._L.psx_table_load_rows(
             self._ctx, table_id, first_row, a.shape[0], ctypes.c_void_p(a.ctypes.data), 0))
+
+    def read_rows_device(self, table_id, first_row, num_rows, out):
+        """psx_table_read_rows into a CUDA tensor of num_rows x row_capacity values (absent
+        rows read as zero); synchronous."""
+        import torch
+        info = self.tables[table_id]
+        assert out.is_cuda and out.is_contiguous() and out.numel() == num_rows * info.row_capacity
+        assert out.element_size() == np.dtype(self._np(table_id)).itemsize
+        _check(self._L, self._ctx, self._L.psx_table_read_rows(
+            self._ctx, table_id, first_row, num_rows, out.data_ptr(), 1))
+        _check(self._L, self._ctx, self._L.psx_sync(self._ctx))
+        torch.cuda.synchronize(out.device)
+        return out
 
     def read_rows(self, table_id, first_row, num_rows):
         info = self.tables[table_id]
@@ -393,23 +411,34 @@ class Server:
             res += (rws[:nrec],)
         return res if len(res) > 1 else out
 
-    def split_stream(self, msg, row_begin, record_offsets=None):
+    def split_stream(self, msg, row_begin, record_offsets=None, formats=None, out=None, sync_current=True):
         """psx_split_stream: the per-server split of one device message (CUDA uint8 tensor)
         over row-range owners (row_begin: nowners + 1 ascending row ids).  Returns (out, sizes):
-        a CUDA uint8 tensor with the owners' sub-streams back to back and their byte counts."""
+        a CUDA uint8 tensor with the owners' sub-streams back to back and their byte counts.
+        formats: {table_id: TableInfo} — split with these record formats
+        (psx_split_stream_formats) instead of this context's tables, so a splitter needs no
+        table storage.  out: a preallocated CUDA uint8 buffer (4-byte aligned) to split into.
+        sync_current: first wait for torch's current stream (the message's producer)."""
         import torch
-        torch.cuda.current_stream(self.device).synchronize()
+        if sync_current:
+            torch.cuda.current_stream(self.device).synchronize()
         rb = (ctypes.c_int64 * len(row_begin))(*[int(x) for x in row_begin])
         nown = len(row_begin) - 1
         sizes = (ctypes.c_uint64 * nown)()
         n = msg.numel()
-        ntab = len(self.tables)
+        ntab = len(formats) if formats is not None else len(self.tables)
         cap = n + nown * (4 + 16 * max(ntab, 1))
-        out = torch.empty((cap + 3) // 4, dtype=torch.int32, device=msg.device).view(torch.uint8)
-        _check(self._L, self._ctx, self._L.psx_split_stream(
-            self._ctx, msg.data_ptr() if n else None, n,
-            record_offsets.data_ptr() if record_offsets is not None else None, nown, rb,
-            out.data_ptr(), out.numel(), sizes))
+        if out is None:
+            out = torch.empty((cap + 3) // 4, dtype=torch.int32, device=msg.device).view(torch.uint8)
+        offs = record_offsets.data_ptr() if record_offsets is not None else None
+        if formats is not None:
+            arr = (psx_table_config * max(len(formats), 1))(*[table_config(t, i) for t, i in formats.items()])
+            st = self._L.psx_split_stream_formats(self._ctx, arr, len(formats), msg.data_ptr() if n else None, n,
+                                                  offs, nown, rb, out.data_ptr(), out.numel(), sizes)
+        else:
+            st = self._L.psx_split_stream(self._ctx, msg.data_ptr() if n else None, n, offs, nown, rb,
+                                          out.data_ptr(), out.numel(), sizes)
+        _check(self._L, self._ctx, st)
         sz = [int(x) for x in sizes]
         return out[:sum(sz)], sz
 
@@ -424,6 +453,15 @@ class Server:
         _check(self._L, self._ctx, self._L.psx_timing_read(self._ctx, kernel.encode(),
                                                            ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    def stats(self, reset=False):
+        """psx_ctx_stats: the STATS_SERVER_ACCUM_APPLY_OPLOG_* counters (server_thread.cpp:240-244)
+        as a dict: calls, messages, oplog_bytes, apply_sec, settled_calls (+ oplog_recv_mb)."""
+        st = _abi.psx_apply_stats()
+        _check(self._L, self._ctx, self._L.psx_ctx_stats(self._ctx, ctypes.byref(st), 1 if reset else 0))
+        d = {k: getattr(st, k) for k, _ in st._fields_}
+        d["oplog_recv_mb"] = d["oplog_bytes"] / float(1 << 20)
+        return d
 
     def timing_reset(self):
         _check(self._L, self._ctx, self._L.psx_timing_reset(self._ctx))

@@ -163,3 +163,99 @@ def test_rccl_exchange_one_rank_self_send():
         assert L.psx_exchange_sizes(comm, bad, rs, ctypes.c_void_p(stream)) == 1
     finally:
         L.psx_comm_destroy(comm)
+
+
+def _formats(K):
+    return {1: psa.TableInfo(row_kind=DENSE, dtype=F32, row_capacity=K),
+            3: psa.TableInfo(row_kind=SORTED_MAP, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                             max_entries=K),
+            4: psa.TableInfo(row_kind=DENSE, dtype=F64, row_capacity=K)}
+
+
+@pytest.mark.parametrize("owners", [1, 5])
+def test_split_with_formats_equals_split_with_tables(owners):
+    """psx_split_stream_formats (a context with no tables, record formats from the caller)
+    writes the same sub-streams as psx_split_stream over a context holding the tables."""
+    rng = np.random.RandomState(40 + owners)
+    R, K = 2500, 24
+    tables = _tables(rng, R, K)
+    msg = np.frombuffer(pack_stream(tables), np.uint8)
+    d = torch.from_numpy(msg.copy()).cuda()
+    bounds = np.linspace(0, R, owners + 1).astype(np.int64)
+    srv = _server(R, K)
+    out_t, sz_t = srv.split_stream(d, bounds)
+    bare = psa.Server(0, 2)
+    out_f, sz_f = bare.split_stream(d, bounds, formats=_formats(K))
+    assert sz_f == sz_t
+    assert torch.equal(out_f, out_t)
+    off = 0
+    for o in range(owners):
+        assert out_f[off:off + sz_f[o]].cpu().numpy().tobytes() == _expected(tables, bounds[o], bounds[o + 1])
+        off += sz_f[o]
+    # a table missing from the formats is an unknown table; a bad format is rejected
+    with pytest.raises(PsxError) as e:
+        bare.split_stream(d, bounds, formats={1: _formats(K)[1]})
+    assert e.value.status == 3
+    with pytest.raises(PsxError) as e:
+        bare.split_stream(d, bounds, formats={1: psa.TableInfo(row_kind=DENSE, dtype=9, row_capacity=K)})
+    assert e.value.status == 1
+    srv.close()
+    bare.close()
+
+
+def test_split_dense_only_formats_into_preallocated_output():
+    """A dense-only split writes into the caller's buffer and needs no record-offset buffer."""
+    rng = np.random.RandomState(77)
+    R, K, N = 50_000, 32, 40_000
+    ids = rng.permutation(R)[:N].astype(np.int32)
+    tables = [dict(table_id=1, dtype=F32, dense_serialized=True, row_ids=ids,
+                   oplogs=rng.normal(0, 1, (N, K)).astype(np.float32))]
+    msg = np.frombuffer(pack_stream(tables), np.uint8)
+    bounds = [0, 10_000, 31_000, R]
+    bare = psa.Server(0, 2)
+    out = torch.empty(msg.size + 3 * 20 + 64, dtype=torch.uint8, device="cuda")
+    part, sizes = bare.split_stream(torch.from_numpy(msg.copy()).cuda(), bounds,
+                                    formats={1: psa.TableInfo(row_kind=DENSE, dtype=F32, row_capacity=K)}, out=out)
+    assert part.data_ptr() == out.data_ptr()
+    host, off = part.cpu().numpy().tobytes(), 0
+    for o in range(3):
+        assert host[off:off + sizes[o]] == _expected(tables, bounds[o], bounds[o + 1])
+        off += sizes[o]
+    bare.close()
+
+
+def test_rccl_exchange_sizes_async_one_rank():
+    """psx_exchange_sizes_async: the sizes land in page-locked memory once the stream passes;
+    a pageable destination is rejected."""
+    from parameter_server_amd.exchange import Exchange
+    xc = Exchange(0)
+    s = torch.cuda.Stream()
+    rs = torch.zeros(1, dtype=torch.int64).pin_memory()
+    xc.sizes_async([1024], rs, s.cuda_stream)
+    s.synchronize()
+    assert int(rs[0]) == 1024
+    for k in range(20):                      # the staging ring wraps
+        xc.sizes_async([4 * k], rs, s.cuda_stream)
+        s.synchronize()
+        assert int(rs[0]) == 4 * k
+    with pytest.raises(AssertionError):
+        xc.sizes_async([8], torch.zeros(1, dtype=torch.int64), s.cuda_stream)
+    L = _abi.load()
+    page = (ctypes.c_uint64 * 1)()
+    assert L.psx_exchange_sizes_async(xc._c, (ctypes.c_uint64 * 1)(8), page, ctypes.c_void_p(s.cuda_stream)) == 1
+    with pytest.raises(ValueError):
+        xc.alltoall(torch.zeros(8, dtype=torch.uint8, device="cuda"), [12])
+    xc.close()
+
+
+@pytest.mark.parametrize("rows,cap,chunk_recs", [(20_000, 64, 3_000), (9_000, 256, 9_000), (7_777, 40, 1_000)])
+def test_shard_exchange_pipeline_one_rank_bit_exact(rows, cap, chunk_recs):
+    """The exchange-bearing step through ShardExchange on one GPU (self exchange): a batch of
+    several < max_bytes messages per step, split (formats only), exchanged, applied in chunk
+    order with chunk k's exchange beside chunk k-1's apply, three steps — bit for bit equal to
+    the in-order f32 sum recomputed from the seeds (bench.exchange_measure's check)."""
+    import bench
+    m = bench.exchange_measure(rows, cap, 2, 1, 1, 0, 0, seed=7 + rows, max_bytes=20 + (4 + 4 * cap) * chunk_recs)
+    assert m["parity"] == "bit-exact", m
+    assert m["chunks_per_step"] == -(-rows // chunk_recs)
+    assert m["apply_kernel_ms_per_chunk"] and m["exchange_kernel_ms_per_step"] is not None

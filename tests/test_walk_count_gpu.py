@@ -148,3 +148,75 @@ def test_row_outside_the_shard_fails_and_leaves_counts_clean(walk_count):
     finally:
         L.psx_debug_set_variant(WALK_COUNT, old[0])
         L.psx_debug_set_variant(DECODE, old[1])
+
+
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+@pytest.mark.parametrize("split", [3, 1], ids=["spill-heavy-first", "concurrent"])
+def test_pipelined_walk_counts_without_sync_between_calls(kind, split):
+    """Six walked calls enqueued back to back with PSX_PIPELINE_ALL and no sync between them
+    (the device buffers all kept alive), so call k's walk counts into its slot while call
+    k-1's ordered work still runs on the other slot's counts; the fourth call names a row
+    outside the shard.  One sync at the end reports that call's error; every other call is
+    applied, and the rows equal the oracle fed the five good calls byte for byte (sorted map:
+    entry order; map: {col -> value})."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, 1), L.psx_debug_set_variant(ORD_SPLIT, split),
+           L.psx_debug_set_variant(DECODE, 1)]
+    rng = np.random.RandomState(90 + split)
+    rows, K, bgs = 8_000, 1024, [100, 101, 102, 103]
+    calls = _batches(rng, rows, K, 6, per_batch=3_000)
+    bad = 3
+    recs = [(5, np.array([1, 2], np.int32), np.array([1, 1], np.int32)),
+            (rows + 3, np.array([3], np.int32), np.array([1], np.int32)),
+            (7, np.array([4], np.int32), np.array([2], np.int32))]
+    calls[bad] = list(calls[bad])
+    calls[bad][2] = wire.sparse_stream_np(3, 4, recs)
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(PIPELINE_ALL)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        L.psx_debug_set_variant(WALK_CALLS, 0)
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, msgs in enumerate(dev):
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)])
+        with pytest.raises(PsxError) as e:
+            srv.sync()
+        assert e.value.status == 5
+        walked = L.psx_debug_get_variant(WALK_CALLS)
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(ORD_SPLIT, old[1])
+        L.psx_debug_set_variant(DECODE, old[2])
+    assert walked == len(calls)
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    ov = 0
+    for v, msgs in enumerate(calls):
+        if v == bad:
+            continue
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, ov) == 0
+        ov += 1
+    want = orc.serialize_records(3, list(range(rows)))
+    orc.close()
+    if kind == SORTED_MAP:
+        assert got == want
+    else:
+        assert _map_rows(got) == _map_rows(want)
+
+
+def _map_rows(body):
+    """{row: {col: value}} of RecordBuff records {int32 row; size_t size; Entry<int32>[n]}."""
+    import struct
+    out, off = {}, 0
+    while off < len(body):
+        rid, size = struct.unpack_from("<iQ", body, off)
+        off += 12
+        e = np.frombuffer(body[off:off + size], np.int32).reshape(-1, 2)
+        out[rid] = dict(zip(e[:, 0].tolist(), e[:, 1].tolist()))
+        off += size
+    return out

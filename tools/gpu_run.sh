@@ -20,6 +20,7 @@
 #   c3lib   C3 with this tree's libpsx and ab_old/libpsx.so (PSX_LIB), interleaved twice
 #   oldheavy the all-rows-heavy-and-spilling test on ab_old/libpsx.so (reported, never fatal)
 #   splittests the split-apply / sparse / KAT GPU test files only
+#   xtests  the split / exchange pipeline / walk-count / multi-rank GPU test files only
 #   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
@@ -131,6 +132,7 @@ for db, ks in d.items():
           for f in $O/c3wc_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     wctests) run wctests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_count_gpu.py tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py tests/test_indexed_rows_gpu.py ;;
     oldheavy) say oldheavy; timeout -k 10 300 env PSX_LIB=ab_old/libpsx.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ord_split_gpu.py -k every_row_heavy > "$O/oldheavy.log" 2>&1; echo "oldheavy rc=$? (the pre-fix library: a failure here is the collision)"; tail -5 "$O/oldheavy.log" ;;
+    xtests) run xtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_split_gpu.py tests/test_walk_count_gpu.py tests/test_multi_rank_gpu.py ;;
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -692,6 +692,9 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
 
     progress(f"{len(chunks)} chunks of {rpc} records; warmup", rank)
     verbose = (lambda m: progress(m, rank)) if os.environ.get("PSX_BENCH_VERBOSE") else None
+    if verbose and os.environ.get("PSX_BENCH_STACK_AFTER"):
+        import faulthandler        # diagnosis: where the host waits if a step never finishes
+        faulthandler.dump_traceback_later(float(os.environ["PSX_BENCH_STACK_AFTER"]), exit=True)
     for _ in range(warmup):
         ex.run(chunks, log=verbose)
         sync()

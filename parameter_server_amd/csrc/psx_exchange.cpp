@@ -190,11 +190,23 @@ psx_status psx_exchange_streams(psx_comm *c, const void *send, const uint64_t *s
       return comm_fail(c, "exchange_streams: null buffer with a nonzero size", PSX_ERR_INVALID_ARG);
   hipStream_t st = (hipStream_t)hip_stream;
   HIPX_TRY(c, hipSetDevice(c->device));
+  // Each sub-stream crosses in pieces of at most kPiece bytes (sends and receives to one
+  // peer match in issue order inside the group): this RCCL (2.26) delivers a single
+  // point-to-point transfer of ~2 GiB corrupted (measured: a 2,147,481,620-byte self
+  // send/recv arrived wrong while the same bytes in 512 MiB pieces arrive intact,
+  // tests/test_split_gpu.py::test_rccl_exchange_large_sub_stream_in_pieces).
+  constexpr uint64_t kPiece = (uint64_t)512 << 20;
   uint64_t so = 0, ro = 0;
   NCCL_TRY(c, ncclGroupStart());
   for (int p = 0; p < c->nranks; ++p) {
-    if (send_sizes[p]) NCCL_TRY_G(c, ncclSend((const uint8_t *)send + so, send_sizes[p], ncclUint8, p, c->comm, st));
-    if (recv_sizes[p]) NCCL_TRY_G(c, ncclRecv((uint8_t *)recv + ro, recv_sizes[p], ncclUint8, p, c->comm, st));
+    for (uint64_t o = 0; o < send_sizes[p]; o += kPiece) {
+      const uint64_t n = send_sizes[p] - o < kPiece ? send_sizes[p] - o : kPiece;
+      NCCL_TRY_G(c, ncclSend((const uint8_t *)send + so + o, n, ncclUint8, p, c->comm, st));
+    }
+    for (uint64_t o = 0; o < recv_sizes[p]; o += kPiece) {
+      const uint64_t n = recv_sizes[p] - o < kPiece ? recv_sizes[p] - o : kPiece;
+      NCCL_TRY_G(c, ncclRecv((uint8_t *)recv + ro + o, n, ncclUint8, p, c->comm, st));
+    }
     so += send_sizes[p];
     ro += recv_sizes[p];
   }

@@ -259,3 +259,19 @@ def test_shard_exchange_pipeline_one_rank_bit_exact(rows, cap, chunk_recs):
     assert m["parity"] == "bit-exact", m
     assert m["chunks_per_step"] == -(-rows // chunk_recs)
     assert m["apply_kernel_ms_per_chunk"] and m["exchange_kernel_ms_per_step"] is not None
+
+
+@pytest.mark.parametrize("nbytes", [(1 << 31) - 2028, (1 << 31) + 4096 * 3])
+def test_rccl_exchange_large_sub_stream_in_pieces(nbytes):
+    """A sub-stream near and past 2 GiB crosses intact (psx_exchange_streams sends it in
+    512 MiB pieces: this RCCL corrupts a single ~2 GiB point-to-point transfer)."""
+    from parameter_server_amd.exchange import Exchange
+    xc = Exchange(0)
+    g = torch.Generator(device="cuda").manual_seed(nbytes)
+    send = torch.randint(-2 ** 31, 2 ** 31 - 1, (nbytes // 4,), generator=g, dtype=torch.int32,
+                         device="cuda").view(torch.uint8)
+    recv, rs = xc.alltoall(send, [nbytes])
+    torch.cuda.synchronize()
+    assert rs == [nbytes]
+    assert torch.equal(recv, send)
+    xc.close()

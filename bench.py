@@ -1092,94 +1092,239 @@ def c5_cpu_baseline(args, wl, seconds):
                       f"1 thread: {n1} clocks in {e1:.1f} s (oracle: apply + ClockUntil + per-client push bodies)"}
 
 
+C5_STALENESS = 4
+
+
+def c5_schedule(B, clocks, staleness=C5_STALENESS, speeds=None):
+    """The order in which the server receives the workers' per-clock messages under SSP
+    (a discrete-event simulation in virtual time; the server is taken to be instantaneous).
+    Worker w needs speeds[w] time units per clock.  Before computing clock c a worker's Get
+    blocks until the server has pushed clock >= c - staleness
+    (SSPPushConsistencyController::Get, ssp_push_consistency_controller.cpp:70-88); when its
+    clock ends it sends the clock's message (is_clock, ClientSendOpLogMsg).  The server
+    ticks the sender's clock on each message (Server::ClockUntil, server.cpp:62-79) and
+    pushes when the minimum advances (server_thread.cpp:262-288), which releases gated
+    workers.  Returns (arrivals, stats): arrivals lists (worker, clock, push) in arrival
+    order, push = the new min clock if this message advanced it, else 0; simulated until
+    every worker has sent `clocks` messages."""
+    import heapq
+    speeds = speeds or [1.0 + 0.25 * w for w in range(B)]   # worker 7 is 2.75x slower than worker 0
+    vclock = [0] * B          # messages the server has from each worker
+    pushed = 0                # the last pushed (min) clock
+    blocked = []              # workers waiting in Get: (clock they want to start, worker)
+    ev = [(speeds[w], w, 0) for w in range(B)]    # (finish time, worker, clock finished)
+    heapq.heapify(ev)
+    arrivals, n_blocked, max_lead = [], 0, 0
+    while ev:
+        t, w, c = heapq.heappop(ev)
+        vclock[w] = c + 1
+        new_min = min(vclock)
+        push = new_min if new_min > pushed else 0
+        max_lead = max(max_lead, max(vclock) - min(vclock))
+        arrivals.append((w, c, push))
+        nxt = []
+        if push:
+            pushed = push
+            still = []
+            for cw, bw in blocked:
+                (nxt if pushed >= cw - staleness else still).append((cw, bw))
+            blocked = still
+        if c + 1 < clocks:
+            if pushed >= (c + 1) - staleness:
+                nxt.append((c + 1, w))
+            else:
+                blocked.append((c + 1, w))
+                n_blocked += 1
+        for cw, bw in nxt:
+            heapq.heappush(ev, (t + speeds[bw], bw, cw))
+    return arrivals, {"max_clock_lead": max_lead, "gate_blocks": n_blocked, "staleness": staleness,
+                      "worker_speeds": speeds}
+
+
 def run_c5(args):
-    """mixed dense + sparse tables, a continuous stream with clocks under
-    SSPPush.  8 workers (= 8 clients) each send one message per clock carrying both tables
-    (a C2-like dense f32 table, 2^18 x 256, half the rows per worker; a C3-like
-    SortedVectorMapRow<int32> table, 100K x 1024, 1250 Zipf rows per worker); each client
-    subscribed to the rows of its messages (its row requests, server_thread.cpp:185-200).
-    Per clock the server applies the 8 messages (one fused call), advances every sender's
-    clock (Server::ClockUntil, server.cpp:62-79) and, when the min clock moves
-    (server_thread.cpp:262-288), builds one push body per client from its subscriptions
-    (CreateSendServerPushRowMsgs, server.cpp:189-309) into host memory.  Staleness 4 is the
-    client's Get gate (ssp_push_consistency_controller.cpp:70-88): workers may run up to 4
-    clocks ahead, and the server sees the same stream.  Reports clocks/s, the split, the
-    bound (device share at HBM peak + push bodies at the PCIe spec) and the CPU port."""
+    """SURVEY §8(d) C5, end to end: mixed dense + sparse tables, a continuous update stream
+    under SSPPush with staleness 4, messages arriving from host memory and push bodies
+    leaving to host memory.
+
+    8 workers (= 8 clients), each sending one message per clock with both tables (a C2-like
+    dense f32 table, 2^18 x 256, half the rows per worker; a C3-like SortedVectorMapRow<int32>
+    table, 100K x 1024, 1250 Zipf rows per worker); each client subscribed to the rows of its
+    messages (its row requests, server_thread.cpp:185-200).  The workers run at different
+    speeds and the SSP gate lets the fast ones run up to 4 clocks ahead (c5_schedule), so the
+    server receives later clocks' messages before it can push earlier ones.  The server
+    (server_thread.cpp:224-299) takes the messages in arrival order: each run of arrivals up
+    to the one that advances the min clock is copied host-to-device from page-locked memory
+    (the worker socket buffers) and applied in one fused call, every sender's clock ticks
+    (ClockUntil), and the push bodies (one per client, CreateSendServerPushRowMsgs,
+    server.cpp:189-309) go device-to-host.  The next run's host-to-device copy overlaps this
+    run's apply and push.  WORLD_SIZE > 1: the tables are row-range sharded over the ranks;
+    each worker's message is split per owner, as the reference client splits per server
+    (abstract_bg_worker.cpp:590-649), and each rank serves its own shard with no collective.
+    value = pushed clocks per second (max over ranks)."""
+    import numpy as np
     import torch
+    import torch.distributed as dist
     import parameter_server_amd as psa
+    from parameter_server_amd import wire
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     wl = c5_workload()
     rows_d, cap, rows_s, K, B = wl["rows_d"], wl["cap"], wl["rows_s"], wl["K"], wl["B"]
-    msgs, subs = wl["msgs"], wl["subs"]
-    dev = [torch.from_numpy(m).cuda() for m in msgs]
+    # this rank's row ranges and the workers' per-owner messages
+    d_lo, d_hi = rank * rows_d // world, (rank + 1) * rows_d // world
+    s_lo, s_hi = rank * rows_s // world, (rank + 1) * rows_s // world
+    msgs, subs = [], []
+    for ids_d, upd, ids_s, cnt in wl["parts"]:
+        md, ms = (ids_d >= d_lo) & (ids_d < d_hi), (ids_s >= s_lo) & (ids_s < s_hi)
+        msgs.append(wire.pack_np([dict(table_id=1, dense_serialized=True, row_ids=ids_d[md], oplogs=upd[md]),
+                                  dict(table_id=3, dense_serialized=False, row_ids=ids_s[ms], oplogs=cnt[ms])]))
+        subs.append((ids_d[md], ids_s[ms]))
+    host = [torch.from_numpy(m).pin_memory() for m in msgs]           # the worker socket buffers
+    mmax = max(max(m.size for m in msgs), 4)
+    slots = [[torch.empty(mmax, dtype=torch.uint8, device="cuda") for _ in range(16)] for _ in range(2)]
     bgs = [100 + b for b in range(B)]
-    srv = psa.Server(0, 1, bgs)
-    srv.set_stream(torch.cuda.current_stream().cuda_stream)
-    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows_d))
+    srv = psa.Server(local, 1 + rank, bgs)
+    s_apply, s_in = torch.cuda.Stream(), torch.cuda.Stream()
+    srv.set_stream(s_apply.cuda_stream)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
+                                     row_offset=d_lo, max_rows=d_hi - d_lo))
     srv.CreateTable(3, psa.TableInfo(row_kind=psa.ROW_SORTED_MAP, dtype=psa.I32, row_capacity=K,
-                                     oplog_dense_serialized=False, max_rows=rows_s, max_entries=K))
+                                     oplog_dense_serialized=False, row_offset=s_lo, max_rows=s_hi - s_lo,
+                                     max_entries=K))
     srv.set_num_clients(B)
     for b, (ids_d, ids_s) in enumerate(subs):
         srv.subscribe(1, ids_d, b)
         srv.subscribe(3, ids_s, b)
-    ver = [0]
-    pushed, pushes = [0], [0]
-    t_apply, t_clock = [0.0], [0.0]
+    W, Kc = args.warmup, args.steps
+    arrivals, gate = c5_schedule(B, W + Kc + C5_STALENESS + 2)
+    # runs of arrivals: each ends with the message that advances the min clock
+    runs, cur = [], []
+    for w, c, push in arrivals:
+        cur.append((w, c))
+        if push or len(cur) == 16:        # a fused call takes <= 16 messages
+            runs.append((cur, push))
+            cur = []
+    ver = [0] * B
+    ev_in = [torch.cuda.Event(), torch.cuda.Event()]
+    ev_used = [torch.cuda.Event(), torch.cuda.Event()]
+    acct = {"h2d": 0, "d2h": 0, "msgs": 0, "pushes": 0, "apply_s": 0.0, "push_s": 0.0, "lead_at_push": 0}
 
-    def clock():
-        t = time.perf_counter()
-        srv.apply_device([(d.data_ptr(), d.numel(), bgs[b], ver[0]) for b, d in enumerate(dev)])
-        srv.sync()
-        t2 = time.perf_counter()
-        t_apply[0] += t2 - t
+    def h2d(j):
+        if j >= len(runs):
+            return
+        k = j % 2
+        s_in.wait_event(ev_used[k])                    # run j-2's apply has read slot set k
+        with torch.cuda.stream(s_in):
+            for i, (w, c) in enumerate(runs[j][0]):       # message i of the run -> slot i
+                if host[w].numel():
+                    slots[k][i][:host[w].numel()].copy_(host[w], non_blocking=True)
+        ev_in[k].record(s_in)
+
+    def serve(j):
+        """One run: apply (fused), ClockUntil per message, push if the min clock moved."""
+        k = j % 2
+        group, push = runs[j]
+        t0 = time.perf_counter()
+        s_apply.wait_event(ev_in[k])
+        call = []
+        for i, (w, c) in enumerate(group):
+            call.append((slots[k][i].data_ptr(), int(host[w].numel()), bgs[w], ver[w]))
+            ver[w] += 1
+        srv.apply_device(call)
+        ev_used[k].record(s_apply)
+        h2d(j + 1)                                     # the next run's copy beside this apply and push
         changed = 0
-        for bg in bgs:                       # each worker's clock message (is_clock, bg_clock)
-            changed = srv.ClockUntil(bg, ver[0] + 1) or changed
-        if changed:                          # the min clock moved: one push body per client
-            pushed[0] += sum(x.size for x in srv.serialize_push(clear=True, as_bytes=False))
-            pushes[0] += 1
-        t_clock[0] += time.perf_counter() - t2
-        ver[0] += 1
+        for w, c in group:
+            changed = srv.ClockUntil(bgs[w], c + 1) or changed
+        t1 = time.perf_counter()
+        pushed_bytes = 0
+        if changed:
+            bodies = srv.serialize_push(clear=True, as_bytes=False)    # settles the apply; D2H
+            pushed_bytes = sum(x.size for x in bodies)
+        else:
+            srv.sync()
+        t2 = time.perf_counter()
+        return len(group), sum(int(host[w].numel()) for w, _ in group), pushed_bytes, bool(changed), t1 - t0, t2 - t1
 
-    for _ in range(args.warmup):
-        clock()
-    pushed[0] = pushes[0] = 0
-    t_apply[0] = t_clock[0] = 0.0
+    # warmup: the runs up to the W-th push
+    j, pushes = 0, 0
+    h2d(0)
+    while j < len(runs) and pushes < W:
+        pushes += runs[j][1] > 0
+        serve(j)
+        j += 1
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        clock()
+    done = 0
+    while j < len(runs) and done < Kc:
+        n, hb, db, ch, ta, tp = serve(j)
+        acct["msgs"] += n
+        acct["h2d"] += hb
+        acct["d2h"] += db
+        acct["apply_s"] += ta
+        acct["push_s"] += tp
+        done += runs[j][1] > 0
+        j += 1
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        tot = torch.tensor([acct["h2d"], acct["d2h"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        h2d_all, d2h_all = (float(x) for x in tot.tolist())
+    else:
+        h2d_all, d2h_all = float(acct["h2d"]), float(acct["d2h"])
     srv.close()
-    del dev
-    msg_bytes = sum(m.size for m in msgs)
-    push_per_clock = pushed[0] / args.steps
+    del slots
+    torch.cuda.empty_cache()
+    ms = el / max(done, 1) * 1e3
     touched_d = len(set().union(*[set(a.tolist()) for a, _ in subs]))
-    device_bytes = msg_bytes + 2 * touched_d * cap * 4
-    step_bytes = device_bytes + push_per_clock
-    bound_ms = (device_bytes / (HBM_PEAK_GBS * 1e9) + push_per_clock / (PCIE_PEAK_GBS * 1e9)) * 1e3
-    ms = el / args.steps * 1e3
-    cpu = c5_cpu_baseline(args, wl, min(args.cpu_seconds, 12.0)) if args.cpu_seconds > 0 else None
-    line = {
-        "metric": "C5 mixed dense+sparse clock under SSPPush (apply + ClockUntil + per-client push to host)",
-        "value": round(args.steps / el, 2), "unit": "clocks/s",
-        "GBps_algorithmic": round(step_bytes * args.steps / el / 1e9, 2),
-        "ms_per_clock": round(ms, 3),
-        "apply_ms_per_clock": round(t_apply[0] / args.steps * 1e3, 3),
-        "clock_and_push_ms_per_clock": round(t_clock[0] / args.steps * 1e3, 3),
-        "pushes": pushes[0], "pushed_bytes_per_clock": int(push_per_clock),
-        "message_bytes_per_clock": msg_bytes,
-        "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
-                  "device_ms_at_hbm_peak": round(device_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 3),
-                  "push_ms_at_pcie_spec": round(push_per_clock / (PCIE_PEAK_GBS * 1e9) * 1e3, 3),
-                  "what": "messages + dense row read/write at 8 TB/s, plus every client's push body to host "
-                          "memory at the PCIe Gen5 x16 spec (63 GB/s); the push is the path's end in host memory"},
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "dtype": "f32+int32",
-        "data": "synthetic", "config": {"workload": "C5: dense 2^18x256 f32 + sorted-map 100Kx1024 int32, "
-                                                    "8 clients x 1 msg/clock, SSPPush, staleness 4 (client gate)"},
-        "cpu_baseline": cpu,
-    }
-    print(json.dumps(line), flush=True)
+    dev_bytes = acct["h2d"] / max(done, 1) + 2 * touched_d * cap * 4 / 1.0
+    h2d_pc, d2h_pc = acct["h2d"] / max(done, 1), acct["d2h"] / max(done, 1)
+    bound_ms = (max(h2d_pc, d2h_pc) / (PCIE_PEAK_GBS * 1e9) + dev_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    bound_serial_ms = ((h2d_pc + d2h_pc) / (PCIE_PEAK_GBS * 1e9) + dev_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    cpu = c5_cpu_baseline(args, wl, min(args.cpu_seconds, 12.0)) if args.cpu_seconds > 0 and world == 1 else None
+    if rank == 0:
+        line = {
+            "metric": "C5 mixed dense+sparse clocks under SSPPush, end to end (H2D of the workers' messages, apply, "
+                      "ClockUntil, per-client push bodies D2H)",
+            "value": round(done / el, 2), "unit": "clocks/s",
+            "ms_per_clock": round(ms, 3),
+            "n_gpus": world, "steps": done, "warmup": W, "higher_is_better": True,
+            "h2d_bytes_per_clock_all_ranks": int(h2d_all / max(done, 1)),
+            "d2h_bytes_per_clock_all_ranks": int(d2h_all / max(done, 1)),
+            "pcie_GBps_per_rank": {"h2d": round(h2d_pc / (ms / 1e3) / 1e9, 2), "d2h": round(d2h_pc / (ms / 1e3) / 1e9, 2)},
+            "messages_per_clock": round(acct["msgs"] / max(done, 1), 2),
+            "apply_and_clock_ms_per_clock": round(acct["apply_s"] / max(done, 1) * 1e3, 3),
+            "push_ms_per_clock": round(acct["push_s"] / max(done, 1) * 1e3, 3),
+            "ssp_gate": dict(gate, what="c5_schedule: worker w takes 1 + 0.25 w time units per clock; Get blocks "
+                                        "until pushed clock >= clock - staleness; the server applies messages in "
+                                        "arrival order, so fast workers' later clocks are applied before the push "
+                                        "of earlier ones"),
+            "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
+                      "serial_ms_per_clock": round(bound_serial_ms, 3),
+                      "what": "per rank: max(H2D, D2H) bytes at the PCIe Gen5 x16 spec (63 GB/s per direction, "
+                              "full duplex) + the device bytes (messages + dense row read/write) at 8 TB/s; "
+                              "serial_ms: both directions in turn"},
+            "dtype": "f32+int32", "data": "synthetic",
+            "config": {"workload": f"C5: dense {rows_d}x{cap} f32 + sorted-map {rows_s}x{K} int32, {B} clients x 1 msg/"
+                                   f"clock, SSPPush, staleness {C5_STALENESS}, row-range shards x{world}",
+                       "scaling": "strong (fixed workload split over the ranks)"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():

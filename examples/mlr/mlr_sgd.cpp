@@ -8,16 +8,21 @@
 //
 // with the reference's run_lr_synth.sh settings (row_oplog_type 0, --oplog_dense_serialized).
 // Written against include/petuum_ps_common only (no gflags/glog/boost): flags are
-// "--name value".  Data: a synthetic, linearly separable-ish multiclass set (--seed), split
-// evenly over the worker threads.
+// "--name value".  Data: a synthetic, linearly separable-ish multiclass set (--seed), or a
+// libsvm file with its .meta (--train_file; the reference's ReadDataLabelLibSVM input, e.g.
+// apps/mlr/datasets/covtype.scale.train.small: feature_dim 54, 7 labels, one-based features
+// and labels), split evenly over the worker threads.
 //
 //   mlr_sgd --num_labels 8 --feature_dim 512 --num_train 4000 --num_worker_threads 2
+//   mlr_sgd --train_file covtype.scale.train.small --num_worker_threads 2
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <map>
+#include <sstream>
 #include <mutex>
 #include <random>
 #include <string>
@@ -59,6 +64,62 @@ void MakeData(uint32_t seed) {
     Y[i] = (int32_t)(g() % (uint32_t)num_labels);
     for (int j = 0; j < feature_dim; ++j) X[i][j] = 0.25f * centers[Y[i]][j] + n01(g);
   }
+}
+
+// The reference's MetafileReader keys (ml/util/metafile_reader.cpp: "key: value" lines).
+std::map<std::string, std::string> ReadMeta(const std::string &path) {
+  std::ifstream f(path);
+  if (!f) fail("cannot open " + path);
+  std::map<std::string, std::string> m;
+  std::string line;
+  while (std::getline(f, line)) {
+    const size_t c = line.find(':');
+    if (c == std::string::npos) continue;
+    std::string v = line.substr(c + 1);
+    v.erase(0, v.find_first_not_of(" \t"));
+    m[line.substr(0, c)] = v;
+  }
+  return m;
+}
+
+// libsvm rows "label idx:val ..." (ReadDataLabelLibSVM, ml/util/data_loading.cpp): features
+// and labels shifted to zero-based when the meta file says they are one-based.
+void ReadLibSVM(const std::string &path, const std::string &meta_path) {
+  auto meta = ReadMeta(meta_path);
+  auto need = [&](const char *k) {
+    auto it = meta.find(k);
+    if (it == meta.end()) fail(meta_path + " has no " + k);
+    return std::atoi(it->second.c_str());
+  };
+  feature_dim = need("feature_dim");
+  num_labels = need("num_labels");
+  const int f1 = need("feature_one_based"), l1 = need("label_one_based");
+  if (meta.count("format") && meta["format"] != "libsvm") fail("format " + meta["format"] + " is not libsvm");
+  std::ifstream f(path);
+  if (!f) fail("cannot open " + path);
+  X.clear();
+  Y.clear();
+  std::string line;
+  while (std::getline(f, line)) {
+    std::istringstream in(line);
+    int label;
+    if (!(in >> label)) continue;
+    std::vector<float> x(feature_dim, 0.f);
+    std::string tok;
+    while (in >> tok) {
+      const size_t c = tok.find(':');
+      if (c == std::string::npos) fail("bad feature " + tok);
+      const int j = std::atoi(tok.substr(0, c).c_str()) - f1;
+      if (j < 0 || j >= feature_dim) fail("feature index out of range: " + tok);
+      x[j] = std::strtof(tok.c_str() + c + 1, nullptr);
+    }
+    label -= l1;
+    if (label < 0 || label >= num_labels) fail("label out of range in " + line);
+    X.push_back(std::move(x));
+    Y.push_back(label);
+  }
+  num_train = (int)X.size();
+  if (!num_train) fail(path + " holds no rows");
 }
 
 class Barrier {
@@ -190,7 +251,13 @@ int main(int argc, char **argv) {
   learning_rate = flag_d("learning_rate", 0.05);
   decay = flag_d("decay_rate", 0.9);
   const int staleness = flag_i("table_staleness", 0);
-  MakeData((uint32_t)flag_i("seed", 1234));
+  if (g_flags.count("train_file")) {
+    const std::string tf = g_flags["train_file"];
+    ReadLibSVM(tf, g_flags.count("meta") ? g_flags["meta"] : tf + ".meta");
+    std::printf("DATA %d %d %d\n", num_train, feature_dim, num_labels);
+  } else {
+    MakeData((uint32_t)flag_i("seed", 1234));
+  }
 
   petuum::TableGroupConfig tg;
   petuum::InitTableGroupConfig(&tg, 2);

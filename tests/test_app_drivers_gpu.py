@@ -8,7 +8,8 @@ libpetuum_ps.so + libpsx.so, each replayed message by message through the CPU or
                           DenseRow<double> llh table, sparse-serialized (run_lda.sh:82-83)
   mlr_sgd                 apps/mlr's W table: DenseRow<float> of feature_dim per label,
                           DenseBatchInc per label and Get of every row per refresh
-                          (mlr_sgd_solver.cpp:66-95)
+                          (mlr_sgd_solver.cpp:66-95); synthetic data, and the reference's own
+                          covtype.scale.train.small (libsvm)
   matrixfact_adarevision  apps/matrixfact's AdaRevision build: R's table registers
                           AdaRevisionServerTableLogic as server_table_logic 1 with
                           version_maintain (matrixfact_adarevision.cpp:633-635,
@@ -87,6 +88,27 @@ def test_mlr_weight_rows_match_oracle_every_clock(tmp_path, channels, staleness)
     assert len(rows) == epochs
     # rows: {epoch, mean loss, accuracy}
     assert rows[-1][1] < rows[0][1] and rows[-1][2] > 2.0 / L, rows
+
+
+@pytest.mark.parametrize("channels,staleness", [(1, 0), (2, 2)])
+def test_mlr_on_the_reference_covtype_data(tmp_path, channels, staleness):
+    """apps/mlr's shipped dataset (apps/mlr/datasets/covtype.scale.train.small + .meta,
+    libsvm, 500 rows, feature_dim 54, 7 labels, one-based; kept as a data fixture under
+    tests/golden/mlr): the driver reads it as ReadDataLabelLibSVM does, trains W (7 rows of 54)
+    and every message, reply and push is replayed through the oracle byte for byte."""
+    data = os.path.join(ROOT, "tests", "golden", "mlr", "covtype.scale.train.small")
+    epochs = 5
+    trace, out = run(tmp_path, "mlr_sgd", ["--train_file", data, "--num_worker_threads", 2, "--num_epochs", epochs,
+                                           "--batch_size", 25, "--learning_rate", 0.1, "--decay_rate", 0.95,
+                                           "--num_comm_channels_per_client", channels, "--table_staleness", staleness])
+    assert "DATA 500 54 7" in out
+    counts = replay(trace, channels, [dict(tid=0, kind=DENSE, dtype=F32, cap=54),
+                                      dict(tid=1, kind=DENSE, dtype=F32, cap=3)])
+    assert counts["push"] > 0 and counts["msg"] > 0
+    rows = [list(map(float, ln.split()[1:])) for ln in out.splitlines() if ln.startswith("LOSS ")]
+    assert len(rows) == epochs
+    assert rows[-1][1] < rows[0][1], rows          # mean cross-entropy falls
+    assert rows[-1][2] > 1.0 / 7, rows              # better than chance
 
 
 def _write_split(prefix, rows=600, cols=300, nnz=4000, seed=77):

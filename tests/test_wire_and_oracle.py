@@ -213,3 +213,17 @@ def test_oracle_half_decompression_all_values(oracle_lib):
     assert np.array_equal(got[~nan], (np.float32(0) + want[~nan]))
     gb = got[nan].view(np.uint32)   # the add quiets the NaN (bit 22); the rest of the payload survives
     assert np.array_equal(gb & 0x003fe000, (h[nan].astype(np.uint32) & 0x1ff) << 13)
+
+
+def test_covtype_fixture_matches_its_meta():
+    """tests/golden/mlr: the reference app's covtype sample (data, not code) as its .meta says."""
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mlr")
+    meta = dict(l.split(":", 1) for l in open(os.path.join(d, "covtype.scale.train.small.meta")) if ":" in l)
+    assert int(meta["feature_dim"]) == 54 and int(meta["num_labels"]) == 7 and meta["format"].strip() == "libsvm"
+    rows = [l.split() for l in open(os.path.join(d, "covtype.scale.train.small")) if l.strip()]
+    assert len(rows) == int(meta["num_train_total"]) == 500
+    labels = {int(r[0]) for r in rows}
+    assert labels <= set(range(1, 8))
+    idx = {int(t.split(":")[0]) for r in rows for t in r[1:]}
+    assert min(idx) >= 1 and max(idx) <= 54

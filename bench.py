@@ -62,6 +62,23 @@ def kernel_signature():
     return h.hexdigest()[:16]
 
 
+C3_PMC_JSON = os.path.join(ROOT, "profiles", "r04", "pmc_c3.json")
+
+
+def c3_kernel_signature():
+    """Identity of the code a C3 step runs (walk, ordered path, decode, the device structs,
+    the flags): the C3 PMC JSON is reported only on the tree it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "parameter_server_amd", "csrc")
+    for f in ("psx_walk.hip", "psx_ordered.hip", "psx_kernels.hip", "psx_device.hpp", "psx_scan.hpp"):
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    for line in open(os.path.join(csrc, "Makefile")):
+        if line.startswith("HIPFLAGS") or line.startswith("           -"):
+            h.update(line.encode())
+    return h.hexdigest()[:16]
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -481,6 +498,28 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
         decode = "one workgroup per message (decode_streams)"
     stream_bytes = sum(s.size for s in streams)
     model = c3_model(batches, rows, K, apply_ms / max(apply_n, 1), split=L.psx_debug_get_variant(6))
+    # algorithmic bytes = the records and headers + a 4-B read and write per
+    # distinct (row, col) the step touches
+    import numpy as np
+    keys = np.unique(np.concatenate([np.int64(rid) * K + c.astype(np.int64) for recs in batches
+                                     for rid, c, _ in recs]))
+    alg = stream_bytes + 8 * int(keys.size)
+    step_s = el / steps
+    apply_s = apply_ms / max(apply_n, 1) / 1e3
+    roof = {"bound": "hbm", "algorithmic_bytes_per_step": alg, "distinct_row_cols_per_step": int(keys.size),
+            "achieved_step_GBps": round(alg / step_s / 1e9, 2), "frac_step": round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel": "ordered_apply", "achieved": round(alg / apply_s / 1e9, 2) if apply_s else None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / apply_s / 1e9 / HBM_PEAK_GBS, 4) if apply_s else None,
+            "traffic": None, "sector_efficiency": None}
+    if os.path.exists(C3_PMC_JSON):
+        pm = json.load(open(C3_PMC_JSON))
+        if pm.get("kernel_signature") == c3_kernel_signature():
+            roof["traffic"] = round(pm["bytes_per_step"])
+            roof["sector_efficiency"] = round(alg / pm["bytes_per_step"], 4)
+            roof["traffic_source"] = os.path.relpath(C3_PMC_JSON, ROOT) + " (L2->fabric request bytes per step, all kernels)"
+        else:
+            roof["traffic_note"] = f"{os.path.relpath(C3_PMC_JSON, ROOT)} is for another kernel signature"
     cpu = c3_cpu_baseline(args, batches, nupd, bgs, cpu_seconds) if cpu_seconds > 0 else None
     return {
         "metric": "sparse int row-update apply (SortedVectorMapRow<int32>), C3",
@@ -498,6 +537,7 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
         "ordered_apply_ms_per_step": round(apply_ms / max(apply_n, 1), 4),
         "kernel_ms_per_step_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
         "latency_model": model,
+        "roofline": roof,
         "cpu_baseline": cpu}
 
 
@@ -1618,8 +1658,8 @@ def main():
                 m = run_child(["--workload", "c3", "--steps", "20", "--warmup", "3"] + flags)
                 other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "decode",
                                                      "ordered_apply_ms_per_step",
-                                                     "kernel_ms_per_step_breakdown_pass", "cpu_baseline",
-                                                     "pipelined")}
+                                                     "kernel_ms_per_step_breakdown_pass", "roofline",
+                                                     "cpu_baseline", "pipelined")}
                 other[name]["config"] = m["config"]["workload"]
                 lm = m.get("latency_model") or {}
                 other[name]["ordered_apply_frac_of_latency_bound"] = lm.get("frac_of_bound")

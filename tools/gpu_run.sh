@@ -63,6 +63,30 @@ for s in "$@"; do
       done
       python3 tools/pmc_summary.py "$R/pmc" "$O/pmc_dense_apply.json" || exit 1
       PMC_JSON=$O/pmc_dense_apply.json ;;
+    pmcc3)
+      say "pmc c3: DRAM-side request bytes"
+      timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
+        -d "$R/pmcc3" -o pmc -- python3 bench.py --workload c3 --steps 10 --warmup 2 --cpu-seconds 0 > "$O/pmcc3.log" 2>&1 \
+        || { echo "!! pmcc3"; tail -5 "$O/pmcc3.log"; exit 1; }
+      python3 tools/pmc_c3.py "$R/pmcc3" "$O/pmc_c3.json" || exit 1 ;;
+    spread)   # C2 spread vs translation: alternating layouts, each a fresh process under the UTCL1 counters
+      i=0
+      for lay in 0 1 0 1 0 1; do
+        i=$((i+1)); say "spread pass $i layout $lay"
+        timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_CLIENT_UTCL1_INFLIGHT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_REQUEST_sum \
+          -d "$R/spread/p$i" -o pmc -- python3 tools/spread_c2.py --layout $lay > "$O/spread_p$i.log" 2>&1 || { echo "!! spread $i"; tail -5 "$O/spread_p$i.log"; exit 1; }
+        grep -h '^{' "$O/spread_p$i.log" | cut -c1-200
+      done
+      for i in 1 2 3 4 5 6; do
+        python3 tools/pmc_db.py $(find "$R/spread/p$i" -name '*.db') > "$O/spread_pmc_p$i.json" || exit 1
+      done
+      for i in 1 2 3 4 5 6; do echo "=== p$i $(grep -h '^{' $O/spread_p$i.log | cut -c1-60)"; python3 -c "
+import json; d=json.load(open('$O/spread_pmc_p$i.json'))
+for db, ks in d.items():
+    for k, v in ks.items():
+        if 'dense_apply' in k:
+            m=v.get('TCP_UTCL1_TRANSLATION_MISS_sum',0); f=v.get('TCP_CLIENT_UTCL1_INFLIGHT_sum',0)
+            print(' miss', round(m), 'inflight/miss', round(f/m,1) if m else None, 'credits', round(v.get('TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum',0)), 'req', round(v.get('TCP_UTCL1_REQUEST_sum',0)))"; done ;;
     listpmc) timeout -s KILL 60 rocprofv3 -L > "$R/counters.txt" 2>&1; echo "listpmc rc=$?"; grep -o "SQ_[A-Z_0-9]*\|TCC_[A-Z_0-9]*\|TCP_[A-Z_0-9]*\|TA_[A-Z_0-9]*\|TD_[A-Z_0-9]*" "$R/counters.txt" | sort -u > "$O/counter_names.txt"; wc -l < "$O/counter_names.txt" ;;
     pmc3)
       P=1

@@ -32,7 +32,10 @@ enum {
   PSX_VARIANT_WALK_CUS = 12,    /* the walk's persistent grid: 0 half the CUs (default), 1 every CU */
   PSX_VARIANT_WALK_COUNT = 13   /* 1 (default): on walked calls the walk counts the records of split
                                    sorted/map tables into the call slot's count state (no
-                                   ordered_count launch); 0: ordered_count counts them */
+                                   ordered_count launch); 0: ordered_count counts them */,
+  PSX_VARIANT_FOLD_FINISH = 14  /* 1 (default): a call whose last launch is an ordered apply on the
+                                   context stream does finish_call's work in that launch's last
+                                   block (no finish_call launch); 0: finish_call launched */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -190,6 +190,11 @@ struct OrdArgs {
                              // launch takes them first
   int32_t counted;           // split tables: the walk already counted this call's records
                              // (WalkCount): ordered_count is not launched
+  // finish_call folded into this apply launch (the call's last): non-null fin_done = a zeroed
+  // block counter; the last block does finish_call's work (psx_ordered.hip finish_tail)
+  uint32_t *fin_sticky;
+  uint32_t *fin_log;
+  uint32_t *fin_done;
 };
 
 // ordered_count's work for one split sorted/map table (grow set), done by the window-parallel

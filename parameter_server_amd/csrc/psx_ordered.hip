@@ -426,8 +426,27 @@ __device__ __forceinline__ double sparse_importance(const uint8_t *vals, int32_t
 
 // DRY: the capacity dry run — same walk on the LDS image, nothing written back; only rows
 // whose entries plus the call's record entries exceed max_entries are simulated.
+// finish_call folded into the call's last apply launch (OrdArgs.fin_done set): every block,
+// once all its waves are done, counts itself; the last one folds the call's status into the
+// sticky word, logs it and frees the ring slot — what finish_call_kernel does, without a
+// launch of its own (an empty launch costs ~4.6 µs per call, profiles/r03/s26).
+__device__ __forceinline__ void finish_tail(const OrdArgs &a) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(a.fin_done, 1u) == gridDim.x - 1) {
+      __threadfence();
+      const uint32_t st = atomicOr(a.call_status, 0u);   // the L2 value: every block's bits
+      atomicOr(a.fin_sticky, st);
+      *a.fin_log = st;
+      atomicExch(a.call_status, 0u);
+      atomicExch(a.fin_done, 0u);
+    }
+  }
+}
+
 template <typename V, int KIND, bool DRY = false>
-__global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
+__device__ __forceinline__ void ordered_apply_lds_rows(OrdArgs a, int wpb) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint64_t sort_scratch[4][64];
   const int lane = threadIdx.x & 63;
@@ -631,6 +650,12 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
   }
 }
 
+template <typename V, int KIND, bool DRY = false>
+__global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
+  ordered_apply_lds_rows<V, KIND, DRY>(a, wpb);
+  if (a.fin_done) finish_tail(a);
+}
+
 // ---------------------------------------------------------------------------
 // Register-resident row image for sorted/map rows of <= 64*J entries: entry i lives in
 // lane i % 64, register i / 64 ("striped").  FindIndex and the insert position are J
@@ -762,7 +787,7 @@ __device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int
 // setup's dependent loads, so more rows in flight pays: C3 apply 0.123 -> 0.114 ms), the
 // VGPR file's limit for J = 16.
 template <typename V, int KIND, int J, bool DRY = false>
-__global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
+__device__ __forceinline__ void ordered_apply_reg_rows(OrdArgs a) {
   __shared__ uint64_t sort_scratch[4][64];
   // Key -> entry-index map of the wave's row (FindIndex in one LDS read instead of J
   // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
@@ -1175,6 +1200,12 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   }
 }
 
+template <typename V, int KIND, int J, bool DRY = false>
+__global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
+  ordered_apply_reg_rows<V, KIND, J, DRY>(a);
+  if (a.fin_done) finish_tail(a);
+}
+
 // ---------------------------------------------------------------------------
 // Serve-back of sorted/map rows: gather (count, entries) for a list of slots.
 template <int ES>
@@ -1274,6 +1305,8 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
   if (a.kind != 0 && a.max_entries <= 1024) {
     const unsigned blocks = row_blocks(a.max_rows, 4);
     OrdArgs small = a, big = a;
+    if (a.grow) small.fin_done = nullptr;   // a folded finish goes with the last launch (big)
+    if (a.grow && !a.spill) big.fin_done = nullptr;   // concurrent launches: finish_call after the join
     if (a.grow) {   // ordered_offsets wrote the two descriptor lists
       small.touched = a.split;
       small.ntouched = a.nsplit;

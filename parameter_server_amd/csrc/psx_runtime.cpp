@@ -39,6 +39,7 @@ int g_decode_walk = 1;
 int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
+int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
 int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: 1 = the walk's persistent grid on every CU (default: half)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
@@ -246,7 +247,8 @@ struct psx_ctx {
   psx::ClientTable *d_client_tabs = nullptr;
   int64_t *d_pack = nullptr;             // psx_pack_stream: sparse record sizes + offsets
   size_t pack_cap = 0;                   // entries
-  uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log
+  uint32_t *d_status = nullptr;          // [0] sticky, [1 + k] call ring, [1 + kRing + k] call log,
+                                         // [1 + 2 kRing] the folded finish's block counter (zero)
   uint8_t *d_zero = nullptr;
   uint8_t *d_staging = nullptr;
   size_t staging_cap = 0;
@@ -788,12 +790,25 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     });
     if (st) return st;
   }
-  // 5) applies: ordered tables, then fast dense tables
+  // 5) applies: ordered tables, then fast dense tables.  When the call's last launch is an
+  //    ordered apply on the context stream, it also does finish_call's work (its last block,
+  //    psx_ordered.hip finish_tail) and no finish launch follows.
+  int last_ord = -1;
+  for (size_t ti = 0; ti < c->tables.size(); ++ti)
+    if (!c->tables[ti].fast() || force_ordered) last_ord = (int)ti;
+  const bool fold_finish = psx::g_fold_finish && fast.n == 0 && last_ord >= 0 &&
+                           !(ord[last_ord].grow && !ord[last_ord].spill);   // concurrent launches: join first
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
     if (t.fast() && !force_ordered) continue;
     const psx::Fork fk{c->aux, c->ev_fork, c->ev_join};
-    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered_apply(t.cfg.dtype, ord[ti], c->stream, fk); });
+    psx::OrdArgs oa = ord[ti];
+    if (fold_finish && (int)ti == last_ord) {
+      oa.fin_sticky = sticky;
+      oa.fin_log = call_log;
+      oa.fin_done = c->d_status + 1 + 2 * kRing;
+    }
+    st = timed(c, "ordered_apply", [&] { return psx::launch_ordered_apply(t.cfg.dtype, oa, c->stream, fk); });
     if (st) return st;
   }
   for (int i = 0; i < fast.n; ++i) {
@@ -831,8 +846,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     st = timed(c, "dense_apply", [&] { return psx::launch_dense_apply(t.cfg.dtype, a, c->stream, t.rec_f16()); });
     if (st) return st;
   }
-  st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
-  if (st) return st;
+  if (!fold_finish) {
+    st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
+    if (st) return st;
+  }
   // every call marks its slot free (a later pipelined call's stage 1 waits on it)
   HIP_TRY(c, hipEventRecord(c->ev_free[slot], c->stream));
   PendingCall pc;
@@ -1119,10 +1136,10 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
       return cleanup(PSX_ERR_DEVICE);
   }
   if (const char *pv = getenv("PSX_PIPELINE")) c->pipeline = atoi(pv);   // A/B runs
-  if (hipMalloc(&c->d_status, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
+  if (hipMalloc(&c->d_status, sizeof(uint32_t) * (2 + 2 * kRing)) != hipSuccess ||
       hipMalloc(&c->d_zero, 4096) != hipSuccess)
     return cleanup(PSX_ERR_OOM);
-  if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (1 + 2 * kRing)) != hipSuccess ||
+  if (hipMemset(c->d_status, 0, sizeof(uint32_t) * (2 + 2 * kRing)) != hipSuccess ||
       hipMemset(c->d_zero, 0, 4096) != hipSuccess)
     return cleanup(PSX_ERR_DEVICE);
   *out = c;
@@ -2682,6 +2699,7 @@ static int *variant_slot(int32_t which) {
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
     case PSX_VARIANT_WALK_COUNT: return &psx::g_walk_count;
+    case PSX_VARIANT_FOLD_FINISH: return &psx::g_fold_finish;
     default: return nullptr;
   }
 }
@@ -2723,6 +2741,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
     if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);
     if (const char *v = getenv("PSX_WALK_COUNT")) psx::g_walk_count = atoi(v);
+    if (const char *v = getenv("PSX_FOLD_FINISH")) psx::g_fold_finish = atoi(v);
   }
 } variant_env;
 }  // namespace

@@ -220,3 +220,28 @@ def _map_rows(body):
         out[rid] = dict(zip(e[:, 0].tolist(), e[:, 1].tolist()))
         off += size
     return out
+
+
+FOLD_FINISH = 14
+
+
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+def test_finish_folded_into_the_last_ordered_launch(kind):
+    """PSX_VARIANT_FOLD_FINISH: a call ending in an ordered apply does finish_call's work in
+    that launch's last block.  Rows after every call equal the unfolded run's, and a failing
+    call's status still reaches psx_sync through the folded finish (the call fails, nothing
+    of it applied, the next call is clean)."""
+    L = _abi.load()
+    rng = np.random.RandomState(71)
+    rows, K = 5_000, 1024
+    calls = _batches(rng, rows, K, 3, per_batch=2_000)
+    old = L.psx_debug_set_variant(FOLD_FINISH, 0)
+    try:
+        a = _run(kind, calls, rows, K, 1, 0, 3)
+        L.psx_debug_set_variant(FOLD_FINISH, 1)
+        b = _run(kind, calls, rows, K, 1, 0, 3)
+    finally:
+        L.psx_debug_set_variant(FOLD_FINISH, old)
+    assert a == b
+    # the error path through the folded finish (the default)
+    test_row_outside_the_shard_fails_and_leaves_counts_clean(1)

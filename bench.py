@@ -1181,6 +1181,38 @@ def c5_schedule(B, clocks, staleness=C5_STALENESS, speeds=None):
                       "worker_speeds": speeds}
 
 
+def pcie_duplex_probe(h2d_bytes, d2h_bytes, reps=3):
+    """This box's PCIe: page-locked host->device alone, device->host alone, and both at once
+    on two streams (GB/s, best of reps)."""
+    import torch
+    hsrc = torch.empty(h2d_bytes, dtype=torch.uint8).pin_memory()
+    ddst = torch.empty(h2d_bytes, dtype=torch.uint8, device="cuda")
+    dsrc = torch.empty(d2h_bytes, dtype=torch.uint8, device="cuda")
+    hdst = torch.empty(d2h_bytes, dtype=torch.uint8).pin_memory()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def timed(h2d, d2h):
+        best = None
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if h2d:
+                with torch.cuda.stream(s1):
+                    ddst.copy_(hsrc, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    hdst.copy_(dsrc, non_blocking=True)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        return best
+    th, td, tb = timed(True, False), timed(False, True), timed(True, True)
+    del hsrc, ddst, dsrc, hdst
+    return {"h2d_GBps": round(h2d_bytes / th / 1e9, 2), "d2h_GBps": round(d2h_bytes / td / 1e9, 2),
+            "both_GBps": round((h2d_bytes + d2h_bytes) / tb / 1e9, 2),
+            "bytes": {"h2d": h2d_bytes, "d2h": d2h_bytes}}
+
+
 def run_c5(args):
     """SURVEY §8(d) C5, end to end: mixed dense + sparse tables, a continuous update stream
     under SSPPush with staleness 4, messages arriving from host memory and push bodies
@@ -1240,6 +1272,7 @@ def run_c5(args):
         srv.subscribe(1, ids_d, b)
         srv.subscribe(3, ids_s, b)
     W, Kc = args.warmup, args.steps
+    pcie = pcie_duplex_probe(sum(m.size for m in msgs), 1 << 30)
     arrivals, gate = c5_schedule(B, W + Kc + C5_STALENESS + 2)
     # runs of arrivals: each ends with the message that advances the min clock
     runs, cur = [], []
@@ -1351,6 +1384,12 @@ def run_c5(args):
                                         "until pushed clock >= clock - staleness; the server applies messages in "
                                         "arrival order, so fast workers' later clocks are applied before the push "
                                         "of earlier ones"),
+            "pcie_probe": pcie,
+            "bound_measured_pcie": {
+                "ms_per_clock": round((h2d_pc + d2h_pc) / (pcie["both_GBps"] * 1e9) * 1e3, 3),
+                "frac": round((h2d_pc + d2h_pc) / (pcie["both_GBps"] * 1e9) * 1e3 / ms, 3),
+                "what": "both directions' bytes at the rate this box's PCIe moved them concurrently (pcie_probe: "
+                        "H2D and D2H on two streams at once): the link does not run both directions at full speed"},
             "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
                       "serial_ms_per_clock": round(bound_serial_ms, 3),
                       "what": "per rank: max(H2D, D2H) bytes at the PCIe Gen5 x16 spec (63 GB/s per direction, "

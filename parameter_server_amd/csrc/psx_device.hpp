@@ -190,12 +190,15 @@ struct OrdArgs {
                              // launch takes them first
   int32_t counted;           // split tables: the walk already counted this call's records
                              // (WalkCount): ordered_count is not launched
-  // finish_call folded into this apply launch (the call's last): non-null fin_done = a zeroed
-  // block counter; the last block does finish_call's work (psx_ordered.hip finish_tail)
-  uint32_t *fin_sticky;
-  uint32_t *fin_log;
-  uint32_t *fin_done;
+  // finish_call folded into this apply launch (the call's last): fin_ring >= 0 is the call's
+  // status ring slot, so call_status = status + 1 + fin_ring and the sticky word, the call's
+  // log entry and the block counter follow from call_status (kCallRing layout); the last
+  // block does finish_call's work (psx_ordered.hip finish_tail).  -1: no fold.
+  int32_t fin_ring;
 };
+// The context's status words (psx_runtime.cpp d_status): [0] sticky, [1 + k] the call ring,
+// [1 + kCallRing + k] the call log, [1 + 2 kCallRing] the folded finish's block counter.
+constexpr int kCallRing = 64;
 
 // ordered_count's work for one split sorted/map table (grow set), done by the window-parallel
 // walk as it writes each record's offset (psx_walk.hip): per record cnt[slot] += 1 and

@@ -430,28 +430,33 @@ __device__ __forceinline__ double sparse_importance(const uint8_t *vals, int32_t
 // once all its waves are done, counts itself; the last one folds the call's status into the
 // sticky word, logs it and frees the ring slot — what finish_call_kernel does, without a
 // launch of its own (an empty launch costs ~4.6 µs per call, profiles/r03/s26).
-__device__ __forceinline__ void finish_tail(const OrdArgs &a) {
+// (derived from call_status and the ring slot, not read from the OrdArgs: the extra pointers
+// live through the row loop spilled the C3 kernel to scratch)
+__device__ __forceinline__ void finish_tail(uint32_t *call_status, int32_t ring) {
   __syncthreads();
   if (threadIdx.x == 0) {
+    uint32_t *status = call_status - 1 - ring;
+    uint32_t *done = status + 1 + 2 * kCallRing;
     __threadfence();
-    if (atomicAdd(a.fin_done, 1u) == gridDim.x - 1) {
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {
       __threadfence();
-      const uint32_t st = atomicOr(a.call_status, 0u);   // the L2 value: every block's bits
-      atomicOr(a.fin_sticky, st);
-      *a.fin_log = st;
-      atomicExch(a.call_status, 0u);
-      atomicExch(a.fin_done, 0u);
+      const uint32_t st = atomicOr(call_status, 0u);   // the L2 value: every block's bits
+      atomicOr(status, st);                            // the sticky word
+      status[1 + kCallRing + ring] = st;               // the call log
+      atomicExch(call_status, 0u);
+      atomicExch(done, 0u);
     }
   }
 }
 
 template <typename V, int KIND, bool DRY = false>
-__device__ __forceinline__ void ordered_apply_lds_rows(OrdArgs a, int wpb) {
+__global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
   extern __shared__ __align__(16) uint8_t dyn[];
   __shared__ uint64_t sort_scratch[4][64];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
-  if (wib >= wpb) return;
+  if (wib >= wpb) goto done;
+  {
   const bool go = o_gate(a) && (!DRY || *a.keyflag);
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
   uint8_t *E = dyn + (size_t)wib * (size_t)a.max_entries * ES;   // this wave's row image
@@ -648,12 +653,9 @@ __device__ __forceinline__ void ordered_apply_lds_rows(OrdArgs a, int wpb) {
       if (a.ver && lane == 0) a.ver[slot] += (uint64_t)L;   // VersionServerRow: +1 per record
     }
   }
-}
-
-template <typename V, int KIND, bool DRY = false>
-__global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) {
-  ordered_apply_lds_rows<V, KIND, DRY>(a, wpb);
-  if (a.fin_done) finish_tail(a);
+  }
+done:
+  if (a.fin_ring >= 0) finish_tail(a.call_status, a.fin_ring);
 }
 
 // ---------------------------------------------------------------------------
@@ -786,8 +788,10 @@ __device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int
 // Occupancy targets: 7 waves/SIMD for the 256-entry image (its rows are bound by their
 // setup's dependent loads, so more rows in flight pays: C3 apply 0.123 -> 0.114 ms), the
 // VGPR file's limit for J = 16.
-template <typename V, int KIND, int J, bool DRY = false>
-__device__ __forceinline__ void ordered_apply_reg_rows(OrdArgs a) {
+// FIN: this instantiation may carry the call's folded finish (a.fin_ring >= 0); the others
+// do not compile the tail (it costs the 7-wave kernel registers it does not have).
+template <typename V, int KIND, int J, bool DRY = false, bool FIN = false>
+__global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
   __shared__ uint64_t sort_scratch[4][64];
   // Key -> entry-index map of the wave's row (FindIndex in one LDS read instead of J
   // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
@@ -799,7 +803,8 @@ __device__ __forceinline__ void ordered_apply_reg_rows(OrdArgs a) {
   const int wib = threadIdx.x >> 6;
   const bool go = o_gate(a) && (!DRY || a.grow || *a.keyflag);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows)
-  if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0)) return;
+  if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0)) goto done;
+  {
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
   for (int32_t k = lane; k < 1024; k += 64) s_pos[wib][k] = -1;
@@ -1198,12 +1203,11 @@ __device__ __forceinline__ void ordered_apply_reg_rows(OrdArgs a) {
       if (a.ver && lane == 0) a.ver[slot] += (uint64_t)L;
     }
   }
-}
-
-template <typename V, int KIND, int J, bool DRY = false>
-__global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) ordered_apply_reg_kernel(OrdArgs a) {
-  ordered_apply_reg_rows<V, KIND, J, DRY>(a);
-  if (a.fin_done) finish_tail(a);
+  }
+done:
+  if constexpr (FIN) {
+    if (a.fin_ring >= 0) finish_tail(a.call_status, a.fin_ring);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1305,8 +1309,8 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
   if (a.kind != 0 && a.max_entries <= 1024) {
     const unsigned blocks = row_blocks(a.max_rows, 4);
     OrdArgs small = a, big = a;
-    if (a.grow) small.fin_done = nullptr;   // a folded finish goes with the last launch (big)
-    if (a.grow && !a.spill) big.fin_done = nullptr;   // concurrent launches: finish_call after the join
+    if (a.grow) small.fin_ring = -1;   // a folded finish goes with the last launch (big)
+    if (a.grow && !a.spill) big.fin_ring = -1;   // concurrent launches: finish_call after the join
     if (a.grow) {   // ordered_offsets wrote the two descriptor lists
       small.touched = a.split;
       small.ntouched = a.nsplit;
@@ -1328,17 +1332,17 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
 #define PSX_REG(V, KIND)                                                                           \
   do {                                                                                             \
     if (a.max_entries <= 64)                                                                       \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1>), dim3(blocks), dim3(256), 0, st, a);   \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, false, true>), dim3(blocks), dim3(256), 0, st, a); \
     else if (a.max_entries <= 256)                                                                 \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, a);   \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, false, true>), dim3(blocks), dim3(256), 0, st, a); \
     else if (a.grow && a.spill) {                                                                  \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(few_row_blocks(a.max_rows)), dim3(256), 0, st, big); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, false, true>), dim3(few_row_blocks(a.max_rows)), dim3(256), 0, st, big); \
     } else if (a.grow) {                                                                           \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, fk.aux, big); \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
     } else                                                                                         \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, st, a);  \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, false, true>), dim3(blocks), dim3(256), 0, st, a); \
   } while (0)
 #define PSX_REGK(V) do { if (a.kind == 1) PSX_REG(V, 1); else PSX_REG(V, 2); } while (0)
     switch (dtype) {

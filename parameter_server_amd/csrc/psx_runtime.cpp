@@ -111,7 +111,7 @@ hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *
 
 namespace {
 
-constexpr int kRing = 64;   // per-call status slots
+constexpr int kRing = psx::kCallRing;   // per-call status slots
 
 int vsize_of(int32_t dt) { return (dt == PSX_F32 || dt == PSX_I32) ? 4 : 8; }
 
@@ -717,6 +717,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (t.fast() && !force_ordered) continue;
     psx::OrdArgs &a = ord[ti];
     a = psx::OrdArgs{};
+    a.fin_ring = -1;
     a.ss = ss;
     a.segs = segs;
     a.t = (int)ti;
@@ -803,11 +804,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (t.fast() && !force_ordered) continue;
     const psx::Fork fk{c->aux, c->ev_fork, c->ev_join};
     psx::OrdArgs oa = ord[ti];
-    if (fold_finish && (int)ti == last_ord) {
-      oa.fin_sticky = sticky;
-      oa.fin_log = call_log;
-      oa.fin_done = c->d_status + 1 + 2 * kRing;
-    }
+    oa.fin_ring = fold_finish && (int)ti == last_ord ? ring : -1;
     st = timed(c, "ordered_apply", [&] { return psx::launch_ordered_apply(t.cfg.dtype, oa, c->stream, fk); });
     if (st) return st;
   }

@@ -1384,12 +1384,10 @@ def run_c5(args):
                                         "until pushed clock >= clock - staleness; the server applies messages in "
                                         "arrival order, so fast workers' later clocks are applied before the push "
                                         "of earlier ones"),
-            "pcie_probe": pcie,
-            "bound_measured_pcie": {
-                "ms_per_clock": round((h2d_pc + d2h_pc) / (pcie["both_GBps"] * 1e9) * 1e3, 3),
-                "frac": round((h2d_pc + d2h_pc) / (pcie["both_GBps"] * 1e9) * 1e3 / ms, 3),
-                "what": "both directions' bytes at the rate this box's PCIe moved them concurrently (pcie_probe: "
-                        "H2D and D2H on two streams at once): the link does not run both directions at full speed"},
+            "pcie_probe": dict(pcie, note="the same copies through torch on two streams, alone and at once; "
+                                          "issued this way the two directions did not overlap (both_GBps ~ one "
+                                          "direction), while C5's own copies (torch H2D + libpsx D2H) move "
+                                          "pcie_GBps_per_rank h2d + d2h together"),
             "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
                       "serial_ms_per_clock": round(bound_serial_ms, 3),
                       "what": "per rank: max(H2D, D2H) bytes at the PCIe Gen5 x16 spec (63 GB/s per direction, "

@@ -431,14 +431,17 @@ __device__ __forceinline__ double sparse_importance(const uint8_t *vals, int32_t
 // sticky word, logs it and frees the ring slot — what finish_call_kernel does, without a
 // launch of its own (an empty launch costs ~4.6 µs per call, profiles/r03/s26).
 // (derived from call_status and the ring slot, not read from the OrdArgs: the extra pointers
-// live through the row loop spilled the C3 kernel to scratch)
-__device__ __forceinline__ void finish_tail(uint32_t *call_status, int32_t ring) {
+// live through the row loop spilled the C3 kernel to scratch).  Only the blocks that take
+// rows count themselves (`working`, from the launch's row count, which no block of it
+// changes); a launch with no rows finishes in block 0 alone — an empty spill launch's 768
+// blocks all counting cost ~11 µs (profiles/r04/s8).
+__device__ __forceinline__ void finish_tail(uint32_t *call_status, int32_t ring, uint32_t working) {
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && (working == 0 ? blockIdx.x == 0 : blockIdx.x < working)) {
     uint32_t *status = call_status - 1 - ring;
     uint32_t *done = status + 1 + 2 * kCallRing;
     __threadfence();
-    if (atomicAdd(done, 1u) == gridDim.x - 1) {
+    if (working == 0 || atomicAdd(done, 1u) == working - 1) {
       __threadfence();
       const uint32_t st = atomicOr(call_status, 0u);   // the L2 value: every block's bits
       atomicOr(status, st);                            // the sticky word
@@ -655,7 +658,7 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
   }
   }
 done:
-  if (a.fin_ring >= 0) finish_tail(a.call_status, a.fin_ring);
+  if (a.fin_ring >= 0) finish_tail(a.call_status, a.fin_ring, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -802,8 +805,10 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   const bool go = o_gate(a) && (!DRY || a.grow || *a.keyflag);
-  // blocks past the touched rows leave before any setup (the grid is sized by max_rows)
-  if (!go || (int64_t)blockIdx.x * 4 >= (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0)) goto done;
+  // blocks past the touched rows leave before any setup (the grid is sized by max_rows); the
+  // row count is final when the launch starts (the folded finish counts the blocks below it)
+  const int64_t launch_rows = (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0);
+  if (!go || (int64_t)blockIdx.x * 4 >= launch_rows) goto done;
   {
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
@@ -1206,7 +1211,10 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   }
 done:
   if constexpr (FIN) {
-    if (a.fin_ring >= 0) finish_tail(a.call_status, a.fin_ring);
+    if (a.fin_ring >= 0) {
+      const int64_t wk = (launch_rows + 3) / 4;
+      finish_tail(a.call_status, a.fin_ring, (uint32_t)(wk < (int64_t)gridDim.x ? wk : (int64_t)gridDim.x));
+    }
   }
 }
 

@@ -62,13 +62,10 @@ struct WalkCtl {      // reset by walk_head for the walk of the same call
   uint32_t dbg[6];    // {ticket, message, window, epoch expected, tag seen (lane 0), lanes tagged}
 };
 
-// The head of each message, published by the walk's prologue as epoch-tagged granules (the
-// data is the flag, as between windows): [0, kGran) the walker state at the message's first
-// sparse record (gran_value order), kGran the first window (96 KiB grid from byte 0),
-// kGran + 1 its window count (0: nothing to walk).
-constexpr int kHeadGran = kGran + 2;
-struct WalkHead {
-  unsigned long long gran[kMaxFused][kHeadGran];
+struct WalkHead {     // written by walk_head, read by the first window of each message
+  WalkState st[kMaxFused];
+  uint32_t wfirst[kMaxFused];   // the message's first window (96 KiB grid from byte 0)
+  uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
 };
 constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
 
@@ -133,16 +130,10 @@ __device__ bool walk_header(const uint8_t *p, uint64_t size, const TableDir &dir
   return true;
 }
 
-__device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i);
-
-// The walk's prologue (formerly the walk_head launch): block b (< B) resets message b's
-// per-call state, walks its table headers up to the first sparse table with records, and
-// publishes the message's head granules.  Block 0 also resets the call's ticket.  The
-// resets are made visible (release fence) before the granules: the windows that wait on
-// them write the same segment words later.
-__device__ void walk_head_block(int b, StreamSet ss, TableDir dir, Seg *segs, uint32_t *call_status,
-                                uint32_t *counters, uint32_t *ntouched, WalkCtl *ctl, WalkHead *head,
-                                const WalkCount *wc, uint32_t epoch) {
+__global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir dir, Seg *segs, uint32_t *call_status,
+                                                        uint32_t *counters, uint32_t *ntouched, WalkCtl *ctl,
+                                                        WalkHead *head, const WalkCount *wc) {
+  const int b = blockIdx.x;
   for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
     Seg s;
     s.rec0 = -1;
@@ -159,8 +150,8 @@ __device__ void walk_head_block(int b, StreamSet ss, TableDir dir, Seg *segs, ui
     }
   }
   if (b == 0 && threadIdx.x == 0) {
-    __hip_atomic_store(&ctl->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ctl->lost, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl->ticket = 0;
+    ctl->lost = 0;
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -189,12 +180,9 @@ __device__ void walk_head_block(int b, StreamSet ss, TableDir dir, Seg *segs, ui
     wf = (uint32_t)(s.pos / kWBytes);
     nwin = (uint32_t)((size + kWBytes - 1) / kWBytes) - wf;
   }
-  __threadfence();   // the resets above before the granules that release the windows
-  gu64 *g = (gu64 *)head->gran[b];
-  for (int i = 0; i < kHeadGran; ++i) {
-    const uint32_t v = i < kGran ? gran_value(s, i) : (i == kGran ? wf : nwin);
-    __hip_atomic_store(g + i, ((uint64_t)epoch << 32) | (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  head->st[b] = s;
+  head->wfirst[b] = wf;
+  head->nwin[b] = nwin;
 }
 
 // The next record start after a speculative record at word q with count word c (n16), or
@@ -233,7 +221,7 @@ __device__ __forceinline__ uint32_t exit_at(uint32_t q, const uint32_t *xc, cons
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)exit_walk(q, jt4, n16, nw, W0, size, spec_wpr));
 }
 
-__device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {  // (declared above)
+__device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
   switch (i) {
     case 0: return (uint32_t)s.pos;
     case 1: return (uint32_t)(s.pos >> 32);
@@ -272,8 +260,7 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
 }
 
 __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
-                                                            uint32_t *call_status, uint32_t *counters, uint32_t *ntouched,
-                                                            WalkCtl *ctl, WalkHead *head,
+                                                            uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace,
                                                             const WalkCount *wc) {
@@ -299,37 +286,10 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
   __shared__ uint8_t seg_t[kMaxSegs];   // the segment's table (walk-counted tables: WalkCount)
   __shared__ uint16_t a16[kWW / 32 + 1], a1[16];
   __shared__ uint32_t sh_nseg, sh_n16, sh_n1, sh_ticket;
-  __shared__ uint32_t sh_nwin[kMaxFused], sh_wfirst[kMaxFused];
   const int tid = threadIdx.x;
   const int B = ss.n;
-  // prologue: message heads (blocks 0 .. B-1), then every block reads every message's
-  // window range from the head granules (lane m: message m; bounded wait, as for windows)
-  if ((int)blockIdx.x < B) walk_head_block((int)blockIdx.x, ss, dir, segs, call_status, counters, ntouched, ctl, head, wc, epoch);
-  if (tid < 64) {
-    uint32_t nwv = 0, wfv = 0;
-    bool ok = true;
-    if (tid < B) {
-      const gu64 *g = (const gu64 *)head->gran[tid];
-      ok = false;
-      for (uint32_t spins = 0; spins <= (1u << 20); ++spins) {
-        const uint64_t a = __hip_atomic_load(g + kGran, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t c = __hip_atomic_load(g + kGran + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(a >> 32) == epoch && (uint32_t)(c >> 32) == epoch) {
-          wfv = (uint32_t)a;
-          nwv = (uint32_t)c;
-          ok = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!ok) atomicOr(call_status, kStWalkLost);   // nothing of the call is applied
-      sh_nwin[tid] = ok ? nwv : 0u;
-      sh_wfirst[tid] = wfv;
-    }
-  }
-  __syncthreads();
   uint32_t maxwin = 0;
-  for (int i = 0; i < B; ++i) maxwin = sh_nwin[i] > maxwin ? sh_nwin[i] : maxwin;
+  for (int i = 0; i < B; ++i) maxwin = head->nwin[i] > maxwin ? head->nwin[i] : maxwin;
   const uint32_t items = (uint32_t)B * maxwin;
 
   for (;;) {
@@ -339,7 +299,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     if (tk >= items) break;
     const int b = (int)(tk % (uint32_t)B);
     const uint32_t j = tk / (uint32_t)B;
-    const uint32_t nwin_b = sh_nwin[b];
+    const uint32_t nwin_b = head->nwin[b];
     if (j >= nwin_b) {
       __syncthreads();   // sh_ticket is rewritten at the top
       continue;
@@ -348,7 +308,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     if (tr && tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
     const uint8_t *p = ss.data[b];
     const uint64_t size = ss.size[b];
-    const uint64_t W0 = ((uint64_t)sh_wfirst[b] + j) * kWBytes;
+    const uint64_t W0 = ((uint64_t)head->wfirst[b] + j) * kWBytes;
     const uint64_t tot = (size - W0) / 4;                   // whole words from W0
     const uint32_t nw = (uint32_t)(tot < (uint64_t)kWW ? tot : (uint64_t)kWW);
     const bool halo = tot > nw;
@@ -423,9 +383,10 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       const uint64_t rk_hi = rk_lo + size / 8 + 1;
       const int lane = tid;
       WalkState s;
-      {
-        // the predecessor window's state, or for a message's first window its head
-        const gu64 *g = j == 0 ? (const gu64 *)head->gran[b] : gran + (uint64_t)(tk - (uint32_t)B) * kGran;
+      if (j == 0) {
+        s = head->st[b];
+      } else {
+        const gu64 *g = gran + (uint64_t)(tk - (uint32_t)B) * kGran;
         uint32_t v = 0, tag = 0;
         bool ok = false;
         for (uint32_t spins = 0;; ++spins) {
@@ -652,12 +613,15 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
+  hipLaunchKernelGGL(walk_head_kernel, dim3(ss.n), dim3(256), 0, st, ss, dir, segs, call_status, counters, ntouched,
+                     ctl, head, wc);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   unsigned long long *trace =
       trace_items ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_trace_offset(trace_items))
                   : nullptr;
-  if (blocks < (unsigned)ss.n) blocks = (unsigned)ss.n;   // the prologue needs one block per message
-  hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, counters,
-                     ntouched, ctl, head, gran, spec_wpr, epoch, trace, wc);
+  hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
+                     head, gran, spec_wpr, epoch, trace, wc);
   return hipGetLastError();
 }
 

@@ -87,6 +87,12 @@ for db, ks in d.items():
         if 'dense_apply' in k:
             m=v.get('TCP_UTCL1_TRANSLATION_MISS_sum',0); f=v.get('TCP_CLIENT_UTCL1_INFLIGHT_sum',0)
             print(' miss', round(m), 'inflight/miss', round(f/m,1) if m else None, 'credits', round(v.get('TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum',0)), 'req', round(v.get('TCP_UTCL1_REQUEST_sum',0)))"; done ;;
+    spread2)  # the same without the profiler: 12 rounds per process, layouts alternating
+      i=0
+      for lay in 0 1 0 1 0 1; do
+        i=$((i+1)); run spread2_p$i 120 python3 tools/spread_c2.py --layout $lay --rounds 12 || exit 1
+      done
+      for i in 1 2 3 4 5 6; do grep -h '^{' $O/spread2_p$i.log | cut -c1-330; done ;;
     listpmc) timeout -s KILL 60 rocprofv3 -L > "$R/counters.txt" 2>&1; echo "listpmc rc=$?"; grep -o "SQ_[A-Z_0-9]*\|TCC_[A-Z_0-9]*\|TCP_[A-Z_0-9]*\|TA_[A-Z_0-9]*\|TD_[A-Z_0-9]*" "$R/counters.txt" | sort -u > "$O/counter_names.txt"; wc -l < "$O/counter_names.txt" ;;
     pmc3)
       P=1
@@ -156,6 +162,8 @@ for db, ks in d.items():
           for f in $O/c3wc_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     wctests) run wctests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_count_gpu.py tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py tests/test_indexed_rows_gpu.py ;;
     oldheavy) say oldheavy; timeout -k 10 300 env PSX_LIB=ab_old/libpsx.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ord_split_gpu.py -k every_row_heavy > "$O/oldheavy.log" 2>&1; echo "oldheavy rc=$? (the pre-fix library: a failure here is the collision)"; tail -5 "$O/oldheavy.log" ;;
+    c3fold) i=0; for v in 1 0 1 0; do i=$((i+1)); run c3fold_${i}_v$v 300 env PSX_FOLD_FINISH=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+            for f in $O/c3fold_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     xtests) run xtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_split_gpu.py tests/test_walk_count_gpu.py tests/test_multi_rank_gpu.py ;;
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;

@@ -35,7 +35,10 @@ enum {
                                    ordered_count launch); 0: ordered_count counts them */,
   PSX_VARIANT_FOLD_FINISH = 14  /* 1 (default): a call whose last launch is an ordered apply on the
                                    context stream does finish_call's work in that launch's last
-                                   block (no finish_call launch); 0: finish_call launched */
+                                   block (no finish_call launch); 0: finish_call launched */,
+  PSX_VARIANT_WALK_LEVELS = 15  /* the walk's composed exit-map levels: window j's exit state follows
+                                   from the state 2^levels windows back (default 4; 0: window by
+                                   window) */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -30,9 +30,10 @@ hipError_t launch_split_scatter(const SplitArgs &a, const int64_t *pos, const ui
                                 hipStream_t st);
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, hipStream_t st);
+                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, uint64_t items, int levels,
+                       hipStream_t st);
 size_t walk_trace_offset(uint64_t items);
-size_t walk_ws_bytes(uint64_t items);
+size_t walk_ws_bytes(uint64_t items, int levels);
 // PSX_VARIANT_DECODE: 1 (default) walked messages with sparse tables decode window-parallel
 // where eligible, 0 one workgroup per message.
 int g_decode_walk = 1;
@@ -40,6 +41,7 @@ int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
+int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
 int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: 1 = the walk's persistent grid on every CU (default: half)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
@@ -613,8 +615,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   for (int i = 0; i < n; ++i) maxw = std::max<uint64_t>(maxw, (s[i].size + kWalkWindowBytes - 1) / kWalkWindowBytes);
   const uint64_t items = (uint64_t)n * maxw;
   if (items == 0 || items > kWalkMaxItems) walk = false;
+  // composed exit maps cost kCand x 8 B per (item, level) of workspace: up to 4,096 items
+  const int walk_levels = items <= 4096 ? std::max(0, std::min(psx::g_walk_levels, 8)) : 0;
   if (walk) {
-    const size_t need = psx::walk_ws_bytes(items);
+    const size_t need = psx::walk_ws_bytes(items, walk_levels);
     if (need > c->walk_cap[slot]) {
       HIP_TRY(c, hipStreamSynchronize(c->stream));
       HIP_TRY(c, hipStreamSynchronize(c->side));
@@ -676,7 +680,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
                                   c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
                                   c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
-                                  wcount ? c->d_wcount[slot] : nullptr, prep);
+                                  wcount ? c->d_wcount[slot] : nullptr, items, walk_levels, prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -2697,6 +2701,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
     case PSX_VARIANT_WALK_COUNT: return &psx::g_walk_count;
     case PSX_VARIANT_FOLD_FINISH: return &psx::g_fold_finish;
+    case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
     default: return nullptr;
   }
 }
@@ -2739,6 +2744,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);
     if (const char *v = getenv("PSX_WALK_COUNT")) psx::g_walk_count = atoi(v);
     if (const char *v = getenv("PSX_FOLD_FINISH")) psx::g_fold_finish = atoi(v);
+    if (const char *v = getenv("PSX_WALK_LEVELS")) psx::g_walk_levels = atoi(v);
   }
 } variant_env;
 }  // namespace

@@ -72,8 +72,14 @@ constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 
 // After the granules: a trace region of kTraceWords 64-bit timestamps per window item
 // (s_memrealtime, 100 MHz), written only when the launch asks for it (psx_debug_walk_trace).
 constexpr int kTraceWords = 6;   // ticket taken, window in LDS, exit map done, predecessor seen, published, expanded
-size_t walk_ws_bytes(uint64_t items) { return kWalkGranOff + items * kGran * 8 + items * kTraceWords * 8; }
 size_t walk_trace_offset(uint64_t items) { return kWalkGranOff + items * kGran * 8; }
+// After the trace region: the composed exit maps (walk levels > 0), kCand tagged entries
+// per (item, level).
+constexpr int kCandW = 1024;
+size_t walk_maps_offset(uint64_t items) { return walk_trace_offset(items) + items * kTraceWords * 8; }
+size_t walk_ws_bytes(uint64_t items, int levels) {
+  return walk_maps_offset(items) + items * (uint64_t)(levels > 0 ? levels : 0) * kCandW * 8;
+}
 
 // One table header at s.pos (SerializedOpLogReader::StartNewTable, :87-121), read directly
 // from the message.  Returns false when the message is done or failed (s.mode = 2).
@@ -263,8 +269,10 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                                                             uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace,
-                                                            const WalkCount *wc) {
+                                                            const WalkCount *wc, unsigned long long *maps_p,
+                                                            int levels) {
   gu64 *gran = (gu64 *)gran_p;
+  gu64 *maps = (gu64 *)maps_p;
   // 96 KiB windows in 150 KiB of LDS, everything but the hand-off done before it.  wbuf
   // first holds the window's words; n16 keeps the clipped record count after each word
   // (the resolve's one read of the words; single-record steps are computed from it,
@@ -372,6 +380,74 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     //    resolve itself): thread q walks q's chain, 16 records a step, then single ones.
     if ((uint32_t)tid < (uint32_t)kCand) xc[tid] = exit_walk((uint32_t)tid, jt4, n16, nw, W0, size, spec_wpr);
     __syncthreads();
+    // 4') composed exit maps (levels > 0): the window's forward map F[q] — from entry
+    //     candidate q, the records up to and including the one that crosses the window's
+    //     end, and the word where the next window's chain starts (a candidate of it, < kCand)
+    //     — then, level by level, P_l(j) = P_{l-1}(j) o P_{l-1}(j - 2^(l-1)): the map over the
+    //     2^l windows ending here (from the message's first window when fewer precede).
+    //     Partner maps come from the blocks of earlier windows of the same message (earlier
+    //     tickets), as epoch-tagged entries.  With them the exit state of window j follows
+    //     from the exit state 2^levels windows back in one lookup (step 4 below), so the
+    //     chain between windows hops 2^levels windows at a time.  Encoding: count << 10 |
+    //     entry word, kNoMap where the chain leaves the table's records, a header or the message.
+    uint32_t *pm = reinterpret_cast<uint32_t *>(sa);          // (sa is free after the squarings)
+    uint32_t *pm2 = pm + kCand;
+    constexpr uint32_t kNoMap = 0xFFFFFFFFu;
+    if (levels > 0) {
+      {
+        const uint32_t q = (uint32_t)tid;
+        uint32_t f = kNoMap;
+        if (!last) {
+          const uint32_t x = xc[q];
+          const uint32_t T = x & 0xFFFFu, cnt = (x >> 16) + 1;
+          if (T + 1 < nw) {
+            const uint16_t cT = n16[T];
+            if (cT < kNBig) {
+              const uint64_t endw = (uint64_t)T + 2 + (uint64_t)cT * spec_wpr;
+              if (endw >= (uint64_t)kWW && W0 + endw * 4 <= size && endw - kWW < (uint64_t)kCand && cnt < (1u << 22) - 1)
+                f = (cnt << 10) | (uint32_t)(endw - kWW);
+            }
+          }
+        }
+        pm[q] = f;
+        __hip_atomic_store(maps + ((uint64_t)tk * levels + 0) * kCand + q, ((uint64_t)epoch << 32) | f,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      for (int l = 1; l <= levels; ++l) {
+        const uint32_t d = 1u << (l - 1);
+        const uint32_t q = (uint32_t)tid;
+        uint32_t v = pm[q];
+        if (j >= d) {
+          // the partner's P_{l-1} covers the windows just before this one's P_{l-1}
+          const gu64 *g = maps + ((uint64_t)(tk - d * (uint32_t)B) * levels + (l - 1)) * kCand + q;
+          uint64_t x = 0;
+          bool ok = false;
+          for (uint32_t spins = 0; spins <= (1u << 20); ++spins) {
+            x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(x >> 32) == epoch) { ok = true; break; }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!ok) atomicOr(call_status, kStWalkLost);
+          const uint32_t u = ok ? (uint32_t)x : kNoMap;
+          v = kNoMap;
+          if (u != kNoMap) {
+            const uint32_t w = pm[u & 1023u];
+            if (w != kNoMap) {
+              const uint32_t c = (u >> 10) + (w >> 10);
+              if (c < (1u << 22) - 1) v = (c << 10) | (w & 1023u);
+            }
+          }
+        }
+        pm2[q] = v;
+        __syncthreads();
+        pm[q] = v;
+        if (l < levels)
+          __hip_atomic_store(maps + ((uint64_t)tk * levels + l) * kCand + q, ((uint64_t)epoch << 32) | v,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+      }
+    }
     if (tr && tid == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
     // 4) wave 0: wait for the predecessor's state, resolve this window (every lane on the
     //    same state, lane 0 writing), publish (lane i its granule i)
@@ -382,6 +458,64 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
                              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ss.recoff_base[b] >> 32)) << 32);
       const uint64_t rk_hi = rk_lo + size / 8 + 1;
       const int lane = tid;
+      // The composed exit: window j's exit state from the exit state of window a - 1, a the
+      // first window P_levels(j) covers (the message's head when a == 0), when that state
+      // enters window a as a candidate inside a sparse table that goes on past window j.
+      bool pub_early = false;
+      if (levels > 0 && !last) {
+        const uint32_t span = 1u << levels;
+        const uint32_t a0 = j + 1 >= span ? j + 1 - span : 0u;
+        WalkState s0;
+        bool ok0 = true;
+        if (a0 == 0) {
+          s0 = head->st[b];
+        } else {
+          const gu64 *g = gran + (uint64_t)(tk - (j - a0 + 1) * (uint32_t)B) * kGran;
+          uint32_t v = 0;
+          ok0 = false;
+          for (uint32_t spins = 0;; ++spins) {
+            uint64_t x = (uint64_t)epoch << 32;
+            if (lane < kGran) x = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = (uint32_t)x;
+            if (__all((uint32_t)(x >> 32) == epoch)) { ok0 = true; break; }
+            if (spins > (1u << 20)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!ok0 && lane == 0) atomicOr(call_status, kStWalkLost);
+          auto rl = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); };
+          auto lo_hi = [&](int i) { return (uint64_t)rl(i) | ((uint64_t)rl(i + 1) << 32); };
+          s0.pos = lo_hi(0);
+          s0.left = lo_hi(2);
+          s0.rk = lo_hi(4);
+          s0.kk = lo_hi(6);
+          s0.seen = lo_hi(8);
+          s0.k = (int32_t)rl(10);
+          s0.t = (int32_t)rl(11);
+          s0.mode = (int32_t)rl(12);
+          s0.ntab = (int32_t)rl(13);
+        }
+        const uint64_t Wa = ((uint64_t)head->wfirst[b] + a0) * kWBytes;
+        if (ok0 && s0.mode == 1 && s0.pos >= Wa && s0.pos - Wa < (uint64_t)kCand * 4 && s0.rk >= rk_lo &&
+            s0.rk + s0.left <= rk_hi) {
+          const uint32_t q0 = (uint32_t)((s0.pos - Wa) / 4);
+          const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)pm[q0]);
+          if (m != kNoMap && s0.left > (uint64_t)(m >> 10)) {
+            WalkState e = s0;
+            const uint64_t c = m >> 10;
+            e.pos = W0 + kWBytes + (uint64_t)(m & 1023u) * 4;
+            e.rk += c;
+            e.kk += c;
+            e.left -= c;
+            uint32_t mine = 0;
+#pragma unroll
+            for (int i = 0; i < kGran; ++i) mine = lane == i ? gran_value(e, i) : mine;
+            if (lane < kGran)
+              __hip_atomic_store(gran + (uint64_t)tk * kGran + lane, ((uint64_t)epoch << 32) | (uint64_t)mine,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pub_early = true;
+          }
+        }
+      }
       WalkState s;
       if (j == 0) {
         s = head->st[b];
@@ -538,7 +672,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       uint32_t mine = 0;
 #pragma unroll
       for (int i = 0; i < kGran; ++i) mine = lane == i ? gran_value(s, i) : mine;
-      if (!last && lane < kGran) {
+      if (!last && !pub_early && lane < kGran) {
         gu64 *g = gran + (uint64_t)tk * kGran;
         __hip_atomic_store(g + lane, ((uint64_t)epoch << 32) | (uint64_t)mine, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -609,7 +743,8 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
 // wc: null, or per table (TableDir index) the walk-counted split tables' WalkCount.
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, hipStream_t st) {
+                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, uint64_t items, int levels,
+                       hipStream_t st) {
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
@@ -620,8 +755,11 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
   unsigned long long *trace =
       trace_items ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_trace_offset(trace_items))
                   : nullptr;
+  unsigned long long *maps =
+      levels > 0 ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_maps_offset(items))
+                 : nullptr;
   hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
-                     head, gran, spec_wpr, epoch, trace, wc);
+                     head, gran, spec_wpr, epoch, trace, wc, maps, levels);
   return hipGetLastError();
 }
 

@@ -26,6 +26,19 @@ def _gpu(built_lib, oracle_lib):
         pytest.skip("no GPU")
 
 
+WALK_LEVELS = 15
+
+
+@pytest.fixture(autouse=True, params=[4, 1, 0], ids=["levels4", "levels1", "levels0"])
+def walk_levels(request, _gpu):
+    """Every test with the walk's composed exit maps at the default 4 levels (a window's exit
+    state from the state 16 windows back), at 1 level (pairs) and off (window by window)."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(WALK_LEVELS, request.param)
+    yield request.param
+    L.psx_debug_set_variant(WALK_LEVELS, old)
+
+
 def _message(tables):
     """tables: list of (table_id, vsize, rows) for sparse tables or (table_id, 'dense', ids,
     payload) for dense ones, in the given order (empty tables kept)."""
@@ -114,6 +127,19 @@ def test_c3_shaped_messages_every_window():
         ids = rng.choice(rows, size=10_000, replace=False, p=p)
         streams.append(wire.sparse_stream_np(3, 4, _rows(rng, ids, K, I32, rng.randint(1, 33, size=ids.size))))
     _run_both([(3, SORTED_MAP, I32, K, False, rows)], streams)
+
+
+def test_long_messages_chain_past_the_composed_span():
+    """Messages of ~85 and ~35 windows with other message lengths beside them: with 4 levels a
+    window's exit state comes from the state 16 windows back, so the chain between windows
+    hops 16 at a time past the first span (and the table ends in the last window)."""
+    rng = np.random.RandomState(17)
+    rows, K = 30_000, 1024
+    streams = []
+    for b, nrec in enumerate((60_000, 25_000, 3_000)):
+        ids = rng.randint(0, rows, size=nrec)
+        streams.append(wire.sparse_stream_np(3, 4, _rows(rng, ids, K, I32, rng.randint(1, 33, size=ids.size))))
+    _run_both([(3, MAP, I32, K, False, rows)], streams)
 
 
 @pytest.mark.parametrize("dt", [F32, F64])

@@ -139,7 +139,7 @@ def test_long_messages_chain_past_the_composed_span():
     for b, nrec in enumerate((60_000, 25_000, 3_000)):
         ids = rng.randint(0, rows, size=nrec)
         streams.append(wire.sparse_stream_np(3, 4, _rows(rng, ids, K, I32, rng.randint(1, 33, size=ids.size))))
-    _run_both([(3, MAP, I32, K, False, rows)], streams)
+    _run_both([(3, SORTED_MAP, I32, K, False, rows)], streams)
 
 
 @pytest.mark.parametrize("dt", [F32, F64])

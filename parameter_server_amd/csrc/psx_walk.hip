@@ -462,6 +462,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       // first window P_levels(j) covers (the message's head when a == 0), when that state
       // enters window a as a candidate inside a sparse table that goes on past window j.
       bool pub_early = false;
+      uint64_t t_early = 0;
       if (levels > 0 && !last) {
         const uint32_t span = 1u << levels;
         const uint32_t a0 = j + 1 >= span ? j + 1 - span : 0u;
@@ -513,6 +514,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
               __hip_atomic_store(gran + (uint64_t)tk * kGran + lane, ((uint64_t)epoch << 32) | (uint64_t)mine,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             pub_early = true;
+            if (tr) t_early = __builtin_amdgcn_s_memrealtime();
           }
         }
       }
@@ -681,7 +683,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         const uint64_t t_pub = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
           tr[3] = t_seen;
-          tr[4] = t_pub;
+          tr[4] = pub_early ? t_early : t_pub;   // when this window's exit state went out
         }
       }
     }

@@ -543,6 +543,13 @@ const char *psx_comm_last_error(psx_comm *comm);
 psx_status psx_exchange_sizes(psx_comm *comm, const uint64_t *send_sizes, uint64_t *recv_sizes, void *hip_stream);
 psx_status psx_exchange_streams(psx_comm *comm, const void *send, const uint64_t *send_sizes, void *recv,
                                 const uint64_t *recv_sizes, void *hip_stream);
+/* ABI 7: psx_exchange_streams with explicit byte displacements (MPI alltoallv's): peer p's
+ * send_sizes[p] bytes start at send + send_displs[p], and p's recv_sizes[p] bytes land at
+ * recv + recv_displs[p].  A zero size skips the peer — e.g. a rank's own sub-stream, which
+ * its owner can apply straight from the send buffer instead of copying it to itself. */
+psx_status psx_exchange_streams_v(psx_comm *comm, const void *send, const uint64_t *send_sizes,
+                                  const uint64_t *send_displs, void *recv, const uint64_t *recv_sizes,
+                                  const uint64_t *recv_displs, void *hip_stream);
 /* ABI 7: psx_exchange_sizes without the synchronization, so that a pipelined caller can
  * enqueue chunk k+1's sizes behind chunk k's bytes: send_sizes is copied before the call
  * returns; recv_sizes (page-locked host memory, else PSX_ERR_INVALID_ARG) is written by

@@ -200,6 +200,7 @@ def load():
         "psx_exchange_sizes": ([vp, vp, vp, vp], ctypes.c_int),
         "psx_exchange_streams": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "psx_exchange_sizes_async": ([vp, vp, vp, vp], ctypes.c_int),
+        "psx_exchange_streams_v": ([vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "psx_debug_set_variant": ([i32, i32], i32),
         "psx_debug_get_variant": ([i32], i32),
         "psx_debug_walk_trace": ([vp, vp, ctypes.c_int64], ctypes.c_int64),

@@ -182,36 +182,57 @@ psx_status psx_exchange_sizes_async(psx_comm *c, const uint64_t *send_sizes, uin
   return PSX_OK;
 }
 
+// One grouped all-to-all-v: peer p gets send_sizes[p] bytes from send + sdis[p] and this rank
+// receives recv_sizes[p] bytes from p at recv + rdis[p].  Each sub-stream crosses in pieces
+// of at most kPiece bytes (sends and receives to one peer match in issue order inside the
+// group): this RCCL (2.26) delivers a single point-to-point transfer of ~2 GiB corrupted
+// (measured: a 2,147,481,620-byte self send/recv arrived wrong while the same bytes in
+// 512 MiB pieces arrive intact, tests/test_split_gpu.py::test_rccl_exchange_large_sub_stream_in_pieces).
+static psx_status exchange_v(psx_comm *c, const void *send, const uint64_t *send_sizes, const uint64_t *sdis,
+                             void *recv, const uint64_t *recv_sizes, const uint64_t *rdis, hipStream_t st) {
+  constexpr uint64_t kPiece = (uint64_t)512 << 20;
+  NCCL_TRY(c, ncclGroupStart());
+  for (int p = 0; p < c->nranks; ++p) {
+    for (uint64_t o = 0; o < send_sizes[p]; o += kPiece) {
+      const uint64_t n = send_sizes[p] - o < kPiece ? send_sizes[p] - o : kPiece;
+      NCCL_TRY_G(c, ncclSend((const uint8_t *)send + sdis[p] + o, n, ncclUint8, p, c->comm, st));
+    }
+    for (uint64_t o = 0; o < recv_sizes[p]; o += kPiece) {
+      const uint64_t n = recv_sizes[p] - o < kPiece ? recv_sizes[p] - o : kPiece;
+      NCCL_TRY_G(c, ncclRecv((uint8_t *)recv + rdis[p] + o, n, ncclUint8, p, c->comm, st));
+    }
+  }
+  NCCL_TRY(c, ncclGroupEnd());
+  return PSX_OK;
+}
+
 psx_status psx_exchange_streams(psx_comm *c, const void *send, const uint64_t *send_sizes, void *recv,
                                 const uint64_t *recv_sizes, void *hip_stream) {
   if (!c || !send_sizes || !recv_sizes) return PSX_ERR_INVALID_ARG;
   for (int p = 0; p < c->nranks; ++p)
     if ((send_sizes[p] && !send) || (recv_sizes[p] && !recv))
       return comm_fail(c, "exchange_streams: null buffer with a nonzero size", PSX_ERR_INVALID_ARG);
-  hipStream_t st = (hipStream_t)hip_stream;
   HIPX_TRY(c, hipSetDevice(c->device));
-  // Each sub-stream crosses in pieces of at most kPiece bytes (sends and receives to one
-  // peer match in issue order inside the group): this RCCL (2.26) delivers a single
-  // point-to-point transfer of ~2 GiB corrupted (measured: a 2,147,481,620-byte self
-  // send/recv arrived wrong while the same bytes in 512 MiB pieces arrive intact,
-  // tests/test_split_gpu.py::test_rccl_exchange_large_sub_stream_in_pieces).
-  constexpr uint64_t kPiece = (uint64_t)512 << 20;
+  std::vector<uint64_t> sdis((size_t)c->nranks), rdis((size_t)c->nranks);
   uint64_t so = 0, ro = 0;
-  NCCL_TRY(c, ncclGroupStart());
   for (int p = 0; p < c->nranks; ++p) {
-    for (uint64_t o = 0; o < send_sizes[p]; o += kPiece) {
-      const uint64_t n = send_sizes[p] - o < kPiece ? send_sizes[p] - o : kPiece;
-      NCCL_TRY_G(c, ncclSend((const uint8_t *)send + so + o, n, ncclUint8, p, c->comm, st));
-    }
-    for (uint64_t o = 0; o < recv_sizes[p]; o += kPiece) {
-      const uint64_t n = recv_sizes[p] - o < kPiece ? recv_sizes[p] - o : kPiece;
-      NCCL_TRY_G(c, ncclRecv((uint8_t *)recv + ro + o, n, ncclUint8, p, c->comm, st));
-    }
+    sdis[p] = so;
+    rdis[p] = ro;
     so += send_sizes[p];
     ro += recv_sizes[p];
   }
-  NCCL_TRY(c, ncclGroupEnd());
-  return PSX_OK;
+  return exchange_v(c, send, send_sizes, sdis.data(), recv, recv_sizes, rdis.data(), (hipStream_t)hip_stream);
+}
+
+psx_status psx_exchange_streams_v(psx_comm *c, const void *send, const uint64_t *send_sizes,
+                                  const uint64_t *send_displs, void *recv, const uint64_t *recv_sizes,
+                                  const uint64_t *recv_displs, void *hip_stream) {
+  if (!c || !send_sizes || !recv_sizes || !send_displs || !recv_displs) return PSX_ERR_INVALID_ARG;
+  for (int p = 0; p < c->nranks; ++p)
+    if ((send_sizes[p] && !send) || (recv_sizes[p] && !recv))
+      return comm_fail(c, "exchange_streams_v: null buffer with a nonzero size", PSX_ERR_INVALID_ARG);
+  HIPX_TRY(c, hipSetDevice(c->device));
+  return exchange_v(c, send, send_sizes, send_displs, recv, recv_sizes, recv_displs, (hipStream_t)hip_stream);
 }
 
 }  // extern "C"

@@ -101,6 +101,20 @@ class Exchange:
         if st:
             raise _abi.PsxError(st, self._L.psx_comm_last_error(self._c).decode())
 
+    def streams_v(self, send, send_sizes, send_displs, recv, recv_sizes, recv_displs, stream):
+        """psx_exchange_streams_v: explicit displacements; a zero size skips the peer."""
+        n = self.world
+        if any(int(o) + int(z) > send.numel() for o, z in zip(send_displs, send_sizes)):
+            raise ValueError("a send sub-stream past the send buffer")
+        if recv is not None and any(int(o) + int(z) > recv.numel() for o, z in zip(recv_displs, recv_sizes)):
+            raise ValueError("a receive sub-stream past the receive buffer")
+        arr = lambda v: (ctypes.c_uint64 * n)(*[int(x) for x in v])
+        st = self._L.psx_exchange_streams_v(self._c, send.data_ptr(), arr(send_sizes), arr(send_displs),
+                                            recv.data_ptr() if recv is not None else None, arr(recv_sizes),
+                                            arr(recv_displs), ctypes.c_void_p(stream))
+        if st:
+            raise _abi.PsxError(st, self._L.psx_comm_last_error(self._c).decode())
+
     def streams_into(self, send, send_sizes, recv, recv_sizes, stream):
         """psx_exchange_streams into a caller-owned recv buffer on `stream` (HIP handle);
         the caller keeps send and recv alive and unused until the stream has passed."""
@@ -206,11 +220,20 @@ class ShardExchange:
             ev.synchronize()                                # sizes known = chunk k-1's bytes arrived
             t2 = time.perf_counter()
             rsz = [int(x) for x in rs.tolist()]
-            # recv slot s was last read by chunk k-2's apply, settled by the last srv.sync()
-            recv = self._grow(self.recv, s, sum(rsz))
+            # The rank's own sub-stream does not cross: its owner applies it from the send
+            # slot (held until that apply has settled: split k+2 reuses the slot after the
+            # srv.sync() of iteration k+1).  The others land back to back in recv slot s,
+            # which chunk k-2's apply last read (settled by the last srv.sync()).
+            me = self.xc.rank
+            sdis = [sum(sizes[:p]) for p in range(n)]
+            xs, xr = list(sizes), list(rsz)
+            xs[me] = xr[me] = 0
+            rdis = [sum(xr[:p]) for p in range(n)]
+            recv = self._grow(self.recv, s, sum(xr))
             a, b = torch_event_pair()
             a.record(self.s_x)
-            self.xc.streams_into(parts, sizes, recv, rsz, self.s_x.cuda_stream)
+            if n > 1:
+                self.xc.streams_v(parts, xs, sdis, recv, xr, rdis, self.s_x.cuda_stream)
             b.record(self.s_x)
             self.ev_sent[s].record(self.s_x)
             self.ev_recv[s].record(self.s_x)
@@ -219,10 +242,10 @@ class ShardExchange:
             self.srv.sync()
             t3 = time.perf_counter()
             self.s_apply.wait_event(self.ev_recv[s])
-            msgs, off = [], 0
+            msgs = []
             for w in range(n):
-                msgs.append((recv.data_ptr() + off, rsz[w], self.bgs[w], self.version))
-                off += rsz[w]
+                ptr = send.data_ptr() + sdis[me] if w == me else recv.data_ptr() + rdis[w]
+                msgs.append((ptr, rsz[w], self.bgs[w], self.version))
             self.srv.apply_device(msgs)
             self.version += 1
             self.split_s += t1 - t0

@@ -275,3 +275,22 @@ def test_rccl_exchange_large_sub_stream_in_pieces(nbytes):
     assert rs == [nbytes]
     assert torch.equal(recv, send)
     xc.close()
+
+
+def test_rccl_exchange_streams_v_displacements_one_rank():
+    """psx_exchange_streams_v: a sub-stream taken from a send displacement lands at the
+    receive displacement; a zero size moves nothing."""
+    from parameter_server_amd.exchange import Exchange
+    xc = Exchange(0)
+    s = torch.cuda.Stream()
+    send = torch.arange(4096, dtype=torch.int32, device="cuda").view(torch.uint8)
+    recv = torch.full((8192,), 7, dtype=torch.uint8, device="cuda")
+    xc.streams_v(send, [1024], [2048], recv, [1024], [4096], s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(recv[4096:5120], send[2048:3072])
+    assert bool((recv[:4096] == 7).all()) and bool((recv[5120:] == 7).all())
+    xc.streams_v(send, [0], [0], recv, [0], [0], s.cuda_stream)
+    s.synchronize()
+    with pytest.raises(ValueError):
+        xc.streams_v(send, [1024], [16000], recv, [1024], [0], s.cuda_stream)
+    xc.close()

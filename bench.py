@@ -132,6 +132,10 @@ def parse():
                    help="run exchange_measure's orchestration and parity check over gloo on the CPU "
                         "(CpuShardExchange in place of the device path): the CPU test of the N > 1 extras")
     p.add_argument("--selftest-reverse", action="store_true", help=argparse.SUPPRESS)   # the check's negative test
+    p.add_argument("--selftest-device", action="store_true",
+                   help="with --selftest-exchange: every rank on cuda:0 with the real device path "
+                        "(ShardExchange: psx split, apply) and the bytes crossing over gloo (GlooExchange) "
+                        "-- the multi-rank GPU test on a one-GPU box")
     p.add_argument("--selftest-launch", action="store_true",
                    help="exercise only the multi-rank harness (rank launch, barriers, max-over-ranks timing, "
                         "the JSON line) over gloo with a no-op step: the CPU test of --gpus N")
@@ -682,6 +686,43 @@ class CpuShardExchange:
         pass
 
 
+class GlooExchange:
+    """Test transport with the interface ShardExchange drives (world, rank, sizes_async,
+    streams_v, close) over the gloo process group on host copies, so that several ranks can
+    share one GPU (RCCL cannot put two ranks on one device).  Synchronous: each call waits for
+    the device (the split that filled `send`), crosses on the host and copies the received
+    bytes into `recv` before returning.  Not a product path: it lets tests/test_split_gpu.py
+    run ShardExchange's multi-rank routing (displacements, the own sub-stream applied from the
+    send slot, per-source versions) with the real split and apply on a one-GPU box."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+
+    def sizes_async(self, send_sizes, recv_sizes, stream):
+        import torch
+        import torch.distributed as dist
+        rs = torch.empty(self.world, dtype=torch.int64)
+        dist.all_to_all_single(rs, torch.tensor([int(x) for x in send_sizes], dtype=torch.int64))
+        recv_sizes[:self.world].copy_(rs)
+
+    def streams_v(self, send, send_sizes, send_displs, recv, recv_sizes, recv_displs, stream):
+        import torch
+        import torch.distributed as dist
+        torch.cuda.synchronize(send.device)
+        parts = [send[int(o):int(o) + int(z)] for o, z in zip(send_displs, send_sizes)]
+        out = torch.cat(parts).cpu() if parts else torch.zeros(0, dtype=torch.uint8)
+        got = torch.empty(sum(int(z) for z in recv_sizes), dtype=torch.uint8)
+        dist.all_to_all_single(got, out, [int(z) for z in recv_sizes], [int(z) for z in send_sizes])
+        for o, z, st in zip(recv_displs, recv_sizes, [sum(int(z) for z in recv_sizes[:p]) for p in range(self.world)]):
+            if int(z):
+                recv[int(o):int(o) + int(z)].copy_(got[st:st + int(z)])
+        torch.cuda.synchronize(send.device)
+
+    def close(self):
+        pass
+
+
 def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242, backend="psx",
                      max_bytes=C4_CHUNK_BYTES):
     """The exchange-bearing step, self-checked.  A dense f32 table of
@@ -693,10 +734,12 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
     exchange beside chunk k-1's apply.  After the timed steps every owner compares its shard
     bit for bit with expected_shard(), recomputed from the seeds (never from the delivered
     bytes): `parity` is "bit-exact" or the count of differing values over all ranks.
-    backend "cpu": the same orchestration with CpuShardExchange under gloo (CPU tests)."""
+    backend "cpu": the same orchestration with CpuShardExchange under gloo (CPU tests);
+    "psx-gloo": ShardExchange on the device with the bytes over gloo (GlooExchange; tests)."""
     import torch
     import torch.distributed as dist
     cpu = backend == "cpu"
+    red_dev = "cpu" if backend != "psx" else None      # gloo reduces host tensors
     dev = torch.device("cpu") if cpu else torch.device("cuda", local)
     assert rows_total % world == 0, "row-range shards of equal size"
     shard = rows_total // world
@@ -718,7 +761,7 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
         srv.CreateTable(1, info)
         srv.load_rows(1, lo, None, on_device_ptr=init.data_ptr(), num_rows=shard)
         torch.cuda.synchronize()
-        xc = Exchange(local)
+        xc = GlooExchange() if backend == "psx-gloo" else Exchange(local)
         ex = ShardExchange(srv, 1, info, bounds, bgs, xc, local)
     del init
     if not cpu:
@@ -786,10 +829,10 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
             float(hbm_used or 0)]
     sums = [float(ndiff), float(st["recv"])]
     if world > 1:
-        t = torch.tensor(vals, dtype=torch.float64, device=dev)
+        t = torch.tensor(vals, dtype=torch.float64, device=red_dev or dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         vals = t.tolist()
-        t = torch.tensor(sums, dtype=torch.float64, device=dev)
+        t = torch.tensor(sums, dtype=torch.float64, device=red_dev or dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         sums = t.tolist()
     el, split_s, wait_s, sync_s, x_ms, apply_ms, gen_s, chk_s, hbm_used = vals
@@ -862,8 +905,15 @@ def selftest_exchange(args):
     if world > 1:
         dist.init_process_group("gloo")
     CpuShardExchange.reverse = args.selftest_reverse
-    m = exchange_measure(4096 * world, 16, args.steps, args.warmup, world, rank, 0, backend="cpu",
-                         max_bytes=20 + 68 * 1000)
+    if args.selftest_device:
+        import torch
+        torch.cuda.set_device(0)
+        # rows of 64 f32, 7 chunks a batch of which the last is short
+        m = exchange_measure(4096 * world, 64, args.steps, args.warmup, world, rank, 0, backend="psx-gloo",
+                             max_bytes=20 + 260 * 600)
+    else:
+        m = exchange_measure(4096 * world, 16, args.steps, args.warmup, world, rank, 0, backend="cpu",
+                             max_bytes=20 + 68 * 1000)
     if rank == 0:
         m["metric"] = "selftest-exchange"
         print(json.dumps(m), flush=True)

@@ -29,7 +29,8 @@ enum {
   PSX_VARIANT_DENSE_STORE = 9,  /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
                                    (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
   PSX_DEBUG_WALK_TRACE = 11,    /* 1: walked calls record per-window timestamps (psx_debug_walk_trace) */
-  PSX_VARIANT_WALK_CUS = 12,    /* the walk's persistent grid: 0 half the CUs (default), 1 every CU */
+  PSX_VARIANT_WALK_CUS = 12,    /* the walk's persistent grid: 0 half the CUs (default), 1 every CU,
+                                   n >= 2 (at most 8): n blocks per CU */
   PSX_VARIANT_WALK_COUNT = 13   /* 1 (default): on walked calls the walk counts the records of split
                                    sorted/map tables into the call slot's count state (no
                                    ordered_count launch); 0: ordered_count counts them */,
@@ -38,17 +39,22 @@ enum {
                                    block (no finish_call launch); 0: finish_call launched */,
   PSX_VARIANT_WALK_LEVELS = 15  /* the walk's composed exit-map levels: window j's exit state follows
                                    from the state 2^levels windows back (default 4; 0: window by
-                                   window) */
+                                   window) */,
+  PSX_VARIANT_WALK_SHAPE = 16   /* the walk's block x window: 0 1,024 threads x 96 KiB (default),
+                                   1 1,024 x 32 KiB, 2 512 x 24 KiB, 3 256 x 16 KiB, 4 512 x 48 KiB */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */
 int32_t psx_debug_set_variant(int32_t which, int32_t variant);
 int32_t psx_debug_get_variant(int32_t which);
 
-/* The last walked call's per-window timestamps (PSX_DEBUG_WALK_TRACE on): 6 uint64 per
+/* The last walked call's per-window timestamps (PSX_DEBUG_WALK_TRACE on): 10 uint64 per
    (window, message) item in ticket order (item = window * B + message) — ticket taken,
    window in LDS, exit map done, predecessor's state seen, own state published, records
-   expanded — in s_memrealtime ticks (100 MHz).  Copies min(items, max_items) items and
+   expanded — in s_memrealtime ticks (100 MHz), then the composed exit's outcome (low bits:
+   tried, predecessor state ok, in a table, entry in range, map found, records left; high 32
+   bits: the map entry), then the speculative phase's steps: every word's count, the jump
+   table, the candidates' exits.  Copies min(items, max_items) items and
    returns the call's item count, 0 when no call walked, -1 on error. */
 int64_t psx_debug_walk_trace(struct psx_ctx *ctx, uint64_t *out, int64_t max_items);
 

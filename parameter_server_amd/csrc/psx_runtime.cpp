@@ -31,9 +31,10 @@ hipError_t launch_split_scatter(const SplitArgs &a, const int64_t *pos, const ui
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
                        uint32_t epoch, uint64_t trace_items, const WalkCount *wc, uint64_t items, int levels,
-                       hipStream_t st);
+                       int shape, hipStream_t st);
 size_t walk_trace_offset(uint64_t items);
 size_t walk_ws_bytes(uint64_t items, int levels);
+uint64_t walk_window_bytes(int shape);
 // PSX_VARIANT_DECODE: 1 (default) walked messages with sparse tables decode window-parallel
 // where eligible, 0 one workgroup per message.
 int g_decode_walk = 1;
@@ -42,7 +43,8 @@ int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window 
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
-int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: 1 = the walk's persistent grid on every CU (default: half)
+int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
+int g_walk_shape = 0;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
@@ -458,14 +460,14 @@ bool has_sparse_serialized(const psx_ctx *c) {
 // keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
 // work takes ~15-20 us); the other half of the chip stays free for the previous call's
 // apply when the decode is pipelined (psx_ctx_set_pipeline).
-constexpr uint64_t kWalkWindowBytes = 98304;   // == psx_walk.hip kWBytes
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
 unsigned walk_blocks(psx_ctx *c) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
     cus = 256;
-  return (unsigned)std::max(1, psx::g_walk_all_cus ? cus : cus / 2);
+  const int v = psx::g_walk_all_cus;
+  return (unsigned)std::max(1, v <= 0 ? cus / 2 : v == 1 ? cus : cus * std::min(v, 8));
 }
 
 // Smallest record of any table in the context: bounds the records a message can hold
@@ -612,7 +614,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     spec_wpr = w;
   }
   uint64_t maxw = 0;
-  for (int i = 0; i < n; ++i) maxw = std::max<uint64_t>(maxw, (s[i].size + kWalkWindowBytes - 1) / kWalkWindowBytes);
+  const int walk_shape = psx::g_walk_shape;
+  const uint64_t wbytes = psx::walk_window_bytes(walk_shape);
+  for (int i = 0; i < n; ++i) maxw = std::max<uint64_t>(maxw, (s[i].size + wbytes - 1) / wbytes);
   const uint64_t items = (uint64_t)n * maxw;
   if (items == 0 || items > kWalkMaxItems) walk = false;
   // composed exit maps cost kCand x 8 B per (item, level) of workspace: up to 4,096 items
@@ -680,7 +684,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
                                   c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
                                   c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
-                                  wcount ? c->d_wcount[slot] : nullptr, items, walk_levels, prep);
+                                  wcount ? c->d_wcount[slot] : nullptr, items, walk_levels, walk_shape, prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -2702,6 +2706,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_COUNT: return &psx::g_walk_count;
     case PSX_VARIANT_FOLD_FINISH: return &psx::g_fold_finish;
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
+    case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
     default: return nullptr;
   }
 }
@@ -2726,7 +2731,7 @@ extern "C" int64_t psx_debug_walk_trace(psx_ctx *c, uint64_t *out, int64_t max_i
   if (!c->d_walk[k] || !items) return 0;
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipStreamSynchronize(c->side) != hipSuccess) return -1;
   const uint64_t n = std::min<uint64_t>(items, (uint64_t)max_items);
-  if (hipMemcpy(out, reinterpret_cast<uint8_t *>(c->d_walk[k]) + psx::walk_trace_offset(items), n * 6 * sizeof(uint64_t),
+  if (hipMemcpy(out, reinterpret_cast<uint8_t *>(c->d_walk[k]) + psx::walk_trace_offset(items), n * 10 * sizeof(uint64_t),
                 hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return (int64_t)items;
@@ -2745,6 +2750,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_WALK_COUNT")) psx::g_walk_count = atoi(v);
     if (const char *v = getenv("PSX_FOLD_FINISH")) psx::g_fold_finish = atoi(v);
     if (const char *v = getenv("PSX_WALK_LEVELS")) psx::g_walk_levels = atoi(v);
+    if (const char *v = getenv("PSX_WALK_SHAPE")) psx::g_walk_shape = atoi(v);
   }
 } variant_env;
 }  // namespace

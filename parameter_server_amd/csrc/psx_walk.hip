@@ -32,9 +32,17 @@
 
 namespace psx {
 
-constexpr int kWalkThreads = 1024;
-constexpr int kWW = 24576;                      // words per window (96 KiB)
-constexpr uint64_t kWBytes = (uint64_t)kWW * 4;
+// Walk shapes (PSX_VARIANT_WALK_SHAPE): threads per block x words per window.  A window's
+// speculative work is LDS-bound inside its CU, so smaller windows spread one call's work
+// over more CUs (several blocks per CU) at the price of more window-to-window hand-offs.
+struct WalkShape {
+  int threads, words;
+};
+constexpr WalkShape kWalkShapes[] = {{1024, 24576}, {1024, 8192}, {512, 6144}, {256, 4096}, {512, 12288}};
+constexpr int kNumWalkShapes = (int)(sizeof(kWalkShapes) / sizeof(kWalkShapes[0]));
+uint64_t walk_window_bytes(int shape) {
+  return (uint64_t)kWalkShapes[shape >= 0 && shape < kNumWalkShapes ? shape : 0].words * 4;
+}
 constexpr uint16_t kNo = 0xFFFFu;               // next record outside the window / bad header
 // n16: the record count word after q (q's n as a record start), clipped to 16 bits
 constexpr uint16_t kNBig = 0xFFFDu;             // n >= kNBig (read the word itself)
@@ -64,14 +72,16 @@ struct WalkCtl {      // reset by walk_head for the walk of the same call
 
 struct WalkHead {     // written by walk_head, read by the first window of each message
   WalkState st[kMaxFused];
-  uint32_t wfirst[kMaxFused];   // the message's first window (96 KiB grid from byte 0)
+  uint32_t wfirst[kMaxFused];   // the message's first window (window grid from byte 0)
   uint32_t nwin[kMaxFused];     // its window count (0: nothing left to walk)
 };
 constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 256;
 
 // After the granules: a trace region of kTraceWords 64-bit timestamps per window item
 // (s_memrealtime, 100 MHz), written only when the launch asks for it (psx_debug_walk_trace).
-constexpr int kTraceWords = 6;   // ticket taken, window in LDS, exit map done, predecessor seen, published, expanded
+constexpr int kTraceWords = 10;  // ticket taken, window in LDS, exit map done, predecessor seen, published, expanded,
+                                 // the composed exit's outcome (walk_trace.py decodes it), n16 done, jump table done,
+                                 // candidates' exits done
 size_t walk_trace_offset(uint64_t items) { return kWalkGranOff + items * kGran * 8; }
 // After the trace region: the composed exit maps (walk levels > 0), kCand tagged entries
 // per (item, level).
@@ -138,7 +148,7 @@ __device__ bool walk_header(const uint8_t *p, uint64_t size, const TableDir &dir
 
 __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir dir, Seg *segs, uint32_t *call_status,
                                                         uint32_t *counters, uint32_t *ntouched, WalkCtl *ctl,
-                                                        WalkHead *head, const WalkCount *wc) {
+                                                        WalkHead *head, const WalkCount *wc, uint64_t wbytes) {
   const int b = blockIdx.x;
   for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
     Seg s;
@@ -183,8 +193,8 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
     s.mode = 2;
   }
   if (s.mode == 1) {
-    wf = (uint32_t)(s.pos / kWBytes);
-    nwin = (uint32_t)((size + kWBytes - 1) / kWBytes) - wf;
+    wf = (uint32_t)(s.pos / wbytes);
+    nwin = (uint32_t)((size + wbytes - 1) / wbytes) - wf;
   }
   head->st[b] = s;
   head->wfirst[b] = wf;
@@ -200,7 +210,8 @@ __device__ __forceinline__ uint16_t next_of(uint32_t q, uint16_t c, uint32_t nw,
   return nxt < nw && W0 + nxt * 4 <= size ? (uint16_t)nxt : kNo;
 }
 
-constexpr int kCand = 1024;   // entry candidates per window (== kWalkThreads)
+// entry candidates per window: the block's thread count (at most kCandW, the exit maps'
+// 10-bit entry field)
 
 // The exit map entry of word q: the last record start on q's chain inside the window and
 // the records from q up to it, packed (16 | 16 bits): 16 records a step on jt4, then
@@ -221,6 +232,7 @@ __device__ __forceinline__ uint32_t exit_walk(uint32_t q, const uint16_t *jt4, c
 
 // The resolve's (wave-uniform) lookup: the candidates' table, or the walk itself for a
 // later entry.
+template <int kCand>
 __device__ __forceinline__ uint32_t exit_at(uint32_t q, const uint32_t *xc, const uint16_t *jt4, const uint16_t *n16,
                                             uint32_t nw, uint64_t W0, uint64_t size, uint32_t spec_wpr) {
   if (q < (uint32_t)kCand) return (uint32_t)__builtin_amdgcn_readfirstlane((int)xc[q]);
@@ -265,15 +277,21 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
   atomicAdd(&w.cnt[d], 1);
 }
 
-__global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
+template <int T_, int WW_>
+__global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
                                                             uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace,
                                                             const WalkCount *wc, unsigned long long *maps_p,
                                                             int levels) {
+  constexpr int kWalkThreads = T_, kWW = WW_, kCand = T_;
+  constexpr uint64_t kWBytes = (uint64_t)WW_ * 4;
+  static_assert(kWW % kWalkThreads == 0 && ((kWW / kWalkThreads) % 8 == 0 || (kWW / kWalkThreads) % 12 == 0) && kWW < 0xFFF0 && kCand <= kCandW,
+                "walk shape");
   gu64 *gran = (gu64 *)gran_p;
   gu64 *maps = (gu64 *)maps_p;
-  // 96 KiB windows in 150 KiB of LDS, everything but the hand-off done before it.  wbuf
+  // Windows of kWW words (96 KiB in 150 KiB of LDS for shape 0), everything but the
+  // hand-off done before it.  wbuf
   // first holds the window's words; n16 keeps the clipped record count after each word
   // (the resolve's one read of the words; single-record steps are computed from it,
   // next_of); then wbuf's two halves (sa, sb) take the 16-bit squarings of the next-record
@@ -324,7 +342,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
     // 1) the window (and its halo word) into LDS
     {
       const uint32_t *src = reinterpret_cast<const uint32_t *>(p + W0);
-      constexpr int PER = 12;   // loads in flight per thread (two passes over 96 KiB)
+      constexpr int PER = (kWW / kWalkThreads) % 12 == 0 ? 12 : 8;   // loads in flight per thread
 #pragma unroll
       for (int h = 0; h < kWW / (PER * kWalkThreads); ++h) {
         uint32_t r[PER];
@@ -350,6 +368,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       n16[q] = c;
     }
     __syncthreads();
+    if (tr && tid == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
     // 3) the 16-record jump table by four squarings of the next-record link in 16 bits,
     //    one barrier each (the words are no longer needed: sa and sb are their buffer)
     {
@@ -374,12 +393,14 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         __syncthreads();
       }
     }
+    if (tr && tid == 0) tr[8] = __builtin_amdgcn_s_memrealtime();
     //    The exit map for the window's first kCand words only — the chain enters a window
     //    inside the record that crosses its start, so in practice within its first few
     //    hundred bytes (a later entry, a record longer than kCand words, is walked by the
     //    resolve itself): thread q walks q's chain, 16 records a step, then single ones.
     if ((uint32_t)tid < (uint32_t)kCand) xc[tid] = exit_walk((uint32_t)tid, jt4, n16, nw, W0, size, spec_wpr);
     __syncthreads();
+    if (tr && tid == 0) tr[9] = __builtin_amdgcn_s_memrealtime();
     // 4') composed exit maps (levels > 0): the window's forward map F[q] — from entry
     //     candidate q, the records up to and including the one that crosses the window's
     //     end, and the word where the next window's chain starts (a candidate of it, < kCand)
@@ -400,7 +421,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         if (!last) {
           const uint32_t x = xc[q];
           const uint32_t T = x & 0xFFFFu, cnt = (x >> 16) + 1;
-          if (T + 1 < nw) {
+          if (T + 1 < nw || (T + 1 == nw && halo)) {   // T's count word in the window or its halo
             const uint16_t cT = n16[T];
             if (cT < kNBig) {
               const uint64_t endw = (uint64_t)T + 2 + (uint64_t)cT * spec_wpr;
@@ -463,7 +484,9 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
       // enters window a as a candidate inside a sparse table that goes on past window j.
       bool pub_early = false;
       uint64_t t_early = 0;
+      uint64_t xdbg = 0;   // trace word 6: bit 0 tried, 1 ok0, 2 mode 1, 3 entry in range, 4 map, 5 left; hi: map
       if (levels > 0 && !last) {
+        xdbg = 1;
         const uint32_t span = 1u << levels;
         const uint32_t a0 = j + 1 >= span ? j + 1 - span : 0u;
         WalkState s0;
@@ -496,10 +519,13 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           s0.ntab = (int32_t)rl(13);
         }
         const uint64_t Wa = ((uint64_t)head->wfirst[b] + a0) * kWBytes;
+        xdbg |= (ok0 ? 2u : 0u) | (s0.mode == 1 ? 4u : 0u);
         if (ok0 && s0.mode == 1 && s0.pos >= Wa && s0.pos - Wa < (uint64_t)kCand * 4 && s0.rk >= rk_lo &&
             s0.rk + s0.left <= rk_hi) {
           const uint32_t q0 = (uint32_t)((s0.pos - Wa) / 4);
           const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)pm[q0]);
+          xdbg |= 8u | (m != kNoMap ? 16u : 0u) | (m != kNoMap && s0.left > (uint64_t)(m >> 10) ? 32u : 0u) |
+                  ((uint64_t)m << 32);
           if (m != kNoMap && s0.left > (uint64_t)(m >> 10)) {
             WalkState e = s0;
             const uint64_t c = m >> 10;
@@ -582,10 +608,10 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         if (s.mode == 1 && !last && s.pos >= W0 && s.pos - W0 < (uint64_t)nw * 4 && s.rk >= rk_lo &&
             s.rk + s.left <= rk_hi) {
           const uint32_t q = (uint32_t)((s.pos - W0) / 4);
-          const uint32_t x = exit_at(q, xc, jt4, n16, nw, W0, size, spec_wpr);
+          const uint32_t x = exit_at<kCand>(q, xc, jt4, n16, nw, W0, size, spec_wpr);
           const uint32_t T = x & 0xFFFFu;
           const uint64_t c = (uint64_t)(x >> 16) + 1;
-          if (s.left > c && T + 1 < nw) {
+          if (s.left > c && (T + 1 < nw || (T + 1 == nw && halo))) {
             const uint32_t cT = (uint32_t)__builtin_amdgcn_readfirstlane((int)n16[T]);
             if (cT < kNBig) {
               const uint64_t endT = W0 + ((uint64_t)T + 2 + (uint64_t)cT * spec_wpr) * 4;
@@ -622,7 +648,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
           // sparse records from s.pos: one exit-map lookup
           const uint32_t q = (uint32_t)((s.pos - W0) / 4);
           if (s.pos - W0 >= (uint64_t)nw * 4) { bad |= kStMalformed; s.mode = 2; break; }   // header past the end
-          const uint32_t x = exit_at(q, xc, jt4, n16, nw, W0, size, spec_wpr);
+          const uint32_t x = exit_at<kCand>(q, xc, jt4, n16, nw, W0, size, spec_wpr);
           const uint32_t T = x & 0xFFFFu;
           const uint64_t c = (uint64_t)(x >> 16) + 1;                                // records q .. T
           const uint64_t take = s.left < c ? s.left : c;
@@ -684,6 +710,7 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
         if (lane == 0) {
           tr[3] = t_seen;
           tr[4] = pub_early ? t_early : t_pub;   // when this window's exit state went out
+          tr[6] = xdbg;
         }
       }
     }
@@ -739,19 +766,20 @@ __global__ void __launch_bounds__(kWalkThreads) walk_kernel(StreamSet ss, TableD
   }
 }
 
-// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's 96 KiB window count);
+// ws: walk_ws_bytes(items) bytes (items >= B x the largest message's window count at `shape`);
 // epoch: nonzero, different from the previous call's on this workspace (granule tags);
 // trace_items: nonzero = write the per-item timestamps (the workspace's item count);
 // wc: null, or per table (TableDir index) the walk-counted split tables' WalkCount.
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
                        uint32_t epoch, uint64_t trace_items, const WalkCount *wc, uint64_t items, int levels,
-                       hipStream_t st) {
+                       int shape, hipStream_t st) {
+  if (shape < 0 || shape >= kNumWalkShapes) shape = 0;
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
   unsigned long long *gran = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + kWalkGranOff);
   hipLaunchKernelGGL(walk_head_kernel, dim3(ss.n), dim3(256), 0, st, ss, dir, segs, call_status, counters, ntouched,
-                     ctl, head, wc);
+                     ctl, head, wc, walk_window_bytes(shape));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   unsigned long long *trace =
@@ -760,8 +788,18 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
   unsigned long long *maps =
       levels > 0 ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_maps_offset(items))
                  : nullptr;
-  hipLaunchKernelGGL(walk_kernel, dim3(blocks), dim3(kWalkThreads), 0, st, ss, dir, segs, recoff, call_status, ctl,
-                     head, gran, spec_wpr, epoch, trace, wc, maps, levels);
+#define PSX_WALK_LAUNCH(S)                                                                                    \
+  hipLaunchKernelGGL((walk_kernel<kWalkShapes[S].threads, kWalkShapes[S].words>), dim3(blocks),                    \
+                     dim3(kWalkShapes[S].threads), 0, st, ss, dir, segs, recoff, call_status, ctl, head, gran, spec_wpr, \
+                     epoch, trace, wc, maps, levels)
+  switch (shape) {
+    case 1: PSX_WALK_LAUNCH(1); break;
+    case 2: PSX_WALK_LAUNCH(2); break;
+    case 3: PSX_WALK_LAUNCH(3); break;
+    case 4: PSX_WALK_LAUNCH(4); break;
+    default: PSX_WALK_LAUNCH(0); break;
+  }
+#undef PSX_WALK_LAUNCH
   return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 """The window-parallel decode (psx_walk.hip) against the one-workgroup-per-message decode
 (decode_streams) and the CPU oracle, on the record-chain shapes that stress it: records
-spanning several 48 KiB windows, windows holding 6,144 records, tables ending mid-window and
+spanning several windows (16-96 KiB by walk shape), windows holding 6,144 records, tables ending mid-window and
 exactly on a window boundary, several sparse and dense tables in one message, empty sparse
 tables, messages of different lengths in one call, and malformed chains (the same error and
 nothing applied).  Reference: SerializedOpLogReader (serialized_oplog_reader.hpp:30-133)."""
@@ -15,7 +15,12 @@ from oracle.oracle import OracleServer, DENSE, SORTED_MAP, MAP, F32, F64, I32, I
 
 pytestmark = pytest.mark.gpu
 DECODE, WALK_CALLS = 7, 8
-WINDOW = 49152   # psx_walk.hip kWBytes: the walk's window grid from byte 0 of a message
+# psx_walk.hip kWalkShapes: the walk's window grid from byte 0 of a message, per shape
+WINDOW_BYTES = {0: 98304, 1: 32768, 2: 24576, 3: 16384, 4: 49152}
+
+
+def _window():
+    return WINDOW_BYTES[_abi.load().psx_debug_get_variant(16)]
 NP = {F32: np.float32, F64: np.float64, I32: np.int32, I64: np.int64}
 VS = {F32: 4, F64: 8, I32: 4, I64: 8}
 
@@ -27,16 +32,27 @@ def _gpu(built_lib, oracle_lib):
 
 
 WALK_LEVELS = 15
+WALK_SHAPE = 16
+WALK_CUS = 12
 
 
-@pytest.fixture(autouse=True, params=[4, 1, 0], ids=["levels4", "levels1", "levels0"])
+@pytest.fixture(autouse=True, params=[(4, 0), (1, 0), (0, 0), (4, 3), (0, 2), (2, 1), (3, 4)],
+                ids=["levels4", "levels1", "levels0", "levels4-256x16K", "levels0-512x24K", "levels2-1024x32K",
+                     "levels3-512x48K"])
 def walk_levels(request, _gpu):
-    """Every test with the walk's composed exit maps at the default 4 levels (a window's exit
-    state from the state 16 windows back), at 1 level (pairs) and off (window by window)."""
+    """Every test with the walk's composed exit maps at 4 levels (a window's exit state from the
+    state 16 windows back), at 1 level (pairs) and off (window by window), on the 96 KiB
+    window shape, and on the smaller shapes (psx_debug.h PSX_VARIANT_WALK_SHAPE) with several
+    blocks per CU."""
     L = _abi.load()
-    old = L.psx_debug_set_variant(WALK_LEVELS, request.param)
-    yield request.param
+    levels, shape = request.param
+    old = L.psx_debug_set_variant(WALK_LEVELS, levels)
+    old_s = L.psx_debug_set_variant(WALK_SHAPE, shape)
+    old_c = L.psx_debug_set_variant(WALK_CUS, 4 if shape else 0)
+    yield levels
     L.psx_debug_set_variant(WALK_LEVELS, old)
+    L.psx_debug_set_variant(WALK_SHAPE, old_s)
+    L.psx_debug_set_variant(WALK_CUS, old_c)
 
 
 def _message(tables):
@@ -166,7 +182,7 @@ def test_records_spanning_windows_and_tiny_records(dt):
 
 def test_several_tables_per_message_ending_anywhere():
     """dense, sparse, dense, sparse, empty sparse, sparse tables in one message; table ends
-    mid-window, on a window boundary (padded to 32 KiB exactly) and at the message end;
+    mid-window, on the first window boundary (padded to it exactly) and at the message end;
     messages of different lengths in one call of 16."""
     rng = np.random.RandomState(13)
     R, K, CAP = 3000, 512, 64
@@ -186,6 +202,7 @@ def test_several_tables_per_message_ending_anywhere():
             # table 2's records end exactly on the first window boundary of the message
             parts[0] = (1, "dense", ids[0][:1], rng.normal(0, 1, (1, CAP)).astype(np.float32))
             head = 4 + 16 + 1 * (4 + 4 * CAP) + 16
+            WINDOW = _window()
             recs, used = [], head
             while used + 8 + 8 * 64 < WINDOW:
                 recs += _rows(rng, [len(recs)], K, I32, [64])

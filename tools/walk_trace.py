@@ -37,10 +37,12 @@ def main():
     for v in range(args.calls):
         srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
     srv.sync()
-    buf = np.zeros(6 * 4096, np.uint64)
+    buf = np.zeros(10 * 4096, np.uint64)
     items = L.psx_debug_walk_trace(srv.handle, buf.ctypes.data_as(ctypes.c_void_p), 4096)
     assert items > 0, items
-    tr = buf[: 6 * items].reshape(items, 6).astype(np.int64)
+    raw = buf[: 10 * items].reshape(items, 10)
+    xdbg = raw[:, 6].copy()
+    tr = np.concatenate([raw[:, :6], raw[:, 7:10]], axis=1).astype(np.int64)
     t0 = tr[tr[:, 0] > 0, 0].min()
     us = (tr - t0) / 100.0   # 100 MHz ticks -> us
     out = {"items": int(items), "messages": B, "windows_per_message": int(items // B), "per_message": []}
@@ -57,8 +59,14 @@ def main():
             "seen_us": [round(x, 2) for x in r[:, 3]],
             "published_us": [round(x, 2) for x in r[:, 4]],
             "expanded_us": [round(x, 2) for x in r[:, 5]],
+            "composed": [f"{int(xdbg[j * B + b]) & 0xFF:02x}:{int(xdbg[j * B + b]) >> 32:x}"
+                         for j in range(items // B) if tr[j * B + b, 0] > 0],
             "load_us_mean": round(float((r[:, 1] - r[:, 0]).mean()), 2),
             "spec_us_mean": round(float((r[:, 2] - r[:, 1]).mean()), 2),
+            "spec_n16_us_mean": round(float((r[:, 6] - r[:, 1]).mean()), 2),
+            "spec_jump_us_mean": round(float((r[:, 7] - r[:, 6]).mean()), 2),
+            "spec_exits_us_mean": round(float((r[:, 8] - r[:, 7]).mean()), 2),
+            "spec_compose_us_mean": round(float((r[:, 2] - r[:, 8]).mean()), 2),
             "resolve_us_mean": round(float((r[:, 4] - r[:, 3]).mean()), 2),
             "hop_us_mean": round(float(hops.mean()), 2) if hops.size else None,
             "expand_us_mean": round(float((r[:, 5] - r[:, 4]).mean()), 2),

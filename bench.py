@@ -724,7 +724,7 @@ class GlooExchange:
 
 
 def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=4242, backend="psx",
-                     max_bytes=C4_CHUNK_BYTES):
+                     max_bytes=C4_CHUNK_BYTES, split_single=False):
     """The exchange-bearing step, self-checked.  A dense f32 table of
     rows_total x cap, row-range sharded over the ranks (initial rows N(0, 0.1)).  Every rank is
     one worker whose batch covers every row once in a random order (updates N(0, 0.01)),
@@ -735,7 +735,8 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
     bit for bit with expected_shard(), recomputed from the seeds (never from the delivered
     bytes): `parity` is "bit-exact" or the count of differing values over all ranks.
     backend "cpu": the same orchestration with CpuShardExchange under gloo (CPU tests);
-    "psx-gloo": ShardExchange on the device with the bytes over gloo (GlooExchange; tests)."""
+    "psx-gloo": ShardExchange on the device with the bytes over gloo (GlooExchange; tests).
+    One rank applies its chunks directly (nothing routes) unless split_single."""
     import torch
     import torch.distributed as dist
     cpu = backend == "cpu"
@@ -762,7 +763,7 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
         srv.load_rows(1, lo, None, on_device_ptr=init.data_ptr(), num_rows=shard)
         torch.cuda.synchronize()
         xc = GlooExchange() if backend == "psx-gloo" else Exchange(local)
-        ex = ShardExchange(srv, 1, info, bounds, bgs, xc, local)
+        ex = ShardExchange(srv, 1, info, bounds, bgs, xc, local, split_single=split_single)
     del init
     if not cpu:
         torch.cuda.synchronize()
@@ -867,7 +868,9 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
                    "parallelism": f"{world} shards; per chunk: device split per owner (psx_split_stream_formats), "
                                   f"libpsx RCCL all-to-all-v (psx_exchange_sizes_async / psx_exchange_streams), "
                                   f"fused in-order apply; chunk k's exchange beside chunk k-1's apply"
-                                  if not cpu else f"{world} shards over gloo (CPU stand-in)"},
+                                  if not cpu and (world > 1 or split_single) else
+                                  "one rank: each chunk applied as it is (nothing routes)" if not cpu else
+                                  f"{world} shards over gloo (CPU stand-in)"},
     }
 
 

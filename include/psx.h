@@ -563,15 +563,17 @@ psx_status psx_exchange_sizes_async(psx_comm *comm, const uint64_t *send_sizes, 
 /* ABI 7: what the reference server thread accumulates around each apply with
  * STATS_SERVER_ACCUM_APPLY_OPLOG_BEGIN/END (server_thread.cpp:240-244 ->
  * server_accum_apply_oplog_sec / server_accum_oplog_recv_mb, stats.cpp:1153-1162), per
- * context, since its creation or the last reset.  Always on (two events per call). */
+ * context, since its creation or the last reset.  Always on, at one event pair per psx_sync
+ * interval (not per call: an event costs the queue a few microseconds). */
 typedef struct psx_apply_stats {
   uint64_t calls;          /* apply calls accepted (psx_apply_stream and the device forms) */
   uint64_t messages;       /* ClientSendOpLogMsg payloads in them */
   uint64_t oplog_bytes;    /* their payload bytes (server_accum_oplog_recv_mb = oplog_bytes / 2^20) */
-  double apply_sec;        /* server_accum_apply_oplog_sec: per settled call, the device time from its
-                              first stage to its finish, summed (pipelined calls overlap: each counts
-                              its own span; a duplicate-row replay, run inside psx_sync, is not in it) */
-  uint64_t settled_calls;  /* calls whose span is in apply_sec (those settled by a psx_sync) */
+  double apply_sec;        /* server_accum_apply_oplog_sec: per psx_sync interval, the device time from
+                              its first call's first stage to its last call's finish, summed (idle
+                              time between the calls of an interval included; a duplicate-row
+                              replay, run inside psx_sync, is not in it) */
+  uint64_t settled_calls;  /* calls whose time is in apply_sec (those settled by a psx_sync) */
 } psx_apply_stats;
 /* Copy the statistics into *out (may be NULL); reset != 0 zeroes them afterwards. */
 psx_status psx_ctx_stats(psx_ctx *ctx, psx_apply_stats *out, int32_t reset);

@@ -29,7 +29,7 @@ enum {
   PSX_VARIANT_DENSE_STORE = 9,  /* dense table rows: bit0 non-temporal store, bit1 non-temporal load
                                    (0 plain/plain, 1 plain load + nt store, 3 nt/nt) */
   PSX_DEBUG_WALK_TRACE = 11,    /* 1: walked calls record per-window timestamps (psx_debug_walk_trace) */
-  PSX_VARIANT_WALK_CUS = 12,    /* the walk's persistent grid: 0 half the CUs (default), 1 every CU,
+  PSX_VARIANT_WALK_CUS = 12,    /* the walk's persistent grid: 0 half the CUs, 1 every CU (default),
                                    n >= 2 (at most 8): n blocks per CU */
   PSX_VARIANT_WALK_COUNT = 13   /* 1 (default): on walked calls the walk counts the records of split
                                    sorted/map tables into the call slot's count state (no
@@ -40,8 +40,12 @@ enum {
   PSX_VARIANT_WALK_LEVELS = 15  /* the walk's composed exit-map levels: window j's exit state follows
                                    from the state 2^levels windows back (default 4; 0: window by
                                    window) */,
-  PSX_VARIANT_WALK_SHAPE = 16   /* the walk's block x window: 0 1,024 threads x 96 KiB (default),
-                                   1 1,024 x 32 KiB, 2 512 x 24 KiB, 3 256 x 16 KiB, 4 512 x 48 KiB */
+  PSX_VARIANT_WALK_SHAPE = 16   /* the walk's block x window: 0 1,024 threads x 96 KiB, 1 1,024 x
+                                   32 KiB, 2 512 x 24 KiB, 3 256 x 16 KiB, 4 512 x 48 KiB (default) */,
+  PSX_VARIANT_CALL_EVENTS = 17  /* events enqueued per call: bit 0 an event pair per call for
+                                   psx_ctx_stats (default 0: one pair per psx_sync interval), bit 1
+                                   the slot-free event on every call (default 0: only while the
+                                   context pipelines) */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

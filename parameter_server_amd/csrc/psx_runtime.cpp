@@ -43,8 +43,10 @@ int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window 
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
-int g_walk_all_cus = 0;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
-int g_walk_shape = 0;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
+int g_walk_all_cus = 1;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
+int g_call_events = 0;   // PSX_VARIANT_CALL_EVENTS: bit 0 an event pair per call for psx_ctx_stats (else one per
+                         // sync interval), bit 1 the slot-free event on every call (else only when pipelining)
+int g_walk_shape = 4;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
@@ -270,6 +272,8 @@ struct psx_ctx {
   std::vector<hipEvent_t> ev_pool;
   std::map<std::string, std::pair<double, int64_t>> times;
   psx_apply_stats stats{};               // psx_ctx_stats (STATS_SERVER_ACCUM_APPLY_OPLOG_*)
+  hipEvent_t stats_open = nullptr;       // the open sync interval's first-call event (psx_ctx_stats)
+  uint64_t stats_open_calls = 0;         // calls accepted since it
 };
 
 namespace {
@@ -453,13 +457,13 @@ bool has_sparse_serialized(const psx_ctx *c) {
   return false;
 }
 
-// Window-parallel decode (psx_walk.hip): 48 KiB windows; a call runs it when its messages
-// have at most kWalkMaxItems (message, window) items (B x the largest message's windows:
-// 6 GiB of windows), on 1,024-thread blocks (149 KB of LDS: one per CU) on half the CUs.
-// The walk is bound by its window-to-window hand-offs (~1.7 us each), which ~100 blocks
-// keep fed (8 messages' chains each resolve a window per hand-off, a window's speculative
-// work takes ~15-20 us); the other half of the chip stays free for the previous call's
-// apply when the decode is pipelined (psx_ctx_set_pipeline).
+// Window-parallel decode (psx_walk.hip): by default 48 KiB windows on 512-thread blocks
+// (77 KB of LDS) over every CU; a call runs it when its messages have at most kWalkMaxItems
+// (message, window) items (B x the largest message's windows).  A window's speculative work
+// is LDS-bound inside its CU (~12 us at 48 KiB), the chain between windows hops 16 windows
+// at a time on the composed exit maps, so spreading the windows over the whole chip is what
+// shortens the walk (the 96 KiB x 1,024-thread shape on half the CUs, round
+// 3's default, is PSX_VARIANT_WALK_SHAPE 0 with PSX_VARIANT_WALK_CUS 0).
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
 unsigned walk_blocks(psx_ctx *c) {
@@ -570,7 +574,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     ~EventGuard() {
       if (e) c->ev_pool.push_back(e);
     }
-  } call_ev{c, force_ordered ? nullptr : get_event(c)};
+  } call_ev{c, force_ordered || !(psx::g_call_events & 1) ? nullptr : get_event(c)};
   psx::TableDir dir{};
   dir.n = (int32_t)c->tables.size();
   for (size_t i = 0; i < c->tables.size(); ++i) {
@@ -587,6 +591,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   uint32_t *counters = c->d_counters[slot];
   if (pipelined) HIP_TRY(c, hipStreamWaitEvent(prep, c->ev_free[slot], 0));
   if (call_ev.e) HIP_TRY(c, hipEventRecord(call_ev.e, prep));
+  if (!force_ordered && !(psx::g_call_events & 1) && !c->stats_open) {
+    // psx_ctx_stats: the interval's device time starts at its first call's first stage
+    c->stats_open = get_event(c);
+    if (c->stats_open) HIP_TRY(c, hipEventRecord(c->stats_open, prep));
+    c->stats_open_calls = 0;
+  }
   if (c->wcount_dirty[slot]) {
     // the slot's last call failed between its counting walk and its ordered prep
     for (auto &t : c->tables) {
@@ -855,8 +865,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     st = timed(c, "finish_call", [&] { return psx::launch_finish(sticky, call_st, call_log, c->stream); });
     if (st) return st;
   }
-  // every call marks its slot free (a later pipelined call's stage 1 waits on it)
-  HIP_TRY(c, hipEventRecord(c->ev_free[slot], c->stream));
+  // a pipelined context's call marks its slot free (a later call's stage 1 waits on it;
+  // psx_ctx_set_pipeline drains the streams when the mode changes, so a stale event is never
+  // waited for with the slot still in use)
+  if (c->pipeline || (psx::g_call_events & 2)) HIP_TRY(c, hipEventRecord(c->ev_free[slot], c->stream));
   PendingCall pc;
   pc.streams.assign(s, s + n);
   pc.ring = ring;
@@ -871,6 +883,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     }
   }
   if (!force_ordered) {
+    if (c->stats_open) c->stats_open_calls++;
     c->stats.calls++;
     c->stats.messages += (uint64_t)n;
     for (int i = 0; i < n; ++i) c->stats.oplog_bytes += s[i].size;
@@ -972,9 +985,29 @@ psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
 
 psx_status sync_impl(psx_ctx *c) {
   HIP_TRY(c, hipSetDevice(c->device));
+  hipEvent_t stats_close = nullptr;
+  if (c->stats_open) {
+    stats_close = get_event(c);
+    if (stats_close && hipEventRecord(stats_close, c->stream) != hipSuccess) {
+      c->ev_pool.push_back(stats_close);
+      stats_close = nullptr;
+    }
+  }
   HIP_TRY(c, hipStreamSynchronize(c->side));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   collect_timing(c);
+  if (c->stats_open) {
+    // the interval's device time: its first call's first stage to the last call's finish
+    float ms = 0.f;
+    if (stats_close && hipEventElapsedTime(&ms, c->stats_open, stats_close) == hipSuccess) {
+      c->stats.apply_sec += ms * 1e-3;
+      c->stats.settled_calls += c->stats_open_calls;
+    }
+    c->ev_pool.push_back(c->stats_open);
+    if (stats_close) c->ev_pool.push_back(stats_close);
+    c->stats_open = nullptr;
+    c->stats_open_calls = 0;
+  }
   uint32_t sticky = 0;
   HIP_TRY(c, hipMemcpy(&sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
   std::vector<PendingCall> pending;
@@ -1167,6 +1200,11 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
     hipEventDestroy(p.b);
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
+  for (auto &p : c->pending) {
+    if (p.ev_a) hipEventDestroy(p.ev_a);
+    if (p.ev_b) hipEventDestroy(p.ev_b);
+  }
+  if (c->stats_open) hipEventDestroy(c->stats_open);
   for (int k = 0; k < 2; ++k) {
     if (c->d_segs[k]) hipFree(c->d_segs[k]);
     if (c->d_counters[k]) hipFree(c->d_counters[k]);
@@ -2621,6 +2659,13 @@ psx_status psx_decode_push_header(const void *msg, size_t msg_size, psx_push_msg
 
 psx_status psx_ctx_set_pipeline(psx_ctx *c, int32_t mode) {
   if (!c || mode < 0 || mode > PSX_PIPELINE_ALL) return PSX_ERR_INVALID_ARG;
+  if (mode != c->pipeline) {
+    // no call in flight across the change: the slot-free events are recorded only while
+    // pipelining, so the first pipelined call must not find a slot still in use
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->side));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
   c->pipeline = mode;
   return PSX_OK;
 }
@@ -2672,7 +2717,10 @@ psx_status psx_timing_read(psx_ctx *c, const char *kernel, double *total_ms, int
 psx_status psx_ctx_stats(psx_ctx *c, psx_apply_stats *out, int32_t reset) {
   if (!c) return PSX_ERR_INVALID_ARG;
   if (out) *out = c->stats;
-  if (reset) c->stats = psx_apply_stats{};
+  if (reset) {
+    c->stats = psx_apply_stats{};
+    c->stats_open_calls = 0;   // the open interval's earlier calls went out with the reset
+  }
   return PSX_OK;
 }
 
@@ -2707,6 +2755,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_FOLD_FINISH: return &psx::g_fold_finish;
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
     case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
+    case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
     default: return nullptr;
   }
 }

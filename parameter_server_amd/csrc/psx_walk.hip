@@ -79,7 +79,7 @@ constexpr size_t kWalkGranOff = kWalkHeadOff + (sizeof(WalkHead) + 255) / 256 * 
 
 // After the granules: a trace region of kTraceWords 64-bit timestamps per window item
 // (s_memrealtime, 100 MHz), written only when the launch asks for it (psx_debug_walk_trace).
-constexpr int kTraceWords = 10;  // ticket taken, window in LDS, exit map done, predecessor seen, published, expanded,
+constexpr int kTraceWords = 10;  // ticket taken, counts loaded, exit map done, predecessor seen, published, expanded,
                                  // the composed exit's outcome (walk_trace.py decodes it), n16 done, jump table done,
                                  // candidates' exits done
 size_t walk_trace_offset(uint64_t items) { return kWalkGranOff + items * kGran * 8; }
@@ -203,11 +203,15 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
 
 // The next record start after a speculative record at word q with count word c (n16), or
 // kNo when it lies outside the window or past the message (a count >= kNBig always does).
+// (32-bit: c < kNBig and spec_wpr <= 3 keep q + 2 + c * spec_wpr far below 2^32; nw never
+// passes the message's end, so a start before nw is inside the message.)
 __device__ __forceinline__ uint16_t next_of(uint32_t q, uint16_t c, uint32_t nw, uint64_t W0, uint64_t size,
                                             uint32_t spec_wpr) {
-  if (q + 1 >= nw || c >= kNBig) return kNo;
-  const uint64_t nxt = (uint64_t)q + 2 + (uint64_t)c * spec_wpr;
-  return nxt < nw && W0 + nxt * 4 <= size ? (uint16_t)nxt : kNo;
+  (void)W0;
+  (void)size;
+  if (c >= kNBig) return kNo;
+  const uint32_t nxt = q + 2 + (uint32_t)c * spec_wpr;
+  return nxt < nw ? (uint16_t)nxt : kNo;
 }
 
 // entry candidates per window: the block's thread count (at most kCandW, the exit maps'
@@ -290,22 +294,19 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
                 "walk shape");
   gu64 *gran = (gu64 *)gran_p;
   gu64 *maps = (gu64 *)maps_p;
-  // Windows of kWW words (96 KiB in 150 KiB of LDS for shape 0), everything but the
-  // hand-off done before it.  wbuf
-  // first holds the window's words; n16 keeps the clipped record count after each word
-  // (the resolve's one read of the words; single-record steps are computed from it,
-  // next_of); then wbuf's two halves (sa, sb) take the 16-bit squarings of the next-record
-  // link — 2, 4, 8, 16 records — and sb ends as jt4, the 16-record jump table; xc is the
-  // exit map of the entry candidates (packed: low 16 bits the last record start on q's
-  // chain inside the window, high 16 the records from q up to it, exclusive).
+  // Windows of kWW words (96 KiB for shape 0), everything but the hand-off done before it.
+  // n16 keeps the clipped record count after each word, loaded straight from the message
+  // (single-record steps are computed from it, next_of); wbuf's two halves (sa, sb) take the
+  // 16-bit squarings of the next-record link — 2, 4, 8, 16 records — and sb ends as jt4, the
+  // 16-record jump table; xc is the exit map of the entry candidates (packed: low 16 bits the
+  // last record start on q's chain inside the window, high 16 the records from q up to it,
+  // exclusive).
   __shared__ uint32_t wbuf[kWW];
-  __shared__ uint16_t n16[kWW];
+  __shared__ __align__(16) uint16_t n16[kWW];
   __shared__ uint32_t xc[kCand];   // exit map of the first kCand words (the entry candidates)
-  uint32_t *const win = wbuf;
   uint16_t *const sa = reinterpret_cast<uint16_t *>(wbuf);
   uint16_t *const sb = sa + kWW;
   uint16_t *const jt4 = sb;
-  __shared__ uint32_t sh_halo;
   __shared__ uint16_t seg_q[kMaxSegs];
   __shared__ uint16_t seg_n[kMaxSegs];
   __shared__ uint64_t seg_rk[kMaxSegs];
@@ -339,56 +340,74 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
     const uint32_t nw = (uint32_t)(tot < (uint64_t)kWW ? tot : (uint64_t)kWW);
     const bool halo = tot > nw;
     const bool last = j + 1 == nwin_b;
-    // 1) the window (and its halo word) into LDS
+    // 1) every word a speculative record start: n16[q], the clipped count word after q,
+    //    straight from the message (coalesced loads, one word ahead; the words themselves are
+    //    not kept — the resolve reads headers from the message)
     {
       const uint32_t *src = reinterpret_cast<const uint32_t *>(p + W0);
+      const uint32_t lim = halo ? nw + 1 : nw;   // words readable from W0 (with the halo word)
       constexpr int PER = (kWW / kWalkThreads) % 12 == 0 ? 12 : 8;   // loads in flight per thread
 #pragma unroll
       for (int h = 0; h < kWW / (PER * kWalkThreads); ++h) {
         uint32_t r[PER];
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-          const uint32_t i = (uint32_t)tid + (uint32_t)(h * PER + k) * kWalkThreads;
-          r[k] = i < nw ? src[i] : 0u;
+          const uint32_t q = (uint32_t)tid + (uint32_t)(h * PER + k) * kWalkThreads;
+          r[k] = q + 1 < lim ? src[q + 1] : 0u;
         }
 #pragma unroll
-        for (int k = 0; k < PER; ++k) win[tid + (h * PER + k) * kWalkThreads] = r[k];
+        for (int k = 0; k < PER; ++k) {
+          const uint32_t q = (uint32_t)tid + (uint32_t)(h * PER + k) * kWalkThreads;
+          const int32_t n = (int32_t)r[k];
+          n16[q] = q + 1 >= lim ? kNNone : n < 0 ? kNNeg : (n >= (int32_t)kNBig ? kNBig : (uint16_t)n);
+        }
       }
-      if (tid == 0) sh_halo = halo ? src[nw] : 0u;
     }
     __syncthreads();
     if (tr && tid == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
-    // 2) every word a speculative record start: n16 from the words
-    for (uint32_t q = tid; q < (uint32_t)kWW; q += kWalkThreads) {
-      uint16_t c = kNNone;
-      if (q + 1 < nw || (q + 1 == nw && halo)) {
-        const int32_t n = (int32_t)(q + 1 < nw ? win[q + 1] : sh_halo);
-        c = n < 0 ? kNNeg : (n >= (int32_t)kNBig ? kNBig : (uint16_t)n);
-      }
-      n16[q] = c;
-    }
-    __syncthreads();
     if (tr && tid == 0) tr[7] = __builtin_amdgcn_s_memrealtime();
-    // 3) the 16-record jump table by four squarings of the next-record link in 16 bits,
-    //    one barrier each (the words are no longer needed: sa and sb are their buffer)
+    // 2) the 16-record jump table by four squarings of the next-record link in 16 bits,
+    //    one barrier each; a thread takes two neighbouring words at a time (32-bit LDS reads
+    //    and writes of the sequential side, 16-bit gathers of the links)
     {
       constexpr int PER = kWW / kWalkThreads;
+      static_assert(PER % 2 == 0, "word pairs");
+      // next_of inside the window: n < kNBig and the next start before nw (nw <= the
+      // message's words from W0, so such a start is inside the message too)
+      auto nx = [&](uint32_t q, uint32_t c) -> uint32_t {
+        if (c >= kNBig) return kNo;
+        const uint32_t nxt = q + 2 + c * spec_wpr;
+        return nxt < nw ? nxt : kNo;
+      };
+      const uint32_t *const n16w = reinterpret_cast<const uint32_t *>(n16);
 #pragma unroll
       for (int lv = 0; lv < 4; ++lv) {
         const uint16_t *src = (lv & 1) ? sa : sb;   // lv 0 reads n16, not sb
         uint16_t *dst = (lv & 1) ? sb : sa;
-#pragma unroll 8
-        for (int k = 0; k < PER; ++k) {
-          const uint32_t q = (uint32_t)tid + (uint32_t)k * kWalkThreads;
-          uint16_t r;
+        const uint32_t *srcw = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *dstw = reinterpret_cast<uint32_t *>(dst);
+#pragma unroll 4
+        for (int k = 0; k < PER / 2; ++k) {
+          const uint32_t i = (uint32_t)tid + (uint32_t)k * kWalkThreads;   // words 2i, 2i + 1
+          uint32_t a0, a1;
           if (lv == 0) {
-            const uint16_t a = next_of(q, n16[q], nw, W0, size, spec_wpr);
-            r = a != kNo ? next_of(a, n16[a], nw, W0, size, spec_wpr) : kNo;
+            const uint32_t cc = n16w[i];
+            a0 = nx(2 * i, cc & 0xFFFFu);
+            a1 = nx(2 * i + 1, cc >> 16);
           } else {
-            const uint16_t a = src[q];
-            r = a != kNo ? src[a] : kNo;
+            const uint32_t aa = srcw[i];
+            a0 = aa & 0xFFFFu;
+            a1 = aa >> 16;
           }
-          dst[q] = r;
+          uint32_t r0 = kNo, r1 = kNo;
+          if (lv == 0) {
+            if (a0 != kNo) r0 = nx(a0, n16[a0]);
+            if (a1 != kNo) r1 = nx(a1, n16[a1]);
+          } else {
+            if (a0 != kNo) r0 = src[a0];
+            if (a1 != kNo) r1 = src[a1];
+          }
+          dstw[i] = r0 | (r1 << 16);
         }
         __syncthreads();
       }
@@ -716,9 +735,13 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
     }
     __syncthreads();
     // 5) expand the window's record offsets: thread 0 collects the 16-record hop starts,
-    //    all threads fill
+    //    one thread per hop lists its 16 records' word offsets in LDS (sa: free once the
+    //    state is out), then one thread per record writes its offset (coalesced) and, for a
+    //    walk-counted table, does ordered_count's work for it
     const uint32_t nseg = sh_nseg;
+    uint16_t *const recq = sa;
     for (uint32_t si = 0; si < nseg; ++si) {
+      if (si) __syncthreads();   // recq and a16 held the previous segment's
       if (tid == 0) {
         uint32_t w = seg_q[si];
         uint32_t rem = seg_n[si];
@@ -742,24 +765,19 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
         uint32_t q = a16[i];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          recoff[rk + 16 * (uint64_t)i + k] = W0 + (uint64_t)q * 4;
+          recq[16 * i + k] = (uint16_t)q;
           if (k < 15) q = next_of(q, n16[q], nw, W0, size, spec_wpr);
         }
       }
-      const uint64_t r1 = rk + 16 * (uint64_t)nh;
-      if (tid < n1) recoff[r1 + tid] = W0 + (uint64_t)a1[tid] * 4;
+      if (tid < n1) recq[16 * nh + tid] = a1[tid];
       __syncthreads();
-      // walk-counted tables: ordered_count's per-record work, one record per thread from
-      // the offsets just written (the block's own stores: visible after the barrier)
-      if (wc) {
-        const int t = seg_t[si];
-        if (wc[t].on) {
-          const uint32_t nrec = 16 * nh + n1;
-          for (uint32_t r = (uint32_t)tid; r < nrec; r += kWalkThreads) {
-            const uint64_t off = recoff[rk + r];
-            if (off + 8 <= size) walk_count(p + off, wc[t], call_status);
-          }
-        }
+      const uint32_t nrec = 16 * nh + n1;
+      const int t = seg_t[si];
+      const bool counted = wc && wc[t].on;
+      for (uint32_t r = (uint32_t)tid; r < nrec; r += kWalkThreads) {
+        const uint64_t off = W0 + (uint64_t)recq[r] * 4;
+        recoff[rk + r] = off;
+        if (counted && off + 8 <= size) walk_count(p + off, wc[t], call_status);
       }
     }
     if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memrealtime();

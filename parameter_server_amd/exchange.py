@@ -149,9 +149,12 @@ class ShardExchange:
     Chunk k's bytes cross while chunk k-1 applies and chunk k+1 splits; two slots of each
     buffer bound the HBM the step needs beyond the batches and the table to about four
     chunks.  Each sender's messages carry consecutive versions (one per chunk round; an
-    owner with no records from a sender gets an empty message, which only bumps it)."""
+    owner with no records from a sender gets an empty message, which only bumps it).  With one
+    rank nothing routes: the chunks are applied as they are, unless split_single asks for the
+    split (and the own sub-stream path) anyway."""
 
-    def __init__(self, server, table_id, info, row_begin, bg_ids, exchange, device, splitter_id=900):
+    def __init__(self, server, table_id, info, row_begin, bg_ids, exchange, device, splitter_id=900,
+                 split_single=False):
         import torch
         from .server import Server
         self.srv, self.xc, self.device = server, exchange, device
@@ -174,6 +177,7 @@ class ShardExchange:
         self.ev_x1 = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
         self.rsz = torch.zeros((2, self.world), dtype=torch.int64).pin_memory()
         self.version = 0
+        self.direct = self.world == 1 and not split_single
         self.reset_counters()
 
     def reset_counters(self):
@@ -204,6 +208,8 @@ class ShardExchange:
         batch in record order) to the owners' shards.  Returns after every apply settled."""
         import time
         n = self.world
+        if self.direct:
+            return self._run_direct(chunks, log)
         for k, msg in enumerate(chunks):
             s = k % 2
             ntab = len(self.formats)
@@ -259,6 +265,22 @@ class ShardExchange:
                 log(f"chunk {k}: split {t1 - t0:.4f} s, sizes wait {t2 - t1:.4f} s, apply wait {t3 - t2:.4f} s")
         self.srv.sync()
         self._collect_x(0)
+
+    def _run_direct(self, chunks, log=None):
+        """One rank: each chunk is its only owner's message; applied in order on s_apply."""
+        import time
+        self.s_apply.wait_stream(torch.cuda.current_stream(self.device))
+        for k, msg in enumerate(chunks):
+            t0 = time.perf_counter()
+            self.srv.apply_device([(msg.data_ptr(), msg.numel(), self.bgs[0], self.version)])
+            self.version += 1
+            self.sync_s += time.perf_counter() - t0
+            self.chunks += 1
+            self.sent_bytes += msg.numel()
+            self.recv_bytes += msg.numel()
+            if log is not None:
+                log(f"chunk {k}: applied directly (one rank)")
+        self.srv.sync()
 
     def close(self):
         self.splitter.close()

@@ -255,10 +255,12 @@ def test_shard_exchange_pipeline_one_rank_bit_exact(rows, cap, chunk_recs):
     order with chunk k's exchange beside chunk k-1's apply, three steps — bit for bit equal to
     the in-order f32 sum recomputed from the seeds (bench.exchange_measure's check)."""
     import bench
-    m = bench.exchange_measure(rows, cap, 2, 1, 1, 0, 0, seed=7 + rows, max_bytes=20 + (4 + 4 * cap) * chunk_recs)
-    assert m["parity"] == "bit-exact", m
-    assert m["chunks_per_step"] == -(-rows // chunk_recs)
-    assert m["apply_kernel_ms_per_chunk"] and m["exchange_kernel_ms_per_step"] is not None
+    for split_single in (True, False):   # the split + own sub-stream path, then the direct one
+        m = bench.exchange_measure(rows, cap, 2, 1, 1, 0, 0, seed=7 + rows, max_bytes=20 + (4 + 4 * cap) * chunk_recs,
+                                   split_single=split_single)
+        assert m["parity"] == "bit-exact", (split_single, m)
+        assert m["chunks_per_step"] == -(-rows // chunk_recs)
+        assert m["apply_kernel_ms_per_chunk"] and m["exchange_kernel_ms_per_step"] is not None
 
 
 @pytest.mark.parametrize("nbytes", [(1 << 31) - 2028, (1 << 31) + 4096 * 3])

@@ -36,19 +36,20 @@ WALK_SHAPE = 16
 WALK_CUS = 12
 
 
-@pytest.fixture(autouse=True, params=[(4, 0), (1, 0), (0, 0), (4, 3), (0, 2), (2, 1), (3, 4)],
+@pytest.fixture(autouse=True, params=[(4, 0, 0), (1, 0, 0), (0, 0, 0), (4, 3, 4), (0, 2, 4), (2, 1, 4), (3, 4, 4), (4, 4, 1)],
                 ids=["levels4", "levels1", "levels0", "levels4-256x16K", "levels0-512x24K", "levels2-1024x32K",
-                     "levels3-512x48K"])
+                     "levels3-512x48K", "levels4-512x48K-default"])
 def walk_levels(request, _gpu):
     """Every test with the walk's composed exit maps at 4 levels (a window's exit state from the
     state 16 windows back), at 1 level (pairs) and off (window by window), on the 96 KiB
-    window shape, and on the smaller shapes (psx_debug.h PSX_VARIANT_WALK_SHAPE) with several
-    blocks per CU."""
+    window shape on half the CUs (round 3's form), on the smaller shapes (psx_debug.h
+    PSX_VARIANT_WALK_SHAPE) with several blocks per CU, and on the default (48 KiB windows
+    on every CU)."""
     L = _abi.load()
-    levels, shape = request.param
+    levels, shape, cus = request.param
     old = L.psx_debug_set_variant(WALK_LEVELS, levels)
     old_s = L.psx_debug_set_variant(WALK_SHAPE, shape)
-    old_c = L.psx_debug_set_variant(WALK_CUS, 4 if shape else 0)
+    old_c = L.psx_debug_set_variant(WALK_CUS, cus)
     yield levels
     L.psx_debug_set_variant(WALK_LEVELS, old)
     L.psx_debug_set_variant(WALK_SHAPE, old_s)

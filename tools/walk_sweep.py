@@ -3,7 +3,7 @@
 (bench.py c3_streams), interleaved in one process: per config a server of its own, rounds of
 `steps` timed walked calls, the step rate in M updates/s (best and median of the rounds).
 Usage: python tools/walk_sweep.py [--rounds 3] [--steps 20] [--configs 0:0:4,3:4:4,...]
-(config = shape:cus:levels)."""
+(config = shape:cus:levels[:call_events], call_events PSX_VARIANT_CALL_EVENTS, default 0)."""
 import argparse
 import json
 import os
@@ -31,7 +31,8 @@ def main():
     B = len(streams)
     bgs = list(range(100, 100 + B))
     dev = [torch.from_numpy(s).cuda() for s in streams]
-    cfgs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
+    cfgs = [tuple(int(x) for x in (c + ":0").split(":")[:4]) if c.count(":") == 2 else
+            tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
     srvs, ver = [], []
     for _ in cfgs:
         srv = psa.Server(0, 1, bgs)
@@ -46,6 +47,7 @@ def main():
             L.psx_debug_set_variant(16, c[0])
             L.psx_debug_set_variant(12, c[1])
             L.psx_debug_set_variant(15, c[2])
+            L.psx_debug_set_variant(17, c[3])
             srv = srvs[i]
 
             def step():
@@ -69,7 +71,7 @@ def main():
     out = []
     for c in cfgs:
         v = sorted(x for x, _ in res[c])
-        out.append({"shape": c[0], "cus": c[1], "levels": c[2], "best_Mups": round(v[-1], 1),
+        out.append({"shape": c[0], "cus": c[1], "levels": c[2], "call_events": c[3], "best_Mups": round(v[-1], 1),
                     "median_Mups": round(v[len(v) // 2], 1), "walked_calls": res[c][-1][1],
                     "us_per_step": round(nupd / v[len(v) // 2], 2)})
     print(json.dumps(out, indent=1))

@@ -45,7 +45,12 @@ enum {
   PSX_VARIANT_CALL_EVENTS = 17  /* events enqueued per call: bit 0 an event pair per call for
                                    psx_ctx_stats (default 0: one pair per psx_sync interval), bit 1
                                    the slot-free event on every call (default 0: only while the
-                                   context pipelines) */
+                                   context pipelines) */,
+  PSX_VARIANT_OFFSETS_GRID = 18, /* ordered_offsets' grid cap (blocks of 256 slots; default 1,024) */
+  PSX_VARIANT_DRY_GRID = 19,    /* the capacity dry run's grid cap (default 128) */
+  PSX_VARIANT_WALK_RANK = 20    /* 1 (default): walk-counted tables also get each record's place in
+                                   its slot's list from the walk (ordered_fill without atomics);
+                                   0: ordered_fill takes the places from the counts */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -189,7 +189,9 @@ struct OrdArgs {
   const uint32_t *nheavy;    // 256-entry list's region), listed backwards; the 256-entry
                              // launch takes them first
   int32_t counted;           // split tables: the walk already counted this call's records
-                             // (WalkCount): ordered_count is not launched
+                             // (WalkCount): ordered_count is not launched; 2: it also placed
+                             // each record in its slot's list (WalkCount.wfill), so
+                             // ordered_offsets zeroes the counts and ordered_fill needs no atomics
   // finish_call folded into this apply launch (the call's last): fin_ring >= 0 is the call's
   // status ring slot, so call_status = status + 1 + fin_ring and the sticky word, the call's
   // log entry and the block counter follow from call_status (kCallRing layout); the last
@@ -213,6 +215,8 @@ struct WalkCount {
   int32_t *tsum;      // its record-range base [0]
   int32_t on;
   int32_t pad;
+  int2 *wfill;        // non-null: per record (its recoff index) {slot, its place in the slot's record
+                      // list} from the count's returned value, for ordered_fill (-1: no slot)
 };
 
 // A side stream and two events for launches that run beside the context stream.

@@ -172,7 +172,9 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
+// wfill (walk-ranked split tables, counted == 2): each record's {slot, place} from the walk;
+// the list entry is written without an atomic and the counts were zeroed by ordered_offsets.
+__global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a, const int2 *wfill) {
   __shared__ RecSpace rs;
   if (threadIdx.x == 0) build_space(a, rs);
   __syncthreads();
@@ -186,6 +188,18 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < a.max_rows; s += G) {
       a.cnt[s] = 0;
       if (a.grow) a.grow[s] = 0;
+    }
+    return;
+  }
+  if (wfill) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
+      int b = 0;
+      while (b + 1 < a.B && rs.pre[b + 1] <= r) ++b;
+      const int64_t idx = rs.first[b] + (r - rs.pre[b]);   // walk-counted tables are sparse
+      const int2 sk = wfill[idx];
+      const uint64_t off = a.recoff[idx];
+      if (sk.x < 0) continue;
+      a.list[a.off[sk.x] + sk.y] = rec_ref(b, off);
     }
     return;
   }
@@ -231,6 +245,36 @@ __device__ __forceinline__ int32_t block_excl_sum(int32_t v, int32_t *sh, int32_
   return pre + incl - v;
 }
 
+// Six exclusive prefix sums at once (one LDS exchange, two barriers instead of twelve).
+__device__ __forceinline__ void block_excl_sum6(const int32_t (&v)[6], int32_t (&pre)[6], int32_t (&total)[6],
+                                                int32_t (*sh)[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t incl[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    incl[i] = v[i];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(incl[i], o, 64);
+      if (lane >= o) incl[i] += y;
+    }
+    if (lane == 63) sh[i][w] = incl[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    int32_t p = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < w) p += sh[i][k];
+      t += sh[i][k];
+    }
+    pre[i] = p + incl[i] - v[i];
+    total[i] = t;
+  }
+  __syncthreads();
+}
+
 // Which apply launch a touched row starts on.  Default: the 1,024-entry one when its image
 // can outgrow 256 entries in this call (entries now + the call's Incs).  Spill mode: only
 // an image already 7/8 full; the rest start on the 256-entry launch and spill if they
@@ -272,13 +316,9 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       if (may_overflow(a, nen, g)) ++nd;
     }
   }
-  int32_t tt, tr, ts, tb, th, td;
-  block_excl_sum(nt, sh[0], tt);
-  block_excl_sum(nr, sh[1], tr);
-  block_excl_sum(ns, sh[2], ts);
-  block_excl_sum(nb, sh[3], tb);
-  block_excl_sum(nh, sh[4], th);
-  block_excl_sum(nd, sh[5], td);
+  int32_t pre1[6], tot1[6];
+  block_excl_sum6({nt, nr, ns, nb, nh, nd}, pre1, tot1, sh);
+  const int32_t tt = tot1[0], tr = tot1[1], ts = tot1[2], tb = tot1[3], th = tot1[4], td = tot1[5];
   if (threadIdx.x == 0) {
     base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
     base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
@@ -308,16 +348,15 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
         heavy = !big && starts_heavy(a, c);
         risky = may_overflow(a, nen, g);
         a.grow[s] = 0;
+        if (a.counted == 2) a.cnt[s] = 0;   // walk-ranked: ordered_fill takes no count back
       }
     }
     const bool t = c > 0;
-    int32_t st, sr, ss2, sb, sh2, sd;
-    (void)block_excl_sum(t ? 1 : 0, sh[0], st);
-    const int32_t pr = block_excl_sum(c, sh[1], sr);
-    const int32_t ps = block_excl_sum(t && !big && !heavy ? 1 : 0, sh[2], ss2);
-    const int32_t pb = block_excl_sum(t && big ? 1 : 0, sh[3], sb);
-    const int32_t ph = block_excl_sum(t && heavy ? 1 : 0, sh[4], sh2);
-    const int32_t pd = block_excl_sum(t && risky ? 1 : 0, sh[5], sd);
+    int32_t pre[6], tot[6];
+    block_excl_sum6({t ? 1 : 0, c, t && !big && !heavy ? 1 : 0, t && big ? 1 : 0, t && heavy ? 1 : 0, t && risky ? 1 : 0},
+                    pre, tot, sh);
+    const int32_t pr = pre[1], ps = pre[2], pb = pre[3], ph = pre[4], pd = pre[5];
+    const int32_t sr = tot[1], ss2 = tot[2], sb = tot[3], sh2 = tot[4], sd = tot[5];
     if (t) {
       const int32_t beg = ar + pr;
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
@@ -1254,6 +1293,8 @@ static unsigned row_blocks(int64_t n, int wpb) {
 // blocks of 4 waves on 256 CUs) and loop over their rows: an empty 4,096-block launch
 // cost 4.7-4.9 µs per C3 step (profiles/r03/s26/c3_kernel_stats.csv).
 static unsigned few_row_blocks(int64_t n) { return std::min(row_blocks(n, 4), 768u); }
+int g_offsets_blocks = 1024;   // PSX_VARIANT_OFFSETS_GRID: ordered_offsets' grid cap
+int g_dry_blocks = 128;        // PSX_VARIANT_DRY_GRID: the capacity dry run's grid cap
 
 static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
   const int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
@@ -1272,7 +1313,9 @@ static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
     a.ntouched = a.nsplit + 3;
     a.desc = 1;
   }
-  const unsigned blocks = few_row_blocks(a.max_rows);
+  // (the rows are rare — keys outside [0, max_entries), images about to overflow — and the
+  // launch runs on every call of a split table: a small grid keeps the empty case cheap)
+  const unsigned blocks = std::min(few_row_blocks(a.max_rows), (unsigned)std::max(1, g_dry_blocks));
   if (a.max_entries <= 64)
     hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 1, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.max_entries <= 256)
@@ -1290,13 +1333,14 @@ static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
 
 // Stage 1 of the ordered path (before any table of the call is applied): record lists by
 // slot, every validation, and the capacity dry run of sorted/map tables.
-hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st) {
+hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, const int2 *wfill, hipStream_t st) {
   if (!a.counted) hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
   if (a.grow)
-    hipLaunchKernelGGL(ordered_offsets_kernel, dim3(std::min(row_blocks(a.max_rows, 256), 256u)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(ordered_offsets_kernel, dim3(std::min(row_blocks(a.max_rows, 256), (unsigned)std::max(1, g_offsets_blocks))),
+                       dim3(256), 0, st, a);
   else
     launch_exclusive_scan<int32_t>(a.cnt, a.max_rows, a.off, a.tsum, st);
-  hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
   if (a.kind != 0 && !a.dense_records && a.keyflag) {
 #define PSX_DRY(V) do { if (a.kind == 1) launch_dry<V, 1>(a, dtype, st); else launch_dry<V, 2>(a, dtype, st); } while (0)
     switch (dtype) {

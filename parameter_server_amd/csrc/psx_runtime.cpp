@@ -44,6 +44,7 @@ int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by t
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
 int g_walk_all_cus = 1;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
+int g_walk_rank = 1;     // PSX_VARIANT_WALK_RANK: walk-counted tables also get each record's list place (wfill)
 int g_call_events = 0;   // PSX_VARIANT_CALL_EVENTS: bit 0 an event pair per call for psx_ctx_stats (else one per
                          // sync interval), bit 1 the slot-free event on every call (else only when pipelining)
 int g_walk_shape = 4;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
@@ -87,7 +88,7 @@ hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st);
 hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t *sizes, int64_t n,
                            uint64_t clients, const uint64_t *subs, int check_only, hipStream_t st);
 hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
-hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, hipStream_t st);
+hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, const int2 *wfill, hipStream_t st);
 hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk);
 extern int g_ord_split;
 hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st);
@@ -223,6 +224,7 @@ struct psx_ctx {
   uint32_t *d_counters[2] = {nullptr, nullptr};
   uint32_t *d_ntouched[2] = {nullptr, nullptr};   // ordered path: touched-row count per table
   uint64_t *d_recoff[2] = {nullptr, nullptr};
+  int2 *d_wfill[2] = {nullptr, nullptr};          // walk-ranked calls: per record {slot, list place}
   size_t recoff_cap[2] = {0, 0};                  // entries
   void *d_walk[2] = {nullptr, nullptr};           // window-parallel decode workspace (psx_walk.hip)
   int walk_last_slot = 0;                         // the last walked call (psx_debug_walk_trace)
@@ -520,9 +522,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     HIP_TRY(c, hipStreamSynchronize(c->side));
     if (rec_need > c->recoff_cap[slot]) {
       if (c->d_recoff[slot]) hipFree(c->d_recoff[slot]);
+      if (c->d_wfill[slot]) hipFree(c->d_wfill[slot]);
       c->d_recoff[slot] = nullptr;
+      c->d_wfill[slot] = nullptr;
       c->recoff_cap[slot] = 0;
       HIP_TRY(c, hipMalloc(&c->d_recoff[slot], rec_need * sizeof(uint64_t)));
+      HIP_TRY(c, hipMalloc(&c->d_wfill[slot], rec_need * sizeof(int2)));
       c->recoff_cap[slot] = rec_need;
     }
     if (any_ordered && list_need > c->list_cap) {
@@ -669,6 +674,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       x.grow = t.d_grow + (int64_t)slot * t.cfg.max_rows;
       x.nsplit = t.d_nsplit + 5 * slot;
       x.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
+      x.wfill = psx::g_walk_rank ? c->d_wfill[slot] : nullptr;
       x.on = 1;
       wcount = true;
     }
@@ -772,9 +778,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       a.split = t.d_split;
       a.nsplit = t.d_nsplit + 5 * slot;
       a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
-      a.counted = wcount && c->h_wcount[slot][ti].on ? 1 : 0;
+      a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1) : 0;
     }
-    st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, c->stream); });
+    const int2 *wfill = a.counted == 2 ? c->d_wfill[slot] : nullptr;
+    st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, wfill, c->stream); });
     if (st) return st;
   }
   c->wcount_dirty[slot] = false;   // every walk-counted table's ordered_fill is enqueued
@@ -1210,6 +1217,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
     if (c->d_counters[k]) hipFree(c->d_counters[k]);
     if (c->d_ntouched[k]) hipFree(c->d_ntouched[k]);
     if (c->d_recoff[k]) hipFree(c->d_recoff[k]);
+    if (c->d_wfill[k]) hipFree(c->d_wfill[k]);
     if (c->d_walk[k]) hipFree(c->d_walk[k]);
     if (c->ev_ready[k]) hipEventDestroy(c->ev_ready[k]);
     if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
@@ -2740,6 +2748,8 @@ psx_status psx_timing_reset(psx_ctx *c) {
 namespace psx {
 extern int g_apply_variant;
 extern int g_ord_split;
+extern int g_offsets_blocks;
+extern int g_dry_blocks;
 }  // namespace psx
 
 static int *variant_slot(int32_t which) {
@@ -2756,6 +2766,9 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
     case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
     case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
+    case PSX_VARIANT_OFFSETS_GRID: return &psx::g_offsets_blocks;
+    case PSX_VARIANT_DRY_GRID: return &psx::g_dry_blocks;
+    case PSX_VARIANT_WALK_RANK: return &psx::g_walk_rank;
     default: return nullptr;
   }
 }

@@ -264,7 +264,8 @@ __device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
 
 // ordered_count for one record of a walk-counted split table (WalkCount): the record's row
 // id and pair count at p (a record the walk accepted: its header lies inside the message).
-__device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w, uint32_t *call_status) {
+__device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w, uint32_t *call_status,
+                                           uint64_t idx) {
   const int32_t rid = *reinterpret_cast<const int32_t *>(p);
   const int32_t n = *reinterpret_cast<const int32_t *>(p + 4);
   int64_t d = (int64_t)rid - w.row_offset;
@@ -275,10 +276,18 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
   }
   if (!ok || d >= w.max_rows) {
     atomicOr(call_status, kStRowRange);
+    if (w.wfill) w.wfill[idx] = int2{-1, 0};
     return;
   }
   atomicAdd(&w.grow[d], n);
-  atomicAdd(&w.cnt[d], 1);
+  if (w.wfill) {
+    // the count's returned value is the record's place in its slot's list (the apply sorts
+    // each list into message order, so any order of these atomics is as good)
+    const int32_t k = atomicAdd(&w.cnt[d], 1);
+    w.wfill[idx] = int2{(int32_t)d, k};
+  } else {
+    atomicAdd(&w.cnt[d], 1);
+  }
 }
 
 template <int T_, int WW_>
@@ -777,7 +786,7 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
       for (uint32_t r = (uint32_t)tid; r < nrec; r += kWalkThreads) {
         const uint64_t off = W0 + (uint64_t)recq[r] * 4;
         recoff[rk + r] = off;
-        if (counted && off + 8 <= size) walk_count(p + off, wc[t], call_status);
+        if (counted && off + 8 <= size) walk_count(p + off, wc[t], call_status, rk + r);
       }
     }
     if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memrealtime();

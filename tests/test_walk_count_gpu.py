@@ -2,7 +2,8 @@
 (PSX_VARIANT_WALK_COUNT, WalkCount in psx_device.hpp): on walked calls the walk adds each
 record to the call slot's cnt/grow as it writes the record's offset and the ordered prep
 launches no ordered_count.  Every form — walk-counted, ordered_count, and walk-counted with
-the decode pipelined beside the previous call's ordered work — must give the oracle's rows byte for byte
+the decode pipelined beside the previous call's ordered work — with and without the walk
+also placing each record in its slot's list (WalkCount.wfill) — must give the oracle's rows byte for byte
 (SortedVectorMapStore, sorted_vector_map_store.hpp:175-197,305-337) over several calls, and a
 call that names a row outside the shard must fail with nothing applied and leave the counts
 clean for the next call (the reference rejects such a row: server_table.hpp FindRow/CreateRow
@@ -25,6 +26,20 @@ PIPELINE_ALL = 2
 def _gpu(built_lib, oracle_lib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+
+
+WALK_RANK = 20
+
+
+@pytest.fixture(autouse=True, params=[1, 0], ids=["walk-ranked", "fill-counted"])
+def walk_rank(request, _gpu):
+    """Every test with the walk also giving each record its list place (ordered_fill without
+    atomics, PSX_VARIANT_WALK_RANK 1, the default) and without (ordered_fill takes the places
+    back from the counts)."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(WALK_RANK, request.param)
+    yield request.param
+    L.psx_debug_set_variant(WALK_RANK, old)
 
 
 def _batches(rng, rows, K, calls, per_batch=6_000, B=4):

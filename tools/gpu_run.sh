@@ -117,6 +117,7 @@ for db, ks in d.items():
               for f in $O/c2sep_* $O/c2buf_*; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["roofline"]["avg_launch_ms"], d["walked"]["value"])')"; done ;;
     c2only) run c2only 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras ;;
     c3) run c3 300 python -u bench.py --workload c3 --steps 20 --warmup 3 ;;
+    c3sweep) run c3sweep 300 python -u tools/walk_sweep.py --configs "${SWEEP:-4:1:4:0}" ;;
     c3idx) run c3idx 300 python -u bench.py --workload c3 --indexed --steps 20 --warmup 3 ;;
     c4) run c4 600 python -u bench.py --workload c4 --steps 3 --warmup 1 ;;
     c5) run c5 300 python -u bench.py --workload c5 --steps 10 --warmup 2 ;;

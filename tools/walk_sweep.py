@@ -31,8 +31,14 @@ def main():
     B = len(streams)
     bgs = list(range(100, 100 + B))
     dev = [torch.from_numpy(s).cuda() for s in streams]
-    cfgs = [tuple(int(x) for x in (c + ":0").split(":")[:4]) if c.count(":") == 2 else
-            tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
+    # config: shape:cus:levels[:call_events][/variant=value...] (other psx_debug.h selectors)
+    cfgs, extra = [], {}
+    for tok in args.configs.split(","):
+        head, *sets = tok.split("/")
+        c = tuple(int(x) for x in (head + ":0").split(":")[:4]) if head.count(":") == 2 else \
+            tuple(int(x) for x in head.split(":"))
+        c = c + tuple((int(k), int(v)) for k, v in (x.split("=") for x in sets))
+        cfgs.append(c)
     srvs, ver = [], []
     for _ in cfgs:
         srv = psa.Server(0, 1, bgs)
@@ -48,6 +54,8 @@ def main():
             L.psx_debug_set_variant(12, c[1])
             L.psx_debug_set_variant(15, c[2])
             L.psx_debug_set_variant(17, c[3])
+            for k, v in c[4:]:
+                L.psx_debug_set_variant(k, v)
             srv = srvs[i]
 
             def step():
@@ -71,7 +79,8 @@ def main():
     out = []
     for c in cfgs:
         v = sorted(x for x, _ in res[c])
-        out.append({"shape": c[0], "cus": c[1], "levels": c[2], "call_events": c[3], "best_Mups": round(v[-1], 1),
+        out.append({"shape": c[0], "cus": c[1], "levels": c[2], "call_events": c[3],
+                    "variants": {str(k): x for k, x in c[4:]}, "best_Mups": round(v[-1], 1),
                     "median_Mups": round(v[len(v) // 2], 1), "walked_calls": res[c][-1][1],
                     "us_per_step": round(nupd / v[len(v) // 2], 2)})
     print(json.dumps(out, indent=1))

@@ -4,7 +4,8 @@ DRAM-side bytes per C3 step that bench.py reports beside C3's algorithmic bytes.
 Per kernel: the mean of TCC_EA0_RDREQ_128B x 128 + TCC_EA0_RDREQ_64B x 64 read bytes and
 TCC_EA0_WRREQ_64B x 64 + (TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B) x 32 write bytes per dispatch
 (the request sizes MI355X_MICROARCH.md's HBM section prescribes), times its dispatches; the
-sum over psx kernels divided by the apply calls (finish_call dispatches, one per C3 step).
+sum over psx kernels divided by the apply calls (walk_head dispatches, one per walked C3 step;
+finish_call's when the calls were not walked — a folded finish has none).
 These are L2 -> fabric requests: Infinity-Cache hits are counted (the guide), so the figure
 is the memory-side traffic the step asks for, an upper bound on HBM bytes.
 
@@ -27,7 +28,7 @@ def main(root, out):
         for k, c, v, d in con.execute("select name, counter_name, counter_value, dispatch_id from pmc_events"):
             per[k][c][(f, d)] = per[k][c].get((f, d), 0.0) + float(v)
         con.close()
-    kernels, calls, total_r, total_w = {}, 0, 0.0, 0.0
+    kernels, calls, fin, total_r, total_w = {}, 0, 0, 0.0, 0.0
     for name, cs in per.items():
         if "psx" not in name[:120]:
             continue
@@ -41,10 +42,13 @@ def main(root, out):
         kernels[short] = {"dispatches": disp, "read_bytes": rd, "write_bytes": wr}
         total_r += rd
         total_w += wr
-        if "finish_call" in name:
+        if "walk_head" in name:
             calls += disp
+        elif "finish_call" in name:
+            fin += disp
+    calls = calls or fin   # one walk_head per walked call; finish_call when the calls were not walked
     if not calls:
-        raise SystemExit("no finish_call dispatches: not a C3 bench profile")
+        raise SystemExit("no walk_head or finish_call dispatches: not a C3 bench profile")
     res = {"kernel_signature": c3_kernel_signature(), "calls": calls,
            "read_bytes_per_step": total_r / calls, "write_bytes_per_step": total_w / calls,
            "bytes_per_step": (total_r + total_w) / calls, "kernels": kernels,

@@ -302,6 +302,46 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * per;
   const int64_t c1 = c0 + per < R ? c0 + per : R;
+  int4 *const desc = reinterpret_cast<int4 *>(a.split);
+  if (per <= (int64_t)blockDim.x) {
+    // one slot per thread (the usual grid): the slot's words loaded once, one scan gives
+    // both the block's totals (one atomic per counter) and each row's place
+    const int64_t s = c0 + threadIdx.x;
+    int32_t c = 0, nen = 0, g = 0;
+    if (s < c1) {
+      c = a.cnt[s];
+      nen = a.nent[s];
+      g = a.grow[s];
+    }
+    const bool t = c > 0;
+    const bool big = t && starts_big(a, nen, g);
+    const bool heavy = t && !big && starts_heavy(a, c);
+    const bool risky = t && may_overflow(a, nen, g);
+    int32_t pre[6], tot[6];
+    block_excl_sum6({t ? 1 : 0, c, t && !big && !heavy ? 1 : 0, big ? 1 : 0, heavy ? 1 : 0, risky ? 1 : 0}, pre, tot,
+                    sh);
+    if (threadIdx.x == 0) {
+      base[0] = tot[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot[0]) : 0;
+      base[1] = tot[1] ? atomicAdd(&a.tsum[0], tot[1]) : 0;
+      base[2] = tot[2] ? (int32_t)atomicAdd(&a.nsplit[0], (uint32_t)tot[2]) : 0;
+      base[3] = tot[3] ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tot[3]) : 0;
+      base[4] = tot[4] ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)tot[4]) : 0;
+      base[5] = tot[5] ? (int32_t)atomicAdd(&a.nsplit[3], (uint32_t)tot[5]) : 0;
+    }
+    __syncthreads();
+    if (t) {
+      a.grow[s] = 0;
+      if (a.counted == 2) a.cnt[s] = 0;   // walk-ranked: ordered_fill takes no count back
+      const int32_t beg = base[1] + pre[1];
+      const int4 d = int4{(int32_t)s, beg, beg + c, nen};
+      a.off[s] = beg;
+      if (risky) desc[2 * R + base[5] + pre[5]] = d;
+      if (big) desc[R + base[3] + pre[3]] = d;
+      else if (heavy) desc[R - 1 - (base[4] + pre[4])] = d;
+      else desc[base[2] + pre[2]] = d;
+    }
+    return;
+  }
   // pass 1: the block's totals, one atomic per counter
   int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0, nd = 0;
   for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
@@ -333,7 +373,6 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   // are distinct touched rows, so the two never meet.  The 1,024-entry region [R, 2R) holds
   // the big rows and, appended behind them by the 256-entry launch, the spilled rows (small
   // or heavy, each at most once): at most the touched count in all.
-  int4 *const desc = reinterpret_cast<int4 *>(a.split);
   int32_t ar = base[1], as = base[2], ab = base[3], ah = base[4], ad = base[5];
   for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
     const int64_t s = t0 + threadIdx.x;

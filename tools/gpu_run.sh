@@ -33,7 +33,7 @@ export TMPDIR=/tmp
 R=/tmp/gr_${TAG:-run}
 mkdir -p "$R"
 PMC_JSON=$O/pmc_dense_apply.json
-[ -f "$PMC_JSON" ] || PMC_JSON=profiles/r03/pmc_dense_apply.json
+[ -f "$PMC_JSON" ] || PMC_JSON=profiles/r04/pmc_dense_apply.json
 say() { echo "== $(date +%T) $*"; }
 run() {  # run NAME SECONDS CMD...: output to $O/NAME.log; on failure print its tail and stop
   local name=$1 secs=$2; shift 2

@@ -48,9 +48,10 @@ enum {
                                    context pipelines) */,
   PSX_VARIANT_OFFSETS_GRID = 18, /* ordered_offsets' grid cap (blocks of 256 slots; default 1,024) */
   PSX_VARIANT_DRY_GRID = 19,    /* the capacity dry run's grid cap (default 128) */
-  PSX_VARIANT_WALK_RANK = 20    /* 1 (default): walk-counted tables also get each record's place in
-                                   its slot's list from the walk (ordered_fill without atomics);
-                                   0: ordered_fill takes the places from the counts */
+  PSX_VARIANT_WALK_RANK = 20    /* 1 (default): split sorted/map tables get each record's place in
+                                   its slot's list from the count (the walk's or ordered_count's),
+                                   so ordered_fill needs no atomics; 0: ordered_fill takes the
+                                   places back from the counts */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

@@ -188,10 +188,11 @@ struct OrdArgs {
   const int32_t *heavy_end;  // heavy-first (spill bit 1): heavy row descriptors end here (the
   const uint32_t *nheavy;    // 256-entry list's region), listed backwards; the 256-entry
                              // launch takes them first
-  int32_t counted;           // split tables: the walk already counted this call's records
+  int32_t counted;           // split tables: 1 the walk already counted this call's records
                              // (WalkCount): ordered_count is not launched; 2: it also placed
-                             // each record in its slot's list (WalkCount.wfill), so
-                             // ordered_offsets zeroes the counts and ordered_fill needs no atomics
+                             // each record in its slot's list (WalkCount.wfill); 3: ordered_count
+                             // counts and places them.  Placed (>= 2): ordered_offsets zeroes
+                             // the counts and ordered_fill needs no atomics
   // finish_call folded into this apply launch (the call's last): fin_ring >= 0 is the call's
   // status ring slot, so call_status = status + 1 + fin_ring and the sticky word, the call's
   // log entry and the block counter follow from call_status (kCallRing layout); the last

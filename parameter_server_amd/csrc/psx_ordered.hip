@@ -111,7 +111,9 @@ __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
+// wfill (counted == 3, split tables): the count's returned value is also the record's place
+// in its slot's list, stored per record (its recoff index) for ordered_fill.
+__global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfill) {
   __shared__ RecSpace rs;
   if (a.grow && blockIdx.x == 0 && threadIdx.x < 5) {   // ordered_offsets' counters
     if (threadIdx.x < 4) a.nsplit[threadIdx.x] = 0;
@@ -139,6 +141,7 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
       s = o_slot(o_ld32(p), a);
       if (s < 0) {
         atomicOr(a.call_status, kStRowRange);
+        if (wfill) wfill[rs.first[b] + (r - rs.pre[b])] = int2{-1, 0};
       } else {
         if (!a.dense_records && a.kind == 0) {
           // sparse record into a dense row: every column must lie inside the row
@@ -151,7 +154,9 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
           if (cols_outside(p, a.max_entries)) atomicOr(a.keyflag, 1u);
         }
         if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
-        if (a.grow)   // split tables: ordered_offsets finds the touched rows from the counts
+        if (a.grow && wfill)   // split tables, ranked: the record's place comes back with the count
+          wfill[rs.first[b] + (r - rs.pre[b])] = int2{(int32_t)s, atomicAdd(&a.cnt[s], 1)};
+        else if (a.grow)   // split tables: ordered_offsets finds the touched rows from the counts
           atomicAdd(&a.cnt[s], 1);
         else
           first = atomicAdd(&a.cnt[s], 1) == 0;
@@ -172,7 +177,8 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a) {
   }
 }
 
-// wfill (walk-ranked split tables, counted == 2): each record's {slot, place} from the walk;
+// wfill (ranked split tables, counted >= 2): each record's {slot, place} from the walk or
+// ordered_count;
 // the list entry is written without an atomic and the counts were zeroed by ordered_offsets.
 __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a, const int2 *wfill) {
   __shared__ RecSpace rs;
@@ -195,7 +201,7 @@ __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a, const int2
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += G) {
       int b = 0;
       while (b + 1 < a.B && rs.pre[b + 1] <= r) ++b;
-      const int64_t idx = rs.first[b] + (r - rs.pre[b]);   // walk-counted tables are sparse
+      const int64_t idx = rs.first[b] + (r - rs.pre[b]);   // ranked tables are sparse
       const int2 sk = wfill[idx];
       const uint64_t off = a.recoff[idx];
       if (sk.x < 0) continue;
@@ -331,7 +337,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     __syncthreads();
     if (t) {
       a.grow[s] = 0;
-      if (a.counted == 2) a.cnt[s] = 0;   // walk-ranked: ordered_fill takes no count back
+      if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
       const int32_t beg = base[1] + pre[1];
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
       a.off[s] = beg;
@@ -387,7 +393,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
         heavy = !big && starts_heavy(a, c);
         risky = may_overflow(a, nen, g);
         a.grow[s] = 0;
-        if (a.counted == 2) a.cnt[s] = 0;   // walk-ranked: ordered_fill takes no count back
+        if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
       }
     }
     const bool t = c > 0;
@@ -1372,8 +1378,9 @@ static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
 
 // Stage 1 of the ordered path (before any table of the call is applied): record lists by
 // slot, every validation, and the capacity dry run of sorted/map tables.
-hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, const int2 *wfill, hipStream_t st) {
-  if (!a.counted) hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a);
+hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, int2 *wfill, hipStream_t st) {
+  if (a.counted == 0 || a.counted == 3)
+    hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a, a.counted == 3 ? wfill : nullptr);
   if (a.grow)
     hipLaunchKernelGGL(ordered_offsets_kernel, dim3(std::min(row_blocks(a.max_rows, 256), (unsigned)std::max(1, g_offsets_blocks))),
                        dim3(256), 0, st, a);

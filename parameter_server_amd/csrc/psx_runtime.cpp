@@ -44,7 +44,7 @@ int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by t
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
 int g_walk_all_cus = 1;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
-int g_walk_rank = 1;     // PSX_VARIANT_WALK_RANK: walk-counted tables also get each record's list place (wfill)
+int g_walk_rank = 1;     // PSX_VARIANT_WALK_RANK: split tables' counts also give each record's list place (wfill)
 int g_call_events = 0;   // PSX_VARIANT_CALL_EVENTS: bit 0 an event pair per call for psx_ctx_stats (else one per
                          // sync interval), bit 1 the slot-free event on every call (else only when pipelining)
 int g_walk_shape = 4;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
@@ -88,7 +88,7 @@ hipError_t launch_ada_apply(const AdaArgs &a, hipStream_t st);
 hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t *sizes, int64_t n,
                            uint64_t clients, const uint64_t *subs, int check_only, hipStream_t st);
 hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
-hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, const int2 *wfill, hipStream_t st);
+hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, int2 *wfill, hipStream_t st);
 hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk);
 extern int g_ord_split;
 hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st);
@@ -778,9 +778,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       a.split = t.d_split;
       a.nsplit = t.d_nsplit + 5 * slot;
       a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
-      a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1) : 0;
+      a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1)
+                  : (psx::g_walk_rank && !t.cfg.oplog_dense_serialized && c->d_wfill[slot] ? 3 : 0);
     }
-    const int2 *wfill = a.counted == 2 ? c->d_wfill[slot] : nullptr;
+    int2 *wfill = a.counted >= 2 ? c->d_wfill[slot] : nullptr;
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, wfill, c->stream); });
     if (st) return st;
   }

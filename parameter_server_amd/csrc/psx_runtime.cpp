@@ -993,12 +993,18 @@ psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
 
 psx_status sync_impl(psx_ctx *c) {
   HIP_TRY(c, hipSetDevice(c->device));
-  hipEvent_t stats_close = nullptr;
+  struct CloseGuard {   // the interval's closing event goes back to the pool on every path
+    psx_ctx *c;
+    hipEvent_t e;
+    ~CloseGuard() {
+      if (e) c->ev_pool.push_back(e);
+    }
+  } stats_close{c, nullptr};
   if (c->stats_open) {
-    stats_close = get_event(c);
-    if (stats_close && hipEventRecord(stats_close, c->stream) != hipSuccess) {
-      c->ev_pool.push_back(stats_close);
-      stats_close = nullptr;
+    stats_close.e = get_event(c);
+    if (stats_close.e && hipEventRecord(stats_close.e, c->stream) != hipSuccess) {
+      c->ev_pool.push_back(stats_close.e);
+      stats_close.e = nullptr;
     }
   }
   HIP_TRY(c, hipStreamSynchronize(c->side));
@@ -1007,12 +1013,11 @@ psx_status sync_impl(psx_ctx *c) {
   if (c->stats_open) {
     // the interval's device time: its first call's first stage to the last call's finish
     float ms = 0.f;
-    if (stats_close && hipEventElapsedTime(&ms, c->stats_open, stats_close) == hipSuccess) {
+    if (stats_close.e && hipEventElapsedTime(&ms, c->stats_open, stats_close.e) == hipSuccess) {
       c->stats.apply_sec += ms * 1e-3;
       c->stats.settled_calls += c->stats_open_calls;
     }
     c->ev_pool.push_back(c->stats_open);
-    if (stats_close) c->ev_pool.push_back(stats_close);
     c->stats_open = nullptr;
     c->stats_open_calls = 0;
   }

@@ -628,6 +628,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (spec_wpr && spec_wpr != w) walk = false;
     spec_wpr = w;
   }
+  if (spec_wpr > 3) walk = false;   // psx_walk.hip next_of's 32-bit link: values of at most 8 bytes
   uint64_t maxw = 0;
   const int walk_shape = psx::g_walk_shape;
   const uint64_t wbytes = psx::walk_window_bytes(walk_shape);

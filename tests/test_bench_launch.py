@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -21,9 +23,9 @@ def test_bench_gpus_2_launches_two_ranks():
     assert rec["n_gpus"] == 2 and rec["steps"] == 3
 
 
-def _selftest_exchange(extra, port):
+def _selftest_exchange(extra, port, world=2):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2",
                           "--warmup", "1", "--selftest-exchange", "--master-port", str(port)] + extra,
                          capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -32,15 +34,16 @@ def _selftest_exchange(extra, port):
     return json.loads(lines[0])
 
 
-def test_exchange_extra_orchestration_and_parity_over_gloo():
-    """The N > 1 exchange extras' code path (exchange_measure: chunked batches spanning both
-    shards, split by owner, all-to-all, in-order apply, then every owner's shard checked bit
-    for bit against the seeds) at world 2 over gloo, with the CPU stand-in of the device
-    split/apply."""
-    rec = _selftest_exchange([], 29535)
-    assert rec["n_gpus"] == 2 and rec["parity"] == "bit-exact"
+@pytest.mark.parametrize("world,port", [(2, 29535), (8, 29537)])
+def test_exchange_extra_orchestration_and_parity_over_gloo(world, port):
+    """The N > 1 exchange extras' code path (exchange_measure: chunked batches spanning every
+    shard, split by owner, all-to-all, in-order apply, then every owner's shard checked bit
+    for bit against the seeds) at world 2 and at the driver's largest, 8, over gloo, with the
+    CPU stand-in of the device split/apply."""
+    rec = _selftest_exchange([], port, world)
+    assert rec["n_gpus"] == world and rec["parity"] == "bit-exact"
     assert rec["chunks_per_step"] > 1
-    assert rec["config"]["shard_rows"] * 2 == 8192
+    assert rec["config"]["shard_rows"] * world == 4096 * world
 
 
 def test_exchange_parity_check_catches_a_reordered_apply():

@@ -315,12 +315,12 @@ def _selftest_device(world, port, extra=()):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world,port", [(2, 29611), (3, 29612)])
+@pytest.mark.parametrize("world,port", [(2, 29611), (3, 29612), (4, 29613)])
 def test_shard_exchange_multi_rank_on_one_gpu_bit_exact(world, port):
     """ShardExchange's N-rank routing with the real device split and apply: `world` ranks
     share cuda:0 and their sub-streams cross over gloo (bench.GlooExchange), each rank's own
     sub-stream applied from its send slot.  Every owner's shard must equal the in-order sum
-    recomputed from the seeds, bit for bit, after 3 steps of 14-21 chunks."""
+    recomputed from the seeds, bit for bit, after 3 steps of 14-28 chunks."""
     rec = _selftest_device(world, port)
     assert rec["n_gpus"] == world and rec["parity"] == "bit-exact", rec
     assert rec["chunks_per_step"] > 5

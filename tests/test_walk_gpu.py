@@ -333,3 +333,47 @@ def test_malformed_chain_same_error_nothing_applied(case):
         finally:
             L.psx_debug_set_variant(DECODE, old)
     assert errs[0] == errs[1]
+
+
+def test_composed_exits_publish_early_on_c3_messages(walk_levels):
+    """The composed exit maps must actually carry the chain (correct results alone would not
+    show it: round 4 found the forward map refusing a record whose count word is the window's
+    halo word, which silently sent most windows back to the one-by-one hand-off).  With the
+    walk trace on, at least 90% of the non-last windows of C3-shaped messages publish their
+    exit state from the composed map (trace word 6: tried, state, table, entry in range, map
+    and records left all set) — the ones that cannot are where a table boundary or the message
+    head breaks the span."""
+    if walk_levels == 0:
+        pytest.skip("composition off")
+    import ctypes
+    L = _abi.load()
+    rng = np.random.RandomState(23)
+    rows, K = 20_000, 1024
+    p = 1.0 / np.arange(1, rows + 1)
+    p /= p.sum()
+    streams = []
+    for b in range(8):
+        ids = rng.choice(rows, size=10_000, replace=False, p=p)
+        streams.append(wire.sparse_stream_np(3, 4, _rows(rng, ids, K, I32, rng.randint(1, 33, size=ids.size))))
+    old = L.psx_debug_set_variant(11, 1)   # PSX_DEBUG_WALK_TRACE
+    try:
+        st = _Setup([(3, SORTED_MAP, I32, K, False, rows)], range(100, 108))
+        st.apply(streams, 0, oracle=False)
+        buf = np.zeros(10 * 8192, np.uint64)
+        items = L.psx_debug_walk_trace(st.srv.handle, buf.ctypes.data_as(ctypes.c_void_p), 8192)
+        st.close()
+    finally:
+        L.psx_debug_set_variant(11, old)
+    assert items > 0
+    tr = buf[: 10 * items].reshape(items, 10)
+    B = 8
+    nwin = items // B
+    tried = early = 0
+    for b in range(B):
+        used = [j for j in range(nwin) if tr[j * B + b, 0] > 0]
+        for j in used[:-1]:   # the message's last window publishes nothing
+            code = int(tr[j * B + b, 6]) & 0xFF
+            tried += 1
+            early += code == 0x3F
+    assert tried > 8 * 10
+    assert early >= 0.9 * tried, f"{early} of {tried} windows published from the composed map"

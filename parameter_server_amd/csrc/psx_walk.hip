@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
         uint16_t *dst = (lv & 1) ? sb : sa;
         const uint32_t *srcw = reinterpret_cast<const uint32_t *>(src);
         uint32_t *dstw = reinterpret_cast<uint32_t *>(dst);
-#pragma unroll 4
+#pragma unroll
         for (int k = 0; k < PER / 2; ++k) {
           const uint32_t i = (uint32_t)tid + (uint32_t)k * kWalkThreads;   // words 2i, 2i + 1
           uint32_t a0, a1;

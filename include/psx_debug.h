@@ -40,8 +40,10 @@ enum {
   PSX_VARIANT_WALK_LEVELS = 15  /* the walk's composed exit-map levels: window j's exit state follows
                                    from the state 2^levels windows back (default 4; 0: window by
                                    window) */,
-  PSX_VARIANT_WALK_SHAPE = 16   /* the walk's block x window: 0 1,024 threads x 96 KiB, 1 1,024 x
-                                   32 KiB, 2 512 x 24 KiB, 3 256 x 16 KiB, 4 512 x 48 KiB (default) */,
+  PSX_VARIANT_WALK_SHAPE = 16   /* the walk's block x window (x entry candidates, = threads unless
+                                   named): 0 1,024 threads x 96 KiB, 1 1,024 x 32 KiB, 2 512 x 24 KiB,
+                                   3 256 x 16 KiB, 4 512 x 48 KiB (default), 5 512 x 48 KiB x 256,
+                                   6 512 x 48 KiB x 128 */,
   PSX_VARIANT_CALL_EVENTS = 17  /* events enqueued per call: bit 0 an event pair per call for
                                    psx_ctx_stats (default 0: one pair per psx_sync interval), bit 1
                                    the slot-free event on every call (default 0: only while the

@@ -36,9 +36,10 @@ namespace psx {
 // speculative work is LDS-bound inside its CU, so smaller windows spread one call's work
 // over more CUs (several blocks per CU) at the price of more window-to-window hand-offs.
 struct WalkShape {
-  int threads, words;
+  int threads, words, cand;   // cand: entry candidates (exit maps), at most threads
 };
-constexpr WalkShape kWalkShapes[] = {{1024, 24576}, {1024, 8192}, {512, 6144}, {256, 4096}, {512, 12288}};
+constexpr WalkShape kWalkShapes[] = {{1024, 24576, 1024}, {1024, 8192, 1024}, {512, 6144, 512}, {256, 4096, 256},
+                                     {512, 12288, 512},   {512, 12288, 256},  {512, 12288, 128}};
 constexpr int kNumWalkShapes = (int)(sizeof(kWalkShapes) / sizeof(kWalkShapes[0]));
 uint64_t walk_window_bytes(int shape) {
   return (uint64_t)kWalkShapes[shape >= 0 && shape < kNumWalkShapes ? shape : 0].words * 4;
@@ -290,14 +291,15 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
   }
 }
 
-template <int T_, int WW_>
+template <int T_, int WW_, int C_>
 __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Seg *segs, uint64_t *recoff,
                                                             uint32_t *call_status, WalkCtl *ctl, const WalkHead *head,
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace,
                                                             const WalkCount *wc, unsigned long long *maps_p,
                                                             int levels) {
-  constexpr int kWalkThreads = T_, kWW = WW_, kCand = T_;
+  constexpr int kWalkThreads = T_, kWW = WW_, kCand = C_;
+  static_assert(C_ <= T_ && C_ % 64 == 0, "candidates");
   constexpr uint64_t kWBytes = (uint64_t)WW_ * 4;
   static_assert(kWW % kWalkThreads == 0 && ((kWW / kWalkThreads) % 8 == 0 || (kWW / kWalkThreads) % 12 == 0) && kWW < 0xFFF0 && kCand <= kCandW,
                 "walk shape");
@@ -443,7 +445,7 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
     uint32_t *pm2 = pm + kCand;
     constexpr uint32_t kNoMap = 0xFFFFFFFFu;
     if (levels > 0) {
-      {
+      if ((uint32_t)tid < (uint32_t)kCand) {
         const uint32_t q = (uint32_t)tid;
         uint32_t f = kNoMap;
         if (!last) {
@@ -466,8 +468,9 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
       for (int l = 1; l <= levels; ++l) {
         const uint32_t d = 1u << (l - 1);
         const uint32_t q = (uint32_t)tid;
-        uint32_t v = pm[q];
-        if (j >= d) {
+        const bool cq = q < (uint32_t)kCand;   // (the block's other threads only keep the barriers)
+        uint32_t v = cq ? pm[q] : kNoMap;
+        if (cq && j >= d) {
           // the partner's P_{l-1} covers the windows just before this one's P_{l-1}
           const gu64 *g = maps + ((uint64_t)(tk - d * (uint32_t)B) * levels + (l - 1)) * kCand + q;
           uint64_t x = 0;
@@ -488,12 +491,14 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
             }
           }
         }
-        pm2[q] = v;
+        if (cq) pm2[q] = v;
         __syncthreads();
-        pm[q] = v;
-        if (l < levels)
-          __hip_atomic_store(maps + ((uint64_t)tk * levels + l) * kCand + q, ((uint64_t)epoch << 32) | v,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cq) {
+          pm[q] = v;
+          if (l < levels)
+            __hip_atomic_store(maps + ((uint64_t)tk * levels + l) * kCand + q, ((uint64_t)epoch << 32) | v,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         __syncthreads();
       }
     }
@@ -816,7 +821,7 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
       levels > 0 ? reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ws) + walk_maps_offset(items))
                  : nullptr;
 #define PSX_WALK_LAUNCH(S)                                                                                    \
-  hipLaunchKernelGGL((walk_kernel<kWalkShapes[S].threads, kWalkShapes[S].words>), dim3(blocks),                    \
+  hipLaunchKernelGGL((walk_kernel<kWalkShapes[S].threads, kWalkShapes[S].words, kWalkShapes[S].cand>), dim3(blocks), \
                      dim3(kWalkShapes[S].threads), 0, st, ss, dir, segs, recoff, call_status, ctl, head, gran, spec_wpr, \
                      epoch, trace, wc, maps, levels)
   switch (shape) {
@@ -824,6 +829,8 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
     case 2: PSX_WALK_LAUNCH(2); break;
     case 3: PSX_WALK_LAUNCH(3); break;
     case 4: PSX_WALK_LAUNCH(4); break;
+    case 5: PSX_WALK_LAUNCH(5); break;
+    case 6: PSX_WALK_LAUNCH(6); break;
     default: PSX_WALK_LAUNCH(0); break;
   }
 #undef PSX_WALK_LAUNCH

@@ -16,7 +16,7 @@ from oracle.oracle import OracleServer, DENSE, SORTED_MAP, MAP, F32, F64, I32, I
 pytestmark = pytest.mark.gpu
 DECODE, WALK_CALLS = 7, 8
 # psx_walk.hip kWalkShapes: the walk's window grid from byte 0 of a message, per shape
-WINDOW_BYTES = {0: 98304, 1: 32768, 2: 24576, 3: 16384, 4: 49152}
+WINDOW_BYTES = {0: 98304, 1: 32768, 2: 24576, 3: 16384, 4: 49152, 5: 49152, 6: 49152}
 
 
 def _window():
@@ -36,9 +36,10 @@ WALK_SHAPE = 16
 WALK_CUS = 12
 
 
-@pytest.fixture(autouse=True, params=[(4, 0, 0), (1, 0, 0), (0, 0, 0), (4, 3, 4), (0, 2, 4), (2, 1, 4), (3, 4, 4), (4, 4, 1)],
+@pytest.fixture(autouse=True, params=[(4, 0, 0), (1, 0, 0), (0, 0, 0), (4, 3, 4), (0, 2, 4), (2, 1, 4), (3, 4, 4), (4, 4, 1),
+                                      (4, 6, 1)],
                 ids=["levels4", "levels1", "levels0", "levels4-256x16K", "levels0-512x24K", "levels2-1024x32K",
-                     "levels3-512x48K", "levels4-512x48K-default"])
+                     "levels3-512x48K", "levels4-512x48K-default", "levels4-512x48Kx128"])
 def walk_levels(request, _gpu):
     """Every test with the walk's composed exit maps at 4 levels (a window's exit state from the
     state 16 windows back), at 1 level (pairs) and off (window by window), on the 96 KiB

@@ -32,7 +32,7 @@ def main():
     bgs = list(range(100, 100 + B))
     dev = [torch.from_numpy(s).cuda() for s in streams]
     # config: shape:cus:levels[:call_events][/variant=value...] (other psx_debug.h selectors)
-    cfgs, extra = [], {}
+    cfgs = []
     for tok in args.configs.split(","):
         head, *sets = tok.split("/")
         c = tuple(int(x) for x in (head + ":0").split(":")[:4]) if head.count(":") == 2 else \

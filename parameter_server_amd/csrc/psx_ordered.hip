@@ -49,6 +49,11 @@ __device__ __forceinline__ bool o_gate(const OrdArgs &a) {
   return true;
 }
 
+__device__ __forceinline__ uint64_t shfl64_up(uint64_t x, int o) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, o, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), o, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Flattened record space r in [0, pre[B]) in (message, position) order.
 struct RecSpace {
   int64_t pre[kMaxFused + 1];
@@ -56,22 +61,32 @@ struct RecSpace {
   int32_t sparse[kMaxFused];
 };
 
+// Run by the block's first wave: lane b reads message b's segment (the B loads in flight
+// together), a wave prefix of the record counts places them.
 __device__ void build_space(const OrdArgs &a, RecSpace &rs) {
-  int64_t acc = 0;
-  for (int b = 0; b < kMaxFused; ++b) {
-    rs.pre[b] = acc;
-    rs.first[b] = 0;
-    rs.sparse[b] = 0;
-    if (b < a.B) {
-      const Seg sg = a.segs[b * kMaxTables + a.t];
-      if (sg.rec0 >= 0) {
-        acc += sg.num_rows;
-        rs.first[b] = sg.rec0;
-        rs.sparse[b] = sg.sparse;
-      }
+  const int lane = threadIdx.x & 63;
+  int64_t nr = 0, first = 0;
+  int32_t sp = 0;
+  if (lane < kMaxFused && lane < a.B) {
+    const Seg sg = a.segs[lane * kMaxTables + a.t];
+    if (sg.rec0 >= 0) {
+      nr = sg.num_rows;
+      first = sg.rec0;
+      sp = sg.sparse;
     }
   }
-  rs.pre[kMaxFused] = acc;
+  int64_t incl = nr;
+#pragma unroll
+  for (int o = 1; o < kMaxFused; o <<= 1) {
+    const int64_t y = (int64_t)shfl64_up((uint64_t)incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane < kMaxFused) {
+    rs.pre[lane] = incl - nr;
+    rs.first[lane] = first;
+    rs.sparse[lane] = sp;
+  }
+  if (lane == kMaxFused - 1) rs.pre[kMaxFused] = incl;
 }
 
 // Locate record r: message b and the byte offset of its row id.
@@ -121,7 +136,7 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfi
   }
   // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
   if (!o_gate(a)) return;
-  if (threadIdx.x == 0) build_space(a, rs);
+  if (threadIdx.x < 64) build_space(a, rs);
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
@@ -182,7 +197,7 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfi
 // the list entry is written without an atomic and the counts were zeroed by ordered_offsets.
 __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a, const int2 *wfill) {
   __shared__ RecSpace rs;
-  if (threadIdx.x == 0) build_space(a, rs);
+  if (threadIdx.x < 64) build_space(a, rs);
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;

@@ -43,10 +43,8 @@ __device__ __forceinline__ int64_t o_slot(int32_t rid, const OrdArgs &a) {
 }
 
 __device__ __forceinline__ bool o_gate(const OrdArgs &a) {
-  const uint32_t st = *a.call_status;
-  if (st & (kStFatal | kStDuplicateRow)) return false;
-  if (!a.force && (*a.sticky & kStDuplicateRow)) return false;
-  return true;
+  const uint32_t st = *a.call_status, sk = *a.sticky;   // both words in flight at once
+  return !(st & (kStFatal | kStDuplicateRow)) && (a.force || !(sk & kStDuplicateRow));
 }
 
 __device__ __forceinline__ uint64_t shfl64_up(uint64_t x, int o) {
@@ -197,11 +195,12 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfi
 // the list entry is written without an atomic and the counts were zeroed by ordered_offsets.
 __global__ void __launch_bounds__(256) ordered_fill_kernel(OrdArgs a, const int2 *wfill) {
   __shared__ RecSpace rs;
+  const bool gate = o_gate(a);   // (its words in flight beside the record space's)
   if (threadIdx.x < 64) build_space(a, rs);
   __syncthreads();
   const int64_t total = rs.pre[kMaxFused];
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
-  if (!o_gate(a)) {
+  if (!gate) {
     // A failed call: ordered_count may have counted some records before a block of it set
     // a fatal bit (and blocks that started after that counted none), and ordered_offsets
     // skipped.  Restore the invariant (cnt and grow zero between calls) over every slot;
@@ -318,15 +317,15 @@ __device__ __forceinline__ bool may_overflow(const OrdArgs &a, int32_t nen, int3
 __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   __shared__ int32_t sh[6][4];
   __shared__ int32_t base[6];   // touched, records, 256-entry list, 1,024-entry list, heavy rows, dry run
-  if (!o_gate(a)) return;
   const int64_t R = a.max_rows;
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * per;
   const int64_t c1 = c0 + per < R ? c0 + per : R;
   int4 *const desc = reinterpret_cast<int4 *>(a.split);
   if (per <= (int64_t)blockDim.x) {
-    // one slot per thread (the usual grid): the slot's words loaded once, one scan gives
-    // both the block's totals (one atomic per counter) and each row's place
+    // one slot per thread (the usual grid): the slot's words loaded once (beside the gate's
+    // words), one scan gives both the block's totals (one atomic per counter) and each
+    // row's place
     const int64_t s = c0 + threadIdx.x;
     int32_t c = 0, nen = 0, g = 0;
     if (s < c1) {
@@ -334,6 +333,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       nen = a.nent[s];
       g = a.grow[s];
     }
+    if (!o_gate(a)) return;
     const bool t = c > 0;
     const bool big = t && starts_big(a, nen, g);
     const bool heavy = t && !big && starts_heavy(a, c);
@@ -363,6 +363,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     }
     return;
   }
+  if (!o_gate(a)) return;
   // pass 1: the block's totals, one atomic per counter
   int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0, nd = 0;
   for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
@@ -903,10 +904,15 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
-  const bool go = o_gate(a) && (!DRY || a.grow || *a.keyflag);
+  // the gate's words and the launch's row counts read at once (not one after another)
+  const uint32_t st0 = *a.call_status, sk0 = *a.sticky;
+  const uint32_t kf0 = DRY && a.keyflag ? *a.keyflag : 0u;
+  const uint32_t nt0 = *a.ntouched, nh0 = a.nheavy ? *a.nheavy : 0u;
+  const bool go = !(st0 & (kStFatal | kStDuplicateRow)) && (a.force || !(sk0 & kStDuplicateRow)) &&
+                  (!DRY || a.grow || kf0);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows); the
   // row count is final when the launch starts (the folded finish counts the blocks below it)
-  const int64_t launch_rows = (int64_t)*a.ntouched + (a.nheavy ? (int64_t)*a.nheavy : 0);
+  const int64_t launch_rows = (int64_t)nt0 + (int64_t)nh0;
   if (!go || (int64_t)blockIdx.x * 4 >= launch_rows) goto done;
   {
 #pragma unroll

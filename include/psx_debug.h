@@ -53,7 +53,11 @@ enum {
   PSX_VARIANT_WALK_RANK = 20    /* 1 (default): split sorted/map tables get each record's place in
                                    its slot's list from the count (the walk's or ordered_count's),
                                    so ordered_fill needs no atomics; 0: ordered_fill takes the
-                                   places back from the counts */
+                                   places back from the counts */,
+  PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from
+                                   its composed maps by one record; the cross-check after the
+                                   window's resolve must fail the call (PSX_ERR_DEVICE, nothing
+                                   applied) */
 };
 
 /* Returns the previous variant, or -1 for an unknown selector. */

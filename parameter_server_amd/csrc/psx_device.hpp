@@ -158,6 +158,7 @@ struct OrdArgs {
   int32_t *off;
   int32_t *tsum;
   uint64_t *list;         // records grouped by slot: (message << 56) | byte offset of the row id
+  uint64_t *list_tmp;     // the list's mirror region: scratch of the long-list sort (> 64 records)
   int32_t *touched;       // slots with >= 1 record this call (unordered)
   uint32_t *ntouched;     // its length (zeroed by decode_streams)
   void *dense;

@@ -116,12 +116,13 @@ psx_status psx_comm_create(const void *id, int32_t nranks, int32_t rank, int32_t
 psx_status psx_comm_destroy(psx_comm *c) {
   if (!c) return PSX_ERR_INVALID_ARG;
   hipSetDevice(c->device);
+  // an async size exchange may still be queued: let every slot's work finish before the
+  // communicator it runs on goes away
+  for (hipEvent_t &e : c->ev)
+    if (e) hipEventSynchronize(e);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t &e : c->ev)
-    if (e) {
-      hipEventSynchronize(e);
-      hipEventDestroy(e);
-    }
+    if (e) hipEventDestroy(e);
   if (c->d_sizes) hipFree(c->d_sizes);
   if (c->h_send) hipHostFree(c->h_send);
   delete c;

@@ -515,6 +515,82 @@ __device__ __forceinline__ uint64_t wave_rank_sort(uint64_t r, int L, int lane, 
   return out;
 }
 
+// A wave's global stores visible to its own later loads (other lanes' addresses included).
+__device__ __forceinline__ void wave_sync_global() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Sort the record list of one slot with L > 64 entries (distinct) ascending, in place:
+// O(L log^2 L / 64) loads per lane, never O(L^2).  A row named by many records of one call
+// (a row repeated inside messages: legal input no reference packer emits, or a corrupted
+// message) used to take lane 0's insertion sort over the list in global memory, which ran
+// for minutes at 500K records.  Runs of 64 are rank-sorted in registers, then bottom-up
+// merge passes place every entry at (its index in its run) + (the entries of the partner
+// run below it), found by a branch-free binary search; kG searches per lane are in flight
+// together.  tmp: scratch of L entries (the list's mirror region).
+__device__ __forceinline__ void wave_sort_long(uint64_t *lst, uint64_t *tmp, int32_t L, int lane, uint64_t *scratch) {
+  for (int32_t c0 = 0; c0 < L; c0 += 64) {
+    const int32_t n = L - c0 < 64 ? L - c0 : 64;
+    uint64_t x = lane < n ? lst[c0 + lane] : ~0ull;
+    x = wave_rank_sort(x, n, lane, scratch);
+    if (lane < n) lst[c0 + lane] = x;
+  }
+  wave_sync_global();
+  constexpr int kG = 4;
+  uint64_t *src = lst, *dst = tmp;
+  for (int32_t w = 64; w < L; w <<= 1) {
+    int steps = 0;
+    while ((1 << steps) <= w) ++steps;   // lower_bound over <= w entries: <= steps halvings
+    for (int32_t i0 = 0; i0 < L; i0 += 64 * kG) {
+      uint64_t x[kG];
+      int32_t base[kG], len[kG], at[kG];
+#pragma unroll
+      for (int g = 0; g < kG; ++g) {
+        const int32_t i = i0 + g * 64 + lane;
+        const int32_t ii = i < L ? i : L - 1;
+        const int32_t lo = ii / (2 * w) * (2 * w);
+        const int32_t mid = lo + w < L ? lo + w : L;
+        const int32_t hi = lo + 2 * w < L ? lo + 2 * w : L;
+        const bool inA = ii < mid;
+        x[g] = src[ii];
+        base[g] = inA ? mid : lo;                 // the partner run [base, base + len)
+        len[g] = inA ? hi - mid : mid - lo;
+        at[g] = lo + (inA ? ii - lo : ii - mid);  // + the partner entries below x
+        if (i >= L) len[g] = -1;                  // (no store)
+      }
+      int32_t b0[kG];
+#pragma unroll
+      for (int g = 0; g < kG; ++g) b0[g] = base[g];
+      for (int st = 0; st < steps; ++st) {
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+          if (len[g] > 0) {
+            const int32_t half = len[g] >> 1;
+            if (src[base[g] + half] < x[g]) {
+              base[g] += half + 1;
+              len[g] -= half + 1;
+            } else {
+              len[g] = half;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < kG; ++g)
+        if (len[g] >= 0) dst[at[g] + (base[g] - b0[g])] = x[g];
+    }
+    wave_sync_global();
+    uint64_t *t = src;
+    src = dst;
+    dst = t;
+  }
+  if (src != lst) {
+    for (int32_t i = lane; i < L; i += 64) lst[i] = src[i];
+    wave_sync_global();
+  }
+}
+
 // NSSumImpCalc::ApplyBatchIncGetImportance (ns_sum_imp_calc.hpp:57-77): sum of |u_i|
 // over a sparse record's values, lane-parallel then a wave butterfly.
 template <typename V>
@@ -587,17 +663,8 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
       uint64_t mine = 0;
       if (L <= 64) {
         mine = wave_rank_sort(lane < L ? lst[lane] : ~0ull, L, lane, sort_scratch[wib]);
-      } else if (lane == 0) {
-        for (int32_t i = 1; i < L; ++i) {   // rare: > 64 records for one row in one call
-          const uint64_t x = lst[i];
-          int32_t j = i - 1;
-          while (j >= 0 && lst[j] > x) { lst[j + 1] = lst[j]; --j; }
-          lst[j + 1] = x;
-        }
-      }
-      if (L > 64) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+      } else {   // rare: > 64 records for one row in one call
+        wave_sort_long(lst, a.list_tmp + beg, L, lane, sort_scratch[wib]);
       }
 
       // stage the row
@@ -612,6 +679,41 @@ __global__ void __launch_bounds__(256) ordered_apply_kernel(OrdArgs a, int wpb) 
       uint8_t *drow = reinterpret_cast<uint8_t *>(a.dense) + slot * a.row_cap * (int64_t)sizeof(V);
       double impt = a.imp ? a.imp[slot] : 0.0;
 
+      if (a.dense_records && !a.imp) {
+        // duplicate-row replay of dense records: the row in registers, kCh elements a lane
+        // per pass, every record added in message order (records in flight together; the
+        // row is loaded and stored once a pass, not once a record)
+        constexpr int kCh = 8;
+        for (int64_t e0 = 0; e0 < a.cap; e0 += 64 * kCh) {
+          V x[kCh];
+#pragma unroll
+          for (int k = 0; k < kCh; ++k) {
+            const int64_t e = e0 + k * 64 + lane;
+            x[k] = e < a.cap ? ldv<V>(drow + e * sizeof(V)) : V(0);
+          }
+          for (int32_t q0 = 0; q0 < L; q0 += 64) {
+            const uint64_t blk = L <= 64 ? mine : (q0 + lane < L ? lst[q0 + lane] : 0ull);
+            const int32_t m = L - q0 < 64 ? L - q0 : 64;
+            for (int32_t qq = 0; qq < m; ++qq) {
+              const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(blk >> 32), qq) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)blk, qq);
+              const uint8_t *body = rec_ptr(a, r) + 4;
+#pragma unroll
+              for (int k = 0; k < kCh; ++k) {
+                const int64_t e = e0 + k * 64 + lane;
+                if (e < a.cap) x[k] = OV<V>::add(x[k], rec_val<V>(body, e, a.rec_f16));
+              }
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < kCh; ++k) {
+            const int64_t e = e0 + k * 64 + lane;
+            if (e < a.cap) stv<V>(drow + e * sizeof(V), x[k]);
+          }
+        }
+        if (a.ver && lane == 0) a.ver[slot] += (uint64_t)L;   // VersionServerRow: +1 per record
+        continue;
+      }
       bool over = false;   // DRY: this row would exceed max_entries
       for (int32_t q = 0; q < L && !over; ++q) {
         const uint64_t r = L <= 64 ? shfl64(mine, q) : lst[q];
@@ -967,17 +1069,8 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       uint64_t mine = 0;
       if (L <= 64) {
         mine = wave_rank_sort(lane < L ? lst[lane] : ~0ull, L, lane, sort_scratch[wib]);
-      } else {
-        if (lane == 0) {
-          for (int32_t i = 1; i < L; ++i) {
-            const uint64_t x = lst[i];
-            int32_t j = i - 1;
-            while (j >= 0 && lst[j] > x) { lst[j + 1] = lst[j]; --j; }
-            lst[j + 1] = x;
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+      } else {   // rare: > 64 records for one row in one call
+        wave_sort_long(lst, a.list_tmp + beg, L, lane, sort_scratch[wib]);
       }
       if constexpr (DRY) {
         int32_t grow = 0;

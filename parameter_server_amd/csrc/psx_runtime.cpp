@@ -42,6 +42,7 @@ int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
+int g_walk_skew = 0;    // PSX_DEBUG_WALK_SKEW: skew early-published walk states (tests the cross-check)
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
 int g_walk_all_cus = 1;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
 int g_walk_rank = 1;     // PSX_VARIANT_WALK_RANK: split tables' counts also give each record's list place (wfill)
@@ -262,7 +263,8 @@ struct psx_ctx {
   size_t staging_cap = 0;
   void *d_split_fixed = nullptr, *d_split_recoff = nullptr, *d_split_scratch = nullptr;   // psx_split_stream
   size_t split_fixed_cap = 0, split_recoff_cap = 0, split_scratch_cap = 0;
-  uint64_t *d_list = nullptr;            // ordered path: record lists ((message << 56) | offset)
+  uint64_t *d_list = nullptr;            // ordered path: record lists ((message << 56) | offset),
+                                         // list_cap entries, then as many of sort scratch
   size_t list_cap = 0;
   std::vector<PendingCall> pending;      // calls since the last psx_sync (duplicate-row replay)
   int64_t call_seq = 0;
@@ -534,7 +536,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       if (c->d_list) hipFree(c->d_list);
       c->d_list = nullptr;
       c->list_cap = 0;
-      HIP_TRY(c, hipMalloc(&c->d_list, list_need * sizeof(uint64_t)));
+      // the lists, then their mirror: the long-list sort's scratch (psx_ordered.hip
+      // wave_sort_long, rows with > 64 records in one call)
+      HIP_TRY(c, hipMalloc(&c->d_list, 2 * list_need * sizeof(uint64_t)));
       c->list_cap = list_need;
     }
   }
@@ -701,7 +705,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
                                   c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
                                   c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
-                                  wcount ? c->d_wcount[slot] : nullptr, items, walk_levels, walk_shape, prep);
+                                  wcount ? c->d_wcount[slot] : nullptr, items,
+                                  walk_levels | (psx::g_walk_skew && walk_levels > 0 ? 0x100 : 0), walk_shape, prep);
         return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
       },
       prep);
@@ -761,7 +766,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.cnt = t.d_cnt + (int64_t)slot * t.cfg.max_rows;
     a.off = t.d_off;
     a.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
-    a.list = c->d_list + list_region * ord_k++;
+    a.list = c->d_list + list_region * ord_k;
+    a.list_tmp = c->d_list + c->list_cap + list_region * ord_k;
+    ++ord_k;
     a.touched = t.d_touched;
     a.ntouched = c->d_ntouched[slot] + ti;
     a.dense = t.d_data;
@@ -973,7 +980,8 @@ psx_status sticky_error(psx_ctx *c, uint32_t sticky) {
     return fail(c, PSX_ERR_STATE, "AdaRevision: a record names a (row, version) without a snapshot");
   if (sticky & psx::kStCapacity) return fail(c, PSX_ERR_CAPACITY, "row capacity exceeded (column >= row_capacity or sorted/map row over max_entries)");
   if (sticky & psx::kStWalkBound)
-    return fail(c, PSX_ERR_DEVICE, "window-parallel decode: a walker state outside its message (internal error; "
+    return fail(c, PSX_ERR_DEVICE, "window-parallel decode: a walker state outside its message, or an exit state "
+                                   "published early that the window's resolve disagrees with (internal error; "
                                    "nothing applied)");
   if (sticky & psx::kStWalkLost) {
     char m[256];
@@ -2734,7 +2742,11 @@ psx_status psx_ctx_stats(psx_ctx *c, psx_apply_stats *out, int32_t reset) {
   if (out) *out = c->stats;
   if (reset) {
     c->stats = psx_apply_stats{};
-    c->stats_open_calls = 0;   // the open interval's earlier calls went out with the reset
+    // the open interval's calls went out with the reset: restart it, so the next sync adds
+    // only the device time of calls made after the reset
+    if (c->stats_open) c->ev_pool.push_back(c->stats_open);
+    c->stats_open = nullptr;
+    c->stats_open_calls = 0;
   }
   return PSX_OK;
 }
@@ -2771,6 +2783,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_COUNT: return &psx::g_walk_count;
     case PSX_VARIANT_FOLD_FINISH: return &psx::g_fold_finish;
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
+    case PSX_DEBUG_WALK_SKEW: return &psx::g_walk_skew;
     case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
     case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
     case PSX_VARIANT_OFFSETS_GRID: return &psx::g_offsets_blocks;

@@ -297,7 +297,12 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
                                                             unsigned long long *gran_p, uint32_t spec_wpr,
                                                             uint32_t epoch, unsigned long long *trace,
                                                             const WalkCount *wc, unsigned long long *maps_p,
-                                                            int levels) {
+                                                            int levels_arg) {
+  // levels_arg: the composed exit-map levels (low byte); bit 8 (PSX_DEBUG_WALK_SKEW, tests
+  // only) skews every early-published exit state by one record, which the cross-check
+  // after the resolve must catch
+  const int levels = levels_arg & 0xff;
+  const bool skew = (levels_arg >> 8) & 1;
   constexpr int kWalkThreads = T_, kWW = WW_, kCand = C_;
   static_assert(C_ <= T_ && C_ % 64 == 0, "candidates");
   constexpr uint64_t kWBytes = (uint64_t)WW_ * 4;
@@ -516,6 +521,7 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
       // first window P_levels(j) covers (the message's head when a == 0), when that state
       // enters window a as a candidate inside a sparse table that goes on past window j.
       bool pub_early = false;
+      uint32_t mine_early = 0;   // this lane's granule of the early-published state
       uint64_t t_early = 0;
       uint64_t xdbg = 0;   // trace word 6: bit 0 tried, 1 ok0, 2 mode 1, 3 entry in range, 4 map, 5 left; hi: map
       if (levels > 0 && !last) {
@@ -566,12 +572,14 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
             e.rk += c;
             e.kk += c;
             e.left -= c;
+            if (skew) e.rk += 1;
             uint32_t mine = 0;
 #pragma unroll
             for (int i = 0; i < kGran; ++i) mine = lane == i ? gran_value(e, i) : mine;
             if (lane < kGran)
               __hip_atomic_store(gran + (uint64_t)tk * kGran + lane, ((uint64_t)epoch << 32) | (uint64_t)mine,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mine_early = mine;
             pub_early = true;
             if (tr) t_early = __builtin_amdgcn_s_memrealtime();
           }
@@ -738,6 +746,11 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
         __hip_atomic_store(g + lane, ((uint64_t)epoch << 32) | (uint64_t)mine, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
+      // The state published early (from the composed maps) must be the one the resolve
+      // reached: later windows started from it.  Any difference fails the call before an
+      // offset is used (kStWalkBound is fatal; the apply stages are gated on it).
+      if (pub_early && __ballot(lane < kGran && mine != mine_early) && lane == 0)
+        atomicOr(call_status, kStWalkBound);
       if (tr) {
         const uint64_t t_pub = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
@@ -804,8 +817,9 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
 // wc: null, or per table (TableDir index) the walk-counted split tables' WalkCount.
 hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff, uint32_t *call_status,
                        uint32_t *counters, uint32_t *ntouched, void *ws, uint32_t spec_wpr, unsigned blocks,
-                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, uint64_t items, int levels,
+                       uint32_t epoch, uint64_t trace_items, const WalkCount *wc, uint64_t items, int levels_arg,
                        int shape, hipStream_t st) {
+  const int levels = levels_arg & 0xff;
   if (shape < 0 || shape >= kNumWalkShapes) shape = 0;
   WalkCtl *ctl = reinterpret_cast<WalkCtl *>(ws);
   WalkHead *head = reinterpret_cast<WalkHead *>(reinterpret_cast<uint8_t *>(ws) + kWalkHeadOff);
@@ -823,7 +837,7 @@ hipError_t launch_walk(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *r
 #define PSX_WALK_LAUNCH(S)                                                                                    \
   hipLaunchKernelGGL((walk_kernel<kWalkShapes[S].threads, kWalkShapes[S].words, kWalkShapes[S].cand>), dim3(blocks), \
                      dim3(kWalkShapes[S].threads), 0, st, ss, dir, segs, recoff, call_status, ctl, head, gran, spec_wpr, \
-                     epoch, trace, wc, maps, levels)
+                     epoch, trace, wc, maps, levels_arg)
   switch (shape) {
     case 1: PSX_WALK_LAUNCH(1); break;
     case 2: PSX_WALK_LAUNCH(2); break;

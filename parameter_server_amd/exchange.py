@@ -205,11 +205,16 @@ class ShardExchange:
 
     def run(self, chunks, log=None):
         """Apply one batch per rank (a list of <= 2 GiB device messages, this rank's worker
-        batch in record order) to the owners' shards.  Returns after every apply settled."""
+        batch in record order) to the owners' shards.  Returns after every apply settled.
+
+        The chunks may still be in production on the caller's current stream (a non_blocking
+        copy, a packing kernel): the split stream waits for it first.  The server stays bound
+        to this exchange's apply stream (set by the constructor) after the call."""
         import time
         n = self.world
         if self.direct:
             return self._run_direct(chunks, log)
+        self.s_split.wait_stream(torch.cuda.current_stream(self.device))
         for k, msg in enumerate(chunks):
             s = k % 2
             ntab = len(self.formats)

@@ -1,0 +1,241 @@
+"""Any input finishes in bounded time, with a status or the exact result.
+
+Round 4 saw a 2 GiB message of corrupted bytes keep the apply running for minutes.  The
+path those bytes took: rows repeated inside one message fail `dense_verify`, so the call is
+replayed on the ordered path (one wave per touched row), and a row with more than 64
+records in the call had its record list sorted by lane 0 with an insertion sort in global
+memory — O(L^2) over ~500K records.  The sort is now a wave merge sort (psx_ordered.hip
+wave_sort_long, O(L log^2 L / 64) per lane) and the dense replay keeps the row in
+registers.  These tests feed the shapes that took the slow path: a >= 256 MiB dense
+message whose row ids are all equal, one whose ids repeat over a few rows, and messages of
+random words; and they check rows with 65 .. 5,000 records in one call against the oracle
+(dense, binary16 records, importance, sorted-map and map rows).  Reference: the apply loop
+that any of these reaches, `Server::ApplyOpLogUpdateVersion` (server.cpp:154-178)."""
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import parameter_server_amd as psa
+from parameter_server_amd import wire, PsxError, _abi
+from oracle.oracle import OracleServer, DENSE, SORTED_MAP, MAP, F32, F64, I32
+
+pytestmark = pytest.mark.gpu
+
+# Generous: the bound is "seconds, not minutes" (the replay of 65,536 records of one row
+# takes well under a second); the old insertion sort took minutes at 500K records.
+TIME_BOUND_S = 20.0
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built_lib, oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _dense_server(rows, cap, dt=F32, bgs=(100,), **kw):
+    srv = psa.Server(0, 1, list(bgs))
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=dt, row_capacity=cap, max_rows=rows, **kw))
+    return srv
+
+
+def _timed_apply(srv, msg, bg=100, ver=0):
+    t0 = time.perf_counter()
+    err = None
+    try:
+        srv.apply_device([(msg.data_ptr(), msg.numel(), bg, ver)])
+        srv.sync()
+    except PsxError as e:
+        err = e
+    return time.perf_counter() - t0, err
+
+
+def _in_order_sum(init, ids, upd):
+    """The reference loop: row += update, record by record, in f32 (numpy adds in order)."""
+    out = init.copy()
+    for i, r in enumerate(ids):
+        out[r] += upd[i]
+    return out
+
+
+@pytest.mark.parametrize("nrows_hit", [1, 3])
+def test_256mib_dense_message_of_repeated_rows_is_exact_and_bounded(nrows_hit):
+    """65,536 records of 1,024 f32 (268.7 MB) whose row ids are all one row, or cycle over
+    three rows: the duplicate-row replay, exact against the in-order f32 sum."""
+    rows, cap, n = 16, 1024, 65536
+    g = torch.Generator(device="cuda").manual_seed(77 + nrows_hit)
+    upd = torch.randn(n, cap, device="cuda", generator=g) * 0.01
+    ids = (torch.arange(n, device="cuda", dtype=torch.int32) % nrows_hit) + 5
+    msg = wire.dense_stream_torch(1, ids, upd)
+    assert msg.numel() >= 256 << 20
+    init = (torch.randn(rows, cap, device="cuda", generator=g) * 0.1).cpu().numpy()
+    srv = _dense_server(rows, cap)
+    srv.load_rows(1, 0, init)
+    torch.cuda.synchronize()
+    dt, err = _timed_apply(srv, msg)
+    assert err is None, err
+    assert dt < TIME_BOUND_S, f"replay of {n} records took {dt:.1f} s"
+    got = srv.read_rows(1, 0, rows)
+    want = _in_order_sum(init, ids.cpu().numpy(), upd.cpu().numpy())
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    srv.close()
+    print(f"{n} records on {nrows_hit} row(s): {dt:.3f} s")
+
+
+def test_256mib_message_of_random_words_fails_fast():
+    """A valid table header, then 256 MiB of random words: row ids out of the shard's range,
+    so the call fails with a status and applies nothing, within the bound."""
+    rows, cap, n = 1 << 16, 1024, 65536
+    g = torch.Generator(device="cuda").manual_seed(5)
+    msg = wire.dense_stream_torch(1, torch.zeros(n, dtype=torch.int32, device="cuda"),
+                                  torch.zeros(n, cap, device="cuda"))
+    body = msg[20:].view(torch.int32)
+    body.copy_(torch.randint(-2**31, 2**31 - 1, (body.numel(),), device="cuda", dtype=torch.int32, generator=g))
+    srv = _dense_server(rows, cap)
+    torch.cuda.synchronize()
+    dt, err = _timed_apply(srv, msg)
+    assert err is not None and err.status == _abi.PSX_ERR_ROW_RANGE
+    assert dt < TIME_BOUND_S
+    assert not srv.row_flags(1, 0, rows).any(), "a failed call created rows"
+    srv.close()
+
+
+def test_random_words_with_in_range_row_ids_are_applied_exactly():
+    """Random words whose row-id words are folded into a 64-row shard (every record legal,
+    every row repeated ~1,000 times, the payload random bits with the exponent's top bit
+    cleared, so every value is finite, denormals included): bounded, and bit for bit the
+    in-order f32 sum."""
+    rows, cap, n = 64, 1024, 65536
+    g = torch.Generator(device="cuda").manual_seed(6)
+    words = torch.randint(-2**31, 2**31 - 1, (n, 1 + cap), device="cuda", dtype=torch.int32, generator=g)
+    words[:, 0] = words[:, 0].abs() % rows
+    # keep the payload finite (exponent field below all-ones) so the expected sum is well defined
+    p = words[:, 1:]
+    p &= ~(1 << 30)
+    msg = torch.empty(5 + words.numel(), dtype=torch.int32, device="cuda")
+    msg[:5] = torch.tensor([1, 1, 4, 0, n], dtype=torch.int32)
+    msg[5:] = words.view(-1)
+    msg = msg.view(torch.uint8)
+    srv = _dense_server(rows, cap)
+    torch.cuda.synchronize()
+    dt, err = _timed_apply(srv, msg)
+    assert err is None, err
+    assert dt < TIME_BOUND_S
+    w = words.cpu().numpy()
+    want = _in_order_sum(np.zeros((rows, cap), np.float32), w[:, 0], w[:, 1:].view(np.float32))
+    got = srv.read_rows(1, 0, rows)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    srv.close()
+
+
+def test_fully_random_message_fails_with_a_status():
+    g = torch.Generator(device="cuda").manual_seed(7)
+    msg = torch.randint(-2**31, 2**31 - 1, ((256 << 20) // 4,), device="cuda", dtype=torch.int32,
+                        generator=g).view(torch.uint8)
+    srv = _dense_server(1 << 16, 1024)
+    torch.cuda.synchronize()
+    dt, err = _timed_apply(srv, msg)
+    assert err is not None
+    assert dt < TIME_BOUND_S
+    assert not srv.row_flags(1, 0, 1 << 16).any()
+    srv.close()
+
+
+# ---- rows with more than 64 records in one call, against the oracle ------------------------
+
+@pytest.mark.parametrize("L", [65, 130, 1000, 5000])
+@pytest.mark.parametrize("dt", [F32, F64])
+def test_long_record_lists_dense_vs_oracle(L, dt):
+    """One message holding L records of row 3 among records of other rows (twice each), in
+    a call of two messages: the long list is sorted into (message, position) order."""
+    rng = np.random.RandomState(L)
+    rows, cap = 40, 48
+    npdt = np.float32 if dt == F32 else np.float64
+    ids = np.concatenate([np.full(L, 3), np.repeat(np.arange(10, 30), 2)]).astype(np.int32)
+    rng.shuffle(ids)
+    msgs = [wire.dense_stream_np(1, ids, rng.normal(0, 1, (ids.size, cap)).astype(npdt)),
+            wire.dense_stream_np(1, np.arange(rows, dtype=np.int32), rng.normal(0, 1, (rows, cap)).astype(npdt))]
+    srv = _dense_server(rows, cap, dt, bgs=(100, 101))
+    orc = OracleServer([100, 101])
+    orc.create_table(1, DENSE, dt, cap)
+    dev = [torch.from_numpy(m).cuda() for m in msgs]
+    torch.cuda.synchronize()
+    srv.apply_device([(d.data_ptr(), d.numel(), 100 + i, 0) for i, d in enumerate(dev)])
+    srv.sync()
+    for i, m in enumerate(msgs):
+        assert orc.apply_stream(m, 100 + i, 0) == 0
+    got, want = srv.read_rows(1, 0, rows), orc.read_dense_rows(1, 0, rows)
+    bits = np.uint32 if dt == F32 else np.uint64
+    assert np.array_equal(got.view(bits), want.view(bits))
+    srv.close()
+    orc.close()
+
+
+def test_long_record_lists_binary16_and_importance_vs_oracle():
+    rng = np.random.RandomState(3)
+    rows, cap, L = 20, 40, 700
+    ids = np.concatenate([np.full(L, 7), np.arange(rows)]).astype(np.int32)
+    rng.shuffle(ids)
+    for kw, okw in (({"row_oplog_type": 3}, {"f16_records": True}),
+                    ({"accum_importance": True}, {"accum_importance": True})):
+        f16 = "row_oplog_type" in kw
+        pay = rng.normal(0, 1, (ids.size, cap)).astype(np.float16 if f16 else np.float32)
+        msg = wire.dense_variant_stream_np(1, ids, pay, f16=True) if f16 else wire.dense_stream_np(1, ids, pay)
+        srv = _dense_server(rows, cap, F32, **kw)
+        orc = OracleServer([100])
+        orc.create_table(1, DENSE, F32, cap, **okw)
+        d = torch.from_numpy(np.ascontiguousarray(msg)).cuda()
+        torch.cuda.synchronize()
+        srv.apply_device([(d.data_ptr(), d.numel(), 100, 0)])
+        srv.sync()
+        assert orc.apply_stream(msg, 100, 0) == 0
+        got, want = srv.read_rows(1, 0, rows), orc.read_dense_rows(1, 0, rows)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), kw
+        if not f16:
+            imp = srv.row_importance(1, 0, rows)
+            wimp = np.array([orc.importance(1, r) for r in range(rows)])
+            np.testing.assert_allclose(imp, wimp, rtol=1e-12)
+        srv.close()
+        orc.close()
+
+
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP])
+@pytest.mark.parametrize("L", [65, 300, 3000])
+def test_long_record_lists_sparse_vs_oracle(kind, L):
+    """Sorted-map / map rows with L records of one row inside one message (plus other rows):
+    entry order byte-exact for sorted maps, {col: value} for maps."""
+    rng = np.random.RandomState(100 + L)
+    rows, K = 50, 256 if L < 3000 else 1024
+    recs = []
+    for i in range(L + 60):
+        rid = 9 if i < L else int(rng.randint(0, rows))
+        k = int(rng.randint(1, 12))
+        cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+        recs.append((rid, cols, rng.choice([-2, -1, 1, 2, 3], size=k).astype(np.int32)))
+    order = rng.permutation(len(recs))
+    msg = wire.sparse_stream_np(2, 4, [recs[i] for i in order])
+    srv = psa.Server(0, 1, [100])
+    srv.CreateTable(2, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                     max_rows=rows, max_entries=K))
+    orc = OracleServer([100])
+    orc.create_table(2, kind, I32, 0, oplog_dense_serialized=False)
+    d = torch.from_numpy(msg).cuda()
+    torch.cuda.synchronize()
+    srv.apply_device([(d.data_ptr(), d.numel(), 100, 0)])
+    srv.sync()
+    assert orc.apply_stream(msg, 100, 0) == 0
+    if kind == SORTED_MAP:
+        assert srv.serialize_rows(2, list(range(rows))) == orc.serialize_records(2, list(range(rows)))
+    else:
+        def as_map(raw):   # {int32 row_id; size_t size; {int32 col; int32 val}[n]}
+            e = np.frombuffer(raw[12:], np.int32).reshape(-1, 2)
+            return dict(zip(e[:, 0].tolist(), e[:, 1].tolist()))
+        for r in range(rows):
+            g, w = srv.serialize_rows(2, [r]), orc.serialize_records(2, [r])
+            assert len(g) == len(w)
+            if g:
+                assert as_map(g) == as_map(w), r
+    srv.close()
+    orc.close()

@@ -378,3 +378,34 @@ def test_composed_exits_publish_early_on_c3_messages(walk_levels):
             early += code == 0x3F
     assert tried > 8 * 10
     assert early >= 0.9 * tried, f"{early} of {tried} windows published from the composed map"
+
+
+def test_early_published_state_is_cross_checked(walk_levels):
+    """An exit state published early from the composed maps is compared with the state the
+    window's own resolve reaches; a difference fails the call before any record offset is used
+    (later windows started from the early state).  PSX_DEBUG_WALK_SKEW shifts every early
+    state by one record: the call must fail with nothing applied, and the same call with the
+    skew off must then apply exactly as the oracle."""
+    if walk_levels == 0:
+        pytest.skip("composition off")
+    L = _abi.load()
+    rng = np.random.RandomState(31)
+    rows, K = 20_000, 1024
+    p = 1.0 / np.arange(1, rows + 1)
+    p /= p.sum()
+    streams = []
+    for b in range(4):
+        ids = rng.choice(rows, size=10_000, replace=False, p=p)
+        streams.append(wire.sparse_stream_np(3, 4, _rows(rng, ids, K, I32, rng.randint(1, 33, size=ids.size))))
+    SKEW = 21
+    old = L.psx_debug_set_variant(SKEW, 1)
+    try:
+        st = _Setup([(3, SORTED_MAP, I32, K, False, rows)], range(100, 104))
+        before = st.snapshot()
+        with pytest.raises(PsxError):
+            st.apply(streams, 0, oracle=False)
+        assert st.snapshot() == before, "a call with a skewed early state applied something"
+        st.close()
+    finally:
+        L.psx_debug_set_variant(SKEW, old)
+    _run_both([(3, SORTED_MAP, I32, K, False, rows)], streams)

@@ -7,8 +7,17 @@
 // stored by the device path is rejected at CreateTable.
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
+#include <vector>
+// The reference's abstract_row.hpp includes <boost/thread.hpp> (abstract_row.hpp:3), and the
+// apps use boost::barrier and std::atomic through petuum_ps.hpp without including them
+// (apps/lda/src/lda_engine.hpp:54-62): carried the same way where boost is installed.
+#if __has_include(<boost/thread.hpp>)
+#include <boost/thread.hpp>
+#endif
 
 namespace petuum {
 

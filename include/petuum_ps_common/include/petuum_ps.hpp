@@ -1,8 +1,13 @@
 // petuum_ps.hpp — what apps include (src/petuum_ps_common/include/petuum_ps.hpp:1-15).
 #pragma once
 
+// (the reference's petuum_ps.hpp reaches <cassert> through multiplicative_dense_row.hpp, and
+// apps call assert without including it: apps/lda/src/lda_engine.cpp:315)
+#include <cassert>
+
 #include <petuum_ps_common/include/configs.hpp>
 #include <petuum_ps_common/include/init_table_config.hpp>
+#include <petuum_ps_common/include/init_table_group_config.hpp>
 #include <petuum_ps_common/include/ps_table_group.hpp>
 #include <petuum_ps_common/include/table.hpp>
 #include <petuum_ps_common/storage/dense_row.hpp>

@@ -1,15 +1,19 @@
 // utils.hpp — the string-to-config helpers petuum_ps.hpp pulls in (src/petuum_ps_common/util/utils.hpp,
 // utils.cpp:55-171): apps and their flag parsing turn gflags strings into TableGroupConfig /
 // TableInfo enums with these.  An unknown name aborts, as the reference's LOG(FATAL) does.
-// GetHostInfos / GetServerIDsFromHostMap (host files for the ZeroMQ transport) are not here:
-// the transport is out of scope — shards are contexts in this process.
+// GetHostInfos / GetServerIDsFromHostMap read the machine file InitTableGroupConfig names
+// (--hostfile); the hosts are recorded in the config, the ZeroMQ transport that would
+// connect them is out of scope — shards are contexts in this process.
 #pragma once
 
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
+#include <map>
 #include <string>
+#include <vector>
 
 #include <petuum_ps_common/include/configs.hpp>
 
@@ -20,6 +24,26 @@ namespace utils_detail {
   std::abort();
 }
 }  // namespace utils_detail
+
+// One "id ip port" line per host (utils.cpp:15-35); a missing file leaves the map empty.
+inline void GetHostInfos(std::string server_file, std::map<int32_t, HostInfo> *host_map) {
+  std::ifstream input(server_file.c_str());
+  std::string line;
+  while (std::getline(input, line)) {
+    const size_t pos = line.find_first_of("\t ");
+    const size_t pos_ip = line.find_first_of("\t ", pos + 1);
+    const int32_t id = std::atoi(line.substr(0, pos).c_str());
+    host_map->insert(std::make_pair(id, HostInfo(id, line.substr(pos + 1, pos_ip - pos - 1),
+                                                 line.substr(pos_ip + 1))));
+  }
+}
+
+// Every host but the name node (id 0), in id order (utils.cpp:38-52).
+inline void GetServerIDsFromHostMap(std::vector<int32_t> *server_ids, const std::map<int32_t, HostInfo> &host_map) {
+  server_ids->clear();
+  for (const auto &h : host_map)
+    if (h.first != 0) server_ids->push_back(h.first);
+}
 
 inline UpdateSortPolicy GetUpdateSortPolicy(const std::string &p) {
   if (p == "Random") return Random;

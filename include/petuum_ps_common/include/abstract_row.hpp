@@ -76,6 +76,8 @@ class AbstractRow {
   // -1 when the device path cannot store it.
   virtual int32_t psx_row_kind() const { return -1; }
   virtual int32_t psx_dtype() const { return -1; }
+  // 1: the row's bytes are binary16 (DenseRowFloat16: psx_table_config.row_bytes_f16)
+  virtual int32_t psx_row_bytes_f16() const { return 0; }
 };
 
 }  // namespace petuum

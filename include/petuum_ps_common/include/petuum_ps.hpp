@@ -11,6 +11,7 @@
 #include <petuum_ps_common/include/ps_table_group.hpp>
 #include <petuum_ps_common/include/table.hpp>
 #include <petuum_ps_common/storage/dense_row.hpp>
+#include <petuum_ps_common/storage/dense_row_float16.hpp>
 #include <petuum_ps_common/storage/sorted_vector_map_row.hpp>
 #include <petuum_ps_common/storage/sparse_row.hpp>
 #include <petuum_ps_common/util/utils.hpp>

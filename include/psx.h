@@ -94,7 +94,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 7
+#define PSX_ABI_VERSION 8
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -176,7 +176,14 @@ typedef struct psx_table_config {
                                        decompressed to f32 before the add (dense_row_oplog_float16.hpp:144-157;
                                        f32 tables only).  1/2 select sparse row oplogs, which change nothing on
                                        the server for sparse-serialized tables (abstract_row_oplog.hpp:64-78). */
-  int32_t reserved1;                /* must be 0 */
+  /* ABI 4 (was reserved1): */
+  int32_t row_bytes_f16;            /* 1: DenseRowFloat16<float> rows (dense_row_float16.hpp:13; the row type
+                                       apps/matrixfact's matrixfact_split16 registers, :47,560): stored and
+                                       updated in f32, serialized (row reads, pushes) as binary16 uint16[cap]
+                                       through Float16Compressor::compress (vector_store_float16.hpp:91-99;
+                                       the third-party header is unpinned: parity unpinned).  Dense f32 rows
+                                       only.  A client context caching such rows takes pushed bodies through
+                                       psx_apply_push_body only when row_capacity is even (4-byte records). */
 } psx_table_config;
 
 /* One device-resident ClientSendOpLogMsg payload (ps_msgs.hpp:1003-1055 after its

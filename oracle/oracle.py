@@ -61,6 +61,11 @@ def lib():
         L.orc_table_set_importance.argtypes = [vp, i32, ctypes.c_int]
         L.orc_table_set_version_maintain.argtypes = [vp, i32, ctypes.c_int]
         L.orc_table_set_f16_records.argtypes = [vp, i32, ctypes.c_int]
+        L.orc_table_set_f16_rows.argtypes = [vp, i32, ctypes.c_int]
+        L.orc_float_to_half.argtypes = [ctypes.c_float]
+        L.orc_float_to_half.restype = ctypes.c_uint16
+        L.orc_half_to_float.argtypes = [ctypes.c_uint16]
+        L.orc_half_to_float.restype = ctypes.c_float
         L.orc_row_version.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_uint64)]
         L.orc_table_set_adarevision.argtypes = [vp, i32, ctypes.c_float, ctypes.c_int, ctypes.c_uint64, i32]
         L.orc_row_sent.argtypes = [vp, i32, i32, i32]
@@ -116,7 +121,7 @@ class OracleServer:
 
     def create_table(self, table_id, kind, dtype, row_capacity, oplog_dense_serialized=True,
                      dense_row_oplog_capacity=None, accum_importance=False, version_maintain=False,
-                     f16_records=False):
+                     f16_records=False, f16_rows=False):
         cap = row_capacity if dense_row_oplog_capacity is None else dense_row_oplog_capacity
         st = self._L.orc_table_create(self._s, table_id, kind, dtype,
                                       1 if oplog_dense_serialized else 0, row_capacity, cap)
@@ -127,6 +132,8 @@ class OracleServer:
             assert self._L.orc_table_set_version_maintain(self._s, table_id, 1) == ST_OK
         if f16_records:
             assert self._L.orc_table_set_f16_records(self._s, table_id, 1) == ST_OK
+        if f16_rows:
+            assert self._L.orc_table_set_f16_rows(self._s, table_id, 1) == ST_OK
         self.tables[table_id] = (kind, dtype, row_capacity)
 
     def importance(self, table_id, row_id):

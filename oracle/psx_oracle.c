@@ -234,6 +234,7 @@ typedef struct {
   int importance;        /* ApplyRow*AccumImportance selected (server_table.cpp:26-47) */
   int version_maintain;  /* TableInfo.version_maintain (configs.hpp:207) */
   int f16_records;       /* row_oplog_type kDenseRowOpLogFloat16 (configs.hpp:39) */
+  int f16_rows;          /* DenseRowFloat16 rows: served as binary16 (vector_store_float16.hpp:91-99) */
   int ada;               /* AdaRevisionServerTableLogic attached (server_table.cpp:83-93) */
   float ada_step;        /* FLAGS_init_step_size (adarevision_server_table_logic.cpp:8,22) */
   uint64_t ada_upper;    /* FLAGS_old_grad_upper_bound (:9,192-197) */
@@ -691,6 +692,7 @@ static float half_to_float(uint16_t h) {
   memcpy(&f, &bits, 4);
   return f;
 }
+float orc_half_to_float(uint16_t h) { return half_to_float(h); }
 
 /* Bytes of one dense record body after its row id: DenseRowOpLog V[cap]
  * (dense_row_oplog.hpp:138-144), VersionDenseRowOpLog V[cap] + uint64 version + bool
@@ -866,6 +868,45 @@ int orc_table_set_f16_records(orc_server *s, int32_t table_id, int on) {
   return ORC_OK;
 }
 
+/* DenseRowFloat16<float> rows (dense_row_float16.hpp:13, registered by matrixfact_split16.cpp:47,560):
+ * stored as float, Inc adds in float (vector_store_float16.hpp:131-134), serialized as
+ * binary16 through Float16Compressor::compress (:91-99). */
+int orc_table_set_f16_rows(orc_server *s, int32_t table_id, int on) {
+  orc_table *t = find_table(s, table_id);
+  if (!t) return ORC_ERR_INVALID_ARG;
+  if (on && (t->kind != KIND_DENSE || t->dt != DT_F32)) return ORC_ERR_UNSUPPORTED;
+  t->f16_rows = on ? 1 : 0;
+  return ORC_OK;
+}
+
+/* Float16Compressor::compress, the float -> binary16 direction VectorStoreFloat16::Serialize
+ * calls (vector_store_float16.hpp:94-96).  float16_compressor.hpp is fetched unpinned by
+ * third_party/third_party.mk:281-290 and absent here; this restates the published
+ * algorithm of that class (branch-free, bit-level): the magnitude's mantissa is truncated
+ * (round toward zero), values below the smallest normal half become subnormals through a
+ * float multiply by 2^37 converted to int (truncation), values above 65504 become infinity,
+ * NaNs keep the top 10 payload bits (the smallest half NaN when those are zero).  Parity
+ * unpinned: no reference test or fixture holds a compressed value. */
+uint16_t orc_float_to_half(float value) {
+  union { float f; int32_t si; uint32_t ui; } v, sc;
+  const int32_t infN = 0x7F800000, maxN = 0x477FE000, minN = 0x38800000;
+  const int32_t infC = infN >> 13, nanN = (infC + 1) << 13, maxC = maxN >> 13, minC = minN >> 13;
+  const int32_t subC = 0x003FF, maxD = infC - maxC - 1, minD = minC - subC - 1;
+  v.f = value;
+  uint32_t sign = v.ui & 0x80000000u;
+  v.ui ^= sign;
+  sign >>= 16;
+  sc.si = 0x52000000;                                    /* 2^37 */
+  const int32_t sub = minN > v.si ? (int32_t)(sc.f * v.f) : 0;
+  v.si ^= (sub ^ v.si) & -(int32_t)(minN > v.si);
+  v.si ^= (infN ^ v.si) & -(int32_t)((infN > v.si) & (v.si > maxN));
+  v.si ^= (nanN ^ v.si) & -(int32_t)((nanN > v.si) & (v.si > infN));
+  v.ui >>= 13;
+  v.si ^= ((v.si - maxD) ^ v.si) & -(int32_t)(v.si > maxC);
+  v.si ^= ((v.si - minD) ^ v.si) & -(int32_t)(v.si > subC);
+  return (uint16_t)(v.ui | sign);
+}
+
 /* VersionServerRow::get_version (version_server_row.hpp:66); 0 for a plain ServerRow
  * (abstract_server_row.hpp:71) and for absent rows. */
 int orc_row_version(orc_server *s, int32_t table_id, int32_t row_id, uint64_t *out) {
@@ -944,6 +985,17 @@ int64_t orc_serialize_row(orc_server *s, int32_t table_id, int32_t row_id, void 
 
 static int64_t serialize_row_body(orc_table *t, orc_row *r, void *out, size_t cap) {
   size_t vs = dt_size(t->dt);
+  if (t->kind == KIND_DENSE && t->f16_rows) {   /* VectorStoreFloat16::Serialize */
+    size_t nb = (size_t)t->row_capacity * 2;
+    if (nb > cap) return -2;
+    for (int64_t i = 0; i < t->row_capacity; ++i) {
+      float x;
+      memcpy(&x, r->dense + (size_t)i * 4, 4);
+      const uint16_t h = orc_float_to_half(x);
+      memcpy((uint8_t *)out + (size_t)i * 2, &h, 2);
+    }
+    return (int64_t)nb;
+  }
   if (t->kind == KIND_DENSE) {
     size_t nb = (size_t)t->row_capacity * vs;
     if (nb > cap) return -2;

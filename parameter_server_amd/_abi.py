@@ -44,7 +44,7 @@ class psx_table_config(ctypes.Structure):
         ("version_maintain", ctypes.c_int32),
         ("server_push_row_upper_bound", ctypes.c_int64),
         ("row_oplog_type", ctypes.c_int32),
-        ("reserved1", ctypes.c_int32),
+        ("row_bytes_f16", ctypes.c_int32),
     ]
 
 

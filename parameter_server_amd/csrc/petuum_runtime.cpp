@@ -103,6 +103,7 @@ class ClientTableImpl : public AbstractClientTable {
     dense_oplog_ = cfg_.table_info.row_oplog_type == RowOpLogType::kDenseRowOpLog;
     version_ = cfg_.table_info.version_maintain;
   }
+  int32_t row_bytes_f16() const { return sample_->psx_row_bytes_f16(); }
 
   void RegisterThread() override {}
   void DeregisterThread() override {}
@@ -280,6 +281,7 @@ class Runtime {
       pc.max_entries = t->kind() == PSX_ROW_DENSE ? 0 : std::max<int64_t>(pc.row_capacity, 64);
       pc.server_push_row_upper_bound = (int64_t)c.table_info.server_push_row_upper_bound;
       pc.version_maintain = version ? 1 : 0;
+      pc.row_bytes_f16 = t->row_bytes_f16();   // DenseRowFloat16: served as binary16
       check(shards_[ch].ctx, psx_table_create(shards_[ch].ctx, &pc), "psx_table_create");
       if (dl.kind == DeviceTableLogicKind::kAdaRevision) {
         psx_adarevision_config ac{};

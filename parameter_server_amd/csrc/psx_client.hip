@@ -151,7 +151,8 @@ __global__ void __launch_bounds__(256) push_claim_kernel(const PushEntry *ent, c
       body -= 8;
     }
     bool ok;
-    if (c.kind == 0) ok = body % c.vsize == 0 && body <= (uint64_t)c.row_cap * c.vsize;
+    if (c.kind == 0 && c.f16) ok = body % 2 == 0 && body <= (uint64_t)c.row_cap * 2;   // uint16[cap]
+    else if (c.kind == 0) ok = body % c.vsize == 0 && body <= (uint64_t)c.row_cap * c.vsize;
     else if (c.kind == 1) ok = body % c.es == 0;
     else ok = body % (4 + c.vsize) == 0;
     if (!ok) { atomicOr(status, kStMalformed); continue; }
@@ -183,7 +184,16 @@ __global__ void __launch_bounds__(256) push_reset_kernel(const uint8_t *body, co
     if (go) {
       const uint8_t *src = body + e.offset;
       const uint64_t bytes = c.ver ? e.size - 8 : e.size;
-      if (c.kind == 0) {
+      if (c.kind == 0 && c.f16) {
+        // VectorStoreFloat16::ResetData: Float16Compressor::decompress per value
+        // (vector_store_float16.hpp:110-115)
+        float *dst = reinterpret_cast<float *>(c.dense + s * (int64_t)c.row_cap * 4);
+        for (uint64_t e = lane; e < bytes / 2; e += 64) {
+          uint16_t h;
+          __builtin_memcpy(&h, src + 2 * e, 2);
+          dst[e] = __builtin_bit_cast(float, half_to_f32_bits(h));
+        }
+      } else if (c.kind == 0) {
         uint8_t *dst = c.dense + s * (int64_t)c.row_cap * c.vsize;
         for (uint64_t w = lane; w < bytes / 4; w += 64)
           reinterpret_cast<uint32_t *>(dst)[w] = (uint32_t)c_ld32(src + 4 * w);

@@ -255,6 +255,7 @@ struct ServeArgs {
   int64_t nsel;
   int64_t *lsizes;           // record bytes per list entry
   int64_t *loffs;            // exclusive prefix of lsizes + scan tile sums
+  int f16;                   // DenseRowFloat16 rows: row bytes are binary16 (row_cap * 2, records 2-aligned)
 };
 
 // One table of a device-side pack (psx_pack.hip).
@@ -320,6 +321,29 @@ __device__ __forceinline__ uint32_t half_to_f32_bits(uint32_t h) {
   return nan ? (((h & 0x8000u) << 16) | 0x7f800000u | ((h & 0x3ffu) << 13)) : hw;
 }
 
+// Float16Compressor::compress (vector_store_float16.hpp:94-96; unpinned third-party header,
+// restated from its published algorithm):
+// the mantissa truncated, below the smallest normal through float x 2^37 -> int, above
+// 65504 -> infinity, NaN payloads kept (the smallest half NaN when their top bits are 0).
+__device__ __forceinline__ uint32_t f32_to_half_fc(float value) {
+  constexpr int32_t infN = 0x7F800000, maxN = 0x477FE000, minN = 0x38800000;
+  constexpr int32_t infC = infN >> 13, nanN = (infC + 1) << 13, maxC = maxN >> 13, minC = minN >> 13;
+  constexpr int32_t subC = 0x003FF, maxD = infC - maxC - 1, minD = minC - subC - 1;
+  uint32_t u = __builtin_bit_cast(uint32_t, value);
+  uint32_t sign = u & 0x80000000u;
+  int32_t v = (int32_t)(u ^ sign);
+  sign >>= 16;
+  const float mag = __builtin_bit_cast(float, v);
+  const int32_t sub = minN > v ? (int32_t)(__builtin_bit_cast(float, 0x52000000) * mag) : 0;
+  v ^= (sub ^ v) & -(int32_t)(minN > v);
+  v ^= (infN ^ v) & -(int32_t)((infN > v) & (v > maxN));
+  v ^= (nanN ^ v) & -(int32_t)((nanN > v) & (v > infN));
+  v = (int32_t)((uint32_t)v >> 13);
+  v ^= ((v - maxD) ^ v) & -(int32_t)(v > maxC);
+  v ^= ((v - minD) ^ v) & -(int32_t)(v > subC);
+  return ((uint32_t)v | sign) & 0xffffu;
+}
+
 __device__ __forceinline__ uint32_t half_to_f32_bits_hw(uint32_t h) {
   return __builtin_bit_cast(uint32_t, (float)__builtin_bit_cast(_Float16, (uint16_t)h));
 }
@@ -354,6 +378,7 @@ struct ClientTable {
   int32_t *nent;
   uint64_t *ver;     // version tables: the pushed row version
   int32_t *claim;    // per slot, zero between calls
+  int32_t f16;       // DenseRowFloat16 rows: pushed row bytes are binary16, decompressed on reset
 };
 
 // psx_split_stream (psx_split.hip): one table of the message being split, stream order.

@@ -380,6 +380,31 @@ uint64_t rd64h(const uint8_t *p) {
   return v;
 }
 
+// Float16Compressor::compress on the host (psx_serialize_rows; psx_device.hpp f32_to_half_fc
+// is the device twin; tests check both against the CPU restatement).
+uint16_t f32_to_half_fc(float value) {
+  const int32_t infN = 0x7F800000, maxN = 0x477FE000, minN = 0x38800000;
+  const int32_t infC = infN >> 13, nanN = (infC + 1) << 13, maxC = maxN >> 13, minC = minN >> 13;
+  const int32_t subC = 0x003FF, maxD = infC - maxC - 1, minD = minC - subC - 1;
+  uint32_t u;
+  memcpy(&u, &value, 4);
+  uint32_t sign = u & 0x80000000u;
+  int32_t v = (int32_t)(u ^ sign);
+  sign >>= 16;
+  float mag, mul;
+  memcpy(&mag, &v, 4);
+  const int32_t mulN = 0x52000000;
+  memcpy(&mul, &mulN, 4);
+  const int32_t sub = minN > v ? (int32_t)(mul * mag) : 0;
+  v ^= (sub ^ v) & -(int32_t)(minN > v);
+  v ^= (infN ^ v) & -(int32_t)((infN > v) & (v > maxN));
+  v ^= (nanN ^ v) & -(int32_t)((nanN > v) & (v > infN));
+  v = (int32_t)((uint32_t)v >> 13);
+  v ^= ((v - maxD) ^ v) & -(int32_t)(v > maxC);
+  v ^= ((v - minD) ^ v) & -(int32_t)(v > subC);
+  return (uint16_t)(((uint32_t)v | sign) & 0xffffu);
+}
+
 // Host walk of one message (host bytes): SerializedOpLogReader semantics
 // (serialized_oplog_reader.hpp:30-133) — validates everything the device pipeline
 // would flag, so psx_apply_stream can fail synchronously and apply nothing.
@@ -1120,6 +1145,7 @@ psx_status serve_args(psx_ctx *c, TableState &t, psx::ServeArgs *out) {
   a.sizes = t.d_srv_sizes;
   a.offs = t.d_srv_offs;
   a.ver = t.d_ver;
+  a.f16 = t.cfg.row_bytes_f16;
   *out = a;
   return PSX_OK;
 }
@@ -1335,12 +1361,14 @@ psx_status psx_sender_version(psx_ctx *c, int32_t bg_id, int64_t *version) {
 static psx_status table_format(psx_ctx *c, const psx_table_config *cfg, TableState &t) {
   if (cfg->dtype < PSX_F32 || cfg->dtype > PSX_I64) return fail(c, PSX_ERR_INVALID_ARG, "bad dtype");
   if (cfg->row_kind < PSX_ROW_DENSE || cfg->row_kind > PSX_ROW_MAP) return fail(c, PSX_ERR_INVALID_ARG, "bad row kind");
-  if (cfg->reserved1 != 0 || cfg->server_push_row_upper_bound < 0 ||
+  if ((cfg->row_bytes_f16 != 0 && cfg->row_bytes_f16 != 1) || cfg->server_push_row_upper_bound < 0 ||
       (cfg->accum_importance != 0 && cfg->accum_importance != 1) ||
       (cfg->version_maintain != 0 && cfg->version_maintain != 1) || cfg->row_oplog_type < 0 ||
       cfg->row_oplog_type > 3)
     return fail(c, PSX_ERR_INVALID_ARG,
-                "bad accum_importance / version_maintain / row_oplog_type / reserved1 / server_push_row_upper_bound");
+                "bad accum_importance / version_maintain / row_oplog_type / row_bytes_f16 / server_push_row_upper_bound");
+  if (cfg->row_bytes_f16 && (cfg->row_kind != PSX_ROW_DENSE || cfg->dtype != PSX_F32))
+    return fail(c, PSX_ERR_UNSUPPORTED, "binary16 row bytes (DenseRowFloat16) need dense f32 rows (vector_store_float16.hpp:12)");
   const bool f16 = cfg->row_oplog_type == 3 && cfg->oplog_dense_serialized;
   if (cfg->version_maintain && (cfg->row_kind != PSX_ROW_DENSE || !cfg->oplog_dense_serialized || f16))
     // the reference's sparse version records are inconsistent between writer and reader
@@ -1710,7 +1738,9 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
     if (slots[i] < 0 || !(flags[i] & 1)) continue;
     const uint8_t *src = rows.data() + (size_t)i * rb;
     size_t body;
-    if (dense) {
+    if (dense && t->cfg.row_bytes_f16) {
+      body = (size_t)t->cfg.row_capacity * 2;             // VectorStoreFloat16::Serialize
+    } else if (dense) {
       body = rb;                                          // VectorStore::Serialize
     } else if (t->cfg.row_kind == PSX_ROW_SORTED_MAP) {
       body = (size_t)counts[i] * t->es;                   // Entry<V>[n] as stored
@@ -1722,7 +1752,14 @@ psx_status psx_serialize_rows(psx_ctx *c, int32_t table_id, const int32_t *row_i
     uint64_t sz = body + trailer;
     memcpy(o + off, &row_ids[i], 4);
     memcpy(o + off + 4, &sz, 8);
-    if (t->cfg.row_kind == PSX_ROW_MAP) {
+    if (dense && t->cfg.row_bytes_f16) {
+      for (int64_t k = 0; k < t->cfg.row_capacity; ++k) {
+        float x;
+        memcpy(&x, src + (size_t)k * 4, 4);
+        const uint16_t h = f32_to_half_fc(x);
+        memcpy(o + off + 12 + (size_t)k * 2, &h, 2);
+      }
+    } else if (t->cfg.row_kind == PSX_ROW_MAP) {
       uint8_t *d = o + off + 12;
       for (int32_t k = 0; k < counts[i]; ++k) {
         memcpy(d, src + (size_t)k * t->es, 4);
@@ -2548,6 +2585,10 @@ psx_status psx_apply_push_body(psx_ctx *c, const void *body, size_t size, int32_
   if (size == 0) return PSX_OK;
   psx_status st = sync_impl(c);
   if (st) return st;
+  for (auto &t : c->tables)
+    if (t.cfg.row_bytes_f16 && (t.cfg.row_capacity & 1))
+      return fail(c, PSX_ERR_UNSUPPORTED, "push bodies of binary16 rows of odd width (2-byte records) are not walked on "
+                                          "the device");
   const size_t max_ent = size / 12 + 1;
   if (!body_on_device && size > c->push_body_cap) {
     if (c->d_push_body) hipFree(c->d_push_body);
@@ -2585,6 +2626,7 @@ psx_status psx_apply_push_body(psx_ctx *c, const void *body, size_t size, int32_
     x.nent = t.d_nent;
     x.ver = t.d_ver;
     x.claim = t.d_cnt;   // the ordered path's per-slot counts: zero between calls
+    x.f16 = t.cfg.row_bytes_f16;
   }
   const uint8_t *dbody = (const uint8_t *)body;
   if (!body_on_device) {

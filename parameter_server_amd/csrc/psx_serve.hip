@@ -28,7 +28,7 @@ namespace psx {
 
 
 __device__ __forceinline__ int64_t row_bytes(const ServeArgs &a, int64_t s) {
-  if (a.kind == 0) return a.row_cap * a.vsize;
+  if (a.kind == 0) return a.row_cap * (a.f16 ? 2 : a.vsize);   // VectorStoreFloat16: uint16[cap]
   const int64_t es = a.vsize == 4 ? 8 : 16;
   const int64_t n = a.nent[s];
   return a.kind == 1 ? n * es : n * (4 + a.vsize);
@@ -58,11 +58,40 @@ __global__ void __launch_bounds__(256) serve_list_sizes_kernel(ServeArgs a) {
   if (i < a.nsel) a.lsizes[i] = a.sizes[a.sel[i]];
 }
 
+// A 32-bit word at a 2-byte-aligned address (records after binary16 rows of odd width).
+__device__ __forceinline__ void st32_a2(uint8_t *p, uint32_t v) {
+  reinterpret_cast<uint16_t *>(p)[0] = (uint16_t)v;
+  reinterpret_cast<uint16_t *>(p)[1] = (uint16_t)(v >> 16);
+}
+
 // One record {int32 row_id; size_t size; row bytes} for slot s at rec (one wave); with
 // flags_rw, ResetDirty and ResetImportance_ (server_table.cpp:234-235, :398-399).
 __device__ void emit_row(const ServeArgs &a, int64_t s, uint8_t *rec, int lane) {
   const int64_t total = a.sizes[s] - 12;
   const int64_t body = total - (a.ver ? 8 : 0);   // row bytes before the version trailer
+  if (a.f16) {
+    // DenseRowFloat16: VectorStoreFloat16::Serialize, Float16Compressor::compress per value
+    // (vector_store_float16.hpp:91-99); the record may start on a 2-byte boundary
+    if (lane == 0) {
+      const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
+      st32_a2(rec, (uint32_t)rid);
+      st32_a2(rec + 4, (uint32_t)(uint64_t)total);
+      st32_a2(rec + 8, (uint32_t)((uint64_t)total >> 32));
+      if (a.ver) {
+        const uint64_t v = a.ver[s];
+        st32_a2(rec + 12 + body, (uint32_t)v);
+        st32_a2(rec + 16 + body, (uint32_t)(v >> 32));
+      }
+    }
+    const float *src = reinterpret_cast<const float *>(a.dense + s * a.row_cap * 4);
+    uint16_t *dst = reinterpret_cast<uint16_t *>(rec + 12);
+    for (int64_t e = lane; e < a.row_cap; e += 64) dst[e] = (uint16_t)f32_to_half_fc(src[e]);
+    if (lane == 0 && a.flags_rw) {
+      a.flags_rw[s] &= (uint8_t)~2u;
+      if (a.imp_rw) a.imp_rw[s] = 0.0;
+    }
+    return;
+  }
   if (lane == 0) {
     const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
     reinterpret_cast<int32_t *>(rec)[0] = rid;
@@ -165,7 +194,10 @@ hipError_t launch_subscribe(uint8_t *flags, uint64_t *subs, const int64_t *slots
 }
 
 __global__ void put_words_kernel(uint8_t *out, Words w) {
-  for (int i = threadIdx.x; i < w.n; i += blockDim.x) *reinterpret_cast<int32_t *>(out + w.pos[i]) = w.val[i];
+  for (int i = threadIdx.x; i < w.n; i += blockDim.x) {
+    if (w.pos[i] & 3) st32_a2(out + w.pos[i], (uint32_t)w.val[i]);   // after binary16 rows of odd width
+    else *reinterpret_cast<int32_t *>(out + w.pos[i]) = w.val[i];
+  }
 }
 
 hipError_t launch_serve_sizes(const ServeArgs &a, hipStream_t st) {

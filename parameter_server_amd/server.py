@@ -32,6 +32,7 @@ class TableInfo:
     server_push_row_upper_bound: int = 0    # configs.hpp:181; 0 -> 100
     version_maintain: bool = False          # VersionDenseRowOpLog records + VersionServerRow rows (configs.hpp:207)
     row_oplog_type: int = 0                 # RowOpLogType (configs.hpp:35-40); 3 = float16 dense records
+    row_bytes_f16: bool = False             # DenseRowFloat16 rows: served as binary16 (dense_row_float16.hpp:13)
 
 
 def table_config(table_id, info: TableInfo):
@@ -44,7 +45,8 @@ def table_config(table_id, info: TableInfo):
         row_offset=info.row_offset, row_stride=info.row_stride, max_rows=info.max_rows,
         max_entries=info.max_entries, accum_importance=1 if info.accum_importance else 0,
         server_push_row_upper_bound=info.server_push_row_upper_bound,
-        version_maintain=1 if info.version_maintain else 0, row_oplog_type=info.row_oplog_type)
+        version_maintain=1 if info.version_maintain else 0, row_oplog_type=info.row_oplog_type,
+        row_bytes_f16=1 if info.row_bytes_f16 else 0)
 
 
 def _check(L, ctx, st):

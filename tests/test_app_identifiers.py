@@ -29,10 +29,6 @@ NOT_PS_LIBRARY = {
     "petuum::SnapshotProcessor", "petuum::StringBuffer",
     # named only inside comments (mlr_main.cpp:72, mlr_sgd_solver.cpp:123)
     "petuum::SparseFeatureRow",
-    # matrixfact_split16.cpp:47: a row type storing binary16 values on the server
-    # (VectorStoreFloat16); the MI355X server stores f32 rows and takes binary16 *records*
-    # (row_oplog_type 3, DESIGN.md §5 "Variant dense formats") — the float16 row store is not provided
-    "petuum::DenseRowFloat16",
 }
 
 

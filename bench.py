@@ -37,7 +37,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-EXCHANGE_TIMEOUT_S = 420   # N > 1: the exchange extras are abandoned (headline kept, exit 3) past this
+EXCHANGE_TIMEOUT_S = 600   # N > 1: the exchange extras are abandoned (headline kept, exit 3) past this
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 PMC_JSON = os.path.join(ROOT, "profiles", "r04", "pmc_dense_apply.json")
 
@@ -90,9 +90,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of the cpu_baseline sample (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 18,
-                   help="rows of the cpu_baseline sample (a quarter of C2: table and streams far larger than the caches)")
-    p.add_argument("--cpu-threads", type=int, default=16,
-                   help="server threads of the cpu_baseline (capped at the visible CPUs; the GPU box's share is 16)")
+                   help="rows of a generated cpu_baseline sample (configurations that do not hand the baseline "
+                        "their own messages; the C2 line times the oracle on the full C2 messages)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="cap on the cpu_baseline's server threads (0: every usable core -- the affinity mask, "
+                        "cgroup quota and OMP_NUM_THREADS; the GPU box's share is 16)")
     p.add_argument("--pmc-json", default=PMC_JSON,
                    help="per-launch HBM bytes of dense_apply from the rocprofv3 --pmc passes "
                         "(tools/pmc_summary.py); used for roofline.traffic on the default C2 configuration")
@@ -104,6 +106,11 @@ def parse():
                         "c4shard: one GPU's 1.25M-row shard of C4 with its 8 worker messages; "
                         "c5: mixed dense + sparse clocks under SSPPush")
     p.add_argument("--c4-rows", type=int, default=10_000_000, help="C4 total rows (all shards)")
+    p.add_argument("--c5-gloo", action="store_true",
+                   help="C5 with WORLD_SIZE > 1 over gloo (no collective is on C5's data path; the tests put 2 "
+                        "ranks on one GPU)")
+    p.add_argument("--c5-dump", default=None,
+                   help="C5: every rank writes its shard and applied message order to this directory")
     p.add_argument("--adarevision", action="store_true",
                    help="C2 through the AdaRevision server-table logic (adarevision_server_table_logic.cpp): "
                         "per element the adaptive step on accum/z/z_max state beside every row")
@@ -207,27 +214,72 @@ def cpu_model():
         return None
 
 
-def cpu_baseline(args, rows=None, cap=None):
-    """Oracle (CPU restatement of the reference apply loop) on a bounded sample, run as T
-    server threads: rows are sharded row_id % T (the reference's comm-channel placement,
-    context.hpp:291-304) and each thread applies its own shard's messages, as T reference
-    ServerThreads would (the client already splits its oplog per server,
-    abstract_bg_worker.cpp:590-649).  ctypes releases the GIL, so shards run in parallel.
-    A single-thread pass (one reference server thread) is timed beside it."""
+def usable_cores():
+    """CPUs this process may use and where the figure comes from: its affinity mask, capped
+    by a cgroup CPU quota and by OMP_NUM_THREADS (the GPU box runs a job on a 16-CPU share
+    of its host and says so there; nproc / os.cpu_count() show the whole machine)."""
+    info = {"nproc": os.cpu_count()}
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    info["affinity"] = n
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    info["cgroup_quota"] = quota
+    omp = os.environ.get("OMP_NUM_THREADS")
+    info["omp_num_threads"] = int(omp) if omp and omp.isdigit() else None
+    T = min(x for x in (n, quota, info["omp_num_threads"]) if x)
+    return max(1, T), info
+
+
+def cpu_baseline(args, rows=None, cap=None, host_msgs=None, base=0):
+    """Oracle (CPU restatement of the reference apply loop) run as T server threads: rows
+    are sharded row_id % T (the reference's comm-channel placement, context.hpp:291-304) and
+    each thread applies its own shard's messages, as T reference ServerThreads would (the
+    client already splits its oplog per server, abstract_bg_worker.cpp:590-649).  ctypes
+    releases the GIL, so shards run in parallel.  A single-thread pass (one reference server
+    thread) is timed beside it.  With host_msgs (the C2 run's own messages, in host memory)
+    the sample is the whole C2 configuration; otherwise a generated sample of `rows` rows."""
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     from oracle.oracle import OracleServer, DENSE, F32
     from parameter_server_amd import wire
-    rows, cap, B = rows or args.cpu_rows, cap or args.cols, args.batches
-    T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    B = args.batches
+    if host_msgs is not None:
+        rows, cap = args.rows, args.cols
+    else:
+        rows, cap = rows or args.cpu_rows, cap or args.cols
+    T, tinfo = usable_cores()
+    if args.cpu_threads:
+        T = min(T, args.cpu_threads)
     rng = np.random.default_rng(1234)
     init = rng.standard_normal((rows, cap), dtype=np.float32) * np.float32(0.1)
-    perms, upds = [], []
-    for b in range(B):
-        r = np.random.default_rng(1235 + b)
-        perms.append(r.permutation(rows).astype(np.int32))
-        upds.append(r.standard_normal((rows, cap), dtype=np.float32) * np.float32(0.01))
+    recs = []          # per batch: the records as int32 [n, 1 + cap] (row id, then the payload bits)
+    if host_msgs is not None:
+        for m in host_msgs:
+            recs.append(m[20:].view(np.int32).reshape(-1, 1 + cap))
+    else:
+        for b in range(B):
+            r = np.random.default_rng(1235 + b)
+            perm = r.permutation(rows).astype(np.int32)
+            upd = r.standard_normal((rows, cap), dtype=np.float32) * np.float32(0.01)
+            recs.append(wire.dense_stream_np(1, perm, upd)[20:].view(np.int32).reshape(-1, 1 + cap))
+            del upd
     bgs = list(range(100, 100 + B))
+
+    def shard_msg(b, sel):
+        r = recs[b] if sel is None else recs[b][sel]
+        hdr = np.array([1, 1, 4, 0, r.shape[0]], np.int32)   # one table, update_size 4, num_rows
+        return np.concatenate([hdr.view(np.uint8), r.view(np.uint8).reshape(-1)])
 
     def timed_run(nthreads, seconds):
         shards = []
@@ -236,11 +288,13 @@ def cpu_baseline(args, rows=None, cap=None):
             o.create_table(1, DENSE, F32, cap)
             if args.adarevision:
                 assert o.set_adarevision(1, init_step_size=0.1, gaussian_init=False) == 0
-            o.load_dense_rows(1, t, init[t::nthreads], stride=nthreads)
+            o.load_dense_rows(1, base + t, init[t::nthreads], stride=nthreads)
             msgs = []
             for b in range(B):
-                m = (perms[b] % nthreads) == t
-                msgs.append(wire.dense_stream_np(1, perms[b][m], upds[b][m]))
+                if nthreads == 1 and host_msgs is not None:
+                    msgs.append(host_msgs[b])
+                else:
+                    msgs.append(shard_msg(b, None if nthreads == 1 else ((recs[b][:, 0] - base) % nthreads) == t))
             shards.append((o, msgs))
         step_bytes = sum(m.size for _, ms in shards for m in ms) + (8 if args.adarevision else 2) * rows * cap * 4
 
@@ -263,11 +317,15 @@ def cpu_baseline(args, rows=None, cap=None):
 
     v1, n1, e1 = timed_run(1, args.cpu_seconds / 3)
     vt, nt, et = timed_run(T, args.cpu_seconds * 2 / 3) if T > 1 else (v1, n1, e1)
+    what = (f"the C2 run's own {B} messages, copied to the host" if host_msgs is not None else
+            "a generated sample")
     return {"value": round(vt, 3), "unit": "GB/s", "cores": T, "kind": "port", "cpu_model": cpu_model(),
-            "single_thread_GBps": round(v1, 3),
-            "sample": f"{rows} rows x {cap} f32, {B} batches/step; {T} threads (rows % {T} shards): {nt} steps in "
-                      f"{et:.1f} s; 1 thread: {n1} steps in {e1:.1f} s (oracle/psx_oracle.c restatement of "
-                      f"server.cpp:120-179)"}
+            "single_thread_GBps": round(v1, 3), "cores_source": tinfo,
+            "sample": f"{rows} rows x {cap} f32, {B} batches/step ({what}); {T} threads = the usable cores "
+                      f"(affinity {tinfo['affinity']}, cgroup quota {tinfo['cgroup_quota']}, OMP_NUM_THREADS "
+                      f"{tinfo['omp_num_threads']}; nproc {tinfo['nproc']} counts the whole host), rows % {T} "
+                      f"shards: {nt} steps in {et:.1f} s; 1 thread (one reference server thread): {n1} steps in "
+                      f"{e1:.1f} s (oracle/psx_oracle.c restatement of server.cpp:120-179)"}
 
 
 _C3_CACHE = {}
@@ -396,7 +454,9 @@ def c3_cpu_baseline(args, batches, nupd, bgs, seconds):
     from concurrent.futures import ThreadPoolExecutor
     from oracle.oracle import OracleServer, SORTED_MAP, I32
     from parameter_server_amd import wire
-    T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    T = usable_cores()[0]
+    if args.cpu_threads:
+        T = min(T, args.cpu_threads)
 
     def timed_run(nthreads, seconds):
         shards = []
@@ -1025,7 +1085,56 @@ def read_sweep_rate(bufs, reps=5):
     return tot_b / tot_s / 1e9 if tot_s > 0 else None
 
 
-def run_pcie(args, srv, streams, rows, cap, bgs, ver):
+def run_seam(args, host, rows, cap, bgs, base, local):
+    """The drop-in seam as INTEGRATION.md binds it: C2's 8 messages from page-locked host
+    memory (worker socket buffers), one psx_apply_stream call each (Server::
+    ApplyOpLogUpdateVersion, one host message per call, server_thread.cpp:241-243), into a
+    fresh context.  Each call returns once its bytes are in HBM; message k's apply runs
+    beside message k+1's copy.  `value` = message bytes per second (the caller's bytes
+    crossing PCIe, applied); also timed from pageable copies of the same messages."""
+    import torch
+    import parameter_server_amd as psa
+    srv = psa.Server(device=local, server_id=99, bg_ids=bgs)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap,
+                                     row_offset=base, max_rows=rows))
+    ver = [0]
+
+    def step(msgs):
+        for b, m in enumerate(msgs):
+            srv.ApplyOpLogUpdateVersion(m, m.size, bgs[b], ver[0])
+        ver[0] += 1
+
+    pinned = [h.numpy() for h in host]
+    step(pinned)
+    srv.sync()
+    n = max(4, args.steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step(pinned)
+    srv.sync()
+    el = time.perf_counter() - t0
+    pageable = [p.copy() for p in pinned]
+    step(pageable)
+    srv.sync()
+    t1 = time.perf_counter()
+    npg = 2
+    for _ in range(npg):
+        step(pageable)
+    srv.sync()
+    el_p = time.perf_counter() - t1
+    del pageable
+    srv.close()
+    nbytes = sum(p.size for p in pinned)
+    return {"value": round(nbytes * n / el / 1e9, 2), "unit": "GB/s", "ms_per_step": round(el / n * 1e3, 3),
+            "steps": n, "calls_per_step": len(pinned), "bytes_per_step": nbytes,
+            "pageable_GBps": round(nbytes * npg / el_p / 1e9, 2),
+            "what": "C2's 8 messages from page-locked host memory, one psx_apply_stream (ApplyOpLogUpdateVersion) "
+                    "call each, settled by one psx_sync per step: message bytes per second; each call returns once "
+                    "its bytes are in HBM, its apply beside the next call's copy (PSX_SEAM_ASYNC); pageable_GBps: "
+                    "the same from pageable copies"}
+
+
+def run_pcie(args, srv, streams, rows, cap, bgs, ver, host=None):
     """Host-resident form of C2: messages start in pinned host memory (worker socket
     buffers) and every dirty row is served back to host memory each step.
 
@@ -1034,7 +1143,8 @@ def run_pcie(args, srv, streams, rows, cap, bgs, ver):
     rows cross device-to-host on a third; PCIe is full duplex, so the step costs about the
     host-to-device copy alone.  `serial` times the same work one step at a time."""
     import torch
-    host = [s.cpu().pin_memory() for s in streams]
+    if host is None:
+        host = [s.cpu().pin_memory() for s in streams]
     dev = [list(streams), [torch.empty_like(s) for s in streams]]
     table_host = torch.empty(rows * cap, dtype=torch.float32).pin_memory()
     table_dev = torch.empty(rows * cap, dtype=torch.float32, device="cuda")
@@ -1137,7 +1247,9 @@ def c5_cpu_baseline(args, wl, seconds):
     from concurrent.futures import ThreadPoolExecutor
     from oracle.oracle import OracleServer, DENSE, SORTED_MAP, F32, I32
     from parameter_server_amd import wire
-    T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    T = usable_cores()[0]
+    if args.cpu_threads:
+        T = min(T, args.cpu_threads)
     B, bgs = wl["B"], [100 + b for b in range(wl["B"])]
 
     def build(nthreads):
@@ -1274,7 +1386,57 @@ def pcie_duplex_probe(h2d_bytes, d2h_bytes, reps=3):
             "bytes": {"h2d": h2d_bytes, "d2h": d2h_bytes}}
 
 
-def run_c5(args):
+def c5_host_model(wl, runs, upto, d_lo, d_hi, s_lo, s_hi):
+    """Numpy recompute of one rank's C5 shard, for the line's parity field: the runs
+    [0, upto) in arrival order, every message added to the rows it names in f32 (row +=
+    update, one message after another: the reference's loop, server.cpp:154-178) and to the
+    count matrix (the sorted-map rows' {col -> value}, SortedVectorMapStore::Inc's sums),
+    with each push's dirty rows (ServerTable::AppendTableToBuffs) tracked.  Uses neither
+    libpsx nor the oracle.  Returns the dense rows, the counts and the last push's dirty
+    rows (dense, sparse) as shard-relative indices."""
+    import numpy as np
+    cap, K = wl["cap"], wl["K"]
+    per = []
+    for ids_d, upd, ids_s, cnt in wl["parts"]:
+        md, ms = (ids_d >= d_lo) & (ids_d < d_hi), (ids_s >= s_lo) & (ids_s < s_hi)
+        r, c = np.nonzero(cnt[ms])
+        per.append(((ids_d[md] - d_lo).astype(np.int64), upd[md], (ids_s[ms] - s_lo).astype(np.int64)[r],
+                    c.astype(np.int64), cnt[ms][r, c]))
+    tab = np.zeros((d_hi - d_lo, cap), np.float32)
+    cntm = np.zeros((s_hi - s_lo, K), np.int32)
+    dd, ds = np.zeros(d_hi - d_lo, bool), np.zeros(s_hi - s_lo, bool)
+    last = (np.zeros(0, np.int64), np.zeros(0, np.int64))
+    for j in range(upto):
+        group, push = runs[j]
+        for w, _ in group:
+            idx, upd, sr, sc, sv = per[w]
+            tab[idx] += upd
+            cntm[sr, sc] += sv
+            dd[idx] = True
+            ds[sr] = True
+        if push:
+            last = (np.nonzero(dd)[0], np.nonzero(ds)[0])
+            dd[:] = False
+            ds[:] = False
+    return tab, cntm, last
+
+
+def c5_parse_rows(raw, first, n, K):
+    """Sorted-map records {int32 row_id; size_t size; Entry<int32>[n]} -> count matrix."""
+    import numpy as np
+    out = np.zeros((n, K), np.int32)
+    b = np.frombuffer(raw, np.uint8)
+    off = 0
+    while off + 12 <= b.size:
+        rid = int(b[off:off + 4].view(np.int32)[0])
+        size = int(b[off + 4:off + 12].view(np.uint64)[0])
+        e = b[off + 12:off + 12 + size].view(np.int32).reshape(-1, 2)
+        out[rid - first, e[:, 0]] = e[:, 1]
+        off += 12 + size
+    return out
+
+
+def c5_measure(args, world, rank, local, steps, warmup, parity=True, dump_dir=None):
     """SURVEY §8(d) C5, end to end: mixed dense + sparse tables, a continuous update stream
     under SSPPush with staleness 4, messages arriving from host memory and push bodies
     leaving to host memory.
@@ -1290,21 +1452,23 @@ def run_c5(args):
     (the worker socket buffers) and applied in one fused call, every sender's clock ticks
     (ClockUntil), and the push bodies (one per client, CreateSendServerPushRowMsgs,
     server.cpp:189-309) go device-to-host.  The next run's host-to-device copy overlaps this
-    run's apply and push.  WORLD_SIZE > 1: the tables are row-range sharded over the ranks;
-    each worker's message is split per owner, as the reference client splits per server
-    (abstract_bg_worker.cpp:590-649), and each rank serves its own shard with no collective.
-    value = pushed clocks per second (max over ranks)."""
+    run's apply and push.  world > 1 (the process group already up): the tables are
+    row-range sharded over the ranks; each worker's message is split per owner, as the
+    reference client splits per server (abstract_bg_worker.cpp:590-649), and each rank
+    serves its own shard with no collective (reductions of the timings only).
+    value = pushed clocks per second (max over ranks).
+
+    parity: after the timed region one more run to a push, untimed; then each rank's shard
+    (dense rows bit for bit, sorted-map rows as {col -> value}) and that push's bodies (each
+    client's row set, dense bytes, sparse values) against c5_host_model, summed over ranks.
+    dump_dir: every rank also writes its shard (dense rows, sorted-map row bytes) and the
+    messages it applied, in order, to dump_dir/c5_rank<r>.npz (the tests replay them through
+    the oracle).  Returns the line (every rank)."""
     import numpy as np
     import torch
     import torch.distributed as dist
     import parameter_server_amd as psa
     from parameter_server_amd import wire
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     wl = c5_workload()
     rows_d, cap, rows_s, K, B = wl["rows_d"], wl["cap"], wl["rows_s"], wl["K"], wl["B"]
     # this rank's row ranges and the workers' per-owner messages
@@ -1332,9 +1496,9 @@ def run_c5(args):
     for b, (ids_d, ids_s) in enumerate(subs):
         srv.subscribe(1, ids_d, b)
         srv.subscribe(3, ids_s, b)
-    W, Kc = args.warmup, args.steps
+    W, Kc = warmup, steps
     pcie = pcie_duplex_probe(sum(m.size for m in msgs), 1 << 30)
-    arrivals, gate = c5_schedule(B, W + Kc + C5_STALENESS + 2)
+    arrivals, gate = c5_schedule(B, W + Kc + C5_STALENESS + 4)
     # runs of arrivals: each ends with the message that advances the min clock
     runs, cur = [], []
     for w, c, push in arrivals:
@@ -1358,7 +1522,9 @@ def run_c5(args):
                     slots[k][i][:host[w].numel()].copy_(host[w], non_blocking=True)
         ev_in[k].record(s_in)
 
-    def serve(j):
+    last_bodies = [None]
+
+    def serve(j, keep=False):
         """One run: apply (fused), ClockUntil per message, push if the min clock moved."""
         k = j % 2
         group, push = runs[j]
@@ -1377,8 +1543,10 @@ def run_c5(args):
         t1 = time.perf_counter()
         pushed_bytes = 0
         if changed:
-            bodies = srv.serialize_push(clear=True, as_bytes=False)    # settles the apply; D2H
-            pushed_bytes = sum(x.size for x in bodies)
+            bodies = srv.serialize_push(clear=True, as_bytes=keep)    # settles the apply; D2H
+            pushed_bytes = sum(len(x) for x in bodies)
+            if keep:
+                last_bodies[0] = bodies
         else:
             srv.sync()
         t2 = time.perf_counter()
@@ -1409,13 +1577,64 @@ def run_c5(args):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    check = None
+    if parity:
+        # untimed: the runs up to the next push, keeping its bodies; then the shard and the
+        # bodies against the host model
+        while j < len(runs):
+            pushed = runs[j][1] > 0
+            serve(j, keep=pushed)
+            j += 1
+            if pushed:
+                break
+        srv.sync()
+        tab, cntm, (dirty_d, dirty_s) = c5_host_model(wl, runs, j, d_lo, d_hi, s_lo, s_hi)
+        got_d = srv.read_rows(1, d_lo, d_hi - d_lo)
+        bad_dense = int(np.sum(got_d.view(np.uint32) != tab.view(np.uint32)))
+        raw_s = srv.serialize_rows(3, list(range(s_lo, s_hi)))
+        got_s = c5_parse_rows(raw_s, s_lo, s_hi - s_lo, K)
+        if dump_dir:
+            order = np.array([wc for g, _ in runs[:j] for wc in g], np.int32).reshape(-1, 2)
+            np.savez(os.path.join(dump_dir, f"c5_rank{rank}.npz"), dense=got_d,
+                     sparse=np.frombuffer(raw_s, np.uint8), order=order,
+                     bounds=np.array([d_lo, d_hi, s_lo, s_hi], np.int64))
+        bad_sparse = int(np.sum(got_s != cntm))
+        bad_push = 0
+        if last_bodies[0] is None:
+            bad_push = -1
+        else:
+            for b, body in enumerate(last_bodies[0]):
+                parsed = wire.parse_push_body(body)
+                sub_d = np.zeros(d_hi - d_lo, bool)
+                sub_d[subs[b][0] - d_lo] = True
+                sub_s = np.zeros(s_hi - s_lo, bool)
+                sub_s[subs[b][1] - s_lo] = True
+                want_d = sorted(int(r) for r in dirty_d if sub_d[r])
+                want_s = sorted(int(r) for r in dirty_s if sub_s[r])
+                rec_d, rec_s = parsed.get(1, {}), parsed.get(3, {})
+                if sorted(r - d_lo for r in rec_d) != want_d or sorted(r - s_lo for r in rec_s) != want_s:
+                    bad_push += 1
+                    continue
+                for r, payload in rec_d.items():
+                    bad_push += payload != tab[r - d_lo].tobytes()
+                for r, payload in rec_s.items():
+                    e = np.frombuffer(payload, np.int32).reshape(-1, 2)
+                    row = np.zeros(K, np.int32)
+                    row[e[:, 0]] = e[:, 1]
+                    bad_push += not np.array_equal(row, cntm[r - s_lo])
+        check = [bad_dense, bad_sparse, bad_push]
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        rdev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        t = torch.tensor([el], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        tot = torch.tensor([acct["h2d"], acct["d2h"]], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([acct["h2d"], acct["d2h"]], dtype=torch.float64, device=rdev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         h2d_all, d2h_all = (float(x) for x in tot.tolist())
+        if check is not None:
+            ct = torch.tensor([abs(x) for x in check], dtype=torch.int64, device=rdev)
+            dist.all_reduce(ct, op=dist.ReduceOp.SUM)
+            check = [int(x) for x in ct.tolist()]
     else:
         h2d_all, d2h_all = float(acct["h2d"]), float(acct["d2h"])
     srv.close()
@@ -1428,38 +1647,68 @@ def run_c5(args):
     bound_ms = (max(h2d_pc, d2h_pc) / (PCIE_PEAK_GBS * 1e9) + dev_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
     bound_serial_ms = ((h2d_pc + d2h_pc) / (PCIE_PEAK_GBS * 1e9) + dev_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
     cpu = c5_cpu_baseline(args, wl, min(args.cpu_seconds, 12.0)) if args.cpu_seconds > 0 and world == 1 else None
+    par = None
+    if check is not None:
+        par = {"result": "bit-exact" if not any(check) else "MISMATCH",
+               "dense_values_differing": check[0], "sparse_values_differing": check[1],
+               "push_records_differing": check[2],
+               "what": "every rank after the timed region and one more run to a push: its dense shard bit for bit "
+                       "and its sorted-map shard as {col -> value} against a numpy replay of the same arrival-ordered "
+                       "messages (f32 row += update per message; integer sums), and that push's bodies (each "
+                       "client's dirty subscribed rows, dense bytes, sparse values); counts summed over ranks"}
+    return {
+        "metric": "C5 mixed dense+sparse clocks under SSPPush, end to end (H2D of the workers' messages, apply, "
+                  "ClockUntil, per-client push bodies D2H)",
+        "value": round(done / el, 2), "unit": "clocks/s",
+        "ms_per_clock": round(ms, 3),
+        "n_gpus": world, "steps": done, "warmup": W, "higher_is_better": True,
+        "parity": par,
+        "h2d_bytes_per_clock_all_ranks": int(h2d_all / max(done, 1)),
+        "d2h_bytes_per_clock_all_ranks": int(d2h_all / max(done, 1)),
+        "pcie_GBps_per_rank": {"h2d": round(h2d_pc / (ms / 1e3) / 1e9, 2), "d2h": round(d2h_pc / (ms / 1e3) / 1e9, 2)},
+        "messages_per_clock": round(acct["msgs"] / max(done, 1), 2),
+        "apply_and_clock_ms_per_clock": round(acct["apply_s"] / max(done, 1) * 1e3, 3),
+        "push_ms_per_clock": round(acct["push_s"] / max(done, 1) * 1e3, 3),
+        "ssp_gate": dict(gate, what="c5_schedule: worker w takes 1 + 0.25 w time units per clock; Get blocks "
+                                    "until pushed clock >= clock - staleness; the server applies messages in "
+                                    "arrival order, so fast workers' later clocks are applied before the push "
+                                    "of earlier ones"),
+        "pcie_probe": dict(pcie, note="the same copies through torch on two streams, alone and at once; "
+                                      "issued this way the two directions did not overlap (both_GBps ~ one "
+                                      "direction), while C5's own copies (torch H2D + libpsx D2H) move "
+                                      "pcie_GBps_per_rank h2d + d2h together"),
+        "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
+                  "serial_ms_per_clock": round(bound_serial_ms, 3),
+                  "what": "per rank: max(H2D, D2H) bytes at the PCIe Gen5 x16 spec (63 GB/s per direction, "
+                          "full duplex) + the device bytes (messages + dense row read/write) at 8 TB/s; "
+                          "serial_ms: both directions in turn"},
+        "dtype": "f32+int32", "data": "synthetic",
+        "config": {"workload": f"C5: dense {rows_d}x{cap} f32 + sorted-map {rows_s}x{K} int32, {B} clients x 1 msg/"
+                               f"clock, SSPPush, staleness {C5_STALENESS}, row-range shards x{world}",
+                   "scaling": "strong (fixed workload split over the ranks)"},
+        "cpu_baseline": cpu,
+    }
+
+
+def run_c5(args):
+    """`bench.py --workload c5`: c5_measure on WORLD_SIZE ranks (one per GPU; gloo when
+    --c5-gloo, e.g. several ranks sharing one GPU in the tests), rank 0 prints the line;
+    --c5-dump DIR: every rank also writes its shard and its applied message order there."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.c5_gloo:   # ranks may share a GPU (the tests' one-GPU box)
+        local %= max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    if world > 1:
+        if args.c5_gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    line = c5_measure(args, world, rank, local, args.steps, args.warmup, dump_dir=args.c5_dump)
     if rank == 0:
-        line = {
-            "metric": "C5 mixed dense+sparse clocks under SSPPush, end to end (H2D of the workers' messages, apply, "
-                      "ClockUntil, per-client push bodies D2H)",
-            "value": round(done / el, 2), "unit": "clocks/s",
-            "ms_per_clock": round(ms, 3),
-            "n_gpus": world, "steps": done, "warmup": W, "higher_is_better": True,
-            "h2d_bytes_per_clock_all_ranks": int(h2d_all / max(done, 1)),
-            "d2h_bytes_per_clock_all_ranks": int(d2h_all / max(done, 1)),
-            "pcie_GBps_per_rank": {"h2d": round(h2d_pc / (ms / 1e3) / 1e9, 2), "d2h": round(d2h_pc / (ms / 1e3) / 1e9, 2)},
-            "messages_per_clock": round(acct["msgs"] / max(done, 1), 2),
-            "apply_and_clock_ms_per_clock": round(acct["apply_s"] / max(done, 1) * 1e3, 3),
-            "push_ms_per_clock": round(acct["push_s"] / max(done, 1) * 1e3, 3),
-            "ssp_gate": dict(gate, what="c5_schedule: worker w takes 1 + 0.25 w time units per clock; Get blocks "
-                                        "until pushed clock >= clock - staleness; the server applies messages in "
-                                        "arrival order, so fast workers' later clocks are applied before the push "
-                                        "of earlier ones"),
-            "pcie_probe": dict(pcie, note="the same copies through torch on two streams, alone and at once; "
-                                          "issued this way the two directions did not overlap (both_GBps ~ one "
-                                          "direction), while C5's own copies (torch H2D + libpsx D2H) move "
-                                          "pcie_GBps_per_rank h2d + d2h together"),
-            "bound": {"ms_per_clock": round(bound_ms, 3), "frac": round(bound_ms / ms, 3),
-                      "serial_ms_per_clock": round(bound_serial_ms, 3),
-                      "what": "per rank: max(H2D, D2H) bytes at the PCIe Gen5 x16 spec (63 GB/s per direction, "
-                              "full duplex) + the device bytes (messages + dense row read/write) at 8 TB/s; "
-                              "serial_ms: both directions in turn"},
-            "dtype": "f32+int32", "data": "synthetic",
-            "config": {"workload": f"C5: dense {rows_d}x{cap} f32 + sorted-map {rows_s}x{K} int32, {B} clients x 1 msg/"
-                                   f"clock, SSPPush, staleness {C5_STALENESS}, row-range shards x{world}",
-                       "scaling": "strong (fixed workload split over the ranks)"},
-            "cpu_baseline": cpu,
-        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -1702,11 +1951,26 @@ def main():
     # the same run also records, beside `value`, the PCIe-inclusive rate and C3 (N = 1), or
     # the exchange-bearing step over xGMI (N > 1).  None of it is inside the timed region.
     extras = args.extras and c2_dims and not args.adarevision and not args.walked
-    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver) if args.pcie or (extras and world == 1) else None
+    # the messages in page-locked host memory: the PCIe-inclusive pass, the seam and the CPU
+    # baseline (the full C2 messages on the host's cores) all start from them
+    host = None
+    if (args.pcie or extras) and world == 1:
+        host = [s.cpu().pin_memory() for s in streams]
+    elif world == 1 and args.cpu_seconds > 0 and c2_dims and not args.adarevision:
+        host = [s.cpu() for s in streams]
+    pcie = run_pcie(args, srv, streams, rows, cap, bgs, ver, host) if args.pcie or (extras and world == 1) else None
     srv.close()
     del streams, record_rows
     torch.cuda.empty_cache()
-    other, exchange, c4 = None, None, None
+    seam = None
+    if extras and world == 1:
+        try:
+            seam = run_seam(args, host, rows, cap, bgs, base, local)
+            if pcie:
+                seam["frac_of_pcie_inclusive_pipelined"] = round(seam["value"] / pcie["pcie_inclusive_GBps"], 3)
+        except Exception as e:
+            seam = {"error": repr(e)[:400]}
+    other, exchange, c4, c5 = None, None, None, None
     if extras and world > 1:
         # The exchange extras must never cost the headline: if they have not finished within
         # EXCHANGE_TIMEOUT_S (a collective that never completes, say), rank 0 prints the line
@@ -1723,7 +1987,10 @@ def main():
                     ln["walked"] = walked
                 if exchange:
                     ln["exchange"] = exchange
-                ln["c4" if exchange else "exchange"] = {"error": f"not finished within {EXCHANGE_TIMEOUT_S} s: abandoned"}
+                if c4:
+                    ln["c4"] = c4
+                ln["c5" if c4 else "c4" if exchange else "exchange"] = {
+                    "error": f"not finished within {EXCHANGE_TIMEOUT_S} s: abandoned"}
                 print(json.dumps(ln), flush=True)
             sys.stdout.flush()
             sys.stderr.flush()
@@ -1743,6 +2010,13 @@ def main():
                           "the seeds")
         except Exception as e:
             c4 = {"error": repr(e)[:400]}
+        try:
+            # SURVEY C5 (BASELINE configs[4], "8 MI355X"): the mixed dense + sparse SSP stream,
+            # row-range sharded over the ranks, self-checked
+            c5 = c5_measure(args, world, rank, local, 5, 2)
+            c5.pop("metric", None)
+        except Exception as e:
+            c5 = {"error": repr(e)[:400]}
         done.set()
     if extras and world == 1:
         # C3 in child processes (`bench.py --workload c3`), so its device memory and state
@@ -1776,16 +2050,22 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(args)
+            full_c2 = host is not None and c2_dims and not args.adarevision
+            cpu = cpu_baseline(args, host_msgs=[h.numpy() for h in host] if full_c2 else None, base=base)
+        del host
         line = build_line(cpu)
         if walked:
             line["walked"] = walked
         if pcie:
             line["pcie_inclusive"] = pcie
+        if seam:
+            line["seam"] = seam
         if exchange:
             line["exchange"] = exchange
         if c4:
             line["c4"] = c4
+        if c5:
+            line["c5"] = c5
         if other:
             line["other_configs"] = other
         print(json.dumps(line), flush=True)

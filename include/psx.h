@@ -242,9 +242,22 @@ psx_status psx_row_versions(psx_ctx *ctx, int32_t table_id, int64_t first_row,
                             int64_t num_rows, uint64_t *dst);
 
 /* ---- apply (the hot path) -------------------------------------------------- */
-/* Server::ApplyOpLogUpdateVersion: host bytes, borrowed only for the call. */
+/* Server::ApplyOpLogUpdateVersion (server.cpp:120-179): host bytes, borrowed only for the
+ * call (serialized_oplog_reader.hpp:22: the reader does not take ownership; the server
+ * thread frees the message after the call, server_thread.cpp:457-458).
+ * Default (PSX_SEAM_ASYNC): the bytes are copied into one of two HBM staging slots on the
+ * context's copy stream and the call returns as soon as the copy has read them (page-locked
+ * caller memory copies at the PCIe DMA rate); the apply is enqueued behind the copy, so
+ * message k's apply runs beside message k+1's copy.  Version and sender errors return at
+ * once; what only the device sees (framing, unknown tables, row range, capacity) fails the
+ * call with nothing applied and is reported by the next call that settles (psx_sync, a
+ * push, a row read), as for psx_apply_streams_device.  PSX_SEAM_SYNC (psx_ctx_set_seam):
+ * every call also settles before it returns, so its own device errors come back from it. */
 psx_status psx_apply_stream(psx_ctx *ctx, const void *oplog, size_t oplog_size,
                             int32_t bg_id, uint32_t version);
+#define PSX_SEAM_ASYNC 0
+#define PSX_SEAM_SYNC 1
+psx_status psx_ctx_set_seam(psx_ctx *ctx, int32_t mode);
 /* n device-resident messages, applied as if by n ApplyOpLogUpdateVersion calls in
  * array order (per-row update order preserved => bit-exact float sums).  Asynchronous
  * on the context stream; device buffers must stay valid until psx_sync(). */

@@ -39,6 +39,7 @@ struct TableInfo {
   int64_t server_push_row_upper_bound = 0;   // configs.hpp:181; 0 -> 100
   bool version_maintain = false;             // configs.hpp:207 (VersionDenseRowOpLog / VersionServerRow)
   int32_t row_oplog_type = 0;                // configs.hpp:35-40 (3: float16 dense records)
+  bool row_bytes_f16 = false;                // DenseRowFloat16 rows: served as binary16
 };
 
 class Server {
@@ -73,11 +74,15 @@ class Server {
     c.server_push_row_upper_bound = ti.server_push_row_upper_bound;
     c.version_maintain = ti.version_maintain ? 1 : 0;
     c.row_oplog_type = ti.row_oplog_type;
+    c.row_bytes_f16 = ti.row_bytes_f16 ? 1 : 0;
     Check(psx_table_create(ctx_, &c));
   }
 
   // Server::ApplyOpLogUpdateVersion (server.hpp:46-48, server.cpp:120-179): the oplog
-  // bytes are borrowed for the call only, as in the reference.
+  // bytes are borrowed for the call only, as in the reference.  The call returns once they
+  // are copied to HBM; the apply runs beside the next call's copy, and a failure only the
+  // device sees surfaces at the next Sync() (psx.h, PSX_SEAM_ASYNC) — SetSeam(PSX_SEAM_SYNC)
+  // settles every call before it returns.
   void ApplyOpLogUpdateVersion(const void *oplog, size_t oplog_size, int32_t bg_thread_id,
                                uint32_t version) {
     Check(psx_apply_stream(ctx_, oplog, oplog_size, bg_thread_id, version));
@@ -89,6 +94,7 @@ class Server {
   }
 
   void Sync() { Check(psx_sync(ctx_)); }
+  void SetSeam(int32_t mode) { Check(psx_ctx_set_seam(ctx_, mode)); }
 
   // Server::GetBgVersion (server.cpp:186-188).
   int32_t GetBgVersion(int32_t bg_thread_id) {

@@ -64,6 +64,7 @@ def lib():
         L.orc_table_set_f16_rows.argtypes = [vp, i32, ctypes.c_int]
         L.orc_float_to_half.argtypes = [ctypes.c_float]
         L.orc_float_to_half.restype = ctypes.c_uint16
+        L.orc_floats_to_halves.argtypes = [vp, vp, sz]
         L.orc_half_to_float.argtypes = [ctypes.c_uint16]
         L.orc_half_to_float.restype = ctypes.c_float
         L.orc_row_version.argtypes = [vp, i32, i32, ctypes.POINTER(ctypes.c_uint64)]

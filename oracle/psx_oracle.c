@@ -907,6 +907,11 @@ uint16_t orc_float_to_half(float value) {
   return (uint16_t)(v.ui | sign);
 }
 
+/* orc_float_to_half over an array (raw bits in and out: no float conversion on the way) */
+void orc_floats_to_halves(const float *in, uint16_t *out, size_t n) {
+  for (size_t i = 0; i < n; ++i) out[i] = orc_float_to_half(in[i]);
+}
+
 /* VersionServerRow::get_version (version_server_row.hpp:66); 0 for a plain ServerRow
  * (abstract_server_row.hpp:71) and for absent rows. */
 int orc_row_version(orc_server *s, int32_t table_id, int32_t row_id, uint64_t *out) {

@@ -184,6 +184,7 @@ def load():
         "psx_decode_push_header": ([vp, sz, P(psx_push_msg_header)], ctypes.c_int),
         "psx_ctx_set_compat": ([vp, i32], ctypes.c_int),
         "psx_ctx_set_pipeline": ([vp, i32], ctypes.c_int),
+        "psx_ctx_set_seam": ([vp, i32], ctypes.c_int),
         "psx_handle_oplog_msg": ([vp, vp, sz, i32, P(i32)], ctypes.c_int),
         "psx_last_error": ([vp], ctypes.c_char_p),
         "psx_status_string": ([ctypes.c_int], ctypes.c_char_p),

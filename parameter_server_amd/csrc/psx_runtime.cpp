@@ -261,6 +261,16 @@ struct psx_ctx {
   uint8_t *d_zero = nullptr;
   uint8_t *d_staging = nullptr;
   size_t staging_cap = 0;
+  // psx_apply_stream (PSX_SEAM_ASYNC): two HBM staging slots filled on the copy stream; a
+  // slot is reused once the call that read it has applied (ev_seam_free)
+  int seam_mode = PSX_SEAM_ASYNC;
+  hipStream_t h2d = nullptr;
+  uint8_t *d_seam[2] = {nullptr, nullptr};
+  size_t seam_cap[2] = {0, 0};
+  hipEvent_t ev_seam_copied[2] = {nullptr, nullptr};
+  hipEvent_t ev_seam_free[2] = {nullptr, nullptr};
+  bool seam_used[2] = {false, false};
+  int64_t seam_k = 0;
   void *d_split_fixed = nullptr, *d_split_recoff = nullptr, *d_split_scratch = nullptr;   // psx_split_stream
   size_t split_fixed_cap = 0, split_recoff_cap = 0, split_scratch_cap = 0;
   uint64_t *d_list = nullptr;            // ordered path: record lists ((message << 56) | offset),
@@ -405,52 +415,6 @@ uint16_t f32_to_half_fc(float value) {
   return (uint16_t)(((uint32_t)v | sign) & 0xffffu);
 }
 
-// Host walk of one message (host bytes): SerializedOpLogReader semantics
-// (serialized_oplog_reader.hpp:30-133) — validates everything the device pipeline
-// would flag, so psx_apply_stream can fail synchronously and apply nothing.
-psx_status host_validate(psx_ctx *c, const uint8_t *p, size_t size) {
-  if (size == 0) return PSX_OK;
-  if (size < 4) return fail(c, PSX_ERR_MALFORMED, "stream shorter than num_tables");
-  int32_t ntab = (int32_t)rd32h(p);
-  if (ntab < 0) return fail(c, PSX_ERR_MALFORMED, "negative num_tables");
-  size_t off = 4;
-  std::vector<int32_t> seen;
-  for (int32_t k = 0; k < ntab; ++k) {
-    if (off + 16 > size) return fail(c, PSX_ERR_MALFORMED, "truncated table header");
-    int32_t tid = (int32_t)rd32h(p + off);
-    uint64_t usz = rd64h(p + off + 4);
-    int32_t nrows = (int32_t)rd32h(p + off + 12);
-    off += 16;
-    TableState *t = find_table(c, tid);
-    if (!t) return fail(c, PSX_ERR_UNKNOWN_TABLE, "table_id = " + std::to_string(tid) + " not found!");
-    if (usz != (uint64_t)t->vsize || nrows < 0) return fail(c, PSX_ERR_MALFORMED, "bad update_size/num_rows");
-    if (std::find(seen.begin(), seen.end(), tid) != seen.end())
-      return fail(c, PSX_ERR_UNSUPPORTED, "table appears twice in one message");
-    if (!t->cfg.oplog_dense_serialized && (off & 3))
-      return fail(c, PSX_ERR_UNSUPPORTED, "sparse table at an unaligned offset (behind odd-sized version records)");
-    seen.push_back(tid);
-    for (int32_t r = 0; r < nrows; ++r) {
-      if (off + 4 > size) return fail(c, PSX_ERR_MALFORMED, "truncated record");
-      int32_t rid = (int32_t)rd32h(p + off);
-      if (slot_of(*t, rid) < 0)
-        return fail(c, PSX_ERR_ROW_RANGE, "row " + std::to_string(rid) + " not owned by this shard");
-      off += 4;
-      if (t->cfg.oplog_dense_serialized) {
-        size_t rs = (size_t)t->dense_body();
-        if (off + rs > size) return fail(c, PSX_ERR_MALFORMED, "truncated dense record");
-        off += rs;
-      } else {
-        if (off + 4 > size) return fail(c, PSX_ERR_MALFORMED, "truncated sparse record");
-        int32_t n = (int32_t)rd32h(p + off);
-        if (n < 0) return fail(c, PSX_ERR_MALFORMED, "negative record length");
-        size_t rs = 4 + (size_t)n * (4 + t->vsize);
-        if (off + rs > size) return fail(c, PSX_ERR_MALFORMED, "truncated sparse record");
-        off += rs;
-      }
-    }
-  }
-  return PSX_OK;
-}
 
 // Kernel arguments of the AdaRevision kernels for table t (index ti).
 psx::AdaArgs ada_args(TableState &t, int ti) {
@@ -1238,6 +1202,7 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->side) hipStreamSynchronize(c->side);
   if (c->aux) hipStreamSynchronize(c->aux);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->h2d) hipStreamSynchronize(c->h2d);
   for (auto &t : c->tables) free_table(t);
   if (c->d_list) hipFree(c->d_list);
   if (c->d_split_fixed) hipFree(c->d_split_fixed);
@@ -1278,6 +1243,12 @@ psx_status psx_ctx_destroy(psx_ctx *c) {
   if (c->d_client_tabs) hipFree(c->d_client_tabs);
   if (c->d_pack) hipFree(c->d_pack);
   if (c->d_staging) hipFree(c->d_staging);
+  for (int k = 0; k < 2; ++k) {
+    if (c->d_seam[k]) hipFree(c->d_seam[k]);
+    if (c->ev_seam_copied[k]) hipEventDestroy(c->ev_seam_copied[k]);
+    if (c->ev_seam_free[k]) hipEventDestroy(c->ev_seam_free[k]);
+  }
+  if (c->h2d) hipStreamDestroy(c->h2d);
   for (int k = 0; k < 2; ++k)
     if (c->d_wcount[k]) hipFree(c->d_wcount[k]);
   if (c->own) hipStreamDestroy(c->own);
@@ -1652,10 +1623,57 @@ psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, in
     it->second = version;
     return PSX_OK;
   }
-  psx_status st = host_validate(c, p, oplog_size);
-  if (st) return st;
   HIP_TRY(c, hipSetDevice(c->device));
-  // The staging buffer may still feed an earlier call's kernels.
+  psx_status st;
+  if (c->seam_mode == PSX_SEAM_ASYNC) {
+    // The device validates everything before it touches a row (decode, index, ordered
+    // prep); the host only copies.  Slot s last held call seam_k - 2's message.
+    if (!c->h2d) {
+      HIP_TRY(c, hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
+      for (int k = 0; k < 2; ++k) {
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_seam_copied[k], hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_seam_free[k], hipEventDisableTiming));
+      }
+    }
+    const int s = (int)(c->seam_k & 1);
+    if (c->seam_used[s]) {
+      HIP_TRY(c, hipEventSynchronize(c->ev_seam_free[s]));
+      // A duplicate-row replay re-reads its calls' messages when it settles: settle it
+      // while slot s still holds the bytes of every pending call
+      uint32_t sticky = 0;
+      HIP_TRY(c, hipMemcpy(&sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+      if (sticky & psx::kStDuplicateRow) {
+        psx_status d = sync_impl(c);
+        if (d != PSX_OK) c->deferred = d;
+      }
+    }
+    if (oplog_size > c->seam_cap[s]) {
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->side));
+      if (c->d_seam[s]) hipFree(c->d_seam[s]);
+      c->d_seam[s] = nullptr;
+      c->seam_cap[s] = 0;
+      HIP_TRY(c, hipMalloc(&c->d_seam[s], oplog_size));
+      c->seam_cap[s] = oplog_size;
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->d_seam[s], oplog, oplog_size, hipMemcpyHostToDevice, c->h2d));
+    HIP_TRY(c, hipEventRecord(c->ev_seam_copied[s], c->h2d));
+    // the caller's bytes have been read once the copy is done: they may be freed on return
+    HIP_TRY(c, hipEventSynchronize(c->ev_seam_copied[s]));
+    psx_stream one{c->d_seam[s], oplog_size, bg_id, version};
+    if (c->pending_calls >= kRing - 1) {
+      psx_status d = sync_impl(c);
+      if (d != PSX_OK) c->deferred = d;
+    }
+    st = enqueue_apply(c, &one, 1, false);
+    if (st) return st;
+    it->second = version;
+    HIP_TRY(c, hipEventRecord(c->ev_seam_free[s], c->stream));
+    c->seam_used[s] = true;
+    ++c->seam_k;
+    return PSX_OK;
+  }
+  // PSX_SEAM_SYNC.  The staging buffer may still feed an earlier call's kernels.
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (oplog_size > c->staging_cap) {
     if (c->d_staging) hipFree(c->d_staging);
@@ -2732,6 +2750,12 @@ psx_status psx_ctx_set_pipeline(psx_ctx *c, int32_t mode) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   c->pipeline = mode;
+  return PSX_OK;
+}
+
+psx_status psx_ctx_set_seam(psx_ctx *c, int32_t mode) {
+  if (!c || (mode != PSX_SEAM_ASYNC && mode != PSX_SEAM_SYNC)) return PSX_ERR_INVALID_ARG;
+  c->seam_mode = mode;
   return PSX_OK;
 }
 

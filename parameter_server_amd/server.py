@@ -95,6 +95,12 @@ class Server:
     def set_stream(self, hip_stream_handle):
         _check(self._L, self._ctx, self._L.psx_ctx_set_stream(self._ctx, hip_stream_handle))
 
+    def set_seam(self, mode):
+        """psx_ctx_set_seam: 0 (default) ApplyOpLogUpdateVersion returns once its bytes are
+        copied to HBM and the apply is enqueued (device errors surface at the next sync);
+        1 every host call also settles, so its own errors come back from it."""
+        _check(self._L, self._ctx, self._L.psx_ctx_set_seam(self._ctx, int(mode)))
+
     def set_pipeline(self, mode):
         """psx_ctx_set_pipeline: 0 off, 1 calls whose dense tables are all placed from
         record-row lists, 2 every call.  Opt-in: a call's messages must be complete when

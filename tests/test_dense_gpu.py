@@ -123,9 +123,17 @@ def test_modulo_partition_geometry():
     want = orc.read_dense_rows(1, 2, 40, stride=3)
     assert np.array_equal(_bits(got), _bits(want))
     bad = wire.dense_stream_np(1, np.array([3], np.int32), np.ones((1, 16), np.float32))
+    # the seam returns once the bytes are in HBM; the device's row-range check fails the
+    # call at the next sync (PSX_SEAM_ASYNC), or in the call itself with PSX_SEAM_SYNC
+    srv.ApplyOpLogUpdateVersion(bad, bad.size, 100, 1)
     with pytest.raises(PsxError) as e:
-        srv.ApplyOpLogUpdateVersion(bad, bad.size, 100, 1)
+        srv.sync()
     assert e.value.status == 5
+    srv.set_seam(1)
+    with pytest.raises(PsxError) as e:
+        srv.ApplyOpLogUpdateVersion(bad, bad.size, 101, 1)
+    assert e.value.status == 5
+    assert np.array_equal(_bits(srv.read_rows(1, 2, 40)), _bits(want))   # failed calls applied nothing
 
 
 def test_host_path_sequence_matches_oracle():

@@ -121,11 +121,28 @@ def test_device_compressor_on_every_value_class(oracle_lib):
     srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows,
                                      row_bytes_f16=True))
     srv.load_rows(1, 0, pad.reshape(rows, cap))
+    want = np.zeros(pad.size, np.uint16)   # the oracle on the raw bits (signalling NaNs untouched)
+    oracle_lib.orc_floats_to_halves(pad.ctypes.data, want.ctypes.data, pad.size)
+    # the host form (row reads) and the device form (a push body: serve_emit)
     raw = srv.serialize_rows(1, list(range(rows)))
     rec = np.frombuffer(raw, np.uint8).reshape(rows, 12 + 2 * cap)
     got = rec[:, 12:].copy().view(np.uint16).reshape(-1)
-    want = np.array([oracle_lib.orc_float_to_half(ctypes.c_float(x)) for x in pad], np.uint16)
     assert np.array_equal(got, want), int(np.sum(got != want))
+    srv.clear_dirty(1)
+    # make every row dirty without changing a value: a record of zeros (x + 0 keeps x's bits
+    # except -0 + 0 = +0 and NaN payloads quieted: compare against the rows the device now holds)
+    m = wire.dense_stream_np(1, np.arange(rows, dtype=np.int32), np.zeros((rows, cap), np.float32))
+    d = torch.from_numpy(m).cuda()
+    torch.cuda.synchronize()
+    srv.apply_device([(d.data_ptr(), d.numel(), 100, 0)])
+    now = srv.read_rows(1, 0, rows).reshape(-1)
+    want2 = np.zeros(now.size, np.uint16)
+    oracle_lib.orc_floats_to_halves(now.ctypes.data, want2.ctypes.data, now.size)
+    body = bytes(srv.serialize_dirty(clear=True))
+    got2 = np.zeros(now.size, np.uint16)
+    for rid, payload in wire.parse_push_body(body)[1].items():
+        got2[rid * cap:(rid + 1) * cap] = np.frombuffer(payload, np.uint16)
+    assert np.array_equal(got2, want2), int(np.sum(got2 != want2))
     srv.close()
 
 

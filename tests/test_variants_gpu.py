@@ -145,8 +145,9 @@ def test_version_table_then_dense_table_in_one_message():
              oplogs=np.ones((1, cap), np.float32), versions=np.array([0], np.uint64)),
         dict(table_id=3, dense_serialized=False, row_ids=np.array([2], np.int32),
              oplogs=np.ones((1, cap), np.int32))])
+    srv.ApplyOpLogUpdateVersion(bad, bad.size, 101, 0)   # async seam: the device's check fails the call
     with pytest.raises(PsxError) as e:
-        srv.ApplyOpLogUpdateVersion(bad, bad.size, 101, 0)
+        srv.sync()
     assert e.value.status == 10
     d = torch.from_numpy(np.array(bad, copy=True)).cuda()
     torch.cuda.synchronize()

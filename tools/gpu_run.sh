@@ -21,6 +21,7 @@
 #   oldheavy the all-rows-heavy-and-spilling test on ab_old/libpsx.so (reported, never fatal)
 #   splittests the split-apply / sparse / KAT GPU test files only
 #   xtests  the split / exchange pipeline / walk-count / multi-rank GPU test files only
+#   bare    the bare `python bench.py` line, as the driver runs it
 #   t:FILE  pytest -v on one test file (FILE may carry a ::test selector)
 #   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
@@ -172,6 +173,7 @@ for db, ks in d.items():
     xtests) run xtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_split_gpu.py tests/test_walk_count_gpu.py tests/test_multi_rank_gpu.py ;;
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
+    bare) run bare 900 python -u bench.py ;;
     t:*) f=${s#t:}; run t_$(basename "$f" .py) 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread "$f" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

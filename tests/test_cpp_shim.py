@@ -45,3 +45,24 @@ def test_cpp_mirror_matches_oracle(built_lib, oracle_lib, tmp_path):
         assert orc.apply_stream(wire.dense_stream_np(5, ids, vals), 100 + (msg & 1), msg >> 1) == 0
     assert out.read_bytes() == orc.serialize_records(5, list(range(rows)))
     assert "versions 1 1" in r.stdout
+
+
+def test_cpp_exchange_selftest_builds(built_lib):
+    _build(built_lib)
+    assert os.path.exists(os.path.join(CPP, "build", "psx_exchange_selftest"))
+
+
+@pytest.mark.gpu
+def test_cpp_exchange_past_2gib_on_the_images_rccl(built_lib):
+    """libpsx's exchange from a process without torch (tests/cpp/psx_exchange_selftest.cpp):
+    libpsx's -lrccl then loads the ROCm image's RCCL, not torch's copy; a 2 GiB + 12 KiB
+    sub-stream, sent in 512 MiB pieces (psx_exchange.cpp), must arrive intact there too."""
+    import json
+    _build(built_lib)
+    exe = os.path.join(CPP, "build", "psx_exchange_selftest")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    info = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert info["differing_words"] == 0 and info["bytes"] == (2 << 30) + (12 << 10)
+    assert info["rccl"].startswith("/opt/rocm"), info["rccl"]
+    print(info)

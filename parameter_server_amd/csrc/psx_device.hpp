@@ -178,7 +178,7 @@ struct OrdArgs {
                           // can add per slot (zero between calls); null otherwise
   int32_t *split;         // [2][max_rows] row descriptors {slot, list begin, list end, image
                           // size} (int4): touched slots whose image fits 256 entries, the rest
-  uint32_t *nsplit;       // the lists' lengths: 256-entry, 1,024-entry, heavy, capacity dry run
+  uint32_t *nsplit;       // the lists' lengths: 256-entry, 1,024-entry, heavy, capacity dry run, light
   int32_t desc;           // 1: `touched` holds split-list row descriptors (the apply launches)
   int32_t spill;          // split tables, spill mode: ordered_offsets sends only rows already
                           // near 256 entries to the 1,024-entry list; the 256-entry launch
@@ -189,6 +189,9 @@ struct OrdArgs {
   const int32_t *heavy_end;  // heavy-first (spill bit 1): heavy row descriptors end here (the
   const uint32_t *nheavy;    // 256-entry list's region), listed backwards; the 256-entry
                              // launch takes them first
+  int32_t lite;              // split tables: ordered_offsets lists light rows apart (starts_lite)
+  const int32_t *light;      // the 256-entry launch: light row descriptors, taken four to a wave
+  const uint32_t *nlight;    // (lite_quad), after the heavy rows and before the others
   int32_t counted;           // split tables: 1 the walk already counted this call's records
                              // (WalkCount): ordered_count is not launched; 2: it also placed
                              // each record in its slot's list (WalkCount.wfill); 3: ordered_count
@@ -213,7 +216,7 @@ struct WalkCount {
   int64_t row_offset, row_stride, max_rows;
   int32_t *cnt;
   int32_t *grow;
-  uint32_t *nsplit;   // ordered_offsets' list counters [0..3]
+  uint32_t *nsplit;   // ordered_offsets' list counters [0..4]
   int32_t *tsum;      // its record-range base [0]
   int32_t on;
   int32_t pad;

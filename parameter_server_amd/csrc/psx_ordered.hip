@@ -128,8 +128,8 @@ __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
 // in its slot's list, stored per record (its recoff index) for ordered_fill.
 __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfill) {
   __shared__ RecSpace rs;
-  if (a.grow && blockIdx.x == 0 && threadIdx.x < 5) {   // ordered_offsets' counters
-    if (threadIdx.x < 4) a.nsplit[threadIdx.x] = 0;
+  if (a.grow && blockIdx.x == 0 && threadIdx.x < 6) {   // ordered_offsets' counters
+    if (threadIdx.x < 5) a.nsplit[threadIdx.x] = 0;
     else a.tsum[0] = 0;
   }
   // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
@@ -265,13 +265,14 @@ __device__ __forceinline__ int32_t block_excl_sum(int32_t v, int32_t *sh, int32_
   return pre + incl - v;
 }
 
-// Six exclusive prefix sums at once (one LDS exchange, two barriers instead of twelve).
-__device__ __forceinline__ void block_excl_sum6(const int32_t (&v)[6], int32_t (&pre)[6], int32_t (&total)[6],
+// N exclusive prefix sums at once (one LDS exchange, two barriers instead of 2N).
+template <int N>
+__device__ __forceinline__ void block_excl_sumN(const int32_t (&v)[N], int32_t (&pre)[N], int32_t (&total)[N],
                                                 int32_t (*sh)[4]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t incl[6];
+  int32_t incl[N];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < N; ++i) {
     incl[i] = v[i];
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -282,7 +283,7 @@ __device__ __forceinline__ void block_excl_sum6(const int32_t (&v)[6], int32_t (
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < N; ++i) {
     int32_t p = 0, t = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -308,6 +309,15 @@ __device__ __forceinline__ bool starts_heavy(const OrdArgs &a, int32_t c) {
   return (a.spill & 2) && c >= kHeavyRecords;
 }
 
+// Light rows (OrdArgs.lite): the 256-entry launch takes them four to a wave, sixteen lanes
+// each (lite_quad below): few records and an image that stays within 64 entries whatever
+// the call's Incs insert, so a row's dependent chain of loads runs beside three others.
+constexpr int32_t kLiteRecords = 3;
+constexpr int32_t kLiteEntries = 64;
+__device__ __forceinline__ bool starts_lite(const OrdArgs &a, int32_t c, int32_t nen, int32_t grow) {
+  return a.lite && c <= kLiteRecords && (int64_t)nen + grow <= kLiteEntries;
+}
+
 // The capacity dry run's rows: those whose image can outgrow max_entries in this call
 // (entries now + the call's Incs).  Any other row cannot overflow, whatever its keys.
 __device__ __forceinline__ bool may_overflow(const OrdArgs &a, int32_t nen, int32_t grow) {
@@ -315,8 +325,8 @@ __device__ __forceinline__ bool may_overflow(const OrdArgs &a, int32_t nen, int3
 }
 
 __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
-  __shared__ int32_t sh[6][4];
-  __shared__ int32_t base[6];   // touched, records, 256-entry list, 1,024-entry list, heavy rows, dry run
+  __shared__ int32_t sh[7][4];
+  __shared__ int32_t base[7];   // touched, records, 256-entry list, 1,024-entry list, heavy rows, dry run, light rows
   const int64_t R = a.max_rows;
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * per;
@@ -337,10 +347,12 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     const bool t = c > 0;
     const bool big = t && starts_big(a, nen, g);
     const bool heavy = t && !big && starts_heavy(a, c);
+    const bool lite = t && !big && !heavy && starts_lite(a, c, nen, g);
     const bool risky = t && may_overflow(a, nen, g);
-    int32_t pre[6], tot[6];
-    block_excl_sum6({t ? 1 : 0, c, t && !big && !heavy ? 1 : 0, big ? 1 : 0, heavy ? 1 : 0, risky ? 1 : 0}, pre, tot,
-                    sh);
+    int32_t pre[7], tot[7];
+    block_excl_sumN<7>({t ? 1 : 0, c, t && !big && !heavy && !lite ? 1 : 0, big ? 1 : 0, heavy ? 1 : 0,
+                        risky ? 1 : 0, lite ? 1 : 0},
+                       pre, tot, sh);
     if (threadIdx.x == 0) {
       base[0] = tot[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot[0]) : 0;
       base[1] = tot[1] ? atomicAdd(&a.tsum[0], tot[1]) : 0;
@@ -348,6 +360,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       base[3] = tot[3] ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tot[3]) : 0;
       base[4] = tot[4] ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)tot[4]) : 0;
       base[5] = tot[5] ? (int32_t)atomicAdd(&a.nsplit[3], (uint32_t)tot[5]) : 0;
+      base[6] = tot[6] ? (int32_t)atomicAdd(&a.nsplit[4], (uint32_t)tot[6]) : 0;
     }
     __syncthreads();
     if (t) {
@@ -359,13 +372,14 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       if (risky) desc[2 * R + base[5] + pre[5]] = d;
       if (big) desc[R + base[3] + pre[3]] = d;
       else if (heavy) desc[R - 1 - (base[4] + pre[4])] = d;
+      else if (lite) desc[3 * R + base[6] + pre[6]] = d;
       else desc[base[2] + pre[2]] = d;
     }
     return;
   }
   if (!o_gate(a)) return;
   // pass 1: the block's totals, one atomic per counter
-  int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0, nd = 0;
+  int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0, nd = 0, nl = 0;
   for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
     const int32_t c = a.cnt[s];
     if (c > 0) {
@@ -374,13 +388,14 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       const int32_t nen = a.nent[s], g = a.grow[s];
       if (starts_big(a, nen, g)) ++nb;
       else if (starts_heavy(a, c)) ++nh;
+      else if (starts_lite(a, c, nen, g)) ++nl;
       else ++ns;
       if (may_overflow(a, nen, g)) ++nd;
     }
   }
-  int32_t pre1[6], tot1[6];
-  block_excl_sum6({nt, nr, ns, nb, nh, nd}, pre1, tot1, sh);
-  const int32_t tt = tot1[0], tr = tot1[1], ts = tot1[2], tb = tot1[3], th = tot1[4], td = tot1[5];
+  int32_t pre1[7], tot1[7];
+  block_excl_sumN<7>({nt, nr, ns, nb, nh, nd, nl}, pre1, tot1, sh);
+  const int32_t tt = tot1[0], tr = tot1[1], ts = tot1[2], tb = tot1[3], th = tot1[4], td = tot1[5], tl = tot1[6];
   if (threadIdx.x == 0) {
     base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
     base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
@@ -388,6 +403,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tb) : 0;
     base[4] = th ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)th) : 0;
     base[5] = td ? (int32_t)atomicAdd(&a.nsplit[3], (uint32_t)td) : 0;
+    base[6] = tl ? (int32_t)atomicAdd(&a.nsplit[4], (uint32_t)tl) : 0;
   }
   __syncthreads();
   // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row.
@@ -395,11 +411,11 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   // are distinct touched rows, so the two never meet.  The 1,024-entry region [R, 2R) holds
   // the big rows and, appended behind them by the 256-entry launch, the spilled rows (small
   // or heavy, each at most once): at most the touched count in all.
-  int32_t ar = base[1], as = base[2], ab = base[3], ah = base[4], ad = base[5];
+  int32_t ar = base[1], as = base[2], ab = base[3], ah = base[4], ad = base[5], al = base[6];
   for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
     const int64_t s = t0 + threadIdx.x;
     int32_t c = 0, nen = 0;
-    bool big = false, heavy = false, risky = false;
+    bool big = false, heavy = false, risky = false, lite = false;
     if (s < c1) {
       c = a.cnt[s];
       if (c > 0) {
@@ -407,17 +423,19 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
         const int32_t g = a.grow[s];
         big = starts_big(a, nen, g);
         heavy = !big && starts_heavy(a, c);
+        lite = !big && !heavy && starts_lite(a, c, nen, g);
         risky = may_overflow(a, nen, g);
         a.grow[s] = 0;
         if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
       }
     }
     const bool t = c > 0;
-    int32_t pre[6], tot[6];
-    block_excl_sum6({t ? 1 : 0, c, t && !big && !heavy ? 1 : 0, t && big ? 1 : 0, t && heavy ? 1 : 0, t && risky ? 1 : 0},
-                    pre, tot, sh);
-    const int32_t pr = pre[1], ps = pre[2], pb = pre[3], ph = pre[4], pd = pre[5];
-    const int32_t sr = tot[1], ss2 = tot[2], sb = tot[3], sh2 = tot[4], sd = tot[5];
+    int32_t pre[7], tot[7];
+    block_excl_sumN<7>({t ? 1 : 0, c, t && !big && !heavy && !lite ? 1 : 0, t && big ? 1 : 0, t && heavy ? 1 : 0,
+                        t && risky ? 1 : 0, t && lite ? 1 : 0},
+                       pre, tot, sh);
+    const int32_t pr = pre[1], ps = pre[2], pb = pre[3], ph = pre[4], pd = pre[5], pl = pre[6];
+    const int32_t sr = tot[1], ss2 = tot[2], sb = tot[3], sh2 = tot[4], sd = tot[5], sl = tot[6];
     if (t) {
       const int32_t beg = ar + pr;
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
@@ -425,6 +443,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       if (risky) desc[2 * R + ad + pd] = d;   // the capacity dry run's list
       if (big) desc[R + ab + pb] = d;
       else if (heavy) desc[R - 1 - (ah + ph)] = d;
+      else if (lite) desc[3 * R + al + pl] = d;
       else desc[as + ps] = d;
     }
     ar += sr;
@@ -432,6 +451,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     ab += sb;
     ah += sh2;
     ad += sd;
+    al += sl;
   }
 }
 
@@ -900,6 +920,388 @@ __device__ __forceinline__ T bcast(T x, int src) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Light rows, four to a wave (OrdArgs.lite, starts_lite): lane group g = lane / 16 takes
+// row 4q + g of the light list, and its 16 lanes hold the row's image striped as the
+// register kernel's (entry i in lane i % 16 of the group, register i / 16; <= 64 entries
+// for the whole call).  The row's dependent loads (descriptor, record references, headers,
+// image) go out beside three other rows', which is the point: one row per wave left the
+// SIMDs waiting on those chains (DESIGN.md §5, C3 counters).  Control that depends on the
+// row (its records, Incs, found / insert / removal) is group-uniform: groups diverge as
+// wholes, and the one-slot shifts are DPP rotates within a 16-lane row.  FindIndex is four
+// compares and a ballot (no key map at 64 entries).  SortedVectorMapStore::Inc
+// (sorted_vector_map_store.hpp:175-197,305-337) and MapStore::Inc (map_store.hpp:60-65)
+// semantics as the register kernel, Inc by Inc.
+template <typename T>
+__device__ __forceinline__ T row_rot(T x, bool right) {
+  // row_ror:1 (lane l <- l-1 within its row of 16) / row_ror:15 (lane l <- l+1)
+  if constexpr (sizeof(T) == 4) {
+    int v = __builtin_bit_cast(int, x);
+    v = right ? __builtin_amdgcn_update_dpp(0, v, 0x121, 0xf, 0xf, false)
+              : __builtin_amdgcn_update_dpp(0, v, 0x12F, 0xf, 0xf, false);
+    return __builtin_bit_cast(T, v);
+  } else {
+    long long v = __builtin_bit_cast(long long, x);
+    int lo = (int)v, hi = (int)(v >> 32);
+    const int c = right ? 0x121 : 0x12F;
+    if (right) {
+      lo = __builtin_amdgcn_update_dpp(0, lo, 0x121, 0xf, 0xf, false);
+      hi = __builtin_amdgcn_update_dpp(0, hi, 0x121, 0xf, 0xf, false);
+    } else {
+      lo = __builtin_amdgcn_update_dpp(0, lo, 0x12F, 0xf, 0xf, false);
+      hi = __builtin_amdgcn_update_dpp(0, hi, 0x12F, 0xf, 0xf, false);
+    }
+    (void)c;
+    return __builtin_bit_cast(T, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+
+// Lane src (0..15) of the caller's 16-lane group.
+template <typename T>
+__device__ __forceinline__ T gshfl(T x, int src) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __shfl(__builtin_bit_cast(int, x), src, 16));
+  } else {
+    long long v = __builtin_bit_cast(long long, x);
+    const int lo = __shfl((int)v, src, 16), hi = __shfl((int)(v >> 32), src, 16);
+    return __builtin_bit_cast(T, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+
+// Remove entry idx of a group's striped image (the Inc that made it zero): sorted maps move
+// entries (idx, n) down one (RemoveOneEntryAndCompact, sorted_vector_map_store.hpp:289-303,
+// :329-334), maps move the last entry into the hole (MapStore erase, map_store.hpp:63-64).
+// pos: the group's key map (null: none) — the removed key leaves it, moved keys follow.
+template <typename V, int KIND>
+__device__ __forceinline__ void lite_remove(int32_t (&key)[4], V (&val)[4], int32_t &n, int32_t idx, int gl,
+                                            int8_t *pos) {
+  if (pos) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j * 16 + gl == idx) pos[key[j]] = -1;
+  }
+  if constexpr (KIND == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t kl = row_rot(key[j], false);
+      const V vl = row_rot(val[j], false);
+      int32_t kn = 0;
+      V vn = V(0);
+      if (j + 1 < 4) {
+        kn = row_rot(key[j + 1], false);
+        vn = row_rot(val[j + 1], false);
+      }
+      const int32_t i = j * 16 + gl;
+      if (i >= idx && i < n - 1) {
+        key[j] = gl == 15 ? kn : kl;
+        val[j] = gl == 15 ? vn : vl;
+        if (pos) pos[key[j]] = (int8_t)i;
+      }
+    }
+  } else {
+    const int jl = (n - 1) >> 4, lla = (n - 1) & 15;
+    int32_t lk = 0;
+    V lv = V(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j == jl) {
+        lk = gshfl(key[j], lla);
+        lv = gshfl(val[j], lla);
+      }
+    if (idx != n - 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j * 16 + gl == idx) {
+          key[j] = lk;
+          val[j] = lv;
+          if (pos) pos[lk] = (int8_t)idx;
+        }
+    }
+  }
+  --n;
+}
+
+// One Inc(c, dd) on a group's striped image (the inserts between found runs, and every Inc
+// of a row whose keys leave [0, 1024), where the key map cannot index them).
+template <typename V, int KIND>
+__device__ __forceinline__ void lite_inc(int32_t (&key)[4], V (&val)[4], int32_t &n, int32_t c, V dd, int gl, int gb,
+                                         int8_t *pos, const OrdArgs &a) {
+  int32_t idx = -1;                                   // FindIndex :230-238
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t gm = (uint32_t)(__ballot(j * 16 + gl < n && key[j] == c) >> gb) & 0xffffu;
+    if (idx < 0 && gm) idx = j * 16 + __builtin_ctz(gm);
+  }
+  if (idx >= 0) {
+    // found: add in place (no re-sort, :325-327); the owner lane tells the group if it hit 0
+    bool z = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j * 16 + gl == idx) {
+        val[j] = OV<V>::add(val[j], dd);
+        z = val[j] == V(0);
+      }
+    if ((__ballot(z) >> gb) & 0xffffu) lite_remove<V, KIND>(key, val, n, idx, gl, pos);
+    return;
+  }
+  if (n >= a.max_entries) {
+    if (gl == 0) atomicOr(a.call_status, kStCapacity);
+    return;
+  }
+  int32_t p = n;
+  if constexpr (KIND == 1) {
+    // LinearSearchAndMove backward (:264-285): after the last entry whose value is not
+    // strictly smaller than the delta
+    int32_t pmax = -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t gm = (uint32_t)(__ballot(j * 16 + gl < n && !(dd > val[j])) >> gb) & 0xffffu;
+      if (gm) pmax = j * 16 + 31 - __builtin_clz(gm);
+    }
+    p = pmax + 1;
+    // entries [p, n) move up one: descending registers, rotate right within the row
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+      const int32_t kr = row_rot(key[j], true);
+      const V vr = row_rot(val[j], true);
+      int32_t kp = 0;
+      V vp = V(0);
+      if (j > 0) {
+        kp = row_rot(key[j - 1], true);
+        vp = row_rot(val[j - 1], true);
+      }
+      const int32_t i = j * 16 + gl;
+      if (i > p && i <= n) {
+        key[j] = gl == 0 ? kp : kr;
+        val[j] = gl == 0 ? vp : vr;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j * 16 + gl == p) {
+      key[j] = c;
+      val[j] = dd;
+    }
+  ++n;
+  if (pos) {   // entries [p, n) have new indices
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t i = j * 16 + gl;
+      if (i >= p && i < n) pos[key[j]] = (int8_t)i;
+    }
+  }
+}
+
+// A light row's group (16 lanes of the caller's wave) applies its row.  pos: the group's
+// key map (int8 per key of [0, 1024), -1 between rows), sv: its 64-value delta scratch
+// (zero between runs), scr: the wave's 64-entry sort scratch (16 per group).
+// Per record chunk of <= 16 pairs (lane t: pair t), as the register kernel's found_run:
+// every lane looks its key up in the map at once; the pairs up to the chunk's next insert
+// are found keys, applied together (each adds in place, sorted_vector_map_store.hpp:325-327;
+// their deltas scattered by entry index, one add per register; the entries that reached
+// zero removed afterwards, which leaves the same image as removing them in Inc order); the
+// insert then goes Inc by Inc (LinearSearchAndMove, :264-285) and the next run starts.
+template <typename V, int KIND>
+__device__ __forceinline__ void lite_quad(const OrdArgs &a, int64_t q, int64_t nl, uint64_t *scr, int8_t *pos, V *sv,
+                                          int32_t *pc, V *pv, const uint8_t *const *sdata, int lane) {
+  // a record reference's bytes: the messages' base pointers from LDS (an index that differs
+  // across the wave's groups into the kernel arguments would be one more dependent global load)
+  auto rptr = [&](uint64_t e) { return sdata[e >> 56] + (e & kRefOffMask); };
+  constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
+  const int gl = lane & 15, gb = lane & 48;
+  const int64_t r = q * 4 + (lane >> 4);
+  int4 d = int4{0, 0, 0, 0};
+  if (r < nl) d = reinterpret_cast<const int4 *>(a.light)[r];
+  const int64_t slot = d.x;
+  const int32_t beg = d.y, L = d.z - d.y;
+  int32_t n = d.w;
+  const bool live = L > 0;
+  // the record references, each record's pair count and the image go out together
+  const uint64_t ref = gl < L ? a.list[beg + gl] : ~0ull;
+  int32_t hn = 0;
+  if (gl < L) hn = o_ld32(rptr(ref) + 4);
+  const uint8_t *row = a.entries + slot * a.max_entries * ES;
+  int32_t key[4];
+  V val[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int32_t i = j * 16 + gl;
+    key[j] = live && i < n ? o_ld32(row + (int64_t)i * ES) : 0;
+    val[j] = live && i < n ? ldv<V>(row + (int64_t)i * ES + VO) : V(0);
+  }
+  if (live && gl == 0) a.flags[slot] = 3;
+  // records in (message, position) order: a rank sort of the <= kLiteRecords references
+  int rank = 0;
+#pragma unroll
+  for (int k = 0; k < kLiteRecords; ++k) {
+    const uint64_t x = gshfl(ref, k);
+    rank += (k < L && x < ref) ? 1 : 0;
+  }
+  if (gl < L) {
+    scr[gb + rank] = ref;
+    scr[gb + 8 + rank] = (uint64_t)(uint32_t)hn;
+  }
+  // the key map while every key of the row stays in [0, 1024) (group-uniform)
+  bool out = false;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out = out || (j * 16 + gl < n && (uint32_t)key[j] >= 1024u);
+  bool use_pos = live && ((__ballot(out) >> gb) & 0xffffu) == 0;
+  if (use_pos) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j * 16 + gl < n) pos[key[j]] = (int8_t)(j * 16 + gl);
+  }
+  wave_sync();
+  const uint64_t mine = gl < L ? scr[gb + gl] : 0ull;
+  const int32_t mn = gl < L ? (int32_t)scr[gb + 8 + gl] : 0;
+  wave_sync();
+  // Every pair of the row's records (<= 64: the image plus them stays within 64 entries)
+  // loaded at once into the group's LDS staging, in record order: one memory round trip
+  // instead of one per record chunk.
+  const int32_t n0 = gshfl(mn, 0), n1 = L > 1 ? gshfl(mn, 1) : 0, n2 = L > 2 ? gshfl(mn, 2) : 0;
+  const int32_t total = n0 + n1 + n2;
+  {
+    const uint64_t r0 = gshfl(mine, 0), r1 = gshfl(mine, 1), r2 = gshfl(mine, 2);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int32_t k = m * 16 + gl;
+      if (k < total) {
+        const int qq = k >= n0 + n1 ? 2 : k >= n0 ? 1 : 0;
+        const int32_t o = qq == 2 ? k - n0 - n1 : qq == 1 ? k - n0 : k;
+        const int32_t nq = qq == 2 ? n2 : qq == 1 ? n1 : n0;
+        const uint8_t *rp = rptr(qq == 2 ? r2 : qq == 1 ? r1 : r0);
+        pc[k] = o_ld32(rp + 8 + (int64_t)o * 4);
+        pv[k] = ldv<V>(rp + 8 + (int64_t)nq * 4 + (int64_t)o * sizeof(V));
+      }
+    }
+  }
+  wave_sync();
+  for (int q2 = 0; q2 < kLiteRecords; ++q2) {
+    if (q2 >= L || a.lite == 3) break;   // group-uniform (lite 3: timing probe, no Incs applied)
+    const int32_t nn = q2 == 0 ? n0 : q2 == 1 ? n1 : n2;
+    const int32_t pbase = q2 == 0 ? 0 : q2 == 1 ? n0 : n0 + n1;
+    for (int32_t c0 = 0; c0 < nn; c0 += 16) {
+      const int32_t pi = c0 + gl;
+      const int32_t col = pi < nn ? pc[pbase + pi] : 0;
+      const V dv = pi < nn ? pv[pbase + pi] : V(0);
+      const int32_t cnt = nn - c0 < 16 ? nn - c0 : 16;
+      if (use_pos && ((__ballot(gl < cnt && (uint32_t)col >= 1024u) >> gb) & 0xffffu)) {
+        // a key the map cannot index: clear the map (every mapped key is in the image) and
+        // finish the row Inc by Inc
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j * 16 + gl < n) pos[key[j]] = -1;
+        wave_sync();
+        use_pos = false;
+      }
+      if (!use_pos) {
+        for (int32_t t = 0; t < cnt; ++t) {
+          const int32_t c = gshfl(col, t);
+          const V dd = gshfl(dv, t);
+          if (dd == V(0)) continue;                       // :306
+          lite_inc<V, KIND>(key, val, n, c, dd, gl, gb, nullptr, a);
+        }
+        continue;
+      }
+      for (int32_t t = 0; t < cnt;) {
+        wave_sync();
+        const int32_t my_idx = gl < cnt ? (int32_t)pos[col] : -1;
+        const bool lv = gl >= t && gl < cnt && dv != V(0);
+        const uint32_t ins = (uint32_t)(__ballot(lv && my_idx < 0) >> gb) & 0xffffu;
+        const int32_t run_end = ins ? __builtin_ctz(ins) : cnt;
+        if (run_end > t) {
+          // the found run [t, run_end): distinct keys (a record's columns are distinct)
+          const bool run = lv && gl < run_end;
+          if (run) sv[my_idx] = dv;
+          wave_sync();
+          uint32_t rmm[4];
+          bool anyrm = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int32_t i = j * 16 + gl;
+            bool z = false;
+            if (i < n) {
+              const V x = sv[i];
+              if (x != V(0)) {
+                val[j] = OV<V>::add(val[j], x);
+                sv[i] = V(0);
+                z = val[j] == V(0);
+              }
+            }
+            rmm[j] = (uint32_t)(__ballot(z) >> gb) & 0xffffu;
+            anyrm = anyrm || rmm[j] != 0;
+          }
+          if (anyrm) {
+            // highest index first: the lower removed indices stay where they are
+            for (int j = 3; j >= 0; --j) {
+              while (rmm[j]) {
+                const int32_t b = 31 - __builtin_clz(rmm[j]);
+                rmm[j] &= ~(1u << b);
+                lite_remove<V, KIND>(key, val, n, j * 16 + b, gl, pos);
+              }
+            }
+          }
+          t = run_end;
+          continue;
+        }
+        // an insert: pair t is not in the image
+        const int32_t c = gshfl(col, t);
+        const V dd = gshfl(dv, t);
+        lite_inc<V, KIND>(key, val, n, c, dd, gl, gb, pos, a);
+        ++t;
+      }
+    }
+  }
+  if (use_pos) {   // back to all -1: every key the row still maps is in its image
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j * 16 + gl < n) pos[key[j]] = -1;
+  }
+  wave_sync();
+  if (live) {
+    // the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)
+    uint8_t *wrow = a.entries + slot * a.max_entries * ES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t i = j * 16 + gl;
+      if (i < n) {
+        *reinterpret_cast<int32_t *>(wrow + (int64_t)i * ES) = key[j];
+        if (ES == 16) *reinterpret_cast<int32_t *>(wrow + (int64_t)i * ES + 4) = 0;
+        stv<V>(wrow + (int64_t)i * ES + VO, val[j]);
+      }
+    }
+    if (gl == 0) {
+      a.nent[slot] = n;
+      if (a.ver) a.ver[slot] += (uint64_t)L;   // VersionServerRow: +1 per record
+    }
+  }
+}
+
+// The light rows as a launch of their own: wave w takes quads w, w + nwaves, ...
+template <typename V, int KIND>
+__global__ void __launch_bounds__(256) ordered_apply_lite_kernel(OrdArgs a) {
+  __shared__ uint64_t sort_scratch[4][64];
+  __shared__ int8_t s_pos[16][1024];   // per group: key -> entry index, -1 absent
+  __shared__ V s_sv[16][64];           // per group: found-run deltas by entry index
+  __shared__ int32_t s_pc[16][64];     // per group: the row's (column, delta) pairs, record order
+  __shared__ V s_pv[16][64];
+  __shared__ const uint8_t *s_data[kMaxFused];   // the call's message base pointers
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const uint32_t st0 = *a.call_status, sk0 = *a.sticky, nl0 = *a.nlight;
+  const bool go = !(st0 & (kStFatal | kStDuplicateRow)) && (a.force || !(sk0 & kStDuplicateRow));
+  const int64_t nq = ((int64_t)nl0 + 3) / 4;
+  if (!go || (int64_t)blockIdx.x * 4 >= nq) return;
+  const int g = wib * 4 + (lane >> 4);
+  if (threadIdx.x < kMaxFused) s_data[threadIdx.x] = a.ss.data[threadIdx.x];
+  for (int k = lane & 15; k < 1024; k += 16) s_pos[g][k] = -1;
+  for (int k = lane & 15; k < 64; k += 16) s_sv[g][k] = V(0);
+  __syncthreads();
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t q = (int64_t)blockIdx.x * 4 + wib; q < nq; q += nwaves)
+    lite_quad<V, KIND>(a, q, (int64_t)nl0, sort_scratch[wib], s_pos[g], s_sv[g], s_pc[g], s_pv[g], s_data, lane);
+}
+
 // Found-key update of a striped image: entry (jj, l) += d, returning its new value.  jj
 // is wave-uniform, so a binary search over the J registers costs log2(J) uniform branches
 // instead of J guarded blocks.  (A branch-free form — one compare of every register's
@@ -1031,8 +1433,8 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
 
   // one touched row per wave at a time (rows are independent; hot rows spread out);
   // heavy-first: the heavy rows' list (descending from heavy_end) before the rest
-  const int64_t nh = go && a.nheavy ? (int64_t)*a.nheavy : 0;
-  const int64_t nt = go ? nh + (int64_t)*a.ntouched : 0;
+  const int64_t nh = go ? (int64_t)nh0 : 0;
+  const int64_t nt = go ? nh + (int64_t)nt0 : 0;
   // Descriptor lists: the wave's next row's descriptor is loaded a row ahead (a scalar load:
   // the index is wave-uniform), so a row's setup starts from its record list, not from its
   // descriptor.
@@ -1535,12 +1937,17 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
         small.heavy_end = a.split + 4 * a.max_rows;   // end of the 256-entry list's region
         small.nheavy = a.nsplit + 2;
       }
-      if (!a.spill) {
+      if (a.lite) {   // light rows, four to a wave, in a launch of their own
+        small.light = a.split + 12 * a.max_rows;
+        small.nlight = a.nsplit + 4;
+      }
+      if (!a.spill) {   // concurrent launches: the side stream starts behind the prep
         hipError_t e = hipEventRecord(fk.fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(fk.aux, fk.fork, 0);
         if (e != hipSuccess) return e;
       }
     }
+
 #define PSX_REG(V, KIND)                                                                           \
   do {                                                                                             \
     if (a.max_entries <= 64)                                                                       \
@@ -1548,6 +1955,9 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
     else if (a.max_entries <= 256)                                                                 \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4, false, true>), dim3(blocks), dim3(256), 0, st, a); \
     else if (a.grow && a.spill) {                                                                  \
+      if (a.lite)   /* the light rows, four to a wave, before the 256-entry launch */              \
+        hipLaunchKernelGGL((ordered_apply_lite_kernel<V, KIND>), dim3(row_blocks((a.max_rows + 3) / 4, 4)), \
+                           dim3(256), 0, st, small);                                               \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, false, true>), dim3(few_row_blocks(a.max_rows)), dim3(256), 0, st, big); \
     } else if (a.grow) {                                                                           \

@@ -42,6 +42,7 @@ int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
+int g_ord_lite = 1;     // PSX_VARIANT_ORD_LITE: split tables take light rows four to a wave
 int g_walk_skew = 0;    // PSX_DEBUG_WALK_SKEW: skew early-published walk states (tests the cross-check)
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
 int g_walk_all_cus = 1;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU
@@ -775,6 +776,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       a.split = t.d_split;
       a.nsplit = t.d_nsplit + 5 * slot;
       a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
+      // light rows four to a wave (psx_ordered.hip lite_quad): spill mode, sorted/map rows
+      // without importance (the light path does not sum it)
+      a.lite = psx::g_ord_lite && a.spill && !t.d_imp ? psx::g_ord_lite : 0;
       a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1)
                   : (psx::g_walk_rank && !t.cfg.oplog_dense_serialized && c->d_wfill[slot] ? 3 : 0);
     }
@@ -1429,7 +1433,7 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
   if (e == hipSuccess && t.split()) {
     e = hipMalloc(&t.d_grow, 2 * R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, 2 * R * sizeof(int32_t), c->stream);
-    if (e == hipSuccess) e = hipMalloc(&t.d_split, 3 * R * 4 * sizeof(int32_t));   // int4 descriptors x 3 lists
+    if (e == hipSuccess) e = hipMalloc(&t.d_split, 4 * R * 4 * sizeof(int32_t));   // int4 descriptors x 4 lists
     if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * 5 * sizeof(uint32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -2850,6 +2854,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_FOLD_FINISH: return &psx::g_fold_finish;
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
     case PSX_DEBUG_WALK_SKEW: return &psx::g_walk_skew;
+    case PSX_VARIANT_ORD_LITE: return &psx::g_ord_lite;
     case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
     case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
     case PSX_VARIANT_OFFSETS_GRID: return &psx::g_offsets_blocks;
@@ -2892,6 +2897,7 @@ struct VariantEnv {
   VariantEnv() {
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
+    if (const char *v = getenv("PSX_ORD_LITE")) psx::g_ord_lite = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
     if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);

@@ -216,3 +216,77 @@ def test_every_row_heavy_and_spilling():
         srv.close()
     finally:
         L.psx_debug_set_variant(ORD_SPLIT, old)
+
+
+ORD_LITE = 22
+
+
+@pytest.mark.parametrize("lite", [1, 0], ids=["lite", "one-row-per-wave"])
+@pytest.mark.parametrize("kind,dt", [(SORTED_MAP, I32), (SORTED_MAP, F64), (SORTED_MAP, F32), (MAP, I32),
+                                     (MAP, F64)], ids=["sorted-i32", "sorted-f64", "sorted-f32", "map-i32", "map-f64"])
+def test_light_rows_four_to_a_wave(lite, kind, dt):
+    """Light rows (<= 3 records in the call, image + Incs <= 64 entries: PSX_VARIANT_ORD_LITE)
+    go four to a wave, 16 lanes each.  Rows built for every branch of the 16-lane path:
+    inserts at every position (values of both signs and ties with existing values), found
+    keys, entries that reach zero and are removed (first, middle, last, twice in a row),
+    records of 1-48 pairs (1-3 sixteen-pair chunks), images from 0 to 64 entries, a row
+    with exactly 64 entries after the call, and light rows mixed with heavy and 256-entry
+    ones in one call; rows with < 4 live groups in the last quad.  Byte-exact (sorted) /
+    {col -> value} (map) against the oracle over five calls, both with the light path on
+    and off."""
+    L = _abi.load()
+    old_s = L.psx_debug_set_variant(ORD_SPLIT, 3)
+    old_l = L.psx_debug_set_variant(ORD_LITE, lite)
+    try:
+        rng = np.random.RandomState(300 + 10 * kind + dt)
+        rows, K = 1501, 1024     # 1501: the last light quad is partly empty
+        bgs = [100, 101, 102, 103]
+        srv = psa.Server(0, 1, bgs)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=dt, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        orc = OracleServer(bgs)
+        orc.create_table(3, kind, dt, 0, oplog_dense_serialized=False)
+        for v in range(5):
+            msgs = [[] for _ in bgs]
+            for r in range(rows):
+                if rng.rand() < 0.2:
+                    continue
+                cls = r % 10
+                nrec = int(rng.randint(1, 4)) if cls < 8 else int(rng.randint(4, 7))   # light / heavy
+                for m in rng.choice(len(bgs), size=min(nrec, len(bgs)), replace=False):
+                    if cls == 9:      # wide rows: the 256-entry launch
+                        cols = np.sort(rng.choice(K, size=rng.randint(40, 90), replace=False))
+                    elif cls == 7:    # a small key space: found keys, zeros, removals
+                        cols = np.sort(rng.choice(24, size=rng.randint(1, 20), replace=False))
+                    else:
+                        cols = np.sort(rng.choice(60, size=rng.randint(1, 16 if cls < 4 else 48 // nrec),
+                                                  replace=False))
+                    if dt == I32:
+                        vals = rng.randint(1, 3, size=cols.size) * rng.choice([-1, 1], size=cols.size)
+                    else:   # small integers in float: exact zeros and ties happen
+                        vals = (rng.randint(1, 3, size=cols.size) * rng.choice([-1, 1], size=cols.size)).astype(float)
+                    msgs[m].append((r, cols.astype(np.int32), vals.astype(NP[dt])))
+            streams = [wire.sparse_stream_np(3, VS[dt], recs) for recs in msgs]
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+            srv.sync()
+            for s, bg in zip(streams, bgs):
+                assert orc.apply_stream(s, bg, v) == 0
+            ids = list(range(rows))
+            if kind == SORTED_MAP:
+                assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids), f"call {v}"
+            else:
+                for r in ids:
+                    g, w = srv.serialize_rows(3, [r]), orc.serialize_records(3, [r])
+                    assert len(g) == len(w), f"call {v} row {r}"
+                    if g:
+                        assert _as_map(g[12:], dt) == _as_map(w[12:], dt), f"call {v} row {r}"
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(ORD_SPLIT, old_s)
+        L.psx_debug_set_variant(ORD_LITE, old_l)
+
+
+def test_light_path_is_the_default():
+    assert _abi.load().psx_debug_get_variant(ORD_LITE) == 1

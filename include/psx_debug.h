@@ -54,9 +54,10 @@ enum {
                                    its slot's list from the count (the walk's or ordered_count's),
                                    so ordered_fill needs no atomics; 0: ordered_fill takes the
                                    places back from the counts */,
-  PSX_VARIANT_ORD_LITE = 22,    /* 1 (default): split sorted/map tables (256 < max_entries <= 1024) give
-                                   rows of <= 3 records whose image stays within 64 entries to the
-                                   256-entry launch four to a wave, 16 lanes each; 0: one row per wave */
+  PSX_VARIANT_ORD_LITE = 22,    /* 1: split sorted/map tables (256 < max_entries <= 1024) give rows of
+                                   <= 3 records whose image stays within 64 entries to a launch of
+                                   their own, four to a wave, 16 lanes each; 0 (default): one row per
+                                   wave */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from
                                    its composed maps by one record; the cross-check after the
                                    window's resolve must fail the call (PSX_ERR_DEVICE, nothing

@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void lite_quad(const OrdArgs &a, int64_t q, int64_t n
   }
   wave_sync();
   for (int q2 = 0; q2 < kLiteRecords; ++q2) {
-    if (q2 >= L || a.lite == 3) break;   // group-uniform (lite 3: timing probe, no Incs applied)
+    if (q2 >= L) break;   // group-uniform
     const int32_t nn = q2 == 0 ? n0 : q2 == 1 ? n1 : n2;
     const int32_t pbase = q2 == 0 ? 0 : q2 == 1 ? n0 : n0 + n1;
     for (int32_t c0 = 0; c0 < nn; c0 += 16) {

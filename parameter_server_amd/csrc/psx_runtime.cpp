@@ -42,7 +42,8 @@ int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
-int g_ord_lite = 1;     // PSX_VARIANT_ORD_LITE: split tables take light rows four to a wave
+int g_ord_lite = 0;     // PSX_VARIANT_ORD_LITE: 1 = split tables take light rows four to a wave (C3 apply
+                        // 0.054 ms against 0.048 with it off, profiles/r05/s9: a variant, not the default)
 int g_walk_skew = 0;    // PSX_DEBUG_WALK_SKEW: skew early-published walk states (tests the cross-check)
 int g_walk_levels = 4;  // PSX_VARIANT_WALK_LEVELS: composed exit-map levels of the walk (0 = window by window)
 int g_walk_all_cus = 1;  // PSX_VARIANT_WALK_CUS: the walk's persistent grid: 0 half the CUs, 1 every CU, n >= 2 n blocks per CU

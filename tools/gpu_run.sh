@@ -21,7 +21,8 @@
 #   oldheavy the all-rows-heavy-and-spilling test on ab_old/libpsx.so (reported, never fatal)
 #   splittests the split-apply / sparse / KAT GPU test files only
 #   xtests  the split / exchange pipeline / walk-count / multi-rank GPU test files only
-#   c3lite  C3 with the light-row path on and off (PSX_ORD_LITE 1, 0), twice, interleaved
+#   c3ab    C3 A/B over one variant: AB_VAR (an env override, default PSX_ORD_LITE) set to each
+#           of AB_VALUES in turn (default "0 1 0 1")
 #   bare    the bare `python bench.py` line, as the driver runs it
 #   t:FILE  pytest -v on one test file (FILE may carry a ::test selector)
 #   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
@@ -108,9 +109,6 @@ for db, ks in d.items():
         P=$((P+1))
       done
       python3 tools/pmc_db.py $(find "$R/pmc3" -name '*.db' | sort) > "$O/pmc3.json" && echo "pmc3 summarised" ;;
-    c3ab) run c3ab_off 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 &&
-          run c3ab_on 300 env PSX_ORD_PIPELINE=1 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 &&
-          run c3ab_off2 300 env PSX_ORD_PIPELINE=0 python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 ;;
     c3split) i=0; for v in 1 2 3 1 2 3; do i=$((i+1)); run c3split_${i}_v$v 300 env PSX_ORD_SPLIT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
              grep -h '^{' $O/c3split_*.log | cut -c1-400 ;;
     c3walk) i=0; for v in 0 1 0 1; do i=$((i+1)); run c3walk_${i}_cus$v 300 env PSX_WALK_CUS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
@@ -175,8 +173,8 @@ for db, ks in d.items():
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
     bare) run bare 900 python -u bench.py ;;
-    c3lite) i=0; for v in ${LITE_VALUES:-1 0 1 0}; do i=$((i+1)); run c3lite_${i}_v$v 300 env PSX_ORD_LITE=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
-            for f in $O/c3lite_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
+    c3ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c3ab_${i}_v$v 300 env ${AB_VAR:-PSX_ORD_LITE}=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+            for f in $O/c3ab_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     t:*) f=${s#t:}; run t_$(basename "$f" .py) 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread "$f" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -12,7 +12,8 @@
 
 namespace psx {
 
-constexpr int kMaxFused = 16;   // == PSX_MAX_FUSED_STREAMS
+constexpr int kMaxFused = 16;
+constexpr int kNsStride = 32;   // OrdArgs::nsplit: uint32 words between two counters   // == PSX_MAX_FUSED_STREAMS
 constexpr int kMaxTables = 64;  // == PSX_MAX_TABLES
 constexpr int kWave = 64;
 
@@ -179,6 +180,8 @@ struct OrdArgs {
   int32_t *split;         // [2][max_rows] row descriptors {slot, list begin, list end, image
                           // size} (int4): touched slots whose image fits 256 entries, the rest
   uint32_t *nsplit;       // the lists' lengths: 256-entry, 1,024-entry, heavy, capacity dry run, light
+                          // (counter k at nsplit[k * kNsStride]: one 128-B line each, so the
+                          // blocks' atomics on different counters do not queue on one line)
   int32_t desc;           // 1: `touched` holds split-list row descriptors (the apply launches)
   int32_t spill;          // split tables, spill mode: ordered_offsets sends only rows already
                           // near 256 entries to the 1,024-entry list; the 256-entry launch

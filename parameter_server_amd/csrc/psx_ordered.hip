@@ -129,7 +129,7 @@ __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
 __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfill) {
   __shared__ RecSpace rs;
   if (a.grow && blockIdx.x == 0 && threadIdx.x < 6) {   // ordered_offsets' counters
-    if (threadIdx.x < 5) a.nsplit[threadIdx.x] = 0;
+    if (threadIdx.x < 5) a.nsplit[threadIdx.x * kNsStride] = 0;
     else a.tsum[0] = 0;
   }
   // a call whose decode failed has no trustworthy record offsets or sizes: nothing to count
@@ -356,11 +356,11 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     if (threadIdx.x == 0) {
       base[0] = tot[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot[0]) : 0;
       base[1] = tot[1] ? atomicAdd(&a.tsum[0], tot[1]) : 0;
-      base[2] = tot[2] ? (int32_t)atomicAdd(&a.nsplit[0], (uint32_t)tot[2]) : 0;
-      base[3] = tot[3] ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tot[3]) : 0;
-      base[4] = tot[4] ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)tot[4]) : 0;
-      base[5] = tot[5] ? (int32_t)atomicAdd(&a.nsplit[3], (uint32_t)tot[5]) : 0;
-      base[6] = tot[6] ? (int32_t)atomicAdd(&a.nsplit[4], (uint32_t)tot[6]) : 0;
+      base[2] = tot[2] ? (int32_t)atomicAdd(&a.nsplit[0 * kNsStride], (uint32_t)tot[2]) : 0;
+      base[3] = tot[3] ? (int32_t)atomicAdd(&a.nsplit[1 * kNsStride], (uint32_t)tot[3]) : 0;
+      base[4] = tot[4] ? (int32_t)atomicAdd(&a.nsplit[2 * kNsStride], (uint32_t)tot[4]) : 0;
+      base[5] = tot[5] ? (int32_t)atomicAdd(&a.nsplit[3 * kNsStride], (uint32_t)tot[5]) : 0;
+      base[6] = tot[6] ? (int32_t)atomicAdd(&a.nsplit[4 * kNsStride], (uint32_t)tot[6]) : 0;
     }
     __syncthreads();
     if (t) {
@@ -399,11 +399,11 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   if (threadIdx.x == 0) {
     base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
     base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
-    base[2] = ts ? (int32_t)atomicAdd(&a.nsplit[0], (uint32_t)ts) : 0;
-    base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1], (uint32_t)tb) : 0;
-    base[4] = th ? (int32_t)atomicAdd(&a.nsplit[2], (uint32_t)th) : 0;
-    base[5] = td ? (int32_t)atomicAdd(&a.nsplit[3], (uint32_t)td) : 0;
-    base[6] = tl ? (int32_t)atomicAdd(&a.nsplit[4], (uint32_t)tl) : 0;
+    base[2] = ts ? (int32_t)atomicAdd(&a.nsplit[0 * kNsStride], (uint32_t)ts) : 0;
+    base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1 * kNsStride], (uint32_t)tb) : 0;
+    base[4] = th ? (int32_t)atomicAdd(&a.nsplit[2 * kNsStride], (uint32_t)th) : 0;
+    base[5] = td ? (int32_t)atomicAdd(&a.nsplit[3 * kNsStride], (uint32_t)td) : 0;
+    base[6] = tl ? (int32_t)atomicAdd(&a.nsplit[4 * kNsStride], (uint32_t)tl) : 0;
   }
   __syncthreads();
   // pass 2: tiles of 256 slots in slot order, block prefix sums place each touched row.
@@ -1871,7 +1871,7 @@ static void launch_dry(const OrdArgs &a0, int dtype, hipStream_t st) {
   OrdArgs a = a0;
   if (a.grow) {   // split tables: the rows that may overflow (ordered_offsets), as descriptors
     a.touched = a.split + 2 * 4 * a.max_rows;
-    a.ntouched = a.nsplit + 3;
+    a.ntouched = a.nsplit + 3 * kNsStride;
     a.desc = 1;
   }
   // (the rows are rare — keys outside [0, max_entries), images about to overflow — and the
@@ -1927,19 +1927,19 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
     if (a.grow && !a.spill) big.fin_ring = -1;   // concurrent launches: finish_call after the join
     if (a.grow) {   // ordered_offsets wrote the two descriptor lists
       small.touched = a.split;
-      small.ntouched = a.nsplit;
+      small.ntouched = a.nsplit;   // counter 0
       big.touched = a.split + 4 * a.max_rows;
-      big.ntouched = a.nsplit + 1;
+      big.ntouched = a.nsplit + 1 * kNsStride;
       small.desc = big.desc = 1;
       small.spill_list = big.touched;
       small.nspill = big.ntouched;
       if (a.spill & 2) {   // heavy rows: listed backwards
         small.heavy_end = a.split + 4 * a.max_rows;   // end of the 256-entry list's region
-        small.nheavy = a.nsplit + 2;
+        small.nheavy = a.nsplit + 2 * kNsStride;
       }
       if (a.lite) {   // light rows, four to a wave, in a launch of their own
         small.light = a.split + 12 * a.max_rows;
-        small.nlight = a.nsplit + 4;
+        small.nlight = a.nsplit + 4 * kNsStride;
       }
       if (!a.spill) {   // concurrent launches: the side stream starts behind the prep
         hipError_t e = hipEventRecord(fk.fork, st);

@@ -604,7 +604,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       const size_t R = (size_t)t.cfg.max_rows;
       HIP_TRY(c, hipMemsetAsync(t.d_cnt + slot * R, 0, R * sizeof(int32_t), prep));
       if (t.d_grow) HIP_TRY(c, hipMemsetAsync(t.d_grow + slot * R, 0, R * sizeof(int32_t), prep));
-      if (t.d_nsplit) HIP_TRY(c, hipMemsetAsync(t.d_nsplit + 5 * slot, 0, 5 * sizeof(uint32_t), prep));
+      if (t.d_nsplit) HIP_TRY(c, hipMemsetAsync(t.d_nsplit + 5 * psx::kNsStride * slot, 0, 5 * psx::kNsStride * sizeof(uint32_t), prep));
       if (t.d_tsum) HIP_TRY(c, hipMemsetAsync(t.d_tsum + slot * (size_t)t.tsum_slot, 0,
                                               (size_t)t.tsum_slot * sizeof(int32_t), prep));
     }
@@ -668,7 +668,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       x.max_rows = t.cfg.max_rows;
       x.cnt = t.d_cnt + (int64_t)slot * t.cfg.max_rows;
       x.grow = t.d_grow + (int64_t)slot * t.cfg.max_rows;
-      x.nsplit = t.d_nsplit + 5 * slot;
+      x.nsplit = t.d_nsplit + 5 * psx::kNsStride * slot;
       x.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
       x.wfill = psx::g_walk_rank ? c->d_wfill[slot] : nullptr;
       x.on = 1;
@@ -775,7 +775,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     if (t.split() && psx::g_ord_split) {
       a.grow = t.d_grow + (int64_t)slot * t.cfg.max_rows;
       a.split = t.d_split;
-      a.nsplit = t.d_nsplit + 5 * slot;
+      a.nsplit = t.d_nsplit + 5 * psx::kNsStride * slot;
       a.spill = psx::g_ord_split == 2 ? 1 : psx::g_ord_split == 3 ? 3 : 0;
       // light rows four to a wave (psx_ordered.hip lite_quad): spill mode, sorted/map rows
       // without importance (the light path does not sum it)
@@ -1435,7 +1435,7 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     e = hipMalloc(&t.d_grow, 2 * R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, 2 * R * sizeof(int32_t), c->stream);
     if (e == hipSuccess) e = hipMalloc(&t.d_split, 4 * R * 4 * sizeof(int32_t));   // int4 descriptors x 4 lists
-    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * 5 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * 5 * psx::kNsStride * sizeof(uint32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {

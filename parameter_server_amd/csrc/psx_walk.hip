@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) walk_head_kernel(StreamSet ss, TableDir d
     if (b == 0) ntouched[t] = 0;
     if (b == 0 && wc && t < dir.n && wc[t].on) {   // ordered_count's reset of ordered_offsets' counters
 #pragma unroll
-      for (int i = 0; i < 5; ++i) wc[t].nsplit[i] = 0;
+      for (int i = 0; i < 5; ++i) wc[t].nsplit[i * kNsStride] = 0;
       wc[t].tsum[0] = 0;
     }
   }

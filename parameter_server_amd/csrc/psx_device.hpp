@@ -193,6 +193,8 @@ struct OrdArgs {
   const uint32_t *nheavy;    // 256-entry list's region), listed backwards; the 256-entry
                              // launch takes them first
   int32_t lite;              // split tables: ordered_offsets lists light rows apart (starts_lite)
+  int32_t probe;             // PSX_DEBUG_ORD_PROBE (timing only, results wrong): 1 the register
+                             // apply does each row's setup and write-back but no record
   const int32_t *light;      // the 256-entry launch: light row descriptors, taken four to a wave
   const uint32_t *nlight;    // (lite_quad), after the heavy rows and before the others
   int32_t counted;           // split tables: 1 the walk already counted this call's records

@@ -1547,7 +1547,12 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       bool over = false;   // DRY: this row would exceed max_entries
       bool spilled = false;
       const int32_t n0 = n;
-      for (int32_t q = 0; q < L && !over; ++q) {
+      int32_t Lq = L;
+      if (!DRY && (a.probe & 1)) {   // timing probe: the setup's loads arrive, no record is applied
+        asm volatile("" ::"v"(col_n), "v"(d_n));
+        Lq = 0;
+      }
+      for (int32_t q = 0; q < Lq && !over; ++q) {
         const uint8_t *rec = rec_n;
         const int32_t nn = nn_n;
         int32_t col0 = col_n;
@@ -1792,6 +1797,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         }
         continue;
       }
+      if (a.probe & 2) continue;   // timing probe: no write-back
       // write the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)
       uint8_t *wrow = a.entries + slot * a.max_entries * ES;
 #pragma unroll

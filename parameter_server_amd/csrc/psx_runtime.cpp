@@ -42,6 +42,7 @@ int g_walk_calls = 0;    // PSX_STAT_WALK_CALLS
 int g_walk_trace = 0;    // PSX_DEBUG_WALK_TRACE: walked calls write per-window timestamps
 int g_walk_count = 1;   // PSX_VARIANT_WALK_COUNT: 1 = split tables counted by the walk (unpipelined walked calls)
 int g_fold_finish = 1;  // PSX_VARIANT_FOLD_FINISH: 1 = a call ending in an ordered apply finishes in it
+int g_ord_probe = 0;    // PSX_DEBUG_ORD_PROBE: timing probes of the register apply (results wrong)
 int g_ord_lite = 0;     // PSX_VARIANT_ORD_LITE: 1 = split tables take light rows four to a wave (C3 apply
                         // 0.054 ms against 0.048 with it off, profiles/r05/s9: a variant, not the default)
 int g_walk_skew = 0;    // PSX_DEBUG_WALK_SKEW: skew early-published walk states (tests the cross-check)
@@ -780,6 +781,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       // light rows four to a wave (psx_ordered.hip lite_quad): spill mode, sorted/map rows
       // without importance (the light path does not sum it)
       a.lite = psx::g_ord_lite && a.spill && !t.d_imp ? psx::g_ord_lite : 0;
+      a.probe = psx::g_ord_probe;
       a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1)
                   : (psx::g_walk_rank && !t.cfg.oplog_dense_serialized && c->d_wfill[slot] ? 3 : 0);
     }
@@ -2856,6 +2858,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
     case PSX_DEBUG_WALK_SKEW: return &psx::g_walk_skew;
     case PSX_VARIANT_ORD_LITE: return &psx::g_ord_lite;
+    case PSX_DEBUG_ORD_PROBE: return &psx::g_ord_probe;
     case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
     case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
     case PSX_VARIANT_OFFSETS_GRID: return &psx::g_offsets_blocks;
@@ -2899,6 +2902,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_ORD_LITE")) psx::g_ord_lite = atoi(v);
+    if (const char *v = getenv("PSX_ORD_PROBE")) psx::g_ord_probe = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
     if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);

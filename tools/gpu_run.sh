@@ -27,6 +27,7 @@
 #   t:FILE  pytest -v on one test file (FILE may carry a ::test selector)
 #   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
 #   hbm     tools/probe_hbm: copy / read / random-chunk gather / C2-pattern rates (build it first)
+#   prand   tools/probe_rand: dependent-chain latency and random line-request rates vs wave count (build it first)
 # Output: gpurun_out/$TAG/ (TAG from the environment, default "run").
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -128,6 +129,7 @@ for db, ks in d.items():
     imp) run imp 300 python -u bench.py --importance --steps 20 --warmup 3 --cpu-seconds 0 ;;
     probe) run probe 300 tools/probe_ceiling 10 ;;
     hbm) run hbm 400 tools/probe_hbm 10 ;;
+    prand) run prand 300 tools/probe_rand 5 && cat "$O/prand.log" ;;
     abstore) run abstore 300 python -u tools/ab_c2.py --configs 0:1:0,0:1:1,0:1:3,0:0:0,0:0:1,0:0:3 --rounds 5 --steps 5 && cat "$O/abstore.log" | tail -60 ;;
     abdense) run abdense 400 python -u tools/ab_c2.py --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -60 "$O/abdense.log" ;;
     abzeros) run abzeros 400 python -u tools/ab_c2.py --zeros --configs ${ABCONF:-0:1:1,0:0:1} --rounds 5 --steps 5 && tail -30 "$O/abzeros.log" ;;

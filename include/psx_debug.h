@@ -61,7 +61,8 @@ enum {
   PSX_DEBUG_ORD_PROBE = 23,     /* timing only (results wrong), bits: 1 the register apply of split
                                    tables does each row's setup (record references, headers, first
                                    record's pairs, image, key map) but applies no record; 2 it
-                                   writes no row back */
+                                   writes no row back; 4 it loads no record reference, header
+                                   or pair (a row is its image, key map and write-back) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from
                                    its composed maps by one record; the cross-check after the
                                    window's resolve must fail the call (PSX_ERR_DEVICE, nothing

@@ -1466,6 +1466,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       n = __builtin_amdgcn_readfirstlane(a.nent[slot]);
     }
     if (!DRY && lane == 0) a.flags[slot] = 3;
+    if (!DRY && (a.probe & 4)) L = 0;   // timing probe: no record references, headers or pairs
     {
       uint64_t *lst = a.list + beg;
       uint64_t mine = 0;

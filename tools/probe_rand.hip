@@ -9,6 +9,10 @@
 //          line request rate (G * M * hops / launch time).
 //   indep  the same lines, but every lane issues D independent loads per step (no chain):
 //          the rate the memory system sustains with requests always in flight.
+//   rows   each wave reads a 1,200-B row (150 8-byte entries, one load per 64 lanes) at a
+//          random slot of a table of 100K slots of a given stride, the next slot from the
+//          row's data (one row in flight per wave, the ordered apply's image load): does the
+//          slot stride (8 KiB = max_entries 1,024 x 8 B) concentrate rows on few channels?
 //
 // One JSON object per line.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/probe_rand tools/probe_rand.hip
@@ -16,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
@@ -38,6 +43,31 @@ __global__ void __launch_bounds__(256) chase_kernel(const uint32_t *buf, uint32_
   uint32_t cur = mix(w * 64 + lane) % lines;
   for (int h = 0; h < hops; ++h) cur = __builtin_nontemporal_load(buf + (uint64_t)cur * 32);
   if (cur == 0xffffffffu) sink[0] = cur;
+}
+
+// rows: each wave reads one row of R bytes (8-byte entries, lane i: entries i, i + 64, ...)
+// at slot r * stride, then the next row's slot from what it read (one row in flight per
+// wave, as the ordered apply's image load), `hops` rows per wave.
+__global__ void __launch_bounds__(256) rows_kernel(const uint8_t *buf, uint32_t nrows, int64_t stride, int rbytes,
+                                                   int hops, uint32_t magic, uint32_t *sink) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  uint32_t r = mix(w) % nrows;
+  const int ne = rbytes / 8;
+  for (int h = 0; h < hops; ++h) {
+    const uint8_t *row = buf + (int64_t)r * stride;
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = j * 64 + lane;
+      if (i < ne) x += (uint32_t)__builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(row) + i);
+    }
+    // every lane's words feed the next slot: the whole row must arrive first
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    r = mix((uint64_t)x + h + w * 977) % nrows;
+  }
+  if (r == magic) sink[0] = r;   // a run-time value: the chain cannot be folded away
 }
 
 template <int D>
@@ -102,6 +132,21 @@ int main(int argc, char **argv) {
     printf("{\"probe\": \"indep\", \"waves\": %d, \"in_flight_per_lane\": 16, \"ms\": %.4f, \"Greq_per_s\": %.2f, \"GBps_128B\": %.1f}\n",
            g, ms16, r16 / (ms16 * 1e-3) / 1e9, r16 * 128 / (ms16 * 1e-3) / 1e9);
     fflush(stdout);
+  }
+  // the ordered apply's image loads: 150-entry rows (1,200 B) at 8 KiB slots (max_entries
+  // 1,024 x 8 B) and at padded strides
+  for (int64_t stride : {8192LL, 8192LL + 128, 8192LL + 256, 8192LL + 640, 12288LL, 1280LL}) {
+    const uint32_t nrows = (uint32_t)std::min<int64_t>(100000, (int64_t)(bytes / stride) - 1);
+    for (int g : {7168, 14336}) {
+      const int rh = 16;
+      const double ms = time([&] { hipLaunchKernelGGL(rows_kernel, dim3(g / 4), dim3(256), 0, 0, (const uint8_t *)buf, nrows,
+                                                      stride, 1200, rh, 0xffffffffu, sink); });
+      const double lines = (double)g * rh * 10;
+      printf("{\"probe\": \"rows\", \"stride\": %lld, \"rows\": %u, \"row_bytes\": 1200, \"waves\": %d, \"hops\": %d, "
+             "\"ms\": %.4f, \"hop_us\": %.3f, \"Glines_per_s\": %.2f}\n",
+             (long long)stride, nrows, g, rh, ms, ms * 1e3 / rh, lines / (ms * 1e-3) / 1e9);
+      fflush(stdout);
+    }
   }
   CK(hipFree(buf));
   CK(hipFree(sink));

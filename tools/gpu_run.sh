@@ -23,6 +23,7 @@
 #   xtests  the split / exchange pipeline / walk-count / multi-rank GPU test files only
 #   c3ab    C3 A/B over one variant: AB_VAR (an env override, default PSX_ORD_LITE) set to each
 #           of AB_VALUES in turn (default "0 1 0 1")
+#   c2ab    C2 (headline + walked) A/B over one variant: AB_VAR (default PSX_INDEX_SCALAR) over AB_VALUES
 #   bare    the bare `python bench.py` line, as the driver runs it
 #   t:FILE  pytest -v on one test file (FILE may carry a ::test selector)
 #   pcopy   tools/probe_copy: copy / write / read / C2-mix under flat vs persistent grids (build it first)
@@ -175,6 +176,8 @@ for db, ks in d.items():
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
     bare) run bare 900 python -u bench.py ;;
+    c2ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c2ab_${i}_v$v 300 env ${AB_VAR:-PSX_INDEX_SCALAR}=$v python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras || exit 1; done
+            for f in $O/c2ab_*.log; do echo "$f $(grep -h "^{" $f | python3 -c "import json,sys; d=json.load(sys.stdin); print(d[\"value\"], d[\"roofline\"][\"avg_launch_ms\"], d.get(\"walked\",{}).get(\"value\"), d.get(\"walked\",{}).get(\"ms_per_step\"))")"; done ;;
     c3ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c3ab_${i}_v$v 300 env ${AB_VAR:-PSX_ORD_LITE}=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
             for f in $O/c3ab_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     t:*) f=${s#t:}; run t_$(basename "$f" .py) 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread "$f" ;;

@@ -1203,9 +1203,10 @@ __global__ void __launch_bounds__(256) dense_index_s_kernel(StreamSet ss, IdxSet
     int bl = b0;
     if (r0 + 64 <= e0 && !((rows_mask >> b0) & 1u)) {
       // all 64 records in message b0: scalar loads at wave-uniform addresses
-      const uint64_t p0 = (uint64_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(uintptr_t)(base[b0] + (r0 - pre[b0]) * stride)) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                               (int32_t)((uintptr_t)(base[b0] + (r0 - pre[b0]) * stride) >> 32)) << 32);
+      // (both halves zero-extended: a sign-extended low half would set the high bits)
+      const uintptr_t pa = (uintptr_t)(base[b0] + (r0 - pre[b0]) * stride);
+      const uint64_t p0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)pa) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(pa >> 32)) << 32);
       const int64_t st = stride;
 #pragma unroll
       for (int k0 = 0; k0 < 64; k0 += 16) {

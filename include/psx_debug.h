@@ -63,8 +63,6 @@ enum {
                                    record's pairs, image, key map) but applies no record; 2 it
                                    writes no row back; 4 it loads no record reference, header
                                    or pair (a row is its image, key map and write-back) */
-  PSX_VARIANT_INDEX_SCALAR = 24, /* dense_index: 1 the stream's row ids read by scalar loads (64-B DRAM
-                                   requests instead of 128-B), 0 (default) non-temporal vector loads */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from
                                    its composed maps by one record; the cross-check after the
                                    window's resolve must fail the call (PSX_ERR_DEVICE, nothing

@@ -1152,89 +1152,6 @@ __global__ void __launch_bounds__(256) dense_index_v2_kernel(StreamSet ss, IdxSe
   }
 }
 
-// dense_index_s (PSX_VARIANT_INDEX_SCALAR): the row ids read with scalar loads.  A vector
-// load of a 4-byte row id costs a 128-B L2 -> DRAM request, a scalar load a 64-B one
-// (profiles/r02/ab_index_policy.json): on its own the scalar form is slower (0.51 vs 0.26
-// ms), but beside the previous call's HBM-bound apply (PSX_PIPELINE_ALL) what the index
-// costs the step is the DRAM bytes it takes from that apply.  Each wave takes 64
-// consecutive records of the flattened (message, record) space: when they lie in one
-// message, 16 scalar loads in flight at a time (wave-uniform addresses), lane k keeping
-// record k's id; otherwise, and for producer-listed messages, the vector loads of v2.
-__global__ void __launch_bounds__(256) dense_index_s_kernel(StreamSet ss, IdxSet ix, uint32_t rows_mask,
-                                                           const Seg *segs, int t, int B, int64_t stride, Geo g,
-                                                           int32_t *inv, InvLayout L, uint32_t *call_status) {
-  __shared__ int64_t pre[kMaxFused + 1];
-  __shared__ const uint8_t *base[kMaxFused];
-  __shared__ int64_t sstr[kMaxFused];
-  if (threadIdx.x == 0) {
-    int64_t acc = 0;
-    for (int b = 0; b < kMaxFused; ++b) {
-      pre[b] = acc;
-      base[b] = nullptr;
-      sstr[b] = stride;
-      if (b < B) {
-        const Seg sg = segs[b * kMaxTables + t];
-        if (sg.rec0 >= 0 && !sg.sparse) {
-          acc += sg.num_rows;
-          if ((rows_mask >> b) & 1u) {
-            base[b] = reinterpret_cast<const uint8_t *>(ix.rows[b] + sg.ord0);
-            sstr[b] = 4;
-          } else {
-            base[b] = ss.data[b] + sg.rec0;
-          }
-        }
-      }
-    }
-    pre[kMaxFused] = acc;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t total = pre[kMaxFused];
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t r0 = w0 * 64; r0 < total; r0 += nw * 64) {
-    // the wave's first record's message (wave-uniform)
-    int b0 = 0;
-    while (b0 + 1 < B && pre[b0 + 1] <= r0) ++b0;
-    b0 = __builtin_amdgcn_readfirstlane(b0);
-    const int64_t e0 = pre[b0 + 1];
-    const int64_t r = r0 + lane;
-    int32_t rid = 0;
-    int bl = b0;
-    if (r0 + 64 <= e0 && !((rows_mask >> b0) & 1u)) {
-      // all 64 records in message b0: scalar loads at wave-uniform addresses
-      // (both halves zero-extended: a sign-extended low half would set the high bits)
-      const uintptr_t pa = (uintptr_t)(base[b0] + (r0 - pre[b0]) * stride);
-      const uint64_t p0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)pa) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(pa >> 32)) << 32);
-      const int64_t st = stride;
-#pragma unroll
-      for (int k0 = 0; k0 < 64; k0 += 16) {
-        int32_t v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-          v[k] = *reinterpret_cast<const __attribute__((address_space(4))) int32_t *>(p0 + (uint64_t)((k0 + k) * st));
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (lane == k0 + k) rid = v[k];
-      }
-    } else {
-      if (r < total) {
-        while (bl + 1 < B && pre[bl + 1] <= r) ++bl;
-        rid = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(base[bl] + (r - pre[bl]) * sstr[bl]));
-      }
-    }
-    if (r >= total) continue;
-    const int64_t ii = r - pre[bl];
-    const int64_t s = slot_of(rid, g);
-    if (s < 0) {
-      if (!((rows_mask >> bl) & 1u)) atomicOr(call_status, kStRowRange);
-      continue;
-    }
-    inv[s * L.ss + bl * L.sb] = (int32_t)ii;
-  }
-}
-
 // finish_call: fold the per-call status into the sticky word and free the ring slot.
 __global__ void finish_call_kernel(uint32_t *sticky, uint32_t *call_status, uint32_t *call_log) {
   if (threadIdx.x == 0) {
@@ -1313,7 +1230,6 @@ static unsigned resident_blocks(K kernel, int64_t want) {
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
 int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact)
-int g_index_scalar = 0;    // PSX_VARIANT_INDEX_SCALAR: 1 = dense_index_s (row ids by scalar loads)
 
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride, int64_t row_offset, int64_t row_stride, int64_t max_rows,
@@ -1322,12 +1238,8 @@ hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask
   // XCD-local form of the scatter (each XCD writing only its eighth of the slots) was
   // slower, 0.21 vs 0.13 ms on C2 (profiles/r02/ab_index_rows.json).
   Geo g{row_offset, row_stride, max_rows};
-  if (g_index_scalar)
-    hipLaunchKernelGGL(dense_index_s_kernel, dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B, stride, g,
-                       inv, L, call_status);
-  else
-    hipLaunchKernelGGL((dense_index_v2_kernel<8>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B, stride,
-                       g, inv, L, call_status);
+  hipLaunchKernelGGL((dense_index_v2_kernel<8>), dim3(2048), dim3(256), 0, st, ss, ix, rows_mask, segs, t, B, stride,
+                     g, inv, L, call_status);
   return hipGetLastError();
 }
 

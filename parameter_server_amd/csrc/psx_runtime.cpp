@@ -2842,7 +2842,6 @@ extern int g_apply_variant;
 extern int g_ord_split;
 extern int g_offsets_blocks;
 extern int g_dry_blocks;
-extern int g_index_scalar;
 }  // namespace psx
 
 static int *variant_slot(int32_t which) {
@@ -2864,7 +2863,6 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
     case PSX_VARIANT_OFFSETS_GRID: return &psx::g_offsets_blocks;
     case PSX_VARIANT_DRY_GRID: return &psx::g_dry_blocks;
-    case PSX_VARIANT_INDEX_SCALAR: return &psx::g_index_scalar;
     case PSX_VARIANT_WALK_RANK: return &psx::g_walk_rank;
     default: return nullptr;
   }
@@ -2905,7 +2903,6 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_ORD_LITE")) psx::g_ord_lite = atoi(v);
     if (const char *v = getenv("PSX_ORD_PROBE")) psx::g_ord_probe = atoi(v);
-    if (const char *v = getenv("PSX_INDEX_SCALAR")) psx::g_index_scalar = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);
     if (const char *v = getenv("PSX_WALK_CUS")) psx::g_walk_all_cus = atoi(v);

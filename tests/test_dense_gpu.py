@@ -289,27 +289,3 @@ def test_read_sweep_hook_measures_a_rate():
     assert 100.0 < g < 9000.0, g
     assert L.psx_debug_read_sweep(buf.data_ptr() + 4, buf.numel() - 16, 1) == -1.0   # misaligned
     assert L.psx_debug_read_sweep(buf.data_ptr(), 1024, 1) == -1.0                   # below one tile
-
-
-INDEX_SCALAR = 24
-
-
-def test_scalar_row_id_index_bit_exact():
-    """dense_index_s (PSX_VARIANT_INDEX_SCALAR: the stream's row ids by scalar loads, 64 per
-    wave, the vector form where a wave's 64 records cross a message boundary): partial
-    coverage in 1-16 messages of every value type, the modulo geometry, the device-detected
-    errors, a duplicate row's replay, and 2^18 rows x 8 messages against an in-order torch
-    sum — the same results as the vector form."""
-    from parameter_server_amd import _abi
-    L = _abi.load()
-    old = L.psx_debug_set_variant(INDEX_SCALAR, 1)
-    try:
-        for dt in (F32, F64, I32, I64):
-            for B in (1, 3, 16):
-                test_fused_apply_bit_exact(dt, B)
-        test_modulo_partition_geometry()
-        _device_stream_errors()
-        test_duplicate_row_in_one_message_applied_in_order()
-        test_large_fused_apply_against_torch_reference()
-    finally:
-        L.psx_debug_set_variant(INDEX_SCALAR, old)

@@ -1333,22 +1333,21 @@ __device__ __forceinline__ int32_t found_run(int32_t (&key)[J], V (&val)[J], int
   if (run) sv[my_idx] = my_d;
   wave_sync();
   uint64_t rmm[J];
-  bool anyrm = false;
+  // every register at once, selects instead of branches (sv is zero outside the run's
+  // entries, so a miss adds nothing and rewrites the zero it read)
+  uint64_t anym = 0;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    rmm[j] = 0;
-    if (j * 64 < n) {
-      const int32_t i = j * 64 + lane;
-      const V dv = sv[i];
-      const bool hit = dv != V(0);
-      if (hit) {
-        val[j] = OV<V>::add(val[j], dv);
-        sv[i] = V(0);
-      }
-      rmm[j] = __ballot(hit && val[j] == V(0));
-      anyrm = anyrm || rmm[j] != 0;
-    }
+    const int32_t i = j * 64 + lane;
+    const V dv = sv[i];
+    const bool hit = dv != V(0);
+    const V nv = OV<V>::add(val[j], dv);
+    val[j] = hit ? nv : val[j];
+    sv[i] = V(0);
+    rmm[j] = __ballot(hit && nv == V(0));
+    anym |= rmm[j];
   }
+  const bool anyrm = anym != 0;
   if (!anyrm) return n;
   // stable compaction: kept entries to LDS at their new index, the key map updated
   int32_t gone = 0;
@@ -1589,6 +1588,32 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
           // insert/remove shift, after which the chunk's lookups are re-read).
           int32_t my_idx = -1;
           bool stale = true;
+          if constexpr (KIND == 1) {
+            if (use_pos) {
+              // the usual chunk: every live key is in the image — one lookup, one found run,
+              // none of the Inc loop's control (the scalar unit is the apply's busiest)
+              if (pos_dirty) {
+                wave_sync();
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                  const int32_t i = j * 64 + lane;
+                  if (j * 64 < n && i < n) pos[key[j]] = (int16_t)i;
+                }
+                wave_sync();
+                pos_dirty = false;
+              }
+              my_idx = lane < cnt ? (int32_t)pos[my_col] : -1;
+              stale = false;
+              const bool live = lane < cnt && my_d != V(0);
+              if (__ballot(live && my_idx < 0) == 0) {
+                if (__ballot(live)) {
+                  n = found_run<V, J>(key, val, n, live, my_idx, my_d, lane, s_sv[wib], s_ck[wib], pos, stale);
+                  if (stale) pos_dirty = false;   // the compaction rewrote the whole map
+                }
+                continue;
+              }
+            }
+          }
           for (int32_t t = 0; t < cnt && !over; ++t) {
             if constexpr (KIND == 1) {
               if (use_pos) {

@@ -23,6 +23,9 @@
 #   xtests  the split / exchange pipeline / walk-count / multi-rank GPU test files only
 #   c3ab    C3 A/B over one variant: AB_VAR (an env override, default PSX_ORD_LITE) set to each
 #           of AB_VALUES in turn (default "0 1 0 1")
+#   salu    the C3 apply's instruction mix (SALU / VALU / branch / LDS / SMEM / VMEM per dispatch)
+#           under PSX_ORD_PROBE 0 (full), 3 (setup only), 6 (image only)
+#   c3libs  C3 with each build named in LIBS (space-separated PSX_LIB paths; new = this tree's), twice
 #   c2ab    C2 (headline + walked) A/B over one variant: AB_VAR (default PSX_INDEX_SCALAR) over AB_VALUES
 #   bare    the bare `python bench.py` line, as the driver runs it
 #   t:FILE  pytest -v on one test file (FILE may carry a ::test selector)
@@ -111,6 +114,24 @@ for db, ks in d.items():
         P=$((P+1))
       done
       python3 tools/pmc_db.py $(find "$R/pmc3" -name '*.db' | sort) > "$O/pmc3.json" && echo "pmc3 summarised" ;;
+    salu)   # instruction mix of the C3 apply per timing probe (PSX_ORD_PROBE 0 full, 3 setup only, 6 image only)
+      for v in ${SALU_PROBES:-0 3 6}; do
+        say "salu probe $v"
+        PSX_ORD_PROBE=$v timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM \
+          -d "$R/salu/v$v" -o pmc -- python3 bench.py --workload c3 --steps 3 --warmup 1 --cpu-seconds 0 \
+          > "$O/salu_v$v.log" 2>&1 || { echo "!! salu probe $v"; tail -5 "$O/salu_v$v.log"; exit 1; }
+        python3 tools/pmc_db.py $(find "$R/salu/v$v" -name '*.db' | sort) > "$O/salu_v$v.json" || exit 1
+      done
+      python3 - "$O" <<'PY'
+import json, sys, glob, os
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "salu_v*.json"))):
+    d = json.load(open(f))
+    for db, ks in d.items():
+        for k, c in ks.items():
+            if "ordered_apply_reg_kernel<int, 1, 4" in k:
+                print(os.path.basename(f), {x: round(y) for x, y in c.items()})
+PY
+      ;;
     c3split) i=0; for v in 1 2 3 1 2 3; do i=$((i+1)); run c3split_${i}_v$v 300 env PSX_ORD_SPLIT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
              grep -h '^{' $O/c3split_*.log | cut -c1-400 ;;
     c3walk) i=0; for v in 0 1 0 1; do i=$((i+1)); run c3walk_${i}_cus$v 300 env PSX_WALK_CUS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
@@ -147,6 +168,9 @@ for db, ks in d.items():
     c3lib) i=0; for v in new old new old; do i=$((i+1)); L=; [ $v = old ] && L=ab_old/libpsx.so
              run c3lib_${i}_$v 300 env PSX_LIB=$L python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
            for f in $O/c3lib_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"])')"; done ;;
+    c3libs) i=0; for r in 1 2; do for L in ${LIBS:-new}; do i=$((i+1)); n=$(echo "$L" | tr '/' '_'); P=$L; [ "$L" = new ] && P=
+              run c3libs_${i}_$n 300 env PSX_LIB=$P python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done; done
+            for f in $O/c3libs_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"])')"; done ;;
     c2lib) i=0; for v in new old new old; do i=$((i+1)); L=; [ $v = old ] && L=ab_old/libpsx.so
              run c2lib_${i}_$v 300 env PSX_LIB=$L python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras --skip-walked || exit 1; done
            for f in $O/c2lib_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["roofline"]["avg_launch_ms"], d["roofline"]["frac_of_read_sweep"])')"; done ;;

@@ -1405,6 +1405,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   __shared__ int16_t s_pos[4][1024];   // the register kernels serve max_entries <= 1,024
   __shared__ V s_sv[4][J * 64];        // found_run: deltas by entry (zero between runs), compaction values
   __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
+  __shared__ const uint8_t *s_data[kMaxFused];   // the call's message base pointers
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   // the gate's words and the launch's row counts read at once (not one after another)
@@ -1421,6 +1422,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
   for (int32_t k = lane; k < 1024; k += 64) s_pos[wib][k] = -1;
+  if (threadIdx.x < kMaxFused) s_data[threadIdx.x] = a.ss.data[threadIdx.x];
   __syncthreads();
   // split tables check each record chunk's columns here instead (cols_checked below)
   const bool pos_ok = a.keyflag && (a.grow || !*a.keyflag) && a.max_entries <= 1024;
@@ -1484,13 +1486,13 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       // that the first record's chunk loads below wait on the headers only (loads return in
       // order); each record's first 64 (column, value) pairs are loaded one record ahead, so
       // the Inc chain does not wait on a dependent global load per record.
-      int hb = 0;
-      uint64_t hoff = 0;
+      // lane q: record q's address (its message's base from LDS: no per-record kernel
+      // argument load) and pair count
+      uint64_t hp = 0;
       int32_t hn = 0;
       if (L <= 64 && lane < L) {
-        hb = (int)(mine >> 56);
-        hoff = mine & kRefOffMask;
-        hn = o_ld32(a.ss.data[hb] + hoff + 4);
+        hp = (uint64_t)(uintptr_t)(s_data[mine >> 56] + (mine & kRefOffMask));
+        hn = o_ld32(reinterpret_cast<const uint8_t *>((uintptr_t)hp) + 4);
       }
       // load the row image
       const uint8_t *row = a.entries + slot * a.max_entries * ES;
@@ -1506,10 +1508,11 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         int b;
         uint64_t off;
         if (L <= 64) {
-          b = __builtin_amdgcn_readlane(hb, q);
-          off = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(hoff >> 32), q) << 32) |
-                (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)hoff, q);
+          const uint64_t p = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(hp >> 32), q) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)hp, q);
           nn = __builtin_amdgcn_readlane(hn, q);
+          rec = reinterpret_cast<const uint8_t *>((uintptr_t)p);
+          return;
         } else {
           const uint64_t e = lst[q];
           const uint64_t eu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(e >> 32)) << 32) |

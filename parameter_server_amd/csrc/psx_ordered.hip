@@ -1402,7 +1402,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   // Key -> entry-index map of the wave's row (FindIndex in one LDS read instead of J
   // ballots), usable while every key lies in [0, max_entries) (keyflag clear, and checked
   // per row at load): int16 per key, -1 = absent.
-  __shared__ int16_t s_pos[4][1024];   // the register kernels serve max_entries <= 1,024
+  __shared__ int16_t s_pos[4][1024 + 64];   // keys < 1,024 (the register kernels' max_entries), then one spare per lane
   __shared__ V s_sv[4][J * 64];        // found_run: deltas by entry (zero between runs), compaction values
   __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
   __shared__ const uint8_t *s_data[kMaxFused];   // the call's message base pointers
@@ -1543,7 +1543,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       if (use_pos) {   // the map is all -1 between rows (cleared once, then per row below)
 #pragma unroll
         for (int j = 0; j < J; ++j)
-          if (j * 64 + lane < n) pos[key[j]] = (int16_t)(j * 64 + lane);
+          if (j * 64 < n) pos[j * 64 + lane < n ? key[j] : 1024 + lane] = (int16_t)(j * 64 + lane);
         wave_sync();
       }
       double impt = a.imp ? a.imp[slot] : 0.0;
@@ -1600,12 +1600,13 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                   const int32_t i = j * 64 + lane;
-                  if (j * 64 < n && i < n) pos[key[j]] = (int16_t)i;
+                  if (j * 64 < n) pos[i < n ? key[j] : 1024 + lane] = (int16_t)i;
                 }
                 wave_sync();
                 pos_dirty = false;
               }
-              my_idx = lane < cnt ? (int32_t)pos[my_col] : -1;
+              my_idx = (int32_t)pos[my_col];   // lanes past the chunk hold column 0: a harmless read
+              my_idx = lane < cnt ? my_idx : -1;
               stale = false;
               const bool live = lane < cnt && my_d != V(0);
               if (__ballot(live && my_idx < 0) == 0) {
@@ -1815,7 +1816,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         wave_sync();
 #pragma unroll
         for (int j = 0; j < J; ++j)
-          if (j * 64 < n && j * 64 + lane < n) pos[key[j]] = -1;
+          if (j * 64 < n) pos[j * 64 + lane < n ? key[j] : 1024 + lane] = -1;
         wave_sync();
       }
       if (DRY) continue;

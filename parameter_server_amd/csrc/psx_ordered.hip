@@ -1568,11 +1568,49 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         const uint8_t *cols = rec + 8;
         const uint8_t *vals = rec + 8 + (int64_t)nn * 4;
         if (a.imp) impt += sparse_importance<V>(vals, nn, lane);
-        for (int32_t c0 = 0; c0 < nn && !over; c0 += 64) {
+        // (a do-while: a record's one chunk, the usual case, pays no entry test; an empty
+        // record runs it once with no live lane)
+        int32_t c0 = 0;
+        do {
           const int32_t pi = c0 + lane;
           const int32_t my_col = c0 == 0 ? col0 : (pi < nn ? o_ld32(cols + (int64_t)pi * 4) : 0);
           const V my_d = c0 == 0 ? d0 : (pi < nn ? ldv<V>(vals + (int64_t)pi * sizeof(V)) : V(0));
           const int32_t cnt = nn - c0 < 64 ? nn - c0 : 64;
+          // With the key map, lane t looks up its own column once for the whole chunk
+          // (a record's columns are distinct, so an Inc moves no other key except by an
+          // insert/remove shift, after which the chunk's lookups are re-read).
+          int32_t my_idx = -1;
+          bool stale = true;
+          if constexpr (KIND == 1) {
+            if (use_pos) {
+              // the usual chunk: every live key is in the image — one lookup, one found run,
+              // none of the Inc loop's control; a column the map cannot index (split
+              // tables check here) or an insert takes the Inc loop below
+              const bool bad = a.grow && lane < cnt && (uint32_t)my_col >= (uint32_t)a.max_entries;
+              if (pos_dirty) {
+                wave_sync();
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                  const int32_t i = j * 64 + lane;
+                  if (j * 64 < n) pos[i < n ? key[j] : 1024 + lane] = (int16_t)i;
+                }
+                wave_sync();
+                pos_dirty = false;
+              }
+              const int32_t pv = (int32_t)pos[bad ? 0 : my_col];   // lanes past the chunk hold column 0
+              const bool live = lane < cnt && my_d != V(0);
+              my_idx = lane < cnt ? pv : -1;
+              if (__ballot((live && my_idx < 0) || bad) == 0) {
+                stale = false;
+                if (__ballot(live)) {
+                  n = found_run<V, J>(key, val, n, live, my_idx, my_d, lane, s_sv[wib], s_ck[wib], pos, stale);
+                  if (stale) pos_dirty = false;   // the compaction rewrote the whole map
+                }
+                continue;
+              }
+              my_idx = -1;   // the Inc loop looks the chunk up again
+            }
+          }
           if (use_pos && a.grow &&
               __ballot(lane < cnt && (uint32_t)my_col >= (uint32_t)a.max_entries)) {
             // a column outside [0, max_entries) (split tables: no column scan before the
@@ -1585,38 +1623,6 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
             wave_sync();
             use_pos = false;
             pos_dirty = false;
-          }
-          // With the key map, lane t looks up its own column once for the whole chunk
-          // (a record's columns are distinct, so an Inc moves no other key except by an
-          // insert/remove shift, after which the chunk's lookups are re-read).
-          int32_t my_idx = -1;
-          bool stale = true;
-          if constexpr (KIND == 1) {
-            if (use_pos) {
-              // the usual chunk: every live key is in the image — one lookup, one found run,
-              // none of the Inc loop's control (the scalar unit is the apply's busiest)
-              if (pos_dirty) {
-                wave_sync();
-#pragma unroll
-                for (int j = 0; j < J; ++j) {
-                  const int32_t i = j * 64 + lane;
-                  if (j * 64 < n) pos[i < n ? key[j] : 1024 + lane] = (int16_t)i;
-                }
-                wave_sync();
-                pos_dirty = false;
-              }
-              my_idx = (int32_t)pos[my_col];   // lanes past the chunk hold column 0: a harmless read
-              my_idx = lane < cnt ? my_idx : -1;
-              stale = false;
-              const bool live = lane < cnt && my_d != V(0);
-              if (__ballot(live && my_idx < 0) == 0) {
-                if (__ballot(live)) {
-                  n = found_run<V, J>(key, val, n, live, my_idx, my_d, lane, s_sv[wib], s_ck[wib], pos, stale);
-                  if (stale) pos_dirty = false;   // the compaction rewrote the whole map
-                }
-                continue;
-              }
-            }
           }
           for (int32_t t = 0; t < cnt && !over; ++t) {
             if constexpr (KIND == 1) {
@@ -1808,7 +1814,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
               }
             }
           }
-        }
+        } while ((c0 += 64) < nn && !over);
       }
       if (use_pos) {
         // back to all -1: every key the row ever mapped is in the final image or was

@@ -128,7 +128,8 @@ def test_split_forms_match_oracle(split, kind, dt):
 def test_keys_outside_the_key_map_range(split, kind):
     """Split tables no longer scan every record's columns before the apply: the apply checks
     each record chunk's columns and finishes a row whose columns fall outside
-    [0, max_entries) (negative keys, keys far past it) without the key map; the capacity dry
+    [0, max_entries) (negative keys, keys far past it, alone or in one chunk with keys inside
+    it) without the key map; the capacity dry
     run takes only the rows whose entries + Incs exceed max_entries.  Byte-exact (sorted) /
     {col -> value} (map) against the oracle over several calls, mixing such rows with rows
     inside the range and rows whose Incs exceed max_entries without overflowing."""
@@ -152,6 +153,8 @@ def test_keys_outside_the_key_map_range(split, kind):
                     if r % 3 == 0:     # keys outside the map's range, few per row
                         cols = np.unique(rng.choice(np.r_[np.arange(-40, 0), np.arange(cap, cap + 80),
                                                           np.arange(100000, 100040)], size=rng.randint(1, 12)))
+                        if r % 2:      # mixed into a record of keys inside it (one chunk, both kinds)
+                            cols = np.unique(np.r_[cols, rng.choice(cap, size=rng.randint(1, 20))])
                     elif r % 3 == 1:   # many Incs on a few keys: entries + Incs > cap, no overflow
                         cols = np.arange(0, 200, dtype=np.int64)
                     else:

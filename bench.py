@@ -62,7 +62,7 @@ def kernel_signature():
     return h.hexdigest()[:16]
 
 
-C3_PMC_JSON = os.path.join(ROOT, "profiles", "r04", "pmc_c3.json")
+C3_PMC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc_c3.json")
 
 
 def c3_kernel_signature():

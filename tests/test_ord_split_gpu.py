@@ -294,3 +294,51 @@ def test_light_rows_four_to_a_wave(lite, kind, dt):
 def test_light_path_is_a_variant_off_by_default():
     # one row per wave measured faster on C3 (profiles/r05/s9); the light path stays selectable
     assert _abi.load().psx_debug_get_variant(ORD_LITE) == 0
+
+
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted", "map"])
+def test_empty_records_and_one_chunk_rows(kind):
+    """Records with no pairs (a sender may serialize an emptied row oplog), rows whose only
+    records are empty, and empty records between full ones, as the last record of a message
+    too: the apply takes an empty record as a chunk with no live lane.  Against the oracle
+    over three calls on a split sorted-map table (256 < max_entries)."""
+    rng = np.random.RandomState(41 + kind)
+    rows, K = 400, 512
+    bgs = [100, 101]
+    srv = psa.Server(0, 1, bgs)
+    srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                     max_rows=rows, max_entries=K))
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    for v in range(3):
+        streams = []
+        for b in range(2):
+            recs = []
+            for r in rng.choice(rows, size=150, replace=False):
+                r = int(r)
+                if r % 4 == 0:
+                    cols = np.zeros(0, np.int32)                      # an empty record
+                else:
+                    space = K if r % 4 != 1 else 30            # r % 4 == 1: a small key space, overlaps
+                    cols = np.sort(rng.choice(space, size=rng.randint(1, min(40, space)), replace=False))
+                vals = rng.randint(1, 3, size=cols.size) * (1 if v == 0 else rng.choice([-1, 1], size=cols.size))
+                recs.append((r, cols.astype(np.int32), vals.astype(np.int32)))
+            recs.append((int(rng.randint(rows)), np.zeros(0, np.int32), np.zeros(0, np.int32)))   # last: empty
+            streams.append(wire.sparse_stream_np(3, 4, recs))
+        dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in streams]
+        torch.cuda.synchronize()
+        srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+        srv.sync()
+        for s, bg in zip(streams, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    ids = list(range(rows))
+    if kind == SORTED_MAP:
+        assert srv.serialize_rows(3, ids) == orc.serialize_records(3, ids)
+    else:
+        for r in ids:
+            g, w = srv.serialize_rows(3, [r]), orc.serialize_records(3, [r])
+            assert len(g) == len(w), r
+            if g:
+                assert _as_map(g[12:], I32) == _as_map(w[12:], I32), r
+    srv.close()
+    orc.close()

@@ -1,6 +1,6 @@
 // system_gflags_declare.hpp — the system flags every petuum_ps app includes
 // (src/petuum_ps_common/include/system_gflags_declare.hpp:1-52 of the reference; defined,
-// with the reference's defaults, in libpetuum_ps.so: parameter_server_amd/csrc/petuum_gflags.cpp
+// with the reference's defaults, in libpetuum_ps.so: parameter_server_amd/csrc/petuum_flags.cpp
 // restating system_gflags.cpp:6-45).  With gflags on the include path these are gflags
 // flags and InitTableGroupConfig reads them; without it each is a constant at the
 // reference's default (see table_gflags_declare.hpp).
@@ -98,3 +98,23 @@ static const uint64_t FLAGS_num_zmq_threads = 1;
 namespace petuum {
 void InitTableGroupConfig(TableGroupConfig *config, int32_t num_tables);
 }
+
+// Link-time mode check: the app's headers and libpetuum_ps.so must agree on
+// whether the flags are gflags flags.  Each TU that includes a declare header references
+// the marker of the mode IT was compiled in; the library defines only the marker of its
+// own mode, so a mismatch is an undefined-symbol error at link time naming the mode,
+// instead of an app silently reading constant defaults (or missing FLAGS_* definitions).
+#ifndef PETUUM_PS_FLAGS_MODE_CHECK
+#define PETUUM_PS_FLAGS_MODE_CHECK
+namespace petuum {
+namespace flags_mode {
+#if PETUUM_PS_HAVE_GFLAGS
+extern const int libpetuum_ps_built_with_gflags;
+__attribute__((used)) static const int *const app_mode_marker = &libpetuum_ps_built_with_gflags;
+#else
+extern const int libpetuum_ps_built_without_gflags;
+__attribute__((used)) static const int *const app_mode_marker = &libpetuum_ps_built_without_gflags;
+#endif
+}  // namespace flags_mode
+}  // namespace petuum
+#endif

@@ -1,6 +1,6 @@
 // table_gflags_declare.hpp — the table flags every petuum_ps app includes
 // (src/petuum_ps_common/include/table_gflags_declare.hpp:1-22 of the reference; defined,
-// with the reference's defaults, in libpetuum_ps.so: parameter_server_amd/csrc/petuum_gflags.cpp
+// with the reference's defaults, in libpetuum_ps.so: parameter_server_amd/csrc/petuum_flags.cpp
 // restating table_gflags.cpp:8-24).
 //
 // With gflags on the include path (as on any box that builds the reference's apps) these
@@ -59,4 +59,24 @@ static const uint64_t FLAGS_client_send_oplog_upper_bound = 100;
 static const int32_t FLAGS_server_table_logic = -1;
 static const bool FLAGS_version_maintain = false;
 
+#endif
+
+// Link-time mode check: the app's headers and libpetuum_ps.so must agree on
+// whether the flags are gflags flags.  Each TU that includes a declare header references
+// the marker of the mode IT was compiled in; the library defines only the marker of its
+// own mode, so a mismatch is an undefined-symbol error at link time naming the mode,
+// instead of an app silently reading constant defaults (or missing FLAGS_* definitions).
+#ifndef PETUUM_PS_FLAGS_MODE_CHECK
+#define PETUUM_PS_FLAGS_MODE_CHECK
+namespace petuum {
+namespace flags_mode {
+#if PETUUM_PS_HAVE_GFLAGS
+extern const int libpetuum_ps_built_with_gflags;
+__attribute__((used)) static const int *const app_mode_marker = &libpetuum_ps_built_with_gflags;
+#else
+extern const int libpetuum_ps_built_without_gflags;
+__attribute__((used)) static const int *const app_mode_marker = &libpetuum_ps_built_without_gflags;
+#endif
+}  // namespace flags_mode
+}  // namespace petuum
 #endif

@@ -176,7 +176,7 @@ typedef struct psx_table_config {
                                        decompressed to f32 before the add (dense_row_oplog_float16.hpp:144-157;
                                        f32 tables only).  1/2 select sparse row oplogs, which change nothing on
                                        the server for sparse-serialized tables (abstract_row_oplog.hpp:64-78). */
-  /* ABI 4 (was reserved1): */
+  /* ABI 8 (was reserved1): */
   int32_t row_bytes_f16;            /* 1: DenseRowFloat16<float> rows (dense_row_float16.hpp:13; the row type
                                        apps/matrixfact's matrixfact_split16 registers, :47,560): stored and
                                        updated in f32, serialized (row reads, pushes) as binary16 uint16[cap]

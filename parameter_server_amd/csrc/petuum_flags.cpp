@@ -16,51 +16,60 @@
 #include <cstdlib>
 
 #if PETUUM_PS_HAVE_GFLAGS
-DEFINE_int32(table_staleness, 0, "table staleness");
-DEFINE_int32(row_type, 0, "table row type");
-DEFINE_int32(row_oplog_type, petuum::RowOpLogType::kDenseRowOpLog, "row oplog type");
-DEFINE_bool(oplog_dense_serialized, true, "dense serialized oplog");
-DEFINE_string(oplog_type, "Sparse", "use append only oplog?");
-DEFINE_string(append_only_oplog_type, "Inc", "append only oplog type?");
-DEFINE_uint64(append_only_buffer_capacity, 1024 * 1024, "buffer capacity in bytes");
-DEFINE_uint64(append_only_buffer_pool_size, 3, "append_ only buffer pool size");
-DEFINE_int32(bg_apply_append_oplog_freq, 4, "bg apply append oplog freq");
-DEFINE_string(process_storage_type, "BoundedSparse", "proess storage type");
-DEFINE_bool(no_oplog_replay, false, "oplog replay?");
-DEFINE_uint64(server_push_row_upper_bound, 100, "Server push row threshold");
-DEFINE_uint64(client_send_oplog_upper_bound, 100, "client send oplog upper bound");
-DEFINE_int32(server_table_logic, -1, "server table logic");
-DEFINE_bool(version_maintain, false, "version maintain");
+DEFINE_int32(table_staleness, 0, "SSP staleness bound of a table, in clocks");
+DEFINE_int32(row_type, 0, "registered row type id of a table");
+DEFINE_int32(row_oplog_type, petuum::RowOpLogType::kDenseRowOpLog, "client row-oplog kind (0 dense, 1 sparse, 2 sparse vector, 3 dense binary16)");
+DEFINE_bool(oplog_dense_serialized, true, "send dense row oplogs as full-width records");
+DEFINE_string(oplog_type, "Sparse", "client oplog store: Sparse, AppendOnly or Dense");
+DEFINE_string(append_only_oplog_type, "Inc", "append-only oplog mode: Inc, BatchInc or DenseBatchInc");
+DEFINE_uint64(append_only_buffer_capacity, 1024 * 1024, "bytes per append-only oplog buffer");
+DEFINE_uint64(append_only_buffer_pool_size, 3, "append-only buffers per worker thread");
+DEFINE_int32(bg_apply_append_oplog_freq, 4, "append-only buffers a bg thread merges per apply");
+DEFINE_string(process_storage_type, "BoundedSparse", "client row cache: BoundedDense or BoundedSparse");
+DEFINE_bool(no_oplog_replay, false, "skip replaying oplogs onto rows the server sends back");
+DEFINE_uint64(server_push_row_upper_bound, 100, "most rows a server pushes per table per clock (SSPAggr)");
+DEFINE_uint64(client_send_oplog_upper_bound, 100, "most row oplogs a client sends per table per clock (SSPAggr)");
+DEFINE_int32(server_table_logic, -1, "registered server table logic id, -1 for the plain apply");
+DEFINE_bool(version_maintain, false, "keep a version counter in each server row");
 
-DEFINE_string(stats_path, "", "stats file path prefix");
-DEFINE_int32(num_clients, 1, "total number of clients");
-DEFINE_int32(num_comm_channels_per_client, 1, "no. of comm channels per client");
-DEFINE_bool(init_thread_access_table, false, "whether init thread accesses table");
-DEFINE_int32(num_table_threads, 1, "no. of worker threads per client");
-DEFINE_int32(client_id, 0, "This client's ID");
-DEFINE_string(hostfile, "", "path to Petuum PS server configuration file");
-DEFINE_string(consistency_model, "SSPPush", "SSPAggr/SSPPush/SSP");
-DEFINE_uint64(client_bandwidth_mbps, 40, "per-thread bandwidth limit, in mbps");
-DEFINE_uint64(server_bandwidth_mbps, 40, "per-thread bandwidth limit, in mbps");
-DEFINE_uint64(bg_idle_milli, 10, "Bg idle millisecond");
-DEFINE_uint64(thread_oplog_batch_size, 100 * 1000 * 1000, "thread oplog batch size");
-DEFINE_uint64(row_candidate_factor, 5, "server row candidate factor");
-DEFINE_int32(server_idle_milli, 10, "server idle time out in millisec");
-DEFINE_string(update_sort_policy, "Random", "Update sort policy");
-DEFINE_int32(snapshot_clock, -1, "snapshot clock");
-DEFINE_int32(resume_clock, -1, "resume clock");
-DEFINE_string(snapshot_dir, "", "snap shot directory");
-DEFINE_string(resume_dir, "", "resume directory");
-DEFINE_bool(numa_opt, false, "numa opt on?");
-DEFINE_int32(numa_index, 0, "numa node index");
-DEFINE_string(numa_policy, "Even", "numa policy");
-DEFINE_bool(naive_table_oplog_meta, true, "naive table oplog meta");
-DEFINE_bool(suppression_on, false, "suppression on");
-DEFINE_bool(use_approx_sort, true, "use_approx_sort");
-DEFINE_uint64(num_zmq_threads, 1, "number of zmq threads");
+DEFINE_string(stats_path, "", "prefix of the stats output file");
+DEFINE_int32(num_clients, 1, "client processes in the job");
+DEFINE_int32(num_comm_channels_per_client, 1, "server/bg thread pairs per client");
+DEFINE_bool(init_thread_access_table, false, "the init thread also reads and writes tables");
+DEFINE_int32(num_table_threads, 1, "worker threads per client that access tables");
+DEFINE_int32(client_id, 0, "id of this client process");
+DEFINE_string(hostfile, "", "file listing id, ip and port of every server");
+DEFINE_string(consistency_model, "SSPPush", "consistency model: SSP, SSPPush or SSPAggr");
+DEFINE_uint64(client_bandwidth_mbps, 40, "bg thread send budget in Mbit/s (SSPAggr)");
+DEFINE_uint64(server_bandwidth_mbps, 40, "server thread send budget in Mbit/s (SSPAggr)");
+DEFINE_uint64(bg_idle_milli, 10, "bg thread idle period in ms before it sends");
+DEFINE_uint64(thread_oplog_batch_size, 100 * 1000 * 1000, "worker thread oplog bytes buffered before a flush");
+DEFINE_uint64(row_candidate_factor, 5, "candidate rows per pushed row when sorting by importance");
+DEFINE_int32(server_idle_milli, 10, "server thread idle period in ms before it pushes");
+DEFINE_string(update_sort_policy, "Random", "order of partial sends: Random, FIFO, RelativeMagnitude or FIFO_N_ReMag");
+DEFINE_int32(snapshot_clock, -1, "clock interval between table snapshots, -1 for none");
+DEFINE_int32(resume_clock, -1, "clock to resume from, -1 for a fresh start");
+DEFINE_string(snapshot_dir, "", "directory table snapshots are written to");
+DEFINE_string(resume_dir, "", "directory table snapshots are read from");
+DEFINE_bool(numa_opt, false, "pin threads to NUMA nodes");
+DEFINE_int32(numa_index, 0, "NUMA node this client uses");
+DEFINE_string(numa_policy, "Even", "NUMA placement: Even or Center");
+DEFINE_bool(naive_table_oplog_meta, true, "use the simple per-table oplog metadata");
+DEFINE_bool(suppression_on, false, "suppress small updates (SSPAggr)");
+DEFINE_bool(use_approx_sort, true, "sort partial sends approximately");
+DEFINE_uint64(num_zmq_threads, 1, "ZeroMQ I/O threads per context");
 #endif
 
 namespace petuum {
+
+// The flags-mode marker the declare headers reference (see table_gflags_declare.hpp).
+namespace flags_mode {
+#if PETUUM_PS_HAVE_GFLAGS
+extern const int libpetuum_ps_built_with_gflags = 1;
+#else
+extern const int libpetuum_ps_built_without_gflags = 1;
+#endif
+}  // namespace flags_mode
 
 // init_table_config.cpp:13-42
 void InitTableConfig(ClientTableConfig *config) {

@@ -12,8 +12,8 @@
 
 namespace psx {
 
-constexpr int kMaxFused = 16;
-constexpr int kNsStride = 32;   // OrdArgs::nsplit: uint32 words between two counters   // == PSX_MAX_FUSED_STREAMS
+constexpr int kMaxFused = 16;   // == PSX_MAX_FUSED_STREAMS
+constexpr int kNsStride = 32;   // OrdArgs::nsplit: uint32 words between two counters
 constexpr int kMaxTables = 64;  // == PSX_MAX_TABLES
 constexpr int kWave = 64;
 

@@ -628,6 +628,112 @@ def progress(msg, rank=0):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+
+# ---- GPU telemetry (attribute the box-to-box spread of the headline) -----
+# Read-only amdsmi queries: clocks, power, temperatures and throttle state of the GPU this
+# rank drives, matched to torch's device by PCI address.  Never inside a timed region: a
+# snapshot before and after it, and samples from a background thread during an untimed
+# repeat of the same steps.
+SMI_KEYS = ("current_gfxclk", "average_gfxclk_frequency", "current_uclk", "average_uclk_frequency",
+            "current_socket_power", "average_socket_power", "temperature_hotspot", "temperature_mem",
+            "temperature_edge", "gfx_activity", "umc_activity", "mem_activity", "throttle_status",
+            "indep_throttle_status", "current_gfxclks", "current_socclks", "current_vclk0s")
+SMI_VIOLATION_KEYS = ("active_prochot_thrm", "active_ppt_pwr", "active_socket_thrm", "active_vr_thrm",
+                      "active_hbm_thrm", "per_prochot_thrm", "per_ppt_pwr", "per_socket_thrm", "per_vr_thrm",
+                      "per_hbm_thrm", "acc_counter")
+
+
+def _smi_handle(local):
+    import amdsmi
+    import torch
+    amdsmi.amdsmi_init()
+    hs = amdsmi.amdsmi_get_processor_handles()
+    p = torch.cuda.get_device_properties(local)
+    want = (getattr(p, "pci_domain_id", None), getattr(p, "pci_bus_id", None), getattr(p, "pci_device_id", None))
+    for h in hs:
+        try:
+            dom, bus, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
+            if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                return h
+        except Exception:   # noqa: BLE001
+            continue
+    return hs[0] if len(hs) == 1 else None
+
+
+def _smi_clean(v):
+    if isinstance(v, (list, tuple)):
+        vals = [x for x in v if isinstance(x, (int, float)) and x not in (0xFFFF, 0xFFFFFFFF)]
+        return {"min": min(vals), "max": max(vals), "n": len(vals)} if vals else None
+    if isinstance(v, (int, float)) and v not in (0xFFFF, 0xFFFFFFFF, 0xFFFFFFFFFFFFFFFF):
+        return v
+    return None
+
+
+def smi_snapshot(h):
+    import amdsmi
+    out = {}
+    try:
+        m = amdsmi.amdsmi_get_gpu_metrics_info(h)
+        for k in SMI_KEYS:
+            if k in m:
+                out[k] = _smi_clean(m[k])
+    except Exception as e:   # noqa: BLE001 - reported, never fatal
+        out["metrics_error"] = repr(e)[:200]
+    try:
+        v = amdsmi.amdsmi_get_violation_status(h)
+        out["violation"] = {k: _smi_clean(v[k]) for k in SMI_VIOLATION_KEYS if k in v}
+    except Exception as e:   # noqa: BLE001
+        out["violation_error"] = repr(e)[:200]
+    return out
+
+
+class SmiSampler:
+    """Samples smi_snapshot's metrics every `period` s on a thread until stop()."""
+
+    def __init__(self, h, period=0.002):
+        import threading
+        self.h, self.period, self.samples = h, period, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        import amdsmi
+        while not self._stop.is_set():
+            try:
+                m = amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+                self.samples.append({k: _smi_clean(m.get(k)) for k in
+                                     ("current_gfxclk", "current_uclk", "current_socket_power",
+                                      "temperature_hotspot", "temperature_mem", "throttle_status",
+                                      "current_gfxclks")})
+            except Exception:   # noqa: BLE001
+                pass
+            time.sleep(self.period)
+
+    def start(self):
+        self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
+        out = {"samples": len(self.samples)}
+        for k in ("current_gfxclk", "current_uclk", "current_socket_power", "temperature_hotspot",
+                  "temperature_mem", "throttle_status"):
+            xs = sorted(x[k] for x in self.samples if isinstance(x.get(k), (int, float)))
+            if xs:
+                out[k] = {"min": xs[0], "median": xs[len(xs) // 2], "max": xs[-1]}
+        xcd = [x["current_gfxclks"] for x in self.samples if isinstance(x.get("current_gfxclks"), dict)]
+        if xcd:
+            out["current_gfxclks_per_xcc"] = {"min": min(d["min"] for d in xcd), "max": max(d["max"] for d in xcd)}
+        return out
+
+
+def ms_spread(ms):
+    xs = sorted(ms)
+    if not xs:
+        return None
+    return {"min": round(xs[0], 4), "median": round(xs[len(xs) // 2], 4), "max": round(xs[-1], 4), "n": len(xs)}
+
 C4_CHUNK_BYTES = (1 << 31) - 4   # a worker batch travels as Appendix-A messages of < 2 GiB (the
                                  # reference reader's int32 cursor, serialized_oplog_reader.hpp:137)
 
@@ -708,6 +814,7 @@ class CpuShardExchange:
         self.table, self.bounds, self.rank, self.world = init.clone(), bounds, rank, world
         self.chunks = 0
         self.sent_bytes = self.recv_bytes = 0
+        self.peer_sent, self.peer_recv = [0] * world, [0] * world
         self.split_s = self.wait_s = self.sync_s = self.x_ms = 0.0
 
     def reset_counters(self):
@@ -746,6 +853,22 @@ class CpuShardExchange:
             self.chunks += 1
             self.sent_bytes += sum(sizes)
             self.recv_bytes += sum(rs)
+            for p in range(self.world):
+                if p != self.rank:      # what crosses (a rank's own part stays)
+                    self.peer_sent[p] += int(sizes[p])
+                    self.peer_recv[p] += int(rs[p])
+
+    def comm_info(self):
+        import torch.distributed as dist
+        return {"backend": "gloo (CPU stand-in)", "nranks": dist.get_world_size() if dist.is_initialized() else 1,
+                "rank": dist.get_rank() if dist.is_initialized() else 0, "device": None, "rccl_version": None,
+                "librccl": None}
+
+    def peer_bytes(self, reset=False):
+        out = (list(self.peer_sent), list(self.peer_recv))
+        if reset:
+            self.peer_sent, self.peer_recv = [0] * self.world, [0] * self.world
+        return out
 
     def read_table(self):
         return self.table
@@ -766,6 +889,17 @@ class GlooExchange:
     def __init__(self):
         import torch.distributed as dist
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.peer_sent, self.peer_recv = [0] * self.world, [0] * self.world
+
+    def info(self):
+        return {"backend": "gloo (host copies; test transport)", "nranks": self.world, "rank": self.rank,
+                "device": None, "rccl_version": None, "librccl": None}
+
+    def peer_bytes(self, reset=False):
+        out = (list(self.peer_sent), list(self.peer_recv))
+        if reset:
+            self.peer_sent, self.peer_recv = [0] * self.world, [0] * self.world
+        return out
 
     def sizes_async(self, send_sizes, recv_sizes, stream):
         import torch
@@ -786,6 +920,9 @@ class GlooExchange:
             if int(z):
                 recv[int(o):int(o) + int(z)].copy_(got[st:st + int(z)])
         torch.cuda.synchronize(send.device)
+        for p in range(self.world):
+            self.peer_sent[p] += int(send_sizes[p])
+            self.peer_recv[p] += int(recv_sizes[p])
 
     def close(self):
         pass
@@ -852,6 +989,8 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
         sync()
         progress("warmup step done", rank)
     ex.reset_counters()
+    xport = ex if cpu else xc            # whatever carries the bytes: libpsx's RCCL comm, or gloo
+    xport.peer_bytes(reset=True)
     if srv is not None:
         srv.timing(2)
         srv.timing_reset()
@@ -865,6 +1004,7 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    comm = comm_view(xport, world, steps)
     progress(f"{steps} timed steps in {el:.3f} s; checking parity", rank)
     apply_ms, apply_n = srv.timing_read("dense_apply") if srv is not None else (0.0, 0)
     hbm_used = None
@@ -912,6 +1052,8 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
     # workers' records — the all-to-all form)
     apply_bytes = recv_all / steps + 2.0 * rows_total * cap * 4
     xbytes = msg_bytes * (world - 1) / world          # per rank per step, crossing xGMI
+    if comm.get("crossed_bytes_per_step_max_rank"):
+        xbytes = comm["crossed_bytes_per_step_max_rank"]   # measured by the transport itself
     return {
         "value": round(apply_bytes / per_step / 1e9, 2), "unit": "GB/s (algorithmic apply bytes, all ranks)",
         "n_gpus": world, "steps": steps, "warmup": warmup,
@@ -928,6 +1070,10 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
         # share that crosses the links, (n-1)/n of it
         "exchange_algbw_GBps": round(msg_bytes / (x_ms / steps / 1e3) / 1e9, 2) if x_ms > 0 else None,
         "exchange_busbw_GBps": round(xbytes / (x_ms / steps / 1e3) / 1e9, 2) if x_ms > 0 and world > 1 else None,
+        "exchange_note": None if world > 1 else
+                         "one rank: its own sub-stream never crosses (applied where it lies), so no exchange "
+                         "bandwidth exists to report; comm shows the communicator libpsx built",
+        "comm": comm,
         "apply_kernel_ms_per_chunk": round(apply_ms, 3) if apply_ms else None,
         "hbm_used_GB_max_rank": round(hbm_used / 1e9, 2) if hbm_used else None,
         "setup_s": round(gen_s, 2), "check_s": round(chk_s, 2),
@@ -940,6 +1086,59 @@ def exchange_measure(rows_total, cap, steps, warmup, world, rank, local, seed=42
                                   "one rank: each chunk applied as it is (nothing routes)" if not cpu else
                                   f"{world} shards over gloo (CPU stand-in)"},
     }
+
+
+def comm_view(xport, world, steps):
+    """What each rank's transport itself reports, gathered to every rank: for
+    libpsx's RCCL communicator, psx_comm_info (ncclCommCount / ncclCommUserRank /
+    ncclCommCuDevice / ncclGetVersion and the librccl the process loaded) and
+    psx_comm_peer_bytes (bytes enqueued to / from each peer over the timed steps).  A launch
+    whose ranks did not all build one communicator of `world` ranks says so here
+    (`all_ranks_see_world` false), whatever torch's world size is."""
+    import torch.distributed as dist
+    info = xport.info() if hasattr(xport, "info") else xport.comm_info()
+    sent, recv = xport.peer_bytes()
+    mine = dict(info)
+    mine["sent_bytes_per_peer"] = sent
+    mine["recv_bytes_per_peer"] = recv
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
+    crossed = [sum(r["sent_bytes_per_peer"]) - r["sent_bytes_per_peer"][i] for i, r in enumerate(ranks)]
+    return {
+        "backend": ranks[0].get("backend", "rccl (libpsx psx_comm: grouped ncclSend/ncclRecv)"),
+        "ranks": ranks,
+        "all_ranks_see_world": all(r["nranks"] == world and r["rank"] == i for i, r in enumerate(ranks)),
+        "distinct_devices": len({r["device"] for r in ranks}) if ranks[0].get("device") is not None else None,
+        "crossed_bytes_per_step_max_rank": max(crossed) / steps if steps else None,
+        "crossed_bytes_per_step_all_ranks": sum(crossed) / steps if steps else None,
+    }
+
+
+def rank_view(world, rank, local):
+    """Every rank's own identity, gathered (all ranks call it): its torch rank/world, the
+    device it drives (PCI bus id: distinct ids mean distinct GPUs) and the RCCL version
+    torch's process group links.  For paths with no data-path collective (C5's row-range
+    shards, the headline's pre-split batches) this is the evidence of how many GPUs ran."""
+    import torch
+    import torch.distributed as dist
+    p = torch.cuda.get_device_properties(local)
+    try:
+        nv = ".".join(str(x) for x in torch.cuda.nccl.version())
+    except Exception:   # noqa: BLE001 - reported, not fatal
+        nv = None
+    mine = {"rank": rank, "world": world, "local_device": local,
+            "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                   f"{getattr(p, 'pci_device_id', 0):02x}",
+            "name": p.name, "torch_rccl": nv}
+    out = [None] * world
+    if world > 1:
+        dist.all_gather_object(out, mine)
+    else:
+        out = [mine]
+    return {"ranks": out, "distinct_gpus": len({r["pci"] for r in out})}
 
 
 def run_c4(args):
@@ -1798,21 +1997,45 @@ def main():
     srv.sync()
     torch.cuda.synchronize()
 
+    smi = None
+    try:
+        smi = _smi_handle(local)
+    except Exception as e:   # noqa: BLE001 - telemetry is reported, never fatal
+        smi_err = repr(e)[:200]
+    else:
+        smi_err = None if smi is not None else "no amdsmi handle matches this device's PCI address"
+    smi_before = smi_snapshot(smi) if smi is not None else None
     # Timed region: HIP events bracket only the apply launches (timing mode 2), so the
-    # roofline's launch duration comes from the same steps `value` times.
+    # roofline's launch duration comes from the same steps `value` times; one event pair per
+    # step on the step's stream gives the per-step spread.
     srv.timing(2)
     srv.timing_reset()
+    step_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        step_ev[i][0].record()
         step()
+        step_ev[i][1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     srv.sync()
+    step_ms = [a.elapsed_time(b) for a, b in step_ev]
+    smi_after = smi_snapshot(smi) if smi is not None else None
+    # the same steps again, untimed, with a sampler thread reading clocks / power / temperature
+    smi_during = None
+    if smi is not None:
+        sampler = SmiSampler(smi).start()
+        for _ in range(max(40, args.steps)):
+            step()
+        torch.cuda.synchronize()
+        smi_during = sampler.stop()
+        srv.sync()
     apply_kernel = "ada_apply" if args.adarevision else "dense_apply"
     apply_ms, apply_n = srv.timing_read(apply_kernel)
     # Per-kernel breakdown: a separate, untimed pass with events around every kernel.
@@ -1944,6 +2167,16 @@ def main():
                                    "is 0.70 of single-GPU HBM read bandwidth",
             },
             "kernel_ms_per_launch_breakdown_pass": {k: round(v[0] / max(v[1], 1), 4) for k, v in kernels.items()},
+            "step_ms_spread": ms_spread(step_ms),
+            "telemetry": {
+                "gpu": torch.cuda.get_device_properties(local).name,
+                "before_timed": smi_before, "after_timed": smi_after,
+                "during_untimed_repeat": smi_during,
+                "error": smi_err,
+                "note": "amdsmi (read-only) on this rank's GPU, matched by PCI address: a snapshot before and "
+                        "after the timed region, and ~2 ms samples during an untimed repeat of the same steps "
+                        "(the timed region itself runs with no sampler)",
+            },
             "cpu_baseline": cpu,
         }
 
@@ -2015,6 +2248,7 @@ def main():
             # row-range sharded over the ranks, self-checked
             c5 = c5_measure(args, world, rank, local, 5, 2)
             c5.pop("metric", None)
+            c5["ranks_view"] = rank_view(world, rank, local)
         except Exception as e:
             c5 = {"error": repr(e)[:400]}
         done.set()
@@ -2047,6 +2281,12 @@ def main():
                 other[name] = m
             except Exception as e:
                 other[name] = {"error": repr(e)[:400]}
+    rv = None
+    if world > 1:
+        try:
+            rv = rank_view(world, rank, local)
+        except Exception as e:   # noqa: BLE001 - reported, never allowed to drop the headline
+            rv = {"error": repr(e)[:400]}
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
@@ -2054,6 +2294,8 @@ def main():
             cpu = cpu_baseline(args, host_msgs=[h.numpy() for h in host] if full_c2 else None, base=base)
         del host
         line = build_line(cpu)
+        if rv:
+            line["ranks_view"] = rv
         if walked:
             line["walked"] = walked
         if pcie:

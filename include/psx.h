@@ -94,7 +94,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 8
+#define PSX_ABI_VERSION 9
 
 /* Maximum number of messages fused into one psx_apply_streams_device call. */
 #define PSX_MAX_FUSED_STREAMS 16
@@ -578,6 +578,21 @@ psx_status psx_exchange_streams_v(psx_comm *comm, const void *send, const uint64
  * the same order). */
 psx_status psx_exchange_sizes_async(psx_comm *comm, const uint64_t *send_sizes, uint64_t *recv_sizes,
                                     void *hip_stream);
+/* ABI 9: what RCCL itself reports for this communicator, so that a multi-GPU run can show
+ * how many ranks the exchange really spanned (not the launcher's world size):
+ * nranks = ncclCommCount, rank = ncclCommUserRank, device = ncclCommCuDevice, version =
+ * ncclGetVersion (e.g. 22603 for 2.26.3), path = the librccl shared object this process
+ * loaded (dl_iterate_phdr), NUL-terminated and cut to path_cap bytes.  Any out pointer may
+ * be NULL.  The reference's equivalent fact is the server list a client sends to
+ * (GetPartitionServerID, context.hpp:291-304). */
+psx_status psx_comm_info(psx_comm *comm, int32_t *nranks, int32_t *rank, int32_t *device, int32_t *version,
+                         char *path, size_t path_cap);
+/* ABI 9: bytes this rank has enqueued for each peer (sent[p]) and from each peer (recv[p])
+ * through psx_exchange_streams(_v) since psx_comm_create or the last reset (reset != 0
+ * zeroes the counters after reading them); each array holds nranks entries (NULL skips
+ * it).  The per-server byte counts the reference's bg worker accumulates per send
+ * (abstract_bg_worker.cpp:651-689). */
+psx_status psx_comm_peer_bytes(psx_comm *comm, uint64_t *sent, uint64_t *recv, int32_t reset);
 
 /* ---- server statistics ------------------------------------------------------------ */
 /* ABI 7: what the reference server thread accumulates around each apply with

@@ -58,11 +58,13 @@ enum {
                                    <= 3 records whose image stays within 64 entries to a launch of
                                    their own, four to a wave, 16 lanes each; 0 (default): one row per
                                    wave */
-  PSX_DEBUG_ORD_PROBE = 23,     /* timing only (results wrong), bits: 1 the register apply of split
+  PSX_DEBUG_ORD_PROBE = 23,     /* debug build only (libpsx_debug.so; -1 in libpsx.so); timing only (results wrong), bits: 1 the register apply of split
                                    tables does each row's setup (record references, headers, first
                                    record's pairs, image, key map) but applies no record; 2 it
                                    writes no row back; 4 it loads no record reference, header
                                    or pair (a row is its image, key map and write-back) */
+  PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
+                                   4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from
                                    its composed maps by one record; the cross-check after the
                                    window's resolve must fail the call (PSX_ERR_DEVICE, nothing

@@ -202,6 +202,8 @@ def load():
         "psx_exchange_streams": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "psx_exchange_sizes_async": ([vp, vp, vp, vp], ctypes.c_int),
         "psx_exchange_streams_v": ([vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "psx_comm_info": ([vp, P(i32), P(i32), P(i32), P(i32), ctypes.c_char_p, sz], ctypes.c_int),
+        "psx_comm_peer_bytes": ([vp, vp, vp, i32], ctypes.c_int),
         "psx_debug_set_variant": ([i32, i32], i32),
         "psx_debug_get_variant": ([i32], i32),
         "psx_debug_walk_trace": ([vp, vp, ctypes.c_int64], ctypes.c_int64),

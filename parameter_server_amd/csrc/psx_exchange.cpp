@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <link.h>
+
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,6 +35,7 @@ struct psx_comm {
   uint64_t *h_send = nullptr;    // [kSizeSlots][nranks], page-locked
   hipEvent_t ev[kSizeSlots] = {};
   int next_slot = 0;
+  std::vector<uint64_t> sent, recvd;   // bytes enqueued per peer (psx_comm_peer_bytes)
   std::string err;
 };
 
@@ -109,6 +112,8 @@ psx_status psx_comm_create(const void *id, int32_t nranks, int32_t rank, int32_t
   std::memcpy(&u, id, sizeof(u));
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
   if (r != ncclSuccess) return cleanup(comm_fail(nullptr, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
+  c->sent.assign((size_t)nranks, 0);
+  c->recvd.assign((size_t)nranks, 0);
   *out = c;
   return PSX_OK;
 }
@@ -204,6 +209,10 @@ static psx_status exchange_v(psx_comm *c, const void *send, const uint64_t *send
     }
   }
   NCCL_TRY(c, ncclGroupEnd());
+  for (int p = 0; p < c->nranks; ++p) {
+    c->sent[p] += send_sizes[p];
+    c->recvd[p] += recv_sizes[p];
+  }
   return PSX_OK;
 }
 
@@ -234,6 +243,49 @@ psx_status psx_exchange_streams_v(psx_comm *c, const void *send, const uint64_t 
       return comm_fail(c, "exchange_streams_v: null buffer with a nonzero size", PSX_ERR_INVALID_ARG);
   HIPX_TRY(c, hipSetDevice(c->device));
   return exchange_v(c, send, send_sizes, send_displs, recv, recv_sizes, recv_displs, (hipStream_t)hip_stream);
+}
+
+static int find_rccl(struct dl_phdr_info *info, size_t, void *out) {
+  if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+    *(std::string *)out = info->dlpi_name;
+    return 1;
+  }
+  return 0;
+}
+
+psx_status psx_comm_info(psx_comm *c, int32_t *nranks, int32_t *rank, int32_t *device, int32_t *version,
+                         char *path, size_t path_cap) {
+  if (!c || !c->comm) return PSX_ERR_INVALID_ARG;
+  int n = 0, r = 0, d = 0, v = 0;
+  NCCL_TRY(c, ncclCommCount(c->comm, &n));
+  NCCL_TRY(c, ncclCommUserRank(c->comm, &r));
+  NCCL_TRY(c, ncclCommCuDevice(c->comm, &d));
+  NCCL_TRY(c, ncclGetVersion(&v));
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  if (device) *device = d;
+  if (version) *version = v;
+  if (path && path_cap) {
+    std::string p;
+    dl_iterate_phdr(find_rccl, &p);
+    const size_t k = p.size() < path_cap - 1 ? p.size() : path_cap - 1;
+    std::memcpy(path, p.data(), k);
+    path[k] = 0;
+  }
+  return PSX_OK;
+}
+
+psx_status psx_comm_peer_bytes(psx_comm *c, uint64_t *sent, uint64_t *recv, int32_t reset) {
+  if (!c) return PSX_ERR_INVALID_ARG;
+  for (int p = 0; p < c->nranks; ++p) {
+    if (sent) sent[p] = c->sent[p];
+    if (recv) recv[p] = c->recvd[p];
+  }
+  if (reset) {
+    c->sent.assign((size_t)c->nranks, 0);
+    c->recvd.assign((size_t)c->nranks, 0);
+  }
+  return PSX_OK;
 }
 
 }  // extern "C"

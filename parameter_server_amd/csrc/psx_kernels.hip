@@ -1230,6 +1230,7 @@ static unsigned resident_blocks(K kernel, int64_t want) {
 // alternatives stay selectable so the parity suite runs every kernel the product can
 // launch (v2 is the >= 4 GiB fallback, v4 the partial-coverage kernel).
 int g_apply_variant = 0;   // 0: auto, 1: force v2, 2: force v4 (compact)
+int g_dense_last = 0;      // PSX_STAT_DENSE_LAST: the dense apply kernel last launched (2, 3, 4)
 
 hipError_t launch_dense_index(StreamSet ss, const IdxSet &ix, uint32_t rows_mask, const Seg *segs, int t, int B,
                               int64_t stride, int64_t row_offset, int64_t row_stride, int64_t max_rows,
@@ -1256,6 +1257,7 @@ hipError_t launch_dense_verify(const int32_t *inv, InvLayout L, int t, int B, in
 template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>
 static void launch_v2(const DenseArgs &a, hipStream_t st) {
   auto k = dense_apply_v2_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
+  g_dense_last = 2;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
@@ -1264,6 +1266,7 @@ static void launch_v2(const DenseArgs &a, hipStream_t st) {
 template <typename V, int BMAX, int TILE, bool NT, int PAIR, bool IMP = false, int H16 = 0>
 static void launch_v3(const DenseArgs &a, hipStream_t st) {
   auto k = dense_apply_v3_kernel<V, BMAX, TILE, NT, PAIR, IMP, H16>;
+  g_dense_last = 3;
   const int64_t tiles = (a.max_rows + TILE - 1) / TILE;
   const unsigned blocks = resident_blocks(k, (tiles + 3) / 4);
   hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, a);
@@ -1303,6 +1306,7 @@ static void launch_adaptive_imp(const DenseArgs &a, hipStream_t st) {
 
 template <typename V>
 static void launch_v4(const DenseArgs &a, hipStream_t st) {
+  g_dense_last = 4;
   if (a.B > 8) {
     auto k = dense_apply_v4_kernel<V, 16, 16, true, 8, 16>;
     hipLaunchKernelGGL(k, dim3(resident_blocks(k, ((a.max_rows + 15) / 16 + 3) / 4)), dim3(256), 0, st, a);

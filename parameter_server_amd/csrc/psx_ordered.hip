@@ -29,6 +29,14 @@
 
 namespace psx {
 
+// The register apply's timing probes (PSX_DEBUG_ORD_PROBE, results wrong) exist only in the
+// debug build (`make debug`); in libpsx.so the branches are compiled out.
+#ifdef PSX_DEBUG_BUILD
+constexpr bool kOrdProbe = true;
+#else
+constexpr bool kOrdProbe = false;
+#endif
+
 
 __device__ __forceinline__ int32_t o_ld32(const uint8_t *p) { return *reinterpret_cast<const int32_t *>(p); }
 
@@ -1467,7 +1475,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       n = __builtin_amdgcn_readfirstlane(a.nent[slot]);
     }
     if (!DRY && lane == 0) a.flags[slot] = 3;
-    if (!DRY && (a.probe & 4)) L = 0;   // timing probe: no record references, headers or pairs
+    if (!DRY && (kOrdProbe && (a.probe & 4))) L = 0;   // timing probe: no record references, headers or pairs
     {
       uint64_t *lst = a.list + beg;
       uint64_t mine = 0;
@@ -1551,7 +1559,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       bool spilled = false;
       const int32_t n0 = n;
       int32_t Lq = L;
-      if (!DRY && (a.probe & 1)) {   // timing probe: the setup's loads arrive, no record is applied
+      if (!DRY && (kOrdProbe && (a.probe & 1))) {   // timing probe: the setup's loads arrive, no record is applied
         asm volatile("" ::"v"(col_n), "v"(d_n));
         Lq = 0;
       }
@@ -1833,7 +1841,7 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
         }
         continue;
       }
-      if (a.probe & 2) continue;   // timing probe: no write-back
+      if (kOrdProbe && (a.probe & 2)) continue;   // timing probe: no write-back
       // write the row image back (Entry<V> layout; 8-byte V entries carry 4 zero pad bytes)
       uint8_t *wrow = a.entries + slot * a.max_entries * ES;
 #pragma unroll

@@ -781,7 +781,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       // light rows four to a wave (psx_ordered.hip lite_quad): spill mode, sorted/map rows
       // without importance (the light path does not sum it)
       a.lite = psx::g_ord_lite && a.spill && !t.d_imp ? psx::g_ord_lite : 0;
+#ifdef PSX_DEBUG_BUILD
       a.probe = psx::g_ord_probe;
+#endif
       a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1)
                   : (psx::g_walk_rank && !t.cfg.oplog_dense_serialized && c->d_wfill[slot] ? 3 : 0);
     }
@@ -1192,7 +1194,9 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
     if (hipMemset(c->d_counters[k], 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
       return cleanup(PSX_ERR_DEVICE);
   }
-  if (const char *pv = getenv("PSX_PIPELINE")) c->pipeline = atoi(pv);   // A/B runs
+#ifdef PSX_DEBUG_BUILD
+  if (const char *pv = getenv("PSX_PIPELINE")) c->pipeline = atoi(pv);   // A/B runs (debug build only)
+#endif
   if (hipMalloc(&c->d_status, sizeof(uint32_t) * (2 + 2 * kRing)) != hipSuccess ||
       hipMalloc(&c->d_zero, 4096) != hipSuccess)
     return cleanup(PSX_ERR_OOM);
@@ -2839,6 +2843,7 @@ psx_status psx_timing_reset(psx_ctx *c) {
 #include "../../include/psx_debug.h"
 namespace psx {
 extern int g_apply_variant;
+extern int g_dense_last;
 extern int g_ord_split;
 extern int g_offsets_blocks;
 extern int g_dry_blocks;
@@ -2850,6 +2855,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_ORD_SPLIT: return &psx::g_ord_split;
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
+    case PSX_STAT_DENSE_LAST: return &psx::g_dense_last;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
@@ -2858,7 +2864,9 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_LEVELS: return &psx::g_walk_levels;
     case PSX_DEBUG_WALK_SKEW: return &psx::g_walk_skew;
     case PSX_VARIANT_ORD_LITE: return &psx::g_ord_lite;
-    case PSX_DEBUG_ORD_PROBE: return &psx::g_ord_probe;
+#ifdef PSX_DEBUG_BUILD
+    case PSX_DEBUG_ORD_PROBE: return &psx::g_ord_probe;   // timing probes: results wrong
+#endif
     case PSX_VARIANT_WALK_SHAPE: return &psx::g_walk_shape;
     case PSX_VARIANT_CALL_EVENTS: return &psx::g_call_events;
     case PSX_VARIANT_OFFSETS_GRID: return &psx::g_offsets_blocks;
@@ -2894,9 +2902,13 @@ extern "C" int64_t psx_debug_walk_trace(psx_ctx *c, uint64_t *out, int64_t max_i
   return (int64_t)items;
 }
 
+#ifdef PSX_DEBUG_BUILD
 namespace {
-// PSX_APPLY_VARIANT / PSX_ORD_SPLIT override the defaults at load time
-// (A/B runs of bench.py and the parity suite).
+// Debug build only (`make debug` -> libpsx_debug.so, loaded through PSX_LIB): the
+// PSX_* variables override the kernel selectors at load time, for the A/B runs of
+// tools/gpu_run.sh.  The shipped libpsx.so reads no such variable (a stray
+// variable in a user's environment must not change an apply); there the selectors are
+// reachable only through psx_debug_set_variant.
 struct VariantEnv {
   VariantEnv() {
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
@@ -2913,3 +2925,4 @@ struct VariantEnv {
   }
 } variant_env;
 }  // namespace
+#endif  // PSX_DEBUG_BUILD

@@ -55,6 +55,27 @@ class Exchange:
             self._L.psx_comm_destroy(self._c)
             self._c = ctypes.c_void_p()
 
+    def info(self):
+        """What RCCL itself reports for this communicator (psx_comm_info): the rank count and
+        rank it was built with, its device, the RCCL version and the librccl file loaded."""
+        n, r, d, v = (ctypes.c_int32() for _ in range(4))
+        path = ctypes.create_string_buffer(512)
+        st = self._L.psx_comm_info(self._c, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d), ctypes.byref(v),
+                                   path, len(path))
+        if st:
+            raise _abi.PsxError(st, self._L.psx_comm_last_error(self._c).decode())
+        return {"nranks": n.value, "rank": r.value, "device": d.value, "rccl_version": v.value,
+                "librccl": path.value.decode()}
+
+    def peer_bytes(self, reset=False):
+        """(sent[p], received[p]) bytes enqueued per peer since creation or the last reset."""
+        n = self.world
+        s, r = (ctypes.c_uint64 * n)(), (ctypes.c_uint64 * n)()
+        st = self._L.psx_comm_peer_bytes(self._c, s, r, int(bool(reset)))
+        if st:
+            raise _abi.PsxError(st, self._L.psx_comm_last_error(self._c).decode())
+        return [int(x) for x in s], [int(x) for x in r]
+
     def alltoall(self, send, send_sizes, stream=None):
         """send: CUDA uint8 tensor with world sub-streams back to back (owner order).
         Returns (recv, recv_sizes) in source-rank order.  With a `stream` other than the

@@ -69,6 +69,12 @@ int main(int argc, char **argv) {
   PSXCK(nullptr, psx_comm_unique_id(id));
   PSXCK(nullptr, psx_comm_create(id, 1, 0, 0, &comm));
   dl_iterate_phdr(find_rccl, nullptr);
+  int32_t cn = 0, cr = -1, cd = -1, cv = 0;
+  char cpath[512];
+  PSXCK(comm, psx_comm_info(comm, &cn, &cr, &cd, &cv, cpath, sizeof cpath));
+  std::printf("{\"comm_nranks\": %d, \"comm_rank\": %d, \"comm_device\": %d, \"rccl_version\": %d, "
+              "\"comm_librccl\": \"%s\"}\n", cn, cr, cd, cv, cpath);
+  if (cn != 1 || cr != 0 || cd != 0 || std::string(cpath) != g_rccl) return 6;
   uint64_t send_size = n, recv_size = 0, sdis = 0, rdis = displ;
   PSXCK(comm, psx_exchange_sizes(comm, &send_size, &recv_size, st));
   if (recv_size != n) {
@@ -77,6 +83,9 @@ int main(int argc, char **argv) {
   }
   PSXCK(comm, psx_exchange_streams_v(comm, send, &send_size, &sdis, recv, &recv_size, &rdis, st));
   HIPCK(hipStreamSynchronize(st));
+  uint64_t psent = 0, precv = 0;
+  PSXCK(comm, psx_comm_peer_bytes(comm, &psent, &precv, 1));
+  if (psent != n || precv != n) return 7;
   std::vector<uint32_t> back(n / 4);
   HIPCK(hipMemcpy(back.data(), recv + displ, n, hipMemcpyDeviceToHost));
   uint32_t head[16];

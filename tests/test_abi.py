@@ -14,7 +14,7 @@ def test_lib_exports_every_header_symbol(built_lib):
 
 
 def test_abi_version_and_status_strings(built_lib):
-    assert built_lib.psx_abi_version() == 8
+    assert built_lib.psx_abi_version() == 9
     assert built_lib.psx_status_string(0) == b"ok"
     assert built_lib.psx_status_string(2) == b"version gap"
 

@@ -44,6 +44,21 @@ def test_exchange_extra_orchestration_and_parity_over_gloo(world, port):
     assert rec["n_gpus"] == world and rec["parity"] == "bit-exact"
     assert rec["chunks_per_step"] > 1
     assert rec["config"]["shard_rows"] * world == 4096 * world
+    # the transport's own view of the run: every rank's communicator size and
+    # rank, and the bytes it moved to / from each peer over the timed steps
+    comm = rec["comm"]
+    assert comm["all_ranks_see_world"] is True and len(comm["ranks"]) == world
+    for i, r in enumerate(comm["ranks"]):
+        assert r["nranks"] == world and r["rank"] == i
+        for k in ("device", "rccl_version", "librccl"):
+            assert k in r
+        assert len(r["sent_bytes_per_peer"]) == world and len(r["recv_bytes_per_peer"]) == world
+        assert r["sent_bytes_per_peer"][i] == 0 and sum(r["sent_bytes_per_peer"]) > 0
+    # what every rank sent to p is what p received from it
+    for i in range(world):
+        for p in range(world):
+            assert comm["ranks"][i]["sent_bytes_per_peer"][p] == comm["ranks"][p]["recv_bytes_per_peer"][i]
+    assert comm["crossed_bytes_per_step_all_ranks"] > 0
 
 
 def test_exchange_parity_check_catches_a_reordered_apply():

@@ -97,6 +97,61 @@ def test_c4_shard_world8_bit_exact_vs_oracle():
                           orc.read_dense_rows(1, base, S).view(np.uint32))
 
 
+def test_v3_message_between_2_and_4_gib_bit_exact():
+    """dense_apply_v3 addresses records by a 32-bit unsigned offset from an SGPR base (the
+    saddr form).  A 2.5 GiB message of width-1024 records puts the offsets of its last
+    ~130K records past 2^31, where a sign-extended offset would address 4 GiB below the
+    message (the round-5 fault of a removed scalar-load variant came from exactly that
+    kind of extension).  One such message plus seven of 100K records, through
+    both placements (row ids from the stream: apply_device; producer record-row lists:
+    apply_indexed_rows, whose row-id check reads at `base + i*stride - 4`), must be
+    bit-exact against the in-order sum, and v3 must be the kernel taken
+    (PSX_STAT_DENSE_LAST).  Reference: the int32 stream cursor this product lifts,
+    serialized_oplog_reader.hpp:137."""
+    from parameter_server_amd import _abi
+    L = _abi.load()
+    PSX_STAT_DENSE_LAST = 24
+    S, cap = 655_360, 1024
+    g = torch.Generator(device="cuda").manual_seed(2025)
+    table0 = torch.randn(S, cap, device="cuda", generator=g) * 0.1
+    bgs = [100 + w for w in range(8)]
+    srv = psa.Server(0, 1, bgs)
+    srv.set_stream(torch.cuda.current_stream().cuda_stream)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=F32, row_capacity=cap, max_rows=S))
+    srv.load_rows(1, 0, None, on_device_ptr=table0.data_ptr(), num_rows=S)
+    streams, msgs, lists = [], [], []
+    for w in range(8):
+        # 100K records each: over 2 records per row in all, so the auto selection takes v3
+        # (sparse_coverage would pick v4 below that)
+        n = S if w == 0 else 100_000
+        perm = torch.randperm(S, device="cuda", generator=g)[:n]
+        upd = torch.randn(n, cap, device="cuda", generator=g) * 0.01
+        streams.append(wire.dense_stream_torch(1, perm.to(torch.int32), upd))
+        lists.append(perm.to(torch.int32))
+        msgs.append((perm, upd))
+    big = streams[0].numel()
+    assert (1 << 31) + (256 << 20) < big < (4 << 30) - (64 << 10)
+    assert (S - 1) * (4 + 4 * cap) > (1 << 31)       # the last records' offsets have bit 31 set
+    torch.cuda.synchronize()
+    L.psx_debug_set_variant(PSX_STAT_DENSE_LAST, 0)
+    _apply_device(srv, streams, bgs, 0)
+    assert L.psx_debug_get_variant(PSX_STAT_DENSE_LAST) == 3, "v3 not taken (walked call)"
+    L.psx_debug_set_variant(PSX_STAT_DENSE_LAST, 0)
+    srv.apply_indexed_rows([(s.data_ptr(), s.numel(), bg, 1) for s, bg in zip(streams, bgs)],
+                           [r.data_ptr() for r in lists])
+    srv.sync()
+    assert L.psx_debug_get_variant(PSX_STAT_DENSE_LAST) == 3, "v3 not taken (record-row call)"
+    del streams, lists
+    ref = _in_order_reference(_in_order_reference(table0, msgs), msgs)
+    del msgs, table0
+    got = torch.empty_like(ref)
+    assert L.psx_table_read_rows(srv.handle, 1, 0, S, got.data_ptr(), 1) == 0
+    torch.cuda.synchronize()
+    ndiff = int((got.view(torch.int32) != ref.view(torch.int32)).sum().item())
+    assert ndiff == 0, f"{ndiff} values differ"
+    srv.close()
+
+
 def test_c4_stream_over_4gib_bit_exact():
     """A C4 shard message larger than 4 GiB (1.1M width-1024 records = 4.5 GB) followed by
     seven smaller ones: v3's 32-bit record offsets cannot address it, so the runtime takes

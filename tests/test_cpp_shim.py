@@ -62,7 +62,13 @@ def test_cpp_exchange_past_2gib_on_the_images_rccl(built_lib):
     exe = os.path.join(CPP, "build", "psx_exchange_selftest")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
-    info = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    info = lines[-1]
     assert info["differing_words"] == 0 and info["bytes"] == (2 << 30) + (12 << 10)
     assert info["rccl"].startswith("/opt/rocm"), info["rccl"]
-    print(info)
+    # psx_comm_info: RCCL's own view of the communicator (ncclCommCount / UserRank /
+    # CuDevice / GetVersion) and the librccl the process loaded
+    comm = lines[0]
+    assert comm["comm_nranks"] == 1 and comm["comm_rank"] == 0 and comm["comm_device"] == 0, comm
+    assert comm["comm_librccl"] == info["rccl"] and comm["rccl_version"] > 20000, comm
+    print(comm, info)

@@ -1,4 +1,7 @@
 #!/bin/bash
+# Environment overrides of the kernel selectors (PSX_ORD_SPLIT, PSX_WALK_*, PSX_ORD_PROBE, ...)
+# exist only in the debug build (make -C parameter_server_amd/csrc debug -> libpsx_debug.so):
+# the modes that set one load that library through PSX_LIB.
 # One GPU session on the gpurun box: the steps named on the command line, in order, each
 # under its own time limit; the first failing step ends the session.
 #   tests   pytest -m gpu (the whole suite, one process)
@@ -117,7 +120,7 @@ for db, ks in d.items():
     salu)   # instruction mix of the C3 apply per timing probe (PSX_ORD_PROBE 0 full, 3 setup only, 6 image only)
       for v in ${SALU_PROBES:-0 3 6}; do
         say "salu probe $v"
-        PSX_ORD_PROBE=$v timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM \
+        PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_ORD_PROBE=$v timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM \
           -d "$R/salu/v$v" -o pmc -- python3 bench.py --workload c3 --steps 3 --warmup 1 --cpu-seconds 0 \
           > "$O/salu_v$v.log" 2>&1 || { echo "!! salu probe $v"; tail -5 "$O/salu_v$v.log"; exit 1; }
         python3 tools/pmc_db.py $(find "$R/salu/v$v" -name '*.db' | sort) > "$O/salu_v$v.json" || exit 1
@@ -132,11 +135,11 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "salu_v*.json"))):
                 print(os.path.basename(f), {x: round(y) for x, y in c.items()})
 PY
       ;;
-    c3split) i=0; for v in 1 2 3 1 2 3; do i=$((i+1)); run c3split_${i}_v$v 300 env PSX_ORD_SPLIT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+    c3split) i=0; for v in 1 2 3 1 2 3; do i=$((i+1)); run c3split_${i}_v$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_ORD_SPLIT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
              grep -h '^{' $O/c3split_*.log | cut -c1-400 ;;
-    c3walk) i=0; for v in 0 1 0 1; do i=$((i+1)); run c3walk_${i}_cus$v 300 env PSX_WALK_CUS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+    c3walk) i=0; for v in 0 1 0 1; do i=$((i+1)); run c3walk_${i}_cus$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_WALK_CUS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
             for f in $O/c3walk_*.log; do echo "$f $(grep -h '^{' $f | cut -c1-120)"; done ;;
-    wtrace1) run wtrace1 200 env PSX_WALK_CUS=1 python -u tools/walk_trace.py && head -c 1500 "$O/wtrace1.log" ;;
+    wtrace1) run wtrace1 200 env PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_WALK_CUS=1 python -u tools/walk_trace.py && head -c 1500 "$O/wtrace1.log" ;;
     c2layout) for i in 1 2; do run c2sep_$i 300 env PSX_BENCH_SEPARATE=1 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras && run c2buf_$i 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras || exit 1; done
               for f in $O/c2sep_* $O/c2buf_*; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["roofline"]["avg_launch_ms"], d["walked"]["value"])')"; done ;;
     c2only) run c2only 300 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras ;;
@@ -187,22 +190,22 @@ import json; d=json.load(open('$O/tlb.json'))
 for db, ks in d.items():
     for k, v in ks.items():
         if 'dense_apply' in k: print(db[-40:], {c: round(x) for c, x in v.items()})" ;;
-    c3wc) i=0; for v in 1 0 1 0; do i=$((i+1)); run c3wc_${i}_v$v 300 env PSX_WALK_COUNT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+    c3wc) i=0; for v in 1 0 1 0; do i=$((i+1)); run c3wc_${i}_v$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_WALK_COUNT=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
           for f in $O/c3wc_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     wctests) run wctests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_count_gpu.py tests/test_walk_gpu.py tests/test_sparse_gpu.py tests/test_ord_split_gpu.py tests/test_kats_gpu.py tests/test_indexed_rows_gpu.py ;;
     oldheavy) say oldheavy; timeout -k 10 300 env PSX_LIB=ab_old/libpsx.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ord_split_gpu.py -k every_row_heavy > "$O/oldheavy.log" 2>&1; echo "oldheavy rc=$? (the pre-fix library: a failure here is the collision)"; tail -5 "$O/oldheavy.log" ;;
-    c3fold) i=0; for v in 1 0 1 0; do i=$((i+1)); run c3fold_${i}_v$v 300 env PSX_FOLD_FINISH=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+    c3fold) i=0; for v in 1 0 1 0; do i=$((i+1)); run c3fold_${i}_v$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_FOLD_FINISH=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
             for f in $O/c3fold_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
-    c3lev) i=0; for v in 4 0 4 0; do i=$((i+1)); run c3lev_${i}_v$v 300 env PSX_WALK_LEVELS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+    c3lev) i=0; for v in 4 0 4 0; do i=$((i+1)); run c3lev_${i}_v$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so PSX_WALK_LEVELS=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
             for f in $O/c3lev_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     walkonly) run walkonly 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_walk_gpu.py ;;
     xtests) run xtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_split_gpu.py tests/test_walk_count_gpu.py tests/test_multi_rank_gpu.py ;;
     splittests) run splittests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ord_split_gpu.py tests/test_sparse_gpu.py tests/test_kats_gpu.py ;;
     pcopy) run pcopy 300 tools/probe_copy 10 ${PCOPY:-all} && cat "$O/pcopy.log" ;;
     bare) run bare 900 python -u bench.py ;;
-    c2ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c2ab_${i}_v$v 300 env ${AB_VAR:-PSX_INDEX_SCALAR}=$v python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras || exit 1; done
+    c2ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c2ab_${i}_v$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so ${AB_VAR:-PSX_INDEX_SCALAR}=$v python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-extras || exit 1; done
             for f in $O/c2ab_*.log; do echo "$f $(grep -h "^{" $f | python3 -c "import json,sys; d=json.load(sys.stdin); print(d[\"value\"], d[\"roofline\"][\"avg_launch_ms\"], d.get(\"walked\",{}).get(\"value\"), d.get(\"walked\",{}).get(\"ms_per_step\"))")"; done ;;
-    c3ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c3ab_${i}_v$v 300 env ${AB_VAR:-PSX_ORD_LITE}=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
+    c3ab) i=0; for v in ${AB_VALUES:-0 1 0 1}; do i=$((i+1)); run c3ab_${i}_v$v 300 env PSX_LIB=parameter_server_amd/libpsx_debug.so ${AB_VAR:-PSX_ORD_LITE}=$v python -u bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0 || exit 1; done
             for f in $O/c3ab_*.log; do echo "$f $(grep -h '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d["kernel_ms_per_step_breakdown_pass"], d.get("pipelined",{}).get("value"))')"; done ;;
     t:*) f=${s#t:}; run t_$(basename "$f" .py) 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread "$f" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -79,6 +79,12 @@
  * concerned are left unchanged.  Errors discovered by device kernels are reported by the next psx_sync() —
  * or by the next call that reads or serves rows, which first settles the calls in
  * flight (so it sees every accepted message, as the reference server thread does).
+ * Versions of a rejected call: a call the device rejects gives each of its senders'
+ * versions back when the error is settled, unless a later call from that sender was
+ * accepted in between (then the version stays consumed, as an empty message would consume
+ * it); the error text names each rejected (bg_id, version) and which of the two happened.
+ * So a sender that settles before its next message (PSX_SEAM_SYNC, or psx_sync) can send
+ * the corrected message again with the same version.
  *
  * Threading: one host thread per context (one context = one server shard = one
  * reference ServerThread, server_thread.hpp:90).  Buffers are borrowed for the call

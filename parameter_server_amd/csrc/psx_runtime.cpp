@@ -1048,6 +1048,28 @@ psx_status sync_impl(psx_ctx *c) {
     uint32_t zero = 0;
     HIP_TRY(c, hipMemcpy(c->d_status, &zero, sizeof(uint32_t), hipMemcpyHostToDevice));
   }
+  // A call the device rejected applied nothing (kStFatal: framing, table, row range,
+  // capacity, ...).  Its senders' versions are given back where no later call from the same
+  // sender has been accepted since, so the corrected message can be sent again with the same
+  // version (the reference has no such case: it aborts, server.cpp:124 / reader :112).
+  // Otherwise the version stays consumed; the error names the call either way.
+  std::string rejected;
+  if (sticky & psx::kStFatal) {
+    std::vector<uint32_t> log(kRing);
+    HIP_TRY(c, hipMemcpy(log.data(), c->d_status + 1 + kRing, sizeof(uint32_t) * kRing, hipMemcpyDeviceToHost));
+    for (const PendingCall &p : pending) {
+      if (!(log[p.ring] & psx::kStFatal)) continue;
+      for (const psx_stream &m : p.streams) {
+        auto it = c->versions.find(m.bg_id);
+        const bool back = it != c->versions.end() && it->second == (int64_t)m.version;
+        if (back) it->second = (int64_t)m.version - 1;
+        if (rejected.size() < 512)
+          rejected += " [bg_id " + std::to_string(m.bg_id) + " version " + std::to_string(m.version) +
+                      (back ? ": version given back]" : ": version stays consumed, a later call from the sender "
+                                                        "was accepted]");
+      }
+    }
+  }
   // An error stored by an earlier automatic sync is reported after this sync has done
   // its own work (the replay below), so no accepted call is ever dropped.
   const psx_status deferred = c->deferred;
@@ -1092,7 +1114,10 @@ psx_status sync_impl(psx_ctx *c) {
     }
   }
   psx_status e = sticky_error(c, sticky & ~psx::kStDuplicateRow);
-  if (e) return finish(e);
+  if (e) {
+    if (!rejected.empty()) c->err += "; rejected (nothing applied):" + rejected;
+    return finish(e);
+  }
   return finish(sticky_error(c, replay_sticky));
 }
 
@@ -1591,6 +1616,12 @@ psx_status psx_apply_streams_device(psx_ctx *c, const psx_stream *s, int32_t n) 
 
 static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
                                     const uint64_t *const *record_offsets, const int32_t *const *record_rows) {
+  // A full call ring is settled first: the settle may give a rejected call's version back,
+  // which the version check below must see.
+  if (c->pending_calls >= kRing - 1) {
+    psx_status d = sync_impl(c);
+    if (d != PSX_OK) c->deferred = d;
+  }
   // Version rule of Server::ApplyOpLogUpdateVersion (server.cpp:124-126), checked for
   // the whole batch before anything is enqueued.
   std::map<int32_t, int64_t> v = c->versions;
@@ -1608,10 +1639,6 @@ static psx_status apply_device_impl(psx_ctx *c, const psx_stream *s, int32_t n,
     it->second = s[i].version;
   }
   HIP_TRY(c, hipSetDevice(c->device));
-  if (c->pending_calls >= kRing - 1) {
-    psx_status d = sync_impl(c);
-    if (d != PSX_OK) c->deferred = d;
-  }
   psx_status st = enqueue_apply(c, s, n, false, record_offsets, record_rows);
   if (st) return st;
   c->versions = v;
@@ -1624,17 +1651,38 @@ psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, in
   if ((c->compat & PSX_COMPAT_INT32_STREAM_OFFSETS) && oplog_size > (size_t)INT32_MAX)
     return fail(c, PSX_ERR_UNSUPPORTED, "stream of " + std::to_string(oplog_size) +
                                             " bytes: the reference reader's int32 offset_ caps messages below 2 GiB");
+  const uint8_t *p = (const uint8_t *)oplog;
+  const bool empty = oplog_size == 0 || (oplog_size >= 4 && rd32h(p) == 0);   // server.cpp:128, Restart() false
+  const int s = (int)(c->seam_k & 1);   // the staging slot an async call takes
+  if (!empty) {
+    // Settles this call may need happen before its version is checked: a settle may give a
+    // rejected call's version back (sync_impl).
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->pending_calls >= kRing - 1) {
+      psx_status d = sync_impl(c);
+      if (d != PSX_OK) c->deferred = d;
+    }
+    if (c->seam_mode == PSX_SEAM_ASYNC && c->seam_used[s]) {   // slot s last held call seam_k - 2's message
+      HIP_TRY(c, hipEventSynchronize(c->ev_seam_free[s]));
+      // A duplicate-row replay re-reads its calls' messages when it settles: settle it
+      // while slot s still holds the bytes of every pending call
+      uint32_t sticky = 0;
+      HIP_TRY(c, hipMemcpy(&sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+      if (sticky & psx::kStDuplicateRow) {
+        psx_status d = sync_impl(c);
+        if (d != PSX_OK) c->deferred = d;
+      }
+    }
+  }
   auto it = c->versions.find(bg_id);
   if (it == c->versions.end()) return fail(c, PSX_ERR_SENDER, "bg_id " + std::to_string(bg_id) + " not registered");
   if (it->second + 1 != (int64_t)version)
     return fail(c, PSX_ERR_VERSION, "bg_thread_id = " + std::to_string(bg_id) + ": expected version " +
                                         std::to_string(it->second + 1) + ", got " + std::to_string(version));
-  const uint8_t *p = (const uint8_t *)oplog;
-  if (oplog_size == 0 || (oplog_size >= 4 && rd32h(p) == 0)) {   // server.cpp:128, Restart() false
+  if (empty) {
     it->second = version;
     return PSX_OK;
   }
-  HIP_TRY(c, hipSetDevice(c->device));
   psx_status st;
   if (c->seam_mode == PSX_SEAM_ASYNC) {
     // The device validates everything before it touches a row (decode, index, ordered
@@ -1644,18 +1692,6 @@ psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, in
       for (int k = 0; k < 2; ++k) {
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_seam_copied[k], hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_seam_free[k], hipEventDisableTiming));
-      }
-    }
-    const int s = (int)(c->seam_k & 1);
-    if (c->seam_used[s]) {
-      HIP_TRY(c, hipEventSynchronize(c->ev_seam_free[s]));
-      // A duplicate-row replay re-reads its calls' messages when it settles: settle it
-      // while slot s still holds the bytes of every pending call
-      uint32_t sticky = 0;
-      HIP_TRY(c, hipMemcpy(&sticky, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost));
-      if (sticky & psx::kStDuplicateRow) {
-        psx_status d = sync_impl(c);
-        if (d != PSX_OK) c->deferred = d;
       }
     }
     if (oplog_size > c->seam_cap[s]) {
@@ -1672,10 +1708,6 @@ psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, in
     // the caller's bytes have been read once the copy is done: they may be freed on return
     HIP_TRY(c, hipEventSynchronize(c->ev_seam_copied[s]));
     psx_stream one{c->d_seam[s], oplog_size, bg_id, version};
-    if (c->pending_calls >= kRing - 1) {
-      psx_status d = sync_impl(c);
-      if (d != PSX_OK) c->deferred = d;
-    }
     st = enqueue_apply(c, &one, 1, false);
     if (st) return st;
     it->second = version;
@@ -1696,15 +1728,13 @@ psx_status psx_apply_stream(psx_ctx *c, const void *oplog, size_t oplog_size, in
   HIP_TRY(c, hipMemcpyAsync(c->d_staging, oplog, oplog_size, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));   // the caller frees `oplog` after we return
   psx_stream one{c->d_staging, oplog_size, bg_id, version};
-  if (c->pending_calls >= kRing - 1) {
-    psx_status d = sync_impl(c);
-    if (d != PSX_OK) c->deferred = d;
-  }
   st = enqueue_apply(c, &one, 1, false);
   if (st) return st;
   it->second = version;
   // Host messages are applied synchronously, like the reference server thread; this
-  // also lets a duplicate-row replay read the staging buffer before it is reused.
+  // also lets a duplicate-row replay read the staging buffer before it is reused.  A
+  // message the device rejects gives its version back here (sync_impl), so the caller can
+  // correct it and send it again with the same version.
   return sync_impl(c);
 }
 

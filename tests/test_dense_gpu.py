@@ -198,6 +198,54 @@ def _device_stream_errors():
     srv.sync()                                         # error state cleared
 
 
+@pytest.mark.parametrize("entry", ["device", "seam_async", "seam_sync"])
+def test_rejected_call_gives_its_version_back(entry):
+    """a call the device rejects (here a row outside the shard) applies nothing
+    and gives its sender's version back, so the corrected message goes again with the same
+    version — for device batches, the async seam (error at the next settle) and the sync
+    seam (error from the call itself).  If the same sender's next call was accepted before
+    the settle, the rejected version stays consumed and the error says so."""
+    srv, orc = _pair(F32, 10, 8, bgs=[100, 101])
+    if entry == "seam_sync":
+        srv.set_seam(1)
+    bad = wire.dense_stream_np(1, np.array([1, 50], np.int32), np.ones((2, 8), np.float32))
+    good = wire.dense_stream_np(1, np.array([1, 2], np.int32), np.ones((2, 8), np.float32))
+
+    def send(s, bg, v):
+        if entry == "device":
+            d = torch.from_numpy(s).cuda()
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v)])
+            srv.sync()
+        else:
+            srv.ApplyOpLogUpdateVersion(s, s.size, bg, v)
+            srv.sync()
+
+    with pytest.raises(PsxError) as e:
+        send(bad, 100, 0)
+    assert e.value.status == 5 and "version given back" in str(e.value)
+    assert srv.GetBgVersion(100) == -1
+    assert not srv.read_rows(1, 0, 10).any()
+    send(good, 100, 0)                                   # the corrected message, same version
+    assert orc.apply_stream(good, 100, 0) == 0
+    assert srv.GetBgVersion(100) == 0
+    assert np.array_equal(_bits(srv.read_rows(1, 0, 10)), _bits(orc.read_dense_rows(1, 0, 10)))
+    if entry == "device":
+        # a rejected call, then the same sender's next call accepted before the settle
+        d0 = torch.from_numpy(bad.copy()).cuda()
+        d1 = torch.from_numpy(good.copy()).cuda()
+        torch.cuda.synchronize()
+        srv.apply_device([(d0.data_ptr(), d0.numel(), 101, 0)])
+        srv.apply_device([(d1.data_ptr(), d1.numel(), 101, 1)])
+        with pytest.raises(PsxError) as e:
+            srv.sync()
+        assert "stays consumed" in str(e.value)
+        assert srv.GetBgVersion(101) == 1
+        assert orc.apply_stream(np.zeros(0, np.uint8), 101, 0) == 0      # the consumed version
+        assert orc.apply_stream(good, 101, 1) == 0
+        assert np.array_equal(_bits(srv.read_rows(1, 0, 10)), _bits(orc.read_dense_rows(1, 0, 10)))
+
+
 def test_duplicate_row_in_one_message_applied_in_order():
     """A row twice in one message is replayed on the ordered path: both records apply."""
     srv, orc = _pair(F32, 10, 8, bgs=[100])

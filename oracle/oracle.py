@@ -40,6 +40,7 @@ def lib():
         L.orc_register_sender.argtypes = [vp, i32]
         L.orc_table_create.argtypes = [vp, i32, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64, i64]
         L.orc_apply_stream.argtypes = [vp, vp, sz, i32, ctypes.c_uint32]
+        L.orc_apply_stream_once.argtypes = [vp, vp, sz, i32, ctypes.c_uint32]
         L.orc_sender_version.argtypes = [vp, i32]
         L.orc_sender_version.restype = i64
         L.orc_row_exists.argtypes = [vp, i32, i32]
@@ -175,6 +176,14 @@ class OracleServer:
         buf = np.ascontiguousarray(buf)
         return self._L.orc_apply_stream(self._s, _ptr(buf) if buf.size else None,
                                         buf.size, bg, version)
+
+    def apply_stream_once(self, data, bg, version):
+        """The reference's one-pass loop shape (orc_apply_stream_once): for timing only —
+        a malformed stream is found after the records before it were applied."""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        buf = np.ascontiguousarray(buf)
+        return self._L.orc_apply_stream_once(self._s, _ptr(buf) if buf.size else None,
+                                             buf.size, bg, version)
 
     def sender_version(self, bg):
         return self._L.orc_sender_version(self._s, bg)

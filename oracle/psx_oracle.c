@@ -706,10 +706,14 @@ static size_t dense_body_bytes(const orc_table *t) {
 /* Walk the stream exactly as SerializedOpLogReader::Restart/Next/StartNewTable
  * (serialized_oplog_reader.hpp:30-133) with AbstractRowOpLog::ParseSparseSerializedOpLog
  * (abstract_row_oplog.hpp:64-78) / DenseRowOpLog::ParseDenseSerializedOpLog
- * (dense_row_oplog.hpp:138-144).  apply=0 only validates; apply=1 applies each record
- * through ServerTable::ApplyRowOpLog (server_table.cpp:164-189), creating missing rows
- * first (server.cpp:163-166). */
-static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) {
+ * (dense_row_oplog.hpp:138-144).  mode 0 only validates; 1 applies each record through
+ * ServerTable::ApplyRowOpLog (server_table.cpp:164-189), creating missing rows first
+ * (server.cpp:163-166); 2 is the reference's own loop shape, one pass that checks each
+ * record as it reaches it and applies it (server.cpp:154-178) — a malformed stream is
+ * then found part-way, after the records before it were applied (the reference CHECK-
+ * aborts there), so mode 2 is for timing only (bench.py's cpu_baseline legs). */
+static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int mode) {
+  const int apply = mode != 0;
   if (size < 4) return ORC_ERR_MALFORMED;
   int32_t num_tables = rd32(b);
   size_t off = 4;
@@ -774,7 +778,7 @@ static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) 
         size_t rs = 4 + (size_t)n * (4 + vs);
         if (off + rs > size) return ORC_ERR_MALFORMED;
         const int32_t *cols = (const int32_t *)(b + off + 4);
-        if (!apply && t->kind == KIND_DENSE) {
+        if (mode != 1 && t->kind == KIND_DENSE) {
           for (int32_t i = 0; i < n; ++i) {
             int32_t c; memcpy(&c, b + off + 4 + (size_t)i * 4, 4);
             if (c < 0 || c >= t->row_capacity) return ORC_ERR_CAPACITY;
@@ -783,11 +787,12 @@ static int walk_stream(orc_server *s, const uint8_t *b, size_t size, int apply) 
         if (apply) {
           orc_row *r = find_row(t, row_id);
           if (!r) r = create_row(t, row_id);
-          /* cols may be unaligned in a host buffer: copy out */
-          int32_t *cc = (int32_t *)malloc((size_t)(n ? n : 1) * 4);
+          /* cols may be unaligned in a host buffer: copy out (on the stack when short) */
+          int32_t stack_cols[256];
+          int32_t *cc = n <= 256 ? stack_cols : (int32_t *)malloc((size_t)n * 4);
           memcpy(cc, cols, (size_t)n * 4);
           apply_sparse_record(t, r, cc, b + off + 4 + (size_t)n * 4, n);
-          free(cc);
+          if (cc != stack_cols) free(cc);
           r->dirty = 1;
           r->version++;   /* VersionServerRow::ApplyBatchInc* (version_server_row.hpp:28-42) */
         }
@@ -811,6 +816,22 @@ int orc_apply_stream(orc_server *s, const void *oplog, size_t size, int32_t bg, 
   if (st != ORC_OK) return st;
   s->bg_versions[bi] = version;
   return walk_stream(s, b, size, 1);
+}
+
+/* The reference's loop shape for the timed CPU baseline: one walk that validates each
+ * record as it reaches it and applies it (server.cpp:154-178), instead of
+ * orc_apply_stream's validate-then-apply pair of walks (which the checker needs so that a
+ * failed message applies nothing).  Results are identical on well-formed streams. */
+int orc_apply_stream_once(orc_server *s, const void *oplog, size_t size, int32_t bg, uint32_t version) {
+  int bi = -1;
+  for (int i = 0; i < s->nbg; ++i) if (s->bg_ids[i] == bg) bi = i;
+  if (bi < 0) return ORC_ERR_SENDER;
+  if (s->bg_versions[bi] + 1 != (int64_t)version) return ORC_ERR_VERSION;   /* :124-126 */
+  s->bg_versions[bi] = version;
+  if (size == 0) return ORC_OK;                                              /* :128 */
+  const uint8_t *b = (const uint8_t *)oplog;
+  if (size >= 4 && rd32(b) == 0) return ORC_OK;
+  return walk_stream(s, b, size, 2);
 }
 
 int64_t orc_sender_version(orc_server *s, int32_t bg) {

@@ -227,3 +227,31 @@ def test_covtype_fixture_matches_its_meta():
     assert labels <= set(range(1, 8))
     idx = {int(t.split(":")[0]) for r in rows for t in r[1:]}
     assert min(idx) >= 1 and max(idx) <= 54
+
+
+def test_single_pass_apply_matches_two_pass():
+    """orc_apply_stream_once (bench.py's timed CPU baseline: the reference's one-pass loop
+    shape, server.cpp:154-178) gives the checker's two-pass result on well-formed streams,
+    sorted-map entry order and dense bits included."""
+    import numpy as np
+    from oracle.oracle import OracleServer, SORTED_MAP, DENSE, I32, F32
+    from parameter_server_amd import wire
+    rng = np.random.RandomState(3)
+    a, b = OracleServer([100]), OracleServer([100])
+    for o in (a, b):
+        o.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+        o.create_table(4, DENSE, F32, 16)
+    for v in range(6):
+        recs = []
+        for rid in rng.choice(400, size=80, replace=False):
+            k = rng.randint(1, 300)
+            cols = np.sort(rng.choice(1024, size=k, replace=False)).astype(np.int32)
+            recs.append((int(rid), cols, (rng.randint(1, 4, size=k) * rng.choice([-1, 1], size=k)).astype(np.int32)))
+        s = wire.sparse_stream_np(3, 4, recs) if v % 2 == 0 else \
+            wire.dense_stream_np(4, rng.permutation(400)[:50].astype(np.int32),
+                                 rng.normal(0, 1, (50, 16)).astype(np.float32))
+        assert a.apply_stream(s, 100, v) == 0 and b.apply_stream_once(s, 100, v) == 0
+    ids = list(range(400))
+    assert a.serialize_records(3, ids) == b.serialize_records(3, ids)
+    assert np.array_equal(a.read_dense_rows(4, 0, 400).view(np.uint32), b.read_dense_rows(4, 0, 400).view(np.uint32))
+    assert b.apply_stream_once(np.zeros(0, np.uint8), 100, 9) == 2       # version rule kept

@@ -92,35 +92,43 @@ __device__ void emit_row(const ServeArgs &a, int64_t s, uint8_t *rec, int lane) 
     }
     return;
   }
+  // A record behind a binary16 row of odd width (another table earlier in the same push)
+  // starts on a 2-byte boundary: then every word goes out as two 16-bit stores.
+  // The test is per record, so wave-uniform.
+  const bool a2 = ((uintptr_t)rec & 3) != 0;
+  auto put = [&](uint8_t *p, uint32_t v) {
+    if (a2) st32_a2(p, v);
+    else *reinterpret_cast<uint32_t *>(p) = v;
+  };
   if (lane == 0) {
     const int32_t rid = (int32_t)(a.row_offset + s * a.row_stride);
-    reinterpret_cast<int32_t *>(rec)[0] = rid;
-    reinterpret_cast<uint32_t *>(rec)[1] = (uint32_t)(uint64_t)total;          // size_t, 4-aligned
-    reinterpret_cast<uint32_t *>(rec)[2] = (uint32_t)((uint64_t)total >> 32);
+    put(rec, (uint32_t)rid);
+    put(rec + 4, (uint32_t)(uint64_t)total);          // size_t
+    put(rec + 8, (uint32_t)((uint64_t)total >> 32));
     if (a.ver) {
       const uint64_t v = a.ver[s];
-      reinterpret_cast<uint32_t *>(rec + 12 + body)[0] = (uint32_t)v;
-      reinterpret_cast<uint32_t *>(rec + 12 + body)[1] = (uint32_t)(v >> 32);
+      put(rec + 12 + body, (uint32_t)v);
+      put(rec + 16 + body, (uint32_t)(v >> 32));
     }
   }
-  uint32_t *dst = reinterpret_cast<uint32_t *>(rec + 12);
+  uint8_t *dst = rec + 12;
   if (a.kind == 0) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(a.dense + s * a.row_cap * a.vsize);
-    for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
+    for (int64_t w = lane; w < body / 4; w += 64) put(dst + w * 4, src[w]);
   } else if (a.kind == 1) {
     const int64_t es = a.vsize == 4 ? 8 : 16;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(a.entries + s * a.max_entries * es);
-    for (int64_t w = lane; w < body / 4; w += 64) dst[w] = src[w];
+    for (int64_t w = lane; w < body / 4; w += 64) put(dst + w * 4, src[w]);
   } else {
     const int64_t es = a.vsize == 4 ? 8 : 16, vo = a.vsize == 4 ? 4 : 8;
     const uint8_t *src = a.entries + s * a.max_entries * es;
     const int32_t n = a.nent[s];
     const int wpe = 1 + a.vsize / 4;                  // words per packed {int32, V}
     for (int32_t e = lane; e < n; e += 64) {
-      uint32_t *d = dst + (int64_t)e * wpe;
-      d[0] = *reinterpret_cast<const uint32_t *>(src + e * es);
-      d[1] = *reinterpret_cast<const uint32_t *>(src + e * es + vo);
-      if (wpe == 3) d[2] = *reinterpret_cast<const uint32_t *>(src + e * es + vo + 4);
+      uint8_t *d = dst + (int64_t)e * wpe * 4;
+      put(d, *reinterpret_cast<const uint32_t *>(src + e * es));
+      put(d + 4, *reinterpret_cast<const uint32_t *>(src + e * es + vo));
+      if (wpe == 3) put(d + 8, *reinterpret_cast<const uint32_t *>(src + e * es + vo + 4));
     }
   }
   if (lane == 0 && a.flags_rw) {

@@ -182,3 +182,45 @@ def test_odd_width_client_cache_is_refused_and_non_float_rows_rejected():
                                          row_bytes_f16=True))
     assert e.value.status == 10
     cli.close()
+
+
+def test_odd_width_f16_table_then_dense_f64_and_sorted_tables_in_one_push():
+    """an odd-width binary16 table leaves the next table's records on a 2-byte
+    boundary in the same push body; the dense f64 and sorted-map tables behind it must come
+    out byte for byte as the oracle writes them (their word stores go out as 16-bit halves
+    there, psx_serve.hip emit_row)."""
+    from oracle.oracle import SORTED_MAP, F64, I32
+    rng = np.random.RandomState(77)
+    cap, rows, K = 37, 90, 64
+    bgs = [100]
+    srv = psa.Server(0, 1, bgs)
+    orc = OracleServer(bgs)
+    srv.CreateTable(1, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=psa.F32, row_capacity=cap, max_rows=rows,
+                                     row_bytes_f16=True))
+    orc.create_table(1, DENSE, F32, cap, f16_rows=True)
+    srv.CreateTable(2, psa.TableInfo(row_kind=psa.ROW_DENSE, dtype=F64, row_capacity=5, max_rows=rows))
+    orc.create_table(2, DENSE, F64, 5)
+    srv.CreateTable(3, psa.TableInfo(row_kind=SORTED_MAP, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                     max_rows=rows, max_entries=K))
+    orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+    msgs = []
+    ids = rng.permutation(rows)[:31].astype(np.int32)          # an odd number of odd-width rows
+    msgs.append(wire.dense_stream_np(1, ids, _values(rng, (ids.size, cap))))
+    ids2 = rng.permutation(rows)[:40].astype(np.int32)
+    msgs.append(wire.dense_stream_np(2, ids2, rng.normal(0, 1, (ids2.size, 5))))
+    recs = []
+    for rid in rng.choice(rows, size=25, replace=False):
+        k = rng.randint(1, 12)
+        cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+        recs.append((int(rid), cols, rng.randint(1, 4, size=k).astype(np.int32)))
+    msgs.append(wire.sparse_stream_np(3, 4, recs))
+    for v, m in enumerate(msgs):
+        d = torch.from_numpy(m).cuda()
+        torch.cuda.synchronize()
+        srv.apply_device([(d.data_ptr(), d.numel(), 100, v)])
+        srv.sync()
+        assert orc.apply_stream(m, 100, v) == 0
+    got = bytes(srv.serialize_dirty(clear=True))
+    want = bytes(orc.serialize_dirty([1, 2, 3], clear=True))
+    assert got == want
+    srv.close()

@@ -86,6 +86,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU shard")
     p.add_argument("--cols", type=int, default=256)
+    p.add_argument("--variant", action="append", default=[], metavar="ID=VALUE",
+                   help="A/B runs: psx_debug_set_variant(ID, VALUE) before anything runs (include/psx_debug.h)")
     p.add_argument("--batches", type=int, default=8)
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of the cpu_baseline sample (0 disables)")
@@ -504,8 +506,8 @@ def c3_measure(args, indexed, steps, warmup, cpu_seconds, pipeline=False):
     import parameter_server_amd as psa
     rows, K, B = 100_000, 1024, args.batches
     streams, nupd, batches = c3_streams(rows, K, B, with_records=True)
-    # the product's decode (include/psx_debug.h PSX_VARIANT_DECODE; PSX_DECODE_WALK=0|1 in
-    # the environment overrides it at load); the JSON line names the path that ran
+    # the product's decode (include/psx_debug.h PSX_VARIANT_DECODE: `--variant 7=0|1`, or
+    # PSX_DECODE_WALK in the debug build's environment); the JSON line names the path that ran
     from parameter_server_amd import _abi as _ab
     L = _ab.load()
     decode_variant = L.psx_debug_get_variant(7)
@@ -1920,6 +1922,12 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
+    if args.variant:
+        from parameter_server_amd import _abi
+        for kv in args.variant:
+            k, v = (int(x) for x in kv.split("="))
+            if _abi.load().psx_debug_set_variant(k, v) < 0:
+                sys.exit(f"--variant {kv}: unknown selector")
     if args.selftest_launch:
         return selftest_launch(args)
     if args.selftest_exchange:

@@ -63,6 +63,13 @@ enum {
                                    record's pairs, image, key map) but applies no record; 2 it
                                    writes no row back; 4 it loads no record reference, header
                                    or pair (a row is its image, key map and write-back) */
+  PSX_VARIANT_PREP_HALVES = 25, /* 1 (default): a pipelined call's split sorted/map tables do the
+                                   records' half of the ordered prep (ordered_place, ordered_fill)
+                                   on the prep stream beside the previous call's apply and the rows'
+                                   half (ordered_classify, dry run) on the context stream; 0: all of
+                                   it (ordered_offsets, ordered_fill, dry run) on the context stream */
+  PSX_VARIANT_CLASSIFY_GRID = 26, /* ordered_classify's grid cap (blocks of 256 touched rows;
+                                   default 256) */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

@@ -464,6 +464,124 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Pipelined split tables: ordered_offsets in two halves.
+//
+// ordered_place is the half that depends only on the call's records: each touched row's
+// record-list range (a block prefix over the counts, one atomic per block for its base) and
+// one compact entry {slot, list begin, records, entries its records can add} per touched
+// row in the call slot's list `plist`; counts (when ranked) and growth return to zero.  It
+// runs on the prep stream after the walk and before ordered_fill, beside the previous
+// call's apply: nothing it reads or writes is the previous call's (count state, offsets and
+// record lists are per call slot or prep-stream only).
+//
+// ordered_classify is the half that depends on the rows' images after that apply (nent):
+// it reads the compact list only — the touched rows, not every slot — and files each row in
+// the apply launches' descriptor lists (256-entry, 1,024-entry, heavy, light) and the
+// capacity dry run's list, as ordered_offsets does, on the context stream.
+__global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *plist) {
+  __shared__ int32_t sh[2][4];
+  __shared__ int32_t base[2];   // touched, records
+  const int64_t R = a.max_rows;
+  const int64_t per = (R + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = (int64_t)blockIdx.x * per;
+  const int64_t c1 = c0 + per < R ? c0 + per : R;
+  if (!o_gate(a)) return;
+  if (per <= (int64_t)blockDim.x) {   // one slot per thread (the usual grid)
+    const int64_t s = c0 + threadIdx.x;
+    const int32_t c = s < c1 ? a.cnt[s] : 0;
+    const bool t = c > 0;
+    int32_t pre[2], tot[2];
+    block_excl_sumN<2>({t ? 1 : 0, c}, pre, tot, sh);
+    if (threadIdx.x == 0) {
+      base[0] = tot[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot[0]) : 0;
+      base[1] = tot[1] ? atomicAdd(&a.tsum[0], tot[1]) : 0;
+    }
+    __syncthreads();
+    if (t) {
+      const int32_t beg = base[1] + pre[1];
+      a.off[s] = beg;
+      plist[base[0] + pre[0]] = int4{(int32_t)s, beg, c, a.grow[s]};
+      a.grow[s] = 0;
+      if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
+    }
+    return;
+  }
+  int32_t nt = 0, nr = 0;   // pass 1: the block's totals, one atomic per counter
+  for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
+    const int32_t c = a.cnt[s];
+    nt += c > 0;
+    nr += c > 0 ? c : 0;
+  }
+  int32_t pre1[2], tot1[2];
+  block_excl_sumN<2>({nt, nr}, pre1, tot1, sh);
+  if (threadIdx.x == 0) {
+    base[0] = tot1[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot1[0]) : 0;
+    base[1] = tot1[1] ? atomicAdd(&a.tsum[0], tot1[1]) : 0;
+  }
+  __syncthreads();
+  int32_t at = base[0], ar = base[1];
+  for (int64_t t0 = c0; t0 < c1; t0 += blockDim.x) {   // pass 2: tiles of 256 slots in slot order
+    const int64_t s = t0 + threadIdx.x;
+    const int32_t c = s < c1 ? a.cnt[s] : 0;
+    const bool t = c > 0;
+    int32_t pre[2], tot[2];
+    block_excl_sumN<2>({t ? 1 : 0, c}, pre, tot, sh);
+    if (t) {
+      const int32_t beg = ar + pre[1];
+      a.off[s] = beg;
+      plist[at + pre[0]] = int4{(int32_t)s, beg, c, a.grow[s]};
+      a.grow[s] = 0;
+      if (a.counted >= 2) a.cnt[s] = 0;
+    }
+    at += tot[0];
+    ar += tot[1];
+  }
+}
+
+__global__ void __launch_bounds__(256) ordered_classify_kernel(OrdArgs a, const int4 *plist) {
+  __shared__ int32_t sh[5][4];
+  __shared__ int32_t base[5];   // 256-entry list, 1,024-entry list, heavy rows, dry run, light rows
+  const int64_t R = a.max_rows;
+  const int64_t n = (int64_t)*a.ntouched;
+  if (!o_gate(a)) return;
+  int4 *const desc = reinterpret_cast<int4 *>(a.split);
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < n; t0 += G) {   // block-uniform trips
+    const int64_t i = t0 + threadIdx.x;
+    const bool t = i < n;
+    int4 e = int4{0, 0, 0, 0};
+    int32_t nen = 0;
+    if (t) {
+      e = plist[i];
+      nen = a.nent[e.x];
+    }
+    const int32_t c = e.z, g = e.w;
+    const bool big = t && starts_big(a, nen, g);
+    const bool heavy = t && !big && starts_heavy(a, c);
+    const bool lite = t && !big && !heavy && starts_lite(a, c, nen, g);
+    const bool risky = t && may_overflow(a, nen, g);
+    int32_t pre[5], tot[5];
+    block_excl_sumN<5>({t && !big && !heavy && !lite ? 1 : 0, big ? 1 : 0, heavy ? 1 : 0, risky ? 1 : 0,
+                        lite ? 1 : 0},
+                       pre, tot, sh);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) base[k] = tot[k] ? (int32_t)atomicAdd(&a.nsplit[k * kNsStride], (uint32_t)tot[k]) : 0;
+    }
+    __syncthreads();
+    if (t) {
+      const int4 d = int4{e.x, e.y, e.y + c, nen};
+      if (risky) desc[2 * R + base[3] + pre[3]] = d;
+      if (big) desc[R + base[1] + pre[1]] = d;
+      else if (heavy) desc[R - 1 - (base[2] + pre[2])] = d;
+      else if (lite) desc[3 * R + base[4] + pre[4]] = d;
+      else desc[base[0] + pre[0]] = d;
+    }
+    __syncthreads();   // base[] is rewritten by the next tile
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Wave-level helpers.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1906,6 +2024,7 @@ static unsigned row_blocks(int64_t n, int wpb) {
 static unsigned few_row_blocks(int64_t n) { return std::min(row_blocks(n, 4), 768u); }
 int g_offsets_blocks = 1024;   // PSX_VARIANT_OFFSETS_GRID: ordered_offsets' grid cap
 int g_dry_blocks = 128;        // PSX_VARIANT_DRY_GRID: the capacity dry run's grid cap
+int g_classify_blocks = 256;   // PSX_VARIANT_CLASSIFY_GRID: ordered_classify's grid cap
 
 static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
   const int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
@@ -1953,6 +2072,37 @@ hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, int2 *wfill, hipStre
   else
     launch_exclusive_scan<int32_t>(a.cnt, a.max_rows, a.off, a.tsum, st);
   hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
+  if (a.kind != 0 && !a.dense_records && a.keyflag) {
+#define PSX_DRY(V) do { if (a.kind == 1) launch_dry<V, 1>(a, dtype, st); else launch_dry<V, 2>(a, dtype, st); } while (0)
+    switch (dtype) {
+      case 0: PSX_DRY(float); break;
+      case 1: PSX_DRY(double); break;
+      case 2: PSX_DRY(int32_t); break;
+      default: PSX_DRY(int64_t); break;
+    }
+#undef PSX_DRY
+  }
+  return hipGetLastError();
+}
+
+// The pipelined split-table prep in its two halves (ordered_place_kernel above): the records'
+// half on the prep stream (ordered_count where the walk did not count, ordered_place,
+// ordered_fill), the rows' half on the context stream (ordered_classify, the capacity dry
+// run).  A split table only (a.grow).
+hipError_t launch_ordered_prep_records(const OrdArgs &a, int2 *wfill, int4 *plist, hipStream_t st) {
+  if (a.counted == 0 || a.counted == 3)
+    hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a, a.counted == 3 ? wfill : nullptr);
+  hipLaunchKernelGGL(ordered_place_kernel,
+                     dim3(std::min(row_blocks(a.max_rows, 256), (unsigned)std::max(1, g_offsets_blocks))), dim3(256), 0,
+                     st, a, plist);
+  hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
+  return hipGetLastError();
+}
+
+hipError_t launch_ordered_prep_rows(int dtype, const OrdArgs &a, const int4 *plist, hipStream_t st) {
+  hipLaunchKernelGGL(ordered_classify_kernel,
+                     dim3(std::min(row_blocks(a.max_rows, 256), (unsigned)std::max(1, g_classify_blocks))), dim3(256),
+                     0, st, a, plist);
   if (a.kind != 0 && !a.dense_records && a.keyflag) {
 #define PSX_DRY(V) do { if (a.kind == 1) launch_dry<V, 1>(a, dtype, st); else launch_dry<V, 2>(a, dtype, st); } while (0)
     switch (dtype) {

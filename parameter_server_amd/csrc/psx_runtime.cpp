@@ -53,6 +53,7 @@ int g_call_events = 0;   // PSX_VARIANT_CALL_EVENTS: bit 0 an event pair per cal
                          // sync interval), bit 1 the slot-free event on every call (else only when pipelining)
 int g_walk_shape = 4;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
+int g_prep_halves = 1;   // PSX_VARIANT_PREP_HALVES: a pipelined call's split tables prep in two halves
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -93,6 +94,8 @@ hipError_t launch_ada_sent(const AdaArgs &a, const int32_t *list, const int64_t 
                            uint64_t clients, const uint64_t *subs, int check_only, hipStream_t st);
 hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t n, uint64_t *out, hipStream_t st);
 hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, int2 *wfill, hipStream_t st);
+hipError_t launch_ordered_prep_records(const OrdArgs &a, int2 *wfill, int4 *plist, hipStream_t st);
+hipError_t launch_ordered_prep_rows(int dtype, const OrdArgs &a, const int4 *plist, hipStream_t st);
 hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk);
 extern int g_ord_split;
 hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st);
@@ -145,6 +148,8 @@ struct TableState {
   int32_t *d_grow = nullptr;       // split sorted/map tables: per-slot entry growth of a call
   int32_t *d_split = nullptr;      // split sorted/map tables: [3][max_rows] row descriptor lists
   uint32_t *d_nsplit = nullptr;    // their lengths
+  int32_t *d_plist = nullptr;      // split tables, pipelined calls: [2][max_rows] int4 touched-row
+                                   // entries by call slot (ordered_place -> ordered_classify)
   uint64_t *d_subs = nullptr;      // CallBackSubs::subscriptions_ per slot (bit c = client c), lazily
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
@@ -189,7 +194,7 @@ struct TableState {
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_grow, t.d_split, t.d_nsplit, t.d_subs, t.d_srv_sizes, t.d_srv_offs,
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_grow, t.d_split, t.d_nsplit, t.d_plist, t.d_subs, t.d_srv_sizes, t.d_srv_offs,
                   t.d_imp, t.d_ver, t.d_acc, t.d_z, t.d_zmax, t.d_snap_ver, t.d_snap_cnt, t.d_snap_acc,
                   t.d_ada_words, t.d_new_keys, t.d_new_slots, t.d_new_tmp, t.d_init, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
@@ -528,9 +533,11 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       if (c->d_list) hipFree(c->d_list);
       c->d_list = nullptr;
       c->list_cap = 0;
-      // the lists, then their mirror: the long-list sort's scratch (psx_ordered.hip
-      // wave_sort_long, rows with > 64 records in one call)
-      HIP_TRY(c, hipMalloc(&c->d_list, 2 * list_need * sizeof(uint64_t)));
+      // the lists of call slot 0, of call slot 1 (a pipelined call fills its lists on the
+      // prep stream while the previous call's apply reads its own), then the long-list
+      // sort's scratch (psx_ordered.hip wave_sort_long, rows with > 64 records in one call;
+      // the apply's only, on the context stream)
+      HIP_TRY(c, hipMalloc(&c->d_list, 3 * list_need * sizeof(uint64_t)));
       c->list_cap = list_need;
     }
   }
@@ -727,12 +734,14 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
         prep);
     if (st) return st;
   }
-  if (pipelined) {
-    HIP_TRY(c, hipEventRecord(c->ev_ready[slot], prep));
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_ready[slot], 0));
-  }
-  // 2) ordered tables, stage 1: record lists, validation, capacity dry run
+  // 2) ordered tables, stage 1: record lists, validation, capacity dry run.  A split table
+  //    of a pipelined call does the half of it that depends only on the call's records
+  //    (counts, list ranges, record lists: ordered_place + ordered_fill) on the prep stream,
+  //    beside the previous call's apply; the half that depends on the rows' images after
+  //    that apply (ordered_classify, the dry run) on the context stream.  Its record lists
+  //    live in the call slot's own region for that reason.
   std::vector<psx::OrdArgs> ord(c->tables.size());
+  std::vector<char> halves(c->tables.size(), 0);
   size_t ord_k = 0;
   for (size_t ti = 0; ti < c->tables.size(); ++ti) {
     TableState &t = c->tables[ti];
@@ -758,8 +767,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.cnt = t.d_cnt + (int64_t)slot * t.cfg.max_rows;
     a.off = t.d_off;
     a.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
-    a.list = c->d_list + list_region * ord_k;
-    a.list_tmp = c->d_list + c->list_cap + list_region * ord_k;
+    a.list = c->d_list + list_region * ((size_t)slot * n_ord + ord_k);
+    a.list_tmp = c->d_list + 2 * c->list_cap + list_region * ord_k;
     ++ord_k;
     a.touched = t.d_touched;
     a.ntouched = c->d_ntouched[slot] + ti;
@@ -786,6 +795,28 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
 #endif
       a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1)
                   : (psx::g_walk_rank && !t.cfg.oplog_dense_serialized && c->d_wfill[slot] ? 3 : 0);
+      if (pipelined && psx::g_prep_halves) {
+        halves[ti] = 1;
+        int2 *wfill = a.counted >= 2 ? c->d_wfill[slot] : nullptr;
+        int4 *plist = reinterpret_cast<int4 *>(t.d_plist) + (size_t)slot * t.cfg.max_rows;
+        st = timed(c, "ordered_place", [&] { return psx::launch_ordered_prep_records(a, wfill, plist, prep); }, prep);
+        if (st) return st;
+      }
+    }
+  }
+  if (pipelined) {
+    HIP_TRY(c, hipEventRecord(c->ev_ready[slot], prep));
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_ready[slot], 0));
+  }
+  for (size_t ti = 0; ti < c->tables.size(); ++ti) {
+    TableState &t = c->tables[ti];
+    if (t.fast() && !force_ordered) continue;
+    const psx::OrdArgs &a = ord[ti];
+    if (halves[ti]) {
+      const int4 *plist = reinterpret_cast<const int4 *>(t.d_plist) + (size_t)slot * t.cfg.max_rows;
+      st = timed(c, "ordered_classify", [&] { return psx::launch_ordered_prep_rows(t.cfg.dtype, a, plist, c->stream); });
+      if (st) return st;
+      continue;
     }
     int2 *wfill = a.counted >= 2 ? c->d_wfill[slot] : nullptr;
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, wfill, c->stream); });
@@ -1467,6 +1498,7 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     if (e == hipSuccess) e = hipMemsetAsync(t.d_grow, 0, 2 * R * sizeof(int32_t), c->stream);
     if (e == hipSuccess) e = hipMalloc(&t.d_split, 4 * R * 4 * sizeof(int32_t));   // int4 descriptors x 4 lists
     if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * 5 * psx::kNsStride * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&t.d_plist, 2 * R * 4 * sizeof(int32_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
@@ -2874,6 +2906,7 @@ psx_status psx_timing_reset(psx_ctx *c) {
 namespace psx {
 extern int g_apply_variant;
 extern int g_dense_last;
+extern int g_classify_blocks;
 extern int g_ord_split;
 extern int g_offsets_blocks;
 extern int g_dry_blocks;
@@ -2886,6 +2919,8 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_DECODE: return &psx::g_decode_walk;
     case PSX_STAT_WALK_CALLS: return &psx::g_walk_calls;
     case PSX_STAT_DENSE_LAST: return &psx::g_dense_last;
+    case PSX_VARIANT_PREP_HALVES: return &psx::g_prep_halves;
+    case PSX_VARIANT_CLASSIFY_GRID: return &psx::g_classify_blocks;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
@@ -2944,6 +2979,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_APPLY_VARIANT")) psx::g_apply_variant = atoi(v);
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_ORD_LITE")) psx::g_ord_lite = atoi(v);
+    if (const char *v = getenv("PSX_PREP_HALVES")) psx::g_prep_halves = atoi(v);
     if (const char *v = getenv("PSX_ORD_PROBE")) psx::g_ord_probe = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);

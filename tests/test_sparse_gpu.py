@@ -172,7 +172,8 @@ def test_failed_call_then_valid_call_matches_oracle(kind, max_entries, err):
     """A call that ordered_count rejects part-way (a row outside the shard, or a column
     outside a dense row / a sorted map's key range), then a valid call on the same context:
     the failed call applies nothing and leaves no per-slot counts behind, so the next call
-    equals the oracle applying only it (stale counts dropped updates)."""
+    equals the oracle applying only it (stale counts dropped updates); it gives its
+    version back, so the next call reuses it."""
     rng = np.random.RandomState(41)
     rows, K = 600, 96
     srv, orc = _pair(kind, I32, rows, K, max_entries=max_entries, bgs=[100])
@@ -191,9 +192,9 @@ def test_failed_call_then_valid_call_matches_oracle(kind, max_entries, err):
     with pytest.raises(PsxError) as e:
         srv.sync()
     assert e.value.status in (5, 6)
-    assert orc.apply_stream(np.zeros(0, np.uint8), 100, 0) == 0     # the version is consumed
+    assert "version given back" in str(e.value) and srv.GetBgVersion(100) == -1
     good = wire.sparse_stream_np(3, 4, _sparse_rows(rng, rows, K, 500, I32, positive=True))
-    _apply(srv, orc, [good], [100], [1])
+    _apply(srv, orc, [good], [100], [0])                            # the rejected call's version again
     if kind == DENSE:
         assert np.array_equal(srv.read_rows(3, 0, rows), orc.read_dense_rows(3, 0, rows))
     elif kind == SORTED_MAP:

@@ -260,3 +260,53 @@ def test_finish_folded_into_the_last_ordered_launch(kind):
     assert a == b
     # the error path through the folded finish (the default)
     test_row_outside_the_shard_fails_and_leaves_counts_clean(1)
+
+
+PREP_HALVES = 25
+
+
+@pytest.mark.parametrize("halves", [1, 0], ids=["prep-halves", "prep-on-context-stream"])
+@pytest.mark.parametrize("split", [3, 2, 1], ids=["spill-heavy-first", "spill", "concurrent"])
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+def test_pipelined_prep_halves_back_to_back(halves, split, kind, walk_rank):
+    """a pipelined call's split tables run the records' half of the ordered
+    prep (ordered_place, ordered_fill: list ranges and record lists, into the call slot's own
+    list region) on the prep stream beside the previous call's apply, and the rows' half
+    (ordered_classify on the images that apply left, the dry run) on the context stream.
+    Eight walked calls back to back with no sync between them, hot Zipf rows whose images
+    cross 256 entries (spills, heavy and light rows), against the oracle byte for byte —
+    and the same with the whole prep on the context stream (PSX_VARIANT_PREP_HALVES 0)."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, 1), L.psx_debug_set_variant(ORD_SPLIT, split),
+           L.psx_debug_set_variant(DECODE, 1), L.psx_debug_set_variant(PREP_HALVES, halves)]
+    rng = np.random.RandomState(500 + split + 7 * halves)
+    rows, K, bgs = 6_000, 1024, [100, 101, 102, 103]
+    calls = _batches(rng, rows, K, 8, per_batch=2_500)
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(PIPELINE_ALL)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, msgs in enumerate(dev):
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)])
+        srv.sync()
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(ORD_SPLIT, old[1])
+        L.psx_debug_set_variant(DECODE, old[2])
+        L.psx_debug_set_variant(PREP_HALVES, old[3])
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    want = orc.serialize_records(3, list(range(rows)))
+    orc.close()
+    if kind == SORTED_MAP:
+        assert got == want
+    else:
+        assert _map_rows(got) == _map_rows(want)

@@ -1923,6 +1923,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     if args.variant:
+        import torch  # noqa: F401 - torch's HIP runtime first: libpsx must bind to the same one
         from parameter_server_amd import _abi
         for kv in args.variant:
             k, v = (int(x) for x in kv.split("="))

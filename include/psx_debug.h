@@ -70,6 +70,11 @@ enum {
                                    it (ordered_offsets, ordered_fill, dry run) on the context stream */
   PSX_VARIANT_CLASSIFY_GRID = 26, /* ordered_classify's grid cap (blocks of 256 touched rows;
                                    default 256) */
+  PSX_VARIANT_CLASSIFY_DRY = 27, /* 1 (default): with the prep in halves, ordered_classify runs as the
+                                   capacity dry run's prologue (one launch: each block files its 256
+                                   touched rows and dry-runs the ones that may overflow); 0: two launches */
+  PSX_VARIANT_WALK_CUS_PIPELINED = 28, /* PSX_VARIANT_WALK_CUS for pipelined calls (default 0: half
+                                   the CUs, the rest left to the previous call's apply) */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

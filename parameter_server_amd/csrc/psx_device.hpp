@@ -207,6 +207,11 @@ struct OrdArgs {
   // log entry and the block counter follow from call_status (kCallRing layout); the last
   // block does finish_call's work (psx_ordered.hip finish_tail).  -1: no fold.
   int32_t fin_ring;
+  // The capacity dry run doing ordered_classify's work first (pipelined split tables,
+  // psx_ordered.hip launch_ordered_prep_rows): plist/nplist are the call slot's compact
+  // touched list and its length (ordered_place); null otherwise.
+  const int4 *plist;
+  const uint32_t *nplist;
 };
 // The context's status words (psx_runtime.cpp d_status): [0] sticky, [1 + k] the call ring,
 // [1 + kCallRing + k] the call log, [1 + 2 kCallRing] the folded finish's block counter.

@@ -1532,18 +1532,69 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   __shared__ V s_sv[4][J * 64];        // found_run: deltas by entry (zero between runs), compaction values
   __shared__ int32_t s_ck[4][J * 64];  // found_run: compaction keys
   __shared__ const uint8_t *s_data[kMaxFused];   // the call's message base pointers
+  // classify + dry run in one launch (DRY with a.plist): the block's risky rows, in LDS
+  constexpr bool kLocal = DRY && J == 16;   // the only dry run of split tables
+  __shared__ int4 s_risky[kLocal ? 256 : 1];
+  __shared__ int32_t s_cls[kLocal ? 5 : 1][4];
+  __shared__ int32_t s_base[6];
   const int lane = threadIdx.x & 63;
   const int wib = threadIdx.x >> 6;
   // the gate's words and the launch's row counts read at once (not one after another)
   const uint32_t st0 = *a.call_status, sk0 = *a.sticky;
   const uint32_t kf0 = DRY && a.keyflag ? *a.keyflag : 0u;
-  const uint32_t nt0 = *a.ntouched, nh0 = a.nheavy ? *a.nheavy : 0u;
+  const bool local = kLocal && a.plist;
+  const uint32_t nt0 = local ? *a.nplist : *a.ntouched, nh0 = a.nheavy ? *a.nheavy : 0u;
   const bool go = !(st0 & (kStFatal | kStDuplicateRow)) && (a.force || !(sk0 & kStDuplicateRow)) &&
                   (!DRY || a.grow || kf0);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows); the
   // row count is final when the launch starts (the folded finish counts the blocks below it)
   const int64_t launch_rows = (int64_t)nt0 + (int64_t)nh0;
-  if (!go || (int64_t)blockIdx.x * 4 >= launch_rows) goto done;
+  if (!go || (int64_t)blockIdx.x * (local ? 256 : 4) >= launch_rows) goto done;
+  if constexpr (kLocal) {
+    if (local) {
+      // ordered_classify's work for the block's 256 entries of the compact touched list
+      // (ordered_place_kernel): each row filed in the apply launches' descriptor lists on the
+      // images the previous call left; the rows whose image can outgrow max_entries stay in
+      // LDS and this block's waves dry-run them below (one launch instead of two).
+      const int64_t R = a.max_rows;
+      int4 *const desc = reinterpret_cast<int4 *>(a.split);
+      const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+      const bool t = i < (int64_t)nt0;
+      int4 e = int4{0, 0, 0, 0};
+      int32_t nen = 0;
+      if (t) {
+        e = a.plist[i];
+        nen = a.nent[e.x];
+      }
+      const int32_t c = e.z, g = e.w;
+      const bool big = t && starts_big(a, nen, g);
+      const bool heavy = t && !big && starts_heavy(a, c);
+      const bool lite = t && !big && !heavy && starts_lite(a, c, nen, g);
+      const bool risky = t && may_overflow(a, nen, g);
+      int32_t pre[5], tot[5];
+      block_excl_sumN<5>({t && !big && !heavy && !lite ? 1 : 0, big ? 1 : 0, heavy ? 1 : 0, lite ? 1 : 0,
+                          risky ? 1 : 0},
+                         pre, tot, s_cls);
+      if (threadIdx.x == 0) {
+        s_base[0] = tot[0] ? (int32_t)atomicAdd(&a.nsplit[0 * kNsStride], (uint32_t)tot[0]) : 0;
+        s_base[1] = tot[1] ? (int32_t)atomicAdd(&a.nsplit[1 * kNsStride], (uint32_t)tot[1]) : 0;
+        s_base[2] = tot[2] ? (int32_t)atomicAdd(&a.nsplit[2 * kNsStride], (uint32_t)tot[2]) : 0;
+        s_base[3] = tot[3] ? (int32_t)atomicAdd(&a.nsplit[4 * kNsStride], (uint32_t)tot[3]) : 0;
+        s_base[4] = tot[4];
+      }
+      __syncthreads();
+      if (t) {
+        const int4 d = int4{e.x, e.y, e.y + c, nen};
+        if (risky) s_risky[pre[4]] = d;
+        if (big) desc[R + s_base[1] + pre[1]] = d;
+        else if (heavy) desc[R - 1 - (s_base[2] + pre[2])] = d;
+        else if (lite) desc[3 * R + s_base[3] + pre[3]] = d;
+        else desc[s_base[0] + pre[0]] = d;
+      }
+      __syncthreads();
+      if (s_base[4] == 0) goto done;   // no risky row in the block (block-uniform)
+    }
+  }
   {
 #pragma unroll
   for (int j = 0; j < J; ++j) s_sv[wib][j * 64 + lane] = V(0);
@@ -1554,19 +1605,25 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   const bool pos_ok = a.keyflag && (a.grow || !*a.keyflag) && a.max_entries <= 1024;
   int16_t *pos = s_pos[wib];
   constexpr int ES = Ent<V>::ES, VO = Ent<V>::VO;
-  const int64_t wave_g = (int64_t)blockIdx.x * 4 + wib;
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  // (local: this block's own waves over its risky rows in LDS)
+  const int64_t wave_g = local ? (int64_t)wib : (int64_t)blockIdx.x * 4 + wib;
+  const int64_t nwaves = local ? 4 : (int64_t)gridDim.x * 4;
   const int32_t cap = (int32_t)a.max_entries;
 
   // one touched row per wave at a time (rows are independent; hot rows spread out);
   // heavy-first: the heavy rows' list (descending from heavy_end) before the rest
-  const int64_t nh = go ? (int64_t)nh0 : 0;
-  const int64_t nt = go ? nh + (int64_t)nt0 : 0;
+  const int64_t nh = go && !local ? (int64_t)nh0 : 0;
+  const int64_t nt = !go ? 0 : local ? (int64_t)s_base[4] : nh + (int64_t)nt0;
   // Descriptor lists: the wave's next row's descriptor is loaded a row ahead (a scalar load:
   // the index is wave-uniform), so a row's setup starts from its record list, not from its
   // descriptor.
   auto desc_at = [&](int64_t t) -> int4 {
     t = (int64_t)__builtin_amdgcn_readfirstlane((int32_t)t);   // t < nt < 2^31
+    if (kLocal && local) {   // written by this block above: LDS, not the scalar cache
+      const int4 d = s_risky[kLocal ? t : 0];
+      return int4{__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                  __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w)};
+    }
     const int4 *p = t < nh ? reinterpret_cast<const int4 *>(a.heavy_end) - 1 - t
                            : reinterpret_cast<const int4 *>(a.touched) + (t - nh);
     const __attribute__((address_space(4))) int32_t *q = (const __attribute__((address_space(4))) int32_t *)p;
@@ -2025,6 +2082,7 @@ static unsigned few_row_blocks(int64_t n) { return std::min(row_blocks(n, 4), 76
 int g_offsets_blocks = 1024;   // PSX_VARIANT_OFFSETS_GRID: ordered_offsets' grid cap
 int g_dry_blocks = 128;        // PSX_VARIANT_DRY_GRID: the capacity dry run's grid cap
 int g_classify_blocks = 256;   // PSX_VARIANT_CLASSIFY_GRID: ordered_classify's grid cap
+int g_classify_dry = 1;        // PSX_VARIANT_CLASSIFY_DRY: ordered_classify as the dry run's prologue
 
 static void lds_geometry(int dtype, const OrdArgs &a, int *wpb, size_t *lds) {
   const int esz = (dtype == 0 || dtype == 2) ? 8 : 16;
@@ -2099,7 +2157,31 @@ hipError_t launch_ordered_prep_records(const OrdArgs &a, int2 *wfill, int4 *plis
   return hipGetLastError();
 }
 
+// The dry run's kernel (J = 16: split tables have 256 < max_entries <= 1,024) with
+// ordered_classify's work as its prologue, one block per 256 compact-list entries.
+template <typename V, int KIND>
+static void launch_classify_dry(const OrdArgs &a0, const int4 *plist, hipStream_t st) {
+  OrdArgs a = a0;
+  a.plist = plist;
+  a.nplist = a0.ntouched;       // ordered_place's count
+  a.desc = 1;
+  const unsigned blocks = (unsigned)((a.max_rows + 255) / 256);
+  hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, true>), dim3(blocks), dim3(256), 0, st, a);
+}
+
 hipError_t launch_ordered_prep_rows(int dtype, const OrdArgs &a, const int4 *plist, hipStream_t st) {
+  if (g_classify_dry && a.kind != 0 && !a.dense_records && a.keyflag && a.max_entries <= 1024 &&
+      (a.max_rows + 255) / 256 <= 65535) {
+#define PSX_CD(V) do { if (a.kind == 1) launch_classify_dry<V, 1>(a, plist, st); else launch_classify_dry<V, 2>(a, plist, st); } while (0)
+    switch (dtype) {
+      case 0: PSX_CD(float); break;
+      case 1: PSX_CD(double); break;
+      case 2: PSX_CD(int32_t); break;
+      default: PSX_CD(int64_t); break;
+    }
+#undef PSX_CD
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(ordered_classify_kernel,
                      dim3(std::min(row_blocks(a.max_rows, 256), (unsigned)std::max(1, g_classify_blocks))), dim3(256),
                      0, st, a, plist);

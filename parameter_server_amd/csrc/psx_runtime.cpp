@@ -54,6 +54,7 @@ int g_call_events = 0;   // PSX_VARIANT_CALL_EVENTS: bit 0 an event pair per cal
 int g_walk_shape = 4;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block x window words (psx_walk.hip kWalkShapes)
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 int g_prep_halves = 1;   // PSX_VARIANT_PREP_HALVES: a pipelined call's split tables prep in two halves
+int g_walk_cus_pipelined = 0;   // PSX_VARIANT_WALK_CUS_PIPELINED: PSX_VARIANT_WALK_CUS for pipelined calls
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -467,11 +468,14 @@ bool has_sparse_serialized(const psx_ctx *c) {
 // 3's default, is PSX_VARIANT_WALK_SHAPE 0 with PSX_VARIANT_WALK_CUS 0).
 constexpr uint64_t kWalkMaxItems = 1u << 17;
 
-unsigned walk_blocks(psx_ctx *c) {
+unsigned walk_blocks(psx_ctx *c, bool pipelined) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
     cus = 256;
-  const int v = psx::g_walk_all_cus;
+  // a pipelined walk shares the chip with the previous call's apply: on half the CUs it
+  // leaves the apply more of them (C3 pipelined 15,430 -> 15,660 M updates/s; unpipelined,
+  // alone on the chip, it needs them all: 13,800 -> 11,600, profiles/r06/s4)
+  const int v = pipelined ? psx::g_walk_cus_pipelined : psx::g_walk_all_cus;
   return (unsigned)std::max(1, v <= 0 ? cus / 2 : v == 1 ? cus : cus * std::min(v, 8));
 }
 
@@ -702,7 +706,7 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       [&] {
         if (walk)
           return psx::launch_walk(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot],
-                                  c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c)),
+                                  c->d_walk[slot], spec_wpr, (unsigned)std::min<uint64_t>(items, walk_blocks(c, pipelined)),
                                   c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
                                   wcount ? c->d_wcount[slot] : nullptr, items,
                                   walk_levels | (psx::g_walk_skew && walk_levels > 0 ? 0x100 : 0), walk_shape, prep);
@@ -2907,6 +2911,7 @@ namespace psx {
 extern int g_apply_variant;
 extern int g_dense_last;
 extern int g_classify_blocks;
+extern int g_classify_dry;
 extern int g_ord_split;
 extern int g_offsets_blocks;
 extern int g_dry_blocks;
@@ -2921,6 +2926,8 @@ static int *variant_slot(int32_t which) {
     case PSX_STAT_DENSE_LAST: return &psx::g_dense_last;
     case PSX_VARIANT_PREP_HALVES: return &psx::g_prep_halves;
     case PSX_VARIANT_CLASSIFY_GRID: return &psx::g_classify_blocks;
+    case PSX_VARIANT_CLASSIFY_DRY: return &psx::g_classify_dry;
+    case PSX_VARIANT_WALK_CUS_PIPELINED: return &psx::g_walk_cus_pipelined;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
@@ -2980,6 +2987,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_ORD_SPLIT")) psx::g_ord_split = atoi(v);
     if (const char *v = getenv("PSX_ORD_LITE")) psx::g_ord_lite = atoi(v);
     if (const char *v = getenv("PSX_PREP_HALVES")) psx::g_prep_halves = atoi(v);
+    if (const char *v = getenv("PSX_CLASSIFY_DRY")) psx::g_classify_dry = atoi(v);
     if (const char *v = getenv("PSX_ORD_PROBE")) psx::g_ord_probe = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);

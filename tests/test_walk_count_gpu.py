@@ -310,3 +310,80 @@ def test_pipelined_prep_halves_back_to_back(halves, split, kind, walk_rank):
         assert got == want
     else:
         assert _map_rows(got) == _map_rows(want)
+
+
+CLASSIFY_DRY = 27
+
+
+@pytest.mark.parametrize("classify_dry", [1, 0], ids=["classify-in-dry-run", "classify-launch"])
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+def test_pipelined_capacity_overflow_applies_nothing(classify_dry, kind, walk_rank):
+    """The capacity dry run of a pipelined call's split table, with ordered_classify as its
+    prologue (PSX_VARIANT_CLASSIFY_DRY 1, each block dry-running the rows it filed as able
+    to overflow) or as a launch of its own (0): a call that would take one row past
+    max_entries (300) fails with PSX_ERR_CAPACITY and applies nothing, in any row; the
+    call's version comes back, and the corrected call then equals the oracle byte for byte."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, 1), L.psx_debug_set_variant(DECODE, 1),
+           L.psx_debug_set_variant(CLASSIFY_DRY, classify_dry)]
+    rng = np.random.RandomState(61 + classify_dry)
+    rows, cap, bgs = 3000, 300, [100, 101]
+
+    def msg(nrows, lo, hi, extra=None):
+        recs = []
+        for rid in rng.choice(rows, size=nrows, replace=False):
+            if rid == 7:              # row 7's image is set by the calls themselves
+                continue
+            k = int(rng.randint(1, 20))
+            cols = np.sort(rng.choice(np.arange(lo, hi), size=k, replace=False)).astype(np.int32)
+            recs.append((int(rid), cols, rng.randint(1, 4, size=k).astype(np.int32)))
+        if extra:
+            recs.append(extra)
+        return wire.sparse_stream_np(3, 4, recs)
+
+    # call 0: row 7 holds 280 entries (keys 0..279); others a few
+    first = [wire.sparse_stream_np(3, 4, [(7, np.arange(280, dtype=np.int32), np.ones(280, np.int32))]),
+             msg(800, 0, 1000)]
+    # call 1 (bad): row 7 gets 40 new keys -> 320 > 300
+    bad = [msg(900, 0, 1000, (7, np.arange(1000, 1040, dtype=np.int32), np.ones(40, np.int32))), msg(900, 0, 1000)]
+    good = [msg(900, 0, 1000, (7, np.arange(1000, 1010, dtype=np.int32), np.ones(10, np.int32))), msg(900, 0, 1000)]
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(PIPELINE_ALL)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=100_000, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=cap))
+        keep = []
+
+        def send(msgs, v):
+            dev = [torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs]
+            keep.append(dev)
+            torch.cuda.synchronize()
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(dev, bgs)])
+
+        send(first, 0)
+        srv.sync()
+        before = srv.serialize_rows(3, list(range(rows)))
+        send(bad, 1)
+        with pytest.raises(PsxError) as e:
+            srv.sync()
+        assert e.value.status == 6 and "version given back" in str(e.value)
+        assert srv.serialize_rows(3, list(range(rows))) == before
+        send(good, 1)
+        srv.sync()
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(DECODE, old[1])
+        L.psx_debug_set_variant(CLASSIFY_DRY, old[2])
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate([first, good]):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    want = orc.serialize_records(3, list(range(rows)))
+    orc.close()
+    if kind == SORTED_MAP:
+        assert got == want
+    else:
+        assert _map_rows(got) == _map_rows(want)

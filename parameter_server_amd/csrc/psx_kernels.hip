@@ -691,10 +691,13 @@ __global__ void __launch_bounds__(256) dense_apply_v2_kernel(DenseArgs a) {
 }
 
 // dense_apply_v3: dense_apply_v2 with the record addresses kept as one wave-uniform
-// SGPR base per message (its first record's payload) plus a 32-bit per-lane VGPR offset,
-// so the loads are global_load_dwordx4 v, v_off, s[base] (saddr form).  v2 keeps
-// PAIR x BMAX uniform 64-bit record pointers, which overflow the SGPR file and spill to
-// VGPR lanes (~500 v_readlane/v_writelane per row pair).  Streams must be < 4 GiB.
+// base per message (its first record's payload, in SGPRs) plus a 32-bit UNSIGNED per-lane
+// offset.  v2 keeps PAIR x BMAX uniform 64-bit record pointers, which overflow the SGPR
+// file and spill to VGPR lanes (~500 v_readlane/v_writelane per row pair).  Streams must be
+// < 4 GiB.  The offset is zero-extended wherever the address is formed (the compiler builds
+// 64-bit VGPR addresses with v_lshl_add_u64; tests/test_isa.py checks that no v3
+// instantiation sign-extends a per-lane value, tests/test_configs_gpu.py runs offsets with
+// bit 31 set on the GPU).
 typedef const uint8_t __attribute__((address_space(1))) *gbyte_p;
 typedef const u32x4_a4 __attribute__((address_space(1))) *gu32x4_p;
 typedef uint32_t u32x2_a2g __attribute__((ext_vector_type(2), aligned(2)));

@@ -75,6 +75,9 @@ enum {
                                    touched rows and dry-runs the ones that may overflow); 0: two launches */
   PSX_VARIANT_WALK_CUS_PIPELINED = 28, /* PSX_VARIANT_WALK_CUS for pipelined calls (default 0: half
                                    the CUs, the rest left to the previous call's apply) */
+  PSX_VARIANT_STREAM_PRIORITY = 29, /* read at psx_ctx_create: 0 (default) every stream at the normal
+                                   priority; 1 the prep stream at the lowest; 2 also the context's own
+                                   stream at the highest */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

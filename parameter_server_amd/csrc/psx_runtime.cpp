@@ -55,6 +55,7 @@ int g_walk_shape = 4;    // PSX_VARIANT_WALK_SHAPE: the walk's threads per block
 int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 int g_prep_halves = 1;   // PSX_VARIANT_PREP_HALVES: a pipelined call's split tables prep in two halves
 int g_walk_cus_pipelined = 0;   // PSX_VARIANT_WALK_CUS_PIPELINED: PSX_VARIANT_WALK_CUS for pipelined calls
+int g_stream_priority = 0;      // PSX_VARIANT_STREAM_PRIORITY (read when a context is created)
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -1234,9 +1235,17 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
     return s;
   };
   if (hipSetDevice(device) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
-  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return cleanup(PSX_ERR_DEVICE);
+  // Stream priorities (PSX_VARIANT_STREAM_PRIORITY): 1 the prep stream (a pipelined call's
+  // decode, index and records' half of the ordered prep, all beside the previous call's
+  // apply) at the lowest priority, so the dispatcher hands CUs to the apply first; 2 also
+  // the context's own stream at the highest.
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  const int sp = psx::g_stream_priority;
+  if (hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, sp >= 2 ? prio_hi : 0) != hipSuccess)
+    return cleanup(PSX_ERR_DEVICE);
   c->stream = c->own;
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+  if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, sp >= 1 ? prio_lo : 0) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -2928,6 +2937,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_CLASSIFY_GRID: return &psx::g_classify_blocks;
     case PSX_VARIANT_CLASSIFY_DRY: return &psx::g_classify_dry;
     case PSX_VARIANT_WALK_CUS_PIPELINED: return &psx::g_walk_cus_pipelined;
+    case PSX_VARIANT_STREAM_PRIORITY: return &psx::g_stream_priority;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;

@@ -772,7 +772,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     a.cnt = t.d_cnt + (int64_t)slot * t.cfg.max_rows;
     a.off = t.d_off;
     a.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
-    a.list = c->d_list + list_region * ((size_t)slot * n_ord + ord_k);
+    // slot regions at multiples of the allocated capacity, not of this call's need: the
+    // previous call (the other slot) may have sized its lists larger and still be reading them
+    a.list = c->d_list + (size_t)slot * c->list_cap + list_region * ord_k;
     a.list_tmp = c->d_list + 2 * c->list_cap + list_region * ord_k;
     ++ord_k;
     a.touched = t.d_touched;

@@ -387,3 +387,44 @@ def test_pipelined_capacity_overflow_applies_nothing(classify_dry, kind, walk_ra
         assert got == want
     else:
         assert _map_rows(got) == _map_rows(want)
+
+
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+def test_pipelined_prep_halves_calls_of_different_sizes(kind, walk_rank):
+    """The call slots' record-list regions must not overlap whatever each call's size: a
+    large call, then small ones, back to back with no sync (a small call's lists are filled
+    on the prep stream while the large call's apply still reads its own), then large again —
+    byte for byte against the oracle (round 6: the regions sit at multiples of the allocated
+    capacity, not of the current call's need)."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, 1), L.psx_debug_set_variant(DECODE, 1)]
+    rng = np.random.RandomState(808)
+    rows, K, bgs = 8_000, 1024, [100, 101, 102, 103]
+    sizes = [5_000, 200, 150, 4_000, 100, 3_000, 50, 5_000]
+    calls = [_batches(rng, rows, K, 1, per_batch=z)[0] for z in sizes]
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(PIPELINE_ALL)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, msgs in enumerate(dev):
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)])
+        srv.sync()
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(DECODE, old[1])
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    want = orc.serialize_records(3, list(range(rows)))
+    orc.close()
+    if kind == SORTED_MAP:
+        assert got == want
+    else:
+        assert _map_rows(got) == _map_rows(want)

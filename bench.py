@@ -39,7 +39,7 @@ sys.path.insert(0, ROOT)
 
 EXCHANGE_TIMEOUT_S = 600   # N > 1: the exchange extras are abandoned (headline kept, exit 3) past this
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-PMC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc_dense_apply.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "r06", "pmc_dense_apply.json")
 
 
 def kernel_signature():
@@ -62,7 +62,7 @@ def kernel_signature():
     return h.hexdigest()[:16]
 
 
-C3_PMC_JSON = os.path.join(ROOT, "profiles", "r05", "pmc_c3.json")
+C3_PMC_JSON = os.path.join(ROOT, "profiles", "r06", "pmc_c3.json")
 
 
 def c3_kernel_signature():

@@ -78,6 +78,10 @@ enum {
   PSX_VARIANT_STREAM_PRIORITY = 29, /* read at psx_ctx_create: 0 (default) every stream at the normal
                                    priority; 1 the prep stream at the lowest; 2 also the context's own
                                    stream at the highest */
+  PSX_VARIANT_ORD_BUCKET = 30,  /* 1 (default): a split sorted/map table's record lists are buckets of 16
+                                   places per row, written by the count itself (no prefix over the
+                                   counts, no ordered_fill); a row with more records in one call makes
+                                   the call replay with prefix lists.  0: prefix lists */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

@@ -212,6 +212,10 @@ struct OrdArgs {
   // touched list and its length (ordered_place); null otherwise.
   const int4 *plist;
   const uint32_t *nplist;
+  // Bucket lists (split tables, ranked counts): a slot's records sit at list[slot * bucket_m
+  // + place], written by the count (the walk's or ordered_count's) — no prefix over the
+  // counts, no ordered_fill.  0: prefix lists.
+  int32_t bucket_m;
 };
 // The context's status words (psx_runtime.cpp d_status): [0] sticky, [1 + k] the call ring,
 // [1 + kCallRing + k] the call log, [1 + 2 kCallRing] the folded finish's block counter.
@@ -232,6 +236,9 @@ struct WalkCount {
   int32_t pad;
   int2 *wfill;        // non-null: per record (its recoff index) {slot, its place in the slot's record
                       // list} from the count's returned value, for ordered_fill (-1: no slot)
+  uint64_t *bucket;   // non-null (bucket lists): the record's list entry goes straight to
+  int32_t bucket_m;   // bucket[slot * bucket_m + place]; place >= bucket_m sets kStDuplicateRow
+  int32_t pad2;       // (the call is then replayed with prefix lists)
 };
 
 // A side stream and two events for launches that run beside the context stream.

@@ -175,9 +175,14 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfi
           if (cols_outside(p, a.max_entries)) atomicOr(a.keyflag, 1u);
         }
         if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
-        if (a.grow && wfill)   // split tables, ranked: the record's place comes back with the count
-          wfill[rs.first[b] + (r - rs.pre[b])] = int2{(int32_t)s, atomicAdd(&a.cnt[s], 1)};
-        else if (a.grow)   // split tables: ordered_offsets finds the touched rows from the counts
+        if (a.grow && wfill) {   // split tables, ranked: the record's place comes back with the count
+          const int32_t k = atomicAdd(&a.cnt[s], 1);
+          wfill[rs.first[b] + (r - rs.pre[b])] = int2{(int32_t)s, k};
+          if (a.bucket_m) {   // bucket lists: the list entry itself, no ordered_fill
+            if (k < a.bucket_m) a.list[s * a.bucket_m + k] = rec_ref(b, off);
+            else atomicOr(a.call_status, kStDuplicateRow);   // more than a bucket holds: replay
+          }
+        } else if (a.grow)   // split tables: ordered_offsets finds the touched rows from the counts
           atomicAdd(&a.cnt[s], 1);
         else
           first = atomicAdd(&a.cnt[s], 1) == 0;
@@ -351,7 +356,15 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       nen = a.nent[s];
       g = a.grow[s];
     }
-    if (!o_gate(a)) return;
+    if (!o_gate(a)) {
+      // bucket lists have no ordered_fill to restore the counts of a failed call: each block
+      // clears its own slots (cnt and grow zero between calls)
+      if (a.bucket_m && s < c1) {
+        a.cnt[s] = 0;
+        a.grow[s] = 0;
+      }
+      return;
+    }
     const bool t = c > 0;
     const bool big = t && starts_big(a, nen, g);
     const bool heavy = t && !big && starts_heavy(a, c);
@@ -363,7 +376,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
                        pre, tot, sh);
     if (threadIdx.x == 0) {
       base[0] = tot[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot[0]) : 0;
-      base[1] = tot[1] ? atomicAdd(&a.tsum[0], tot[1]) : 0;
+      base[1] = tot[1] && !a.bucket_m ? atomicAdd(&a.tsum[0], tot[1]) : 0;
       base[2] = tot[2] ? (int32_t)atomicAdd(&a.nsplit[0 * kNsStride], (uint32_t)tot[2]) : 0;
       base[3] = tot[3] ? (int32_t)atomicAdd(&a.nsplit[1 * kNsStride], (uint32_t)tot[3]) : 0;
       base[4] = tot[4] ? (int32_t)atomicAdd(&a.nsplit[2 * kNsStride], (uint32_t)tot[4]) : 0;
@@ -374,7 +387,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     if (t) {
       a.grow[s] = 0;
       if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
-      const int32_t beg = base[1] + pre[1];
+      const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : base[1] + pre[1];
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
       a.off[s] = beg;
       if (risky) desc[2 * R + base[5] + pre[5]] = d;
@@ -385,7 +398,14 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     }
     return;
   }
-  if (!o_gate(a)) return;
+  if (!o_gate(a)) {
+    if (a.bucket_m)   // bucket lists: clear this block's slots (no ordered_fill follows)
+      for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
+        a.cnt[s] = 0;
+        a.grow[s] = 0;
+      }
+    return;
+  }
   // pass 1: the block's totals, one atomic per counter
   int32_t nt = 0, nr = 0, ns = 0, nb = 0, nh = 0, nd = 0, nl = 0;
   for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
@@ -406,7 +426,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
   const int32_t tt = tot1[0], tr = tot1[1], ts = tot1[2], tb = tot1[3], th = tot1[4], td = tot1[5], tl = tot1[6];
   if (threadIdx.x == 0) {
     base[0] = tt ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tt) : 0;
-    base[1] = tr ? atomicAdd(&a.tsum[0], tr) : 0;
+    base[1] = tr && !a.bucket_m ? atomicAdd(&a.tsum[0], tr) : 0;
     base[2] = ts ? (int32_t)atomicAdd(&a.nsplit[0 * kNsStride], (uint32_t)ts) : 0;
     base[3] = tb ? (int32_t)atomicAdd(&a.nsplit[1 * kNsStride], (uint32_t)tb) : 0;
     base[4] = th ? (int32_t)atomicAdd(&a.nsplit[2 * kNsStride], (uint32_t)th) : 0;
@@ -445,7 +465,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     const int32_t pr = pre[1], ps = pre[2], pb = pre[3], ph = pre[4], pd = pre[5], pl = pre[6];
     const int32_t sr = tot[1], ss2 = tot[2], sb = tot[3], sh2 = tot[4], sd = tot[5], sl = tot[6];
     if (t) {
-      const int32_t beg = ar + pr;
+      const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : ar + pr;
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
       a.off[s] = beg;
       if (risky) desc[2 * R + ad + pd] = d;   // the capacity dry run's list
@@ -485,7 +505,14 @@ __global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *pli
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = (int64_t)blockIdx.x * per;
   const int64_t c1 = c0 + per < R ? c0 + per : R;
-  if (!o_gate(a)) return;
+  if (!o_gate(a)) {
+    if (a.bucket_m)   // bucket lists: clear this block's slots (no ordered_fill follows)
+      for (int64_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
+        a.cnt[s] = 0;
+        a.grow[s] = 0;
+      }
+    return;
+  }
   if (per <= (int64_t)blockDim.x) {   // one slot per thread (the usual grid)
     const int64_t s = c0 + threadIdx.x;
     const int32_t c = s < c1 ? a.cnt[s] : 0;
@@ -494,11 +521,11 @@ __global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *pli
     block_excl_sumN<2>({t ? 1 : 0, c}, pre, tot, sh);
     if (threadIdx.x == 0) {
       base[0] = tot[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot[0]) : 0;
-      base[1] = tot[1] ? atomicAdd(&a.tsum[0], tot[1]) : 0;
+      base[1] = tot[1] && !a.bucket_m ? atomicAdd(&a.tsum[0], tot[1]) : 0;
     }
     __syncthreads();
     if (t) {
-      const int32_t beg = base[1] + pre[1];
+      const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : base[1] + pre[1];
       a.off[s] = beg;
       plist[base[0] + pre[0]] = int4{(int32_t)s, beg, c, a.grow[s]};
       a.grow[s] = 0;
@@ -516,7 +543,7 @@ __global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *pli
   block_excl_sumN<2>({nt, nr}, pre1, tot1, sh);
   if (threadIdx.x == 0) {
     base[0] = tot1[0] ? (int32_t)atomicAdd(a.ntouched, (uint32_t)tot1[0]) : 0;
-    base[1] = tot1[1] ? atomicAdd(&a.tsum[0], tot1[1]) : 0;
+    base[1] = tot1[1] && !a.bucket_m ? atomicAdd(&a.tsum[0], tot1[1]) : 0;
   }
   __syncthreads();
   int32_t at = base[0], ar = base[1];
@@ -527,7 +554,7 @@ __global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *pli
     int32_t pre[2], tot[2];
     block_excl_sumN<2>({t ? 1 : 0, c}, pre, tot, sh);
     if (t) {
-      const int32_t beg = ar + pre[1];
+      const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : ar + pre[1];
       a.off[s] = beg;
       plist[at + pre[0]] = int4{(int32_t)s, beg, c, a.grow[s]};
       a.grow[s] = 0;
@@ -2129,7 +2156,7 @@ hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, int2 *wfill, hipStre
                        dim3(256), 0, st, a);
   else
     launch_exclusive_scan<int32_t>(a.cnt, a.max_rows, a.off, a.tsum, st);
-  hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
+  if (!a.bucket_m) hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
   if (a.kind != 0 && !a.dense_records && a.keyflag) {
 #define PSX_DRY(V) do { if (a.kind == 1) launch_dry<V, 1>(a, dtype, st); else launch_dry<V, 2>(a, dtype, st); } while (0)
     switch (dtype) {
@@ -2153,7 +2180,7 @@ hipError_t launch_ordered_prep_records(const OrdArgs &a, int2 *wfill, int4 *plis
   hipLaunchKernelGGL(ordered_place_kernel,
                      dim3(std::min(row_blocks(a.max_rows, 256), (unsigned)std::max(1, g_offsets_blocks))), dim3(256), 0,
                      st, a, plist);
-  hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
+  if (!a.bucket_m) hipLaunchKernelGGL(ordered_fill_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
   return hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ int g_dense_store_nt = 1;   // PSX_VARIANT_DENSE_STORE
 int g_prep_halves = 1;   // PSX_VARIANT_PREP_HALVES: a pipelined call's split tables prep in two halves
 int g_walk_cus_pipelined = 0;   // PSX_VARIANT_WALK_CUS_PIPELINED: PSX_VARIANT_WALK_CUS for pipelined calls
 int g_stream_priority = 0;      // PSX_VARIANT_STREAM_PRIORITY (read when a context is created)
+int g_ord_bucket = 1;           // PSX_VARIANT_ORD_BUCKET: split tables' record lists in buckets
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -128,6 +129,12 @@ hipError_t launch_gather_entries(int dtype, const int32_t *nent, const uint8_t *
 namespace {
 
 constexpr int kRing = psx::kCallRing;   // per-call status slots
+// Bucket record lists of split tables (OrdArgs::bucket_m): kBucketM places per slot per call
+// — a well-formed call has at most one record of a row per message and at most 16 messages
+// (PSX_MAX_FUSED_STREAMS); a call with more records for one row (a row repeated inside a
+// message) sets kStDuplicateRow and is replayed with prefix lists.
+constexpr int kBucketM = psx::kMaxFused;
+constexpr int64_t kBucketMaxRows = 2 << 20;
 
 int vsize_of(int32_t dt) { return (dt == PSX_F32 || dt == PSX_I32) ? 4 : 8; }
 
@@ -152,6 +159,8 @@ struct TableState {
   uint32_t *d_nsplit = nullptr;    // their lengths
   int32_t *d_plist = nullptr;      // split tables, pipelined calls: [2][max_rows] int4 touched-row
                                    // entries by call slot (ordered_place -> ordered_classify)
+  uint64_t *d_bucket[2] = {nullptr, nullptr};   // split tables: bucket record lists by call slot,
+                                                // [max_rows][kBucketM] (OrdArgs::bucket_m)
   uint64_t *d_subs = nullptr;      // CallBackSubs::subscriptions_ per slot (bit c = client c), lazily
   int64_t *d_srv_sizes = nullptr;  // serve-back: record bytes per slot
   int64_t *d_srv_offs = nullptr;   // serve-back: exclusive prefix + scan tile sums
@@ -196,7 +205,7 @@ struct TableState {
 
 void free_table(TableState &t) {
   void *ptrs[] = {t.d_data, t.d_nent, t.d_entries, t.d_flags, t.d_inv[0], t.d_inv[1],
-                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_grow, t.d_split, t.d_nsplit, t.d_plist, t.d_subs, t.d_srv_sizes, t.d_srv_offs,
+                  t.d_cnt, t.d_off, t.d_tsum, t.d_touched, t.d_keyflag, t.d_grow, t.d_split, t.d_nsplit, t.d_plist, t.d_bucket[0], t.d_bucket[1], t.d_subs, t.d_srv_sizes, t.d_srv_offs,
                   t.d_imp, t.d_ver, t.d_acc, t.d_z, t.d_zmax, t.d_snap_ver, t.d_snap_cnt, t.d_snap_acc,
                   t.d_ada_words, t.d_new_keys, t.d_new_slots, t.d_new_tmp, t.d_init, t.d_pkeys[0], t.d_pkeys[1], t.d_pvals[0], t.d_pvals[1],
                   t.d_lsizes, t.d_loffs, t.d_sort_tmp};
@@ -490,6 +499,13 @@ size_t min_record_bytes(const psx_ctx *c) {
   return (size_t)m;
 }
 
+// Bucket record lists for split table t on this call: selected, allocated, not a replay
+// (a replay takes prefix lists: it may be the replay of a bucket overflow), and no
+// AdaRevision table in the context (an overflow is replayed, and that logic has no replay).
+bool bucket_ok(const psx_ctx *c, const TableState &t, bool force_ordered) {
+  return psx::g_ord_bucket && t.d_bucket[0] && !force_ordered && !c->has_ada;
+}
+
 // Enqueue the device pipeline for n messages already resident in HBM (versions checked).
 // force_ordered: every table goes through the ordered path (duplicate-row replay).
 //
@@ -684,6 +700,10 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       x.nsplit = t.d_nsplit + 5 * psx::kNsStride * slot;
       x.tsum = t.d_tsum + (int64_t)slot * t.tsum_slot;
       x.wfill = psx::g_walk_rank ? c->d_wfill[slot] : nullptr;
+      if (x.wfill && bucket_ok(c, t, force_ordered)) {
+        x.bucket = t.d_bucket[slot];
+        x.bucket_m = kBucketM;
+      }
       x.on = 1;
       wcount = true;
     }
@@ -802,6 +822,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
 #endif
       a.counted = wcount && c->h_wcount[slot][ti].on ? (c->h_wcount[slot][ti].wfill ? 2 : 1)
                   : (psx::g_walk_rank && !t.cfg.oplog_dense_serialized && c->d_wfill[slot] ? 3 : 0);
+      // bucket lists: the walk (counted 2, WalkCount.bucket set above) or ordered_count
+      // (counted 3) writes each record's list entry at [slot][place]
+      if ((a.counted == 2 && c->h_wcount[slot][ti].bucket) || (a.counted == 3 && bucket_ok(c, t, force_ordered))) {
+        a.bucket_m = kBucketM;
+        a.list = t.d_bucket[slot];
+      }
       if (pipelined && psx::g_prep_halves) {
         halves[ti] = 1;
         int2 *wfill = a.counted >= 2 ? c->d_wfill[slot] : nullptr;
@@ -1514,6 +1540,9 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     if (e == hipSuccess) e = hipMalloc(&t.d_split, 4 * R * 4 * sizeof(int32_t));   // int4 descriptors x 4 lists
     if (e == hipSuccess) e = hipMalloc(&t.d_nsplit, 2 * 5 * psx::kNsStride * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&t.d_plist, 2 * R * 4 * sizeof(int32_t));
+    // bucket lists, up to 2M rows (2 x 256 MiB): a slot's records at [slot][place]
+    if (e == hipSuccess && R <= (int64_t)kBucketMaxRows)
+      for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipMalloc(&t.d_bucket[k], R * kBucketM * sizeof(uint64_t));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
@@ -2940,6 +2969,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_CLASSIFY_DRY: return &psx::g_classify_dry;
     case PSX_VARIANT_WALK_CUS_PIPELINED: return &psx::g_walk_cus_pipelined;
     case PSX_VARIANT_STREAM_PRIORITY: return &psx::g_stream_priority;
+    case PSX_VARIANT_ORD_BUCKET: return &psx::g_ord_bucket;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
@@ -3000,6 +3030,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_ORD_LITE")) psx::g_ord_lite = atoi(v);
     if (const char *v = getenv("PSX_PREP_HALVES")) psx::g_prep_halves = atoi(v);
     if (const char *v = getenv("PSX_CLASSIFY_DRY")) psx::g_classify_dry = atoi(v);
+    if (const char *v = getenv("PSX_ORD_BUCKET")) psx::g_ord_bucket = atoi(v);
     if (const char *v = getenv("PSX_ORD_PROBE")) psx::g_ord_probe = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);

@@ -266,7 +266,7 @@ __device__ __forceinline__ uint32_t gran_value(const WalkState &s, int i) {
 // ordered_count for one record of a walk-counted split table (WalkCount): the record's row
 // id and pair count at p (a record the walk accepted: its header lies inside the message).
 __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w, uint32_t *call_status,
-                                           uint64_t idx) {
+                                           uint64_t idx, uint64_t ref) {
   const int32_t rid = *reinterpret_cast<const int32_t *>(p);
   const int32_t n = *reinterpret_cast<const int32_t *>(p + 4);
   int64_t d = (int64_t)rid - w.row_offset;
@@ -286,6 +286,10 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
     // each list into message order, so any order of these atomics is as good)
     const int32_t k = atomicAdd(&w.cnt[d], 1);
     w.wfill[idx] = int2{(int32_t)d, k};
+    if (w.bucket) {   // bucket lists: the list entry itself, no ordered_fill
+      if (k < w.bucket_m) w.bucket[d * w.bucket_m + k] = ref;
+      else atomicOr(call_status, kStDuplicateRow);   // more records than a bucket holds: replay
+    }
   } else {
     atomicAdd(&w.cnt[d], 1);
   }
@@ -804,7 +808,7 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
       for (uint32_t r = (uint32_t)tid; r < nrec; r += kWalkThreads) {
         const uint64_t off = W0 + (uint64_t)recq[r] * 4;
         recoff[rk + r] = off;
-        if (counted && off + 8 <= size) walk_count(p + off, wc[t], call_status, rk + r);
+        if (counted && off + 8 <= size) walk_count(p + off, wc[t], call_status, rk + r, ((uint64_t)b << 56) | off);
       }
     }
     if (tr && tid == 0) tr[5] = __builtin_amdgcn_s_memrealtime();

@@ -428,3 +428,61 @@ def test_pipelined_prep_halves_calls_of_different_sizes(kind, walk_rank):
         assert got == want
     else:
         assert _map_rows(got) == _map_rows(want)
+
+
+ORD_BUCKET = 30
+
+
+@pytest.mark.parametrize("pipeline", [0, PIPELINE_ALL], ids=["walked", "pipelined"])
+@pytest.mark.parametrize("bucket", [1, 0], ids=["bucket-lists", "prefix-lists"])
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+def test_bucket_lists_and_their_overflow_replay(bucket, pipeline, kind, walk_rank):
+    """Bucket record lists (PSX_VARIANT_ORD_BUCKET 1, the default with ranked counts): the
+    walk writes each record's list entry at [slot][place] for places < 16.  Three calls: an
+    ordinary one; one where row 5 has 20 records (a message repeating it: more than a
+    bucket holds) — that call and the next, enqueued behind it, are replayed with prefix
+    lists at the sync; then an ordinary one.  Byte for byte against the oracle, in both
+    list forms, walked and pipelined."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(WALK_COUNT, 1), L.psx_debug_set_variant(DECODE, 1),
+           L.psx_debug_set_variant(ORD_BUCKET, bucket)]
+    rng = np.random.RandomState(4242 + bucket)
+    rows, K, bgs = 5_000, 1024, [100, 101, 102, 103]
+    calls = _batches(rng, rows, K, 3, per_batch=1_500)
+    recs = []
+    for _ in range(20):      # row 5, 20 records in one message
+        k = int(rng.randint(1, 30))
+        cols = np.sort(rng.choice(K, size=k, replace=False)).astype(np.int32)
+        recs.append((5, cols, (rng.randint(1, 4, size=k) * rng.choice([-1, 1], size=k)).astype(np.int32)))
+    for rid in rng.choice(np.arange(6, rows), size=500, replace=False):
+        cols = np.sort(rng.choice(K, size=8, replace=False)).astype(np.int32)
+        recs.append((int(rid), cols, rng.randint(1, 4, size=8).astype(np.int32)))
+    calls[1] = list(calls[1])
+    calls[1][2] = wire.sparse_stream_np(3, 4, recs)
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(pipeline)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, msgs in enumerate(dev):
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)])
+        srv.sync()
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old[0])
+        L.psx_debug_set_variant(DECODE, old[1])
+        L.psx_debug_set_variant(ORD_BUCKET, old[2])
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    want = orc.serialize_records(3, list(range(rows)))
+    orc.close()
+    if kind == SORTED_MAP:
+        assert got == want
+    else:
+        assert _map_rows(got) == _map_rows(want)

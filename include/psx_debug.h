@@ -80,8 +80,13 @@ enum {
                                    stream at the highest */
   PSX_VARIANT_ORD_BUCKET = 30,  /* 1 (default): a split sorted/map table's record lists are buckets of 16
                                    places per row, written by the count itself (no prefix over the
-                                   counts, no ordered_fill); a row with more records in one call makes
-                                   the call replay with prefix lists.  0: prefix lists */
+                                   counts, no ordered_fill; unpipelined calls classify the slots in the
+                                   dry run's prologue: one launch after the count); a row with more
+                                   records in one call makes the call replay with prefix lists.
+                                   0: prefix lists */
+  PSX_VARIANT_PIPE_SLOTS = 31,  /* pipelined calls with bucket lists: 1 no ordered_place on the prep
+                                   stream, the dry run's prologue classifies the slots themselves on
+                                   the context stream; 0 (default): ordered_place's compact list */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

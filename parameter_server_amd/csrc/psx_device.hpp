@@ -216,6 +216,7 @@ struct OrdArgs {
   // + place], written by the count (the walk's or ordered_count's) — no prefix over the
   // counts, no ordered_fill.  0: prefix lists.
   int32_t bucket_m;
+  int32_t classify_slots;   // the dry run's prologue classifies its 256 slots (bucket lists)
 };
 // The context's status words (psx_runtime.cpp d_status): [0] sticky, [1 + k] the call ring,
 // [1 + kCallRing + k] the call log, [1 + 2 kCallRing] the folded finish's block counter.

@@ -1569,13 +1569,25 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   // the gate's words and the launch's row counts read at once (not one after another)
   const uint32_t st0 = *a.call_status, sk0 = *a.sticky;
   const uint32_t kf0 = DRY && a.keyflag ? *a.keyflag : 0u;
-  const bool local = kLocal && a.plist;
-  const uint32_t nt0 = local ? *a.nplist : *a.ntouched, nh0 = a.nheavy ? *a.nheavy : 0u;
+  // slots: the classification reads the slots themselves (cnt, grow; bucket lists, whose
+  // ranges need no prefix) instead of ordered_place's compact list
+  const bool slots = kLocal && a.classify_slots;
+  const bool local = kLocal && (a.plist || slots);
+  const uint32_t nt0 = slots ? 0u : local ? *a.nplist : *a.ntouched, nh0 = a.nheavy ? *a.nheavy : 0u;
   const bool go = !(st0 & (kStFatal | kStDuplicateRow)) && (a.force || !(sk0 & kStDuplicateRow)) &&
                   (!DRY || a.grow || kf0);
   // blocks past the touched rows leave before any setup (the grid is sized by max_rows); the
   // row count is final when the launch starts (the folded finish counts the blocks below it)
-  const int64_t launch_rows = (int64_t)nt0 + (int64_t)nh0;
+  const int64_t launch_rows = slots ? a.max_rows : (int64_t)nt0 + (int64_t)nh0;
+  if (kLocal && slots && !go) {
+    // a failed call: no ordered_offsets or ordered_fill restores the count state, so each
+    // block clears its own slots (cnt and grow zero between calls)
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s < a.max_rows) {
+      a.cnt[s] = 0;
+      a.grow[s] = 0;
+    }
+  }
   if (!go || (int64_t)blockIdx.x * (local ? 256 : 4) >= launch_rows) goto done;
   if constexpr (kLocal) {
     if (local) {
@@ -1586,12 +1598,27 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       const int64_t R = a.max_rows;
       int4 *const desc = reinterpret_cast<int4 *>(a.split);
       const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-      const bool t = i < (int64_t)nt0;
       int4 e = int4{0, 0, 0, 0};
       int32_t nen = 0;
-      if (t) {
-        e = a.plist[i];
-        nen = a.nent[e.x];
+      bool t;
+      if (slots) {   // slot i itself: its count state is read and cleared here (ordered_offsets')
+        t = false;
+        if (i < a.max_rows) {
+          const int32_t c = a.cnt[i], g = a.grow[i];
+          nen = a.nent[i];
+          t = c > 0;
+          if (t) {
+            e = int4{(int32_t)i, (int32_t)(i * a.bucket_m), c, g};
+            a.grow[i] = 0;
+            if (a.counted >= 2) a.cnt[i] = 0;
+          }
+        }
+      } else {
+        t = i < (int64_t)nt0;
+        if (t) {
+          e = a.plist[i];
+          nen = a.nent[e.x];
+        }
       }
       const int32_t c = e.z, g = e.w;
       const bool big = t && starts_big(a, nen, g);
@@ -2194,6 +2221,44 @@ static void launch_classify_dry(const OrdArgs &a0, const int4 *plist, hipStream_
   a.desc = 1;
   const unsigned blocks = (unsigned)((a.max_rows + 255) / 256);
   hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, true>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+// Bucket lists of a ranked split table (a.bucket_m, a.counted >= 2): no prefix is needed, so
+// the whole prep after the count is the dry run's kernel classifying its 256 slots as its
+// prologue (ordered_offsets' classification) — one launch where the prefix form has
+// ordered_offsets, ordered_fill and the dry run.
+bool ordered_prep_in_dry_run(const OrdArgs &a) {
+  return g_classify_dry && a.bucket_m && a.counted >= 2 && a.kind != 0 && !a.dense_records && a.keyflag &&
+         a.max_entries <= 1024 && (a.max_rows + 255) / 256 <= 65535;
+}
+
+template <typename V, int KIND>
+static void launch_slots_dry(const OrdArgs &a0, hipStream_t st) {
+  OrdArgs a = a0;
+  a.classify_slots = 1;
+  a.plist = nullptr;
+  a.desc = 1;
+  const unsigned blocks = (unsigned)((a.max_rows + 255) / 256);
+  hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, true>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+hipError_t launch_ordered_count(const OrdArgs &a, int2 *wfill, hipStream_t st) {
+  hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
+  return hipGetLastError();
+}
+
+hipError_t launch_ordered_prep_slots(int dtype, const OrdArgs &a, int2 *wfill, bool with_count, hipStream_t st) {
+  if (with_count && a.counted == 3)   // ordered_count ranks and fills the buckets
+    hipLaunchKernelGGL(ordered_count_kernel, dim3(1024), dim3(256), 0, st, a, wfill);
+#define PSX_SD(V) do { if (a.kind == 1) launch_slots_dry<V, 1>(a, st); else launch_slots_dry<V, 2>(a, st); } while (0)
+  switch (dtype) {
+    case 0: PSX_SD(float); break;
+    case 1: PSX_SD(double); break;
+    case 2: PSX_SD(int32_t); break;
+    default: PSX_SD(int64_t); break;
+  }
+#undef PSX_SD
+  return hipGetLastError();
 }
 
 hipError_t launch_ordered_prep_rows(int dtype, const OrdArgs &a, const int4 *plist, hipStream_t st) {

@@ -57,6 +57,7 @@ int g_prep_halves = 1;   // PSX_VARIANT_PREP_HALVES: a pipelined call's split ta
 int g_walk_cus_pipelined = 0;   // PSX_VARIANT_WALK_CUS_PIPELINED: PSX_VARIANT_WALK_CUS for pipelined calls
 int g_stream_priority = 0;      // PSX_VARIANT_STREAM_PRIORITY (read when a context is created)
 int g_ord_bucket = 1;           // PSX_VARIANT_ORD_BUCKET: split tables' record lists in buckets
+int g_pipe_slots = 0;           // PSX_VARIANT_PIPE_SLOTS: pipelined bucket calls classify slots in the dry run
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -99,6 +100,9 @@ hipError_t launch_gather_u64(const uint64_t *src, const int64_t *slots, int32_t 
 hipError_t launch_ordered_prep(int dtype, const OrdArgs &a, int2 *wfill, hipStream_t st);
 hipError_t launch_ordered_prep_records(const OrdArgs &a, int2 *wfill, int4 *plist, hipStream_t st);
 hipError_t launch_ordered_prep_rows(int dtype, const OrdArgs &a, const int4 *plist, hipStream_t st);
+bool ordered_prep_in_dry_run(const OrdArgs &a);
+hipError_t launch_ordered_count(const OrdArgs &a, int2 *wfill, hipStream_t st);
+hipError_t launch_ordered_prep_slots(int dtype, const OrdArgs &a, int2 *wfill, bool with_count, hipStream_t st);
 hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, const Fork &fk);
 extern int g_ord_split;
 hipError_t launch_ada_check(const AdaArgs &a, hipStream_t st);
@@ -829,11 +833,22 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
         a.list = t.d_bucket[slot];
       }
       if (pipelined && psx::g_prep_halves) {
-        halves[ti] = 1;
         int2 *wfill = a.counted >= 2 ? c->d_wfill[slot] : nullptr;
-        int4 *plist = reinterpret_cast<int4 *>(t.d_plist) + (size_t)slot * t.cfg.max_rows;
-        st = timed(c, "ordered_place", [&] { return psx::launch_ordered_prep_records(a, wfill, plist, prep); }, prep);
-        if (st) return st;
+        if (psx::g_pipe_slots && psx::ordered_prep_in_dry_run(a)) {
+          // bucket lists: the records' half is the count alone (if the walk did not do it);
+          // the rows' half classifies the slots inside the dry run (halves = 2)
+          halves[ti] = 2;
+          if (a.counted == 3) {
+            st = timed(c, "ordered_count", [&] { return psx::launch_ordered_count(a, wfill, prep); }, prep);
+            if (st) return st;
+          }
+        } else {
+          halves[ti] = 1;
+          int4 *plist = reinterpret_cast<int4 *>(t.d_plist) + (size_t)slot * t.cfg.max_rows;
+          st = timed(c, "ordered_place", [&] { return psx::launch_ordered_prep_records(a, wfill, plist, prep); },
+                     prep);
+          if (st) return st;
+        }
       }
     }
   }
@@ -845,6 +860,11 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
     TableState &t = c->tables[ti];
     if (t.fast() && !force_ordered) continue;
     const psx::OrdArgs &a = ord[ti];
+    if (halves[ti] == 2) {
+      st = timed(c, "ordered_classify", [&] { return psx::launch_ordered_prep_slots(t.cfg.dtype, a, nullptr, false, c->stream); });
+      if (st) return st;
+      continue;
+    }
     if (halves[ti]) {
       const int4 *plist = reinterpret_cast<const int4 *>(t.d_plist) + (size_t)slot * t.cfg.max_rows;
       st = timed(c, "ordered_classify", [&] { return psx::launch_ordered_prep_rows(t.cfg.dtype, a, plist, c->stream); });
@@ -852,6 +872,11 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
       continue;
     }
     int2 *wfill = a.counted >= 2 ? c->d_wfill[slot] : nullptr;
+    if (psx::ordered_prep_in_dry_run(a)) {   // bucket lists: the prep is the dry run's prologue
+      st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep_slots(t.cfg.dtype, a, wfill, true, c->stream); });
+      if (st) return st;
+      continue;
+    }
     st = timed(c, "ordered_prep", [&] { return psx::launch_ordered_prep(t.cfg.dtype, a, wfill, c->stream); });
     if (st) return st;
   }
@@ -2970,6 +2995,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_WALK_CUS_PIPELINED: return &psx::g_walk_cus_pipelined;
     case PSX_VARIANT_STREAM_PRIORITY: return &psx::g_stream_priority;
     case PSX_VARIANT_ORD_BUCKET: return &psx::g_ord_bucket;
+    case PSX_VARIANT_PIPE_SLOTS: return &psx::g_pipe_slots;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;
@@ -3031,6 +3057,7 @@ struct VariantEnv {
     if (const char *v = getenv("PSX_PREP_HALVES")) psx::g_prep_halves = atoi(v);
     if (const char *v = getenv("PSX_CLASSIFY_DRY")) psx::g_classify_dry = atoi(v);
     if (const char *v = getenv("PSX_ORD_BUCKET")) psx::g_ord_bucket = atoi(v);
+    if (const char *v = getenv("PSX_PIPE_SLOTS")) psx::g_pipe_slots = atoi(v);
     if (const char *v = getenv("PSX_ORD_PROBE")) psx::g_ord_probe = atoi(v);
     if (const char *v = getenv("PSX_DECODE_WALK")) psx::g_decode_walk = atoi(v);
     if (const char *v = getenv("PSX_DENSE_STORE_NT")) psx::g_dense_store_nt = atoi(v);

@@ -433,19 +433,24 @@ def test_pipelined_prep_halves_calls_of_different_sizes(kind, walk_rank):
 ORD_BUCKET = 30
 
 
-@pytest.mark.parametrize("pipeline", [0, PIPELINE_ALL], ids=["walked", "pipelined"])
+PIPE_SLOTS = 31
+
+
+@pytest.mark.parametrize("pipeline,pipe_slots", [(0, 0), (PIPELINE_ALL, 0), (PIPELINE_ALL, 1)],
+                         ids=["walked", "pipelined", "pipelined-slots"])
 @pytest.mark.parametrize("bucket", [1, 0], ids=["bucket-lists", "prefix-lists"])
 @pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
-def test_bucket_lists_and_their_overflow_replay(bucket, pipeline, kind, walk_rank):
+def test_bucket_lists_and_their_overflow_replay(bucket, pipeline, pipe_slots, kind, walk_rank):
     """Bucket record lists (PSX_VARIANT_ORD_BUCKET 1, the default with ranked counts): the
-    walk writes each record's list entry at [slot][place] for places < 16.  Three calls: an
+    walk writes each record's list entry at [slot][place] for places < 16, and the dry run's
+    prologue classifies the slots (unpipelined calls, or PSX_VARIANT_PIPE_SLOTS 1).  Three calls: an
     ordinary one; one where row 5 has 20 records (a message repeating it: more than a
     bucket holds) — that call and the next, enqueued behind it, are replayed with prefix
     lists at the sync; then an ordinary one.  Byte for byte against the oracle, in both
     list forms, walked and pipelined."""
     L = _abi.load()
     old = [L.psx_debug_set_variant(WALK_COUNT, 1), L.psx_debug_set_variant(DECODE, 1),
-           L.psx_debug_set_variant(ORD_BUCKET, bucket)]
+           L.psx_debug_set_variant(ORD_BUCKET, bucket), L.psx_debug_set_variant(PIPE_SLOTS, pipe_slots)]
     rng = np.random.RandomState(4242 + bucket)
     rows, K, bgs = 5_000, 1024, [100, 101, 102, 103]
     calls = _batches(rng, rows, K, 3, per_batch=1_500)
@@ -475,6 +480,7 @@ def test_bucket_lists_and_their_overflow_replay(bucket, pipeline, kind, walk_ran
         L.psx_debug_set_variant(WALK_COUNT, old[0])
         L.psx_debug_set_variant(DECODE, old[1])
         L.psx_debug_set_variant(ORD_BUCKET, old[2])
+        L.psx_debug_set_variant(PIPE_SLOTS, old[3])
     orc = OracleServer(bgs)
     orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
     for v, msgs in enumerate(calls):

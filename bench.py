@@ -2279,7 +2279,7 @@ def main():
         for name, flags in (("C3_walked", ["--cpu-seconds", cs]),
                             ("C3_indexed", ["--indexed", "--cpu-seconds", "0"])):
             try:
-                m = run_child(["--workload", "c3", "--steps", "20", "--warmup", "3"] + flags)
+                m = run_child(["--workload", "c3", "--steps", "50", "--warmup", "5"] + flags)
                 other[name] = {k: m.get(k) for k in ("value", "unit", "ms_per_step", "decode",
                                                      "ordered_apply_ms_per_step",
                                                      "kernel_ms_per_step_breakdown_pass", "roofline",

@@ -315,12 +315,14 @@ def test_pipelined_prep_halves_back_to_back(halves, split, kind, walk_rank):
 CLASSIFY_DRY = 27
 
 
+@pytest.mark.parametrize("pipeline", [PIPELINE_ALL, 0], ids=["pipelined", "walked"])
 @pytest.mark.parametrize("classify_dry", [1, 0], ids=["classify-in-dry-run", "classify-launch"])
 @pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
-def test_pipelined_capacity_overflow_applies_nothing(classify_dry, kind, walk_rank):
-    """The capacity dry run of a pipelined call's split table, with ordered_classify as its
-    prologue (PSX_VARIANT_CLASSIFY_DRY 1, each block dry-running the rows it filed as able
-    to overflow) or as a launch of its own (0): a call that would take one row past
+def test_pipelined_capacity_overflow_applies_nothing(classify_dry, kind, pipeline, walk_rank):
+    """The capacity dry run of a split table, with the classification as its prologue
+    (PSX_VARIANT_CLASSIFY_DRY 1: a pipelined call's compact list, or an unpipelined call's
+    slots with bucket lists; each block dry-runs the rows it filed as able to overflow) or as
+    a launch of its own (0): a call that would take one row past
     max_entries (300) fails with PSX_ERR_CAPACITY and applies nothing, in any row; the
     call's version comes back, and the corrected call then equals the oracle byte for byte."""
     L = _abi.load()
@@ -349,7 +351,7 @@ def test_pipelined_capacity_overflow_applies_nothing(classify_dry, kind, walk_ra
     good = [msg(900, 0, 1000, (7, np.arange(1000, 1010, dtype=np.int32), np.ones(10, np.int32))), msg(900, 0, 1000)]
     try:
         srv = psa.Server(0, 1, bgs)
-        srv.set_pipeline(PIPELINE_ALL)
+        srv.set_pipeline(pipeline)
         srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=100_000, oplog_dense_serialized=False,
                                          max_rows=rows, max_entries=cap))
         keep = []

@@ -1139,13 +1139,13 @@ def rank_view(world, rank, local):
     mine = {"rank": rank, "world": world, "local_device": local,
             "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
                    f"{getattr(p, 'pci_device_id', 0):02x}",
-            "name": p.name, "torch_rccl": nv}
+            "uuid": str(getattr(p, "uuid", "")), "name": p.name, "torch_rccl": nv}
     out = [None] * world
     if world > 1:
         dist.all_gather_object(out, mine)
     else:
         out = [mine]
-    return {"ranks": out, "distinct_gpus": len({r["pci"] for r in out})}
+    return {"ranks": out, "distinct_gpus": len({(r["pci"], r["uuid"]) for r in out})}
 
 
 def run_c4(args):

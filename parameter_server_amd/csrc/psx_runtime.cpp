@@ -1146,9 +1146,14 @@ psx_status sync_impl(psx_ctx *c) {
   if (sticky & psx::kStFatal) {
     std::vector<uint32_t> log(kRing);
     HIP_TRY(c, hipMemcpy(log.data(), c->d_status + 1 + kRing, sizeof(uint32_t) * kRing, hipMemcpyDeviceToHost));
-    for (const PendingCall &p : pending) {
+    // newest call first, so that consecutive rejected calls of one sender all come back
+    for (auto pi = pending.rbegin(); pi != pending.rend(); ++pi) {
+      const PendingCall &p = *pi;
       if (!(log[p.ring] & psx::kStFatal)) continue;
-      for (const psx_stream &m : p.streams) {
+      // last message first: a call may carry several messages of one sender (consecutive
+      // versions), which come back newest to oldest
+      for (auto mi = p.streams.rbegin(); mi != p.streams.rend(); ++mi) {
+        const psx_stream &m = *mi;
         auto it = c->versions.find(m.bg_id);
         const bool back = it != c->versions.end() && it->second == (int64_t)m.version;
         if (back) it->second = (int64_t)m.version - 1;

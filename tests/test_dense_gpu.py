@@ -244,6 +244,16 @@ def test_rejected_call_gives_its_version_back(entry):
         assert orc.apply_stream(np.zeros(0, np.uint8), 101, 0) == 0      # the consumed version
         assert orc.apply_stream(good, 101, 1) == 0
         assert np.array_equal(_bits(srv.read_rows(1, 0, 10)), _bits(orc.read_dense_rows(1, 0, 10)))
+        # two rejected calls of one sender back to back, and a batch carrying two of its
+        # messages: every version comes back, newest first
+        d2 = torch.from_numpy(bad.copy()).cuda()
+        torch.cuda.synchronize()
+        srv.apply_device([(d2.data_ptr(), d2.numel(), 100, 1)])
+        srv.apply_device([(d2.data_ptr(), d2.numel(), 100, 2), (d2.data_ptr(), d2.numel(), 100, 3)])
+        with pytest.raises(PsxError) as e:
+            srv.sync()
+        assert "stays consumed" not in str(e.value)
+        assert srv.GetBgVersion(100) == 0
 
 
 def test_duplicate_row_in_one_message_applied_in_order():

@@ -58,6 +58,7 @@ int g_walk_cus_pipelined = 0;   // PSX_VARIANT_WALK_CUS_PIPELINED: PSX_VARIANT_W
 int g_stream_priority = 0;      // PSX_VARIANT_STREAM_PRIORITY (read when a context is created)
 int g_ord_bucket = 1;           // PSX_VARIANT_ORD_BUCKET: split tables' record lists in buckets
 int g_pipe_slots = 0;           // PSX_VARIANT_PIPE_SLOTS: pipelined bucket calls classify slots in the dry run
+int g_side_cu_mask = 0;        // PSX_VARIANT_SIDE_CU_MASK (read when a context is created)
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -490,6 +491,8 @@ unsigned walk_blocks(psx_ctx *c, bool pipelined) {
   // leaves the apply more of them (C3 pipelined 15,430 -> 15,660 M updates/s; unpipelined,
   // alone on the chip, it needs them all: 13,800 -> 11,600, profiles/r06/s4)
   const int v = pipelined ? psx::g_walk_cus_pipelined : psx::g_walk_all_cus;
+  if (pipelined && v <= 0 && std::abs(psx::g_side_cu_mask) >= 2)   // one block per CU of the prep stream's mask
+    return (unsigned)std::max(1, cus / std::abs(psx::g_side_cu_mask));
   return (unsigned)std::max(1, v <= 0 ? cus / 2 : v == 1 ? cus : cus * std::min(v, 8));
 }
 
@@ -1300,10 +1303,27 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
   const int sp = psx::g_stream_priority;
-  if (hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, sp >= 2 ? prio_hi : 0) != hipSuccess)
-    return cleanup(PSX_ERR_DEVICE);
+  // CU masks (PSX_VARIANT_SIDE_CU_MASK k >= 2): the prep stream on one 32-bit word of the
+  // queue's CU mask in k; -k also confines the context's own stream to the other words
+  const int km = std::abs(psx::g_side_cu_mask);
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
+  const uint32_t words = (uint32_t)(ncu + 31) / 32;
+  std::vector<uint32_t> side_mask(words), own_mask(words);
+  for (uint32_t w = 0; w < words; ++w) {
+    const uint32_t all = (int)(32 * w + 32) <= ncu ? ~0u : (1u << (ncu - 32 * w)) - 1;
+    side_mask[w] = w % (uint32_t)std::max(km, 1) == 0 ? all : 0;
+    own_mask[w] = all & ~side_mask[w];
+  }
+  hipError_t own_e = km >= 2 && psx::g_side_cu_mask < 0 && words > 0
+                         ? hipExtStreamCreateWithCUMask(&c->own, words, own_mask.data())
+                         : hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, sp >= 2 ? prio_hi : 0);
+  if (own_e != hipSuccess) return cleanup(PSX_ERR_DEVICE);
   c->stream = c->own;
-  if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, sp >= 1 ? prio_lo : 0) != hipSuccess ||
+  hipError_t side_e = km >= 2 && words > 0
+                          ? hipExtStreamCreateWithCUMask(&c->side, words, side_mask.data())
+                          : hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, sp >= 1 ? prio_lo : 0);
+  if (side_e != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -3001,6 +3021,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_STREAM_PRIORITY: return &psx::g_stream_priority;
     case PSX_VARIANT_ORD_BUCKET: return &psx::g_ord_bucket;
     case PSX_VARIANT_PIPE_SLOTS: return &psx::g_pipe_slots;
+    case PSX_VARIANT_SIDE_CU_MASK: return &psx::g_side_cu_mask;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;

@@ -89,7 +89,8 @@ enum {
                                    the context stream; 0 (default): ordered_place's compact list */
   PSX_VARIANT_SIDE_CU_MASK = 32, /* read at psx_ctx_create: 0 (default) no CU masks; k >= 2 the prep
                                    stream on one 32-bit word of the CU mask in k (a pipelined call's
-                                   walk then takes one block per CU of it); -k also the context's own
+                                   walk then takes max(PSX_VARIANT_WALK_CUS_PIPELINED, 1)
+                                   blocks per CU of it); -k also the context's own
                                    stream on the other words */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */

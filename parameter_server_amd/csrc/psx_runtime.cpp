@@ -491,8 +491,8 @@ unsigned walk_blocks(psx_ctx *c, bool pipelined) {
   // leaves the apply more of them (C3 pipelined 15,430 -> 15,660 M updates/s; unpipelined,
   // alone on the chip, it needs them all: 13,800 -> 11,600, profiles/r06/s4)
   const int v = pipelined ? psx::g_walk_cus_pipelined : psx::g_walk_all_cus;
-  if (pipelined && v <= 0 && std::abs(psx::g_side_cu_mask) >= 2)   // one block per CU of the prep stream's mask
-    return (unsigned)std::max(1, cus / std::abs(psx::g_side_cu_mask));
+  if (pipelined && std::abs(psx::g_side_cu_mask) >= 2)   // max(v, 1) blocks per CU of the prep stream's mask
+    return (unsigned)std::max(1, cus / std::abs(psx::g_side_cu_mask) * std::max(v, 1));
   return (unsigned)std::max(1, v <= 0 ? cus / 2 : v == 1 ? cus : cus * std::min(v, 8));
 }
 

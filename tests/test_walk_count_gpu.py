@@ -494,3 +494,43 @@ def test_bucket_lists_and_their_overflow_replay(bucket, pipeline, pipe_slots, ki
         assert got == want
     else:
         assert _map_rows(got) == _map_rows(want)
+
+
+SIDE_CU_MASK = 32
+
+
+@pytest.mark.parametrize("mask", [2, 4, -2], ids=["prep-on-half", "prep-on-quarter", "disjoint-halves"])
+def test_cu_masked_streams_leave_results_unchanged(mask, walk_rank):
+    """PSX_VARIANT_SIDE_CU_MASK (read when the context is created): the prep stream — and with
+    a negative value the context's own stream too — on CU-mask subsets, the pipelined walk
+    sized to its CUs.  Six pipelined calls back to back against the oracle byte for byte."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(SIDE_CU_MASK, mask), L.psx_debug_set_variant(DECODE, 1)]
+    rng = np.random.RandomState(700 + mask)
+    rows, K, bgs = 6_000, 1024, [100, 101, 102, 103]
+    calls = _batches(rng, rows, K, 6, per_batch=2_500)
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(PIPELINE_ALL)
+        srv.CreateTable(3, psa.TableInfo(row_kind=SORTED_MAP, dtype=I32, row_capacity=K,
+                                         oplog_dense_serialized=False, max_rows=rows, max_entries=K))
+        L.psx_debug_set_variant(WALK_CALLS, 0)
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, msgs in enumerate(dev):
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)])
+        srv.sync()
+        walked = L.psx_debug_get_variant(WALK_CALLS)
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(SIDE_CU_MASK, old[0])
+        L.psx_debug_set_variant(DECODE, old[1])
+    assert walked == len(calls)
+    orc = OracleServer(bgs)
+    orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    assert got == orc.serialize_records(3, list(range(rows)))
+    orc.close()

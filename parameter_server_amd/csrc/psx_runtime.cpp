@@ -712,6 +712,9 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
         x.bucket_m = kBucketM;
       }
       x.on = 1;
+#ifdef PSX_DEBUG_BUILD
+      x.pad2 = (psx::g_ord_probe >> 8) & 3;   // walk timing probes (results unchanged)
+#endif
       wcount = true;
     }
     if (wcount) {

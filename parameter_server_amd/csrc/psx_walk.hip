@@ -281,6 +281,15 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
     return;
   }
   atomicAdd(&w.grow[d], n);
+#ifdef PSX_DEBUG_BUILD
+  // timing probes (PSX_ORD_PROBE bits 8, 9): one more fire-and-forget count atomic, or one
+  // more returning one, that change nothing
+  if (w.pad2 & 1) atomicAdd(&w.grow[d], 0);
+  if (w.pad2 & 2) {
+    const int32_t z = atomicAdd(&w.cnt[d], 0);
+    if (z == -12345) atomicOr(call_status, 0u);
+  }
+#endif
   if (w.wfill) {
     // the count's returned value is the record's place in its slot's list (the apply sorts
     // each list into message order, so any order of these atomics is as good)

@@ -224,7 +224,9 @@ constexpr int kCallRing = 64;
 
 // ordered_count's work for one split sorted/map table (grow set), done by the window-parallel
 // walk as it writes each record's offset (psx_walk.hip): per record cnt[slot] += 1 and
-// grow[slot] += its pairs, kStRowRange for a row outside the shard; walk_head zeroes
+// grow[slot] += its pairs (prefix lists; with bucket lists the record's list entry instead,
+// and the prep sums the pairs, psx_ordered.hip o_grow), kStRowRange for a row outside the
+// shard; walk_head zeroes
 // ordered_offsets' counters.  The pointers are the call slot's count state (a pipelined walk
 // runs beside the previous call's ordered work, which uses the other slot's).
 struct WalkCount {

@@ -112,6 +112,30 @@ __device__ __forceinline__ const uint8_t *rec_ptr(const OrdArgs &a, uint64_t e) 
   return a.ss.data[e >> 56] + (e & kRefOffMask);
 }
 
+// Entries slot s's c records can add: the sum of their pair counts.  Prefix lists: the
+// count's atomic sum (grow).  Bucket lists: the count adds nothing to grow — one
+// device-scope atomic per record less in the walk, its costliest step (an extra one costs
+// the C3 walk 8.5 us, profiles/r06/s15) — but stores each record's pair count beside its
+// list entry (bucket_pairs), summed here: one 64-B line per slot.
+__device__ __forceinline__ const int32_t *bucket_pairs(uint64_t *bucket, int64_t max_rows, int32_t m) {
+  return reinterpret_cast<const int32_t *>(bucket + max_rows * m);
+}
+__device__ __forceinline__ int32_t o_grow(const OrdArgs &a, int64_t s, int32_t c) {
+  if (!a.bucket_m) return a.grow[s];
+  static_assert(kMaxFused == 16, "four int4 per slot");
+  const int m = c < kMaxFused ? c : kMaxFused;   // (more records: the call replays, any value)
+  const int4 *q = reinterpret_cast<const int4 *>(bucket_pairs(a.list, a.max_rows, a.bucket_m) + s * kMaxFused);
+  int4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = 4 * k < m ? q[k] : int4{0, 0, 0, 0};
+  int32_t g = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    g += (4 * k < m ? v[k].x : 0) + (4 * k + 1 < m ? v[k].y : 0) + (4 * k + 2 < m ? v[k].z : 0) +
+         (4 * k + 3 < m ? v[k].w : 0);
+  return g;
+}
+
 // Does any column of the sparse record at p lie outside [0, lim)?  Eight loads in flight
 // per step, no early exit (the columns are one record's, a few cache lines).
 __device__ __forceinline__ bool cols_outside(const uint8_t *p, int64_t lim) {
@@ -174,13 +198,18 @@ __global__ void __launch_bounds__(256) ordered_count_kernel(OrdArgs a, int2 *wfi
           // key map's columns in the apply: no column scan here)
           if (cols_outside(p, a.max_entries)) atomicOr(a.keyflag, 1u);
         }
-        if (a.grow) atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
+        if (a.grow && !(wfill && a.bucket_m))   // (bucket lists: o_grow sums the pairs later)
+          atomicAdd(&a.grow[s], a.dense_records ? (int32_t)a.cap : o_ld32(p + 4));
         if (a.grow && wfill) {   // split tables, ranked: the record's place comes back with the count
           const int32_t k = atomicAdd(&a.cnt[s], 1);
           wfill[rs.first[b] + (r - rs.pre[b])] = int2{(int32_t)s, k};
           if (a.bucket_m) {   // bucket lists: the list entry itself, no ordered_fill
-            if (k < a.bucket_m) a.list[s * a.bucket_m + k] = rec_ref(b, off);
-            else atomicOr(a.call_status, kStDuplicateRow);   // more than a bucket holds: replay
+            if (k < a.bucket_m) {
+              a.list[s * a.bucket_m + k] = rec_ref(b, off);
+              const_cast<int32_t *>(bucket_pairs(a.list, a.max_rows, a.bucket_m))[s * a.bucket_m + k] = o_ld32(p + 4);
+            } else {
+              atomicOr(a.call_status, kStDuplicateRow);   // more than a bucket holds: replay
+            }
           }
         } else if (a.grow)   // split tables: ordered_offsets finds the touched rows from the counts
           atomicAdd(&a.cnt[s], 1);
@@ -354,7 +383,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     if (s < c1) {
       c = a.cnt[s];
       nen = a.nent[s];
-      g = a.grow[s];
+      if (!a.bucket_m) g = a.grow[s];
     }
     if (!o_gate(a)) {
       // bucket lists have no ordered_fill to restore the counts of a failed call: each block
@@ -366,6 +395,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       return;
     }
     const bool t = c > 0;
+    if (t && a.bucket_m) g = o_grow(a, s, c);   // (behind the gate)
     const bool big = t && starts_big(a, nen, g);
     const bool heavy = t && !big && starts_heavy(a, c);
     const bool lite = t && !big && !heavy && starts_lite(a, c, nen, g);
@@ -385,7 +415,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     }
     __syncthreads();
     if (t) {
-      a.grow[s] = 0;
+      if (!a.bucket_m) a.grow[s] = 0;
       if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
       const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : base[1] + pre[1];
       const int4 d = int4{(int32_t)s, beg, beg + c, nen};
@@ -413,7 +443,7 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
     if (c > 0) {
       ++nt;
       nr += c;
-      const int32_t nen = a.nent[s], g = a.grow[s];
+      const int32_t nen = a.nent[s], g = o_grow(a, s, c);
       if (starts_big(a, nen, g)) ++nb;
       else if (starts_heavy(a, c)) ++nh;
       else if (starts_lite(a, c, nen, g)) ++nl;
@@ -448,12 +478,12 @@ __global__ void __launch_bounds__(256) ordered_offsets_kernel(OrdArgs a) {
       c = a.cnt[s];
       if (c > 0) {
         nen = a.nent[s];
-        const int32_t g = a.grow[s];
+        const int32_t g = o_grow(a, s, c);
         big = starts_big(a, nen, g);
         heavy = !big && starts_heavy(a, c);
         lite = !big && !heavy && starts_lite(a, c, nen, g);
         risky = may_overflow(a, nen, g);
-        a.grow[s] = 0;
+        if (!a.bucket_m) a.grow[s] = 0;
         if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
       }
     }
@@ -527,8 +557,8 @@ __global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *pli
     if (t) {
       const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : base[1] + pre[1];
       a.off[s] = beg;
-      plist[base[0] + pre[0]] = int4{(int32_t)s, beg, c, a.grow[s]};
-      a.grow[s] = 0;
+      plist[base[0] + pre[0]] = int4{(int32_t)s, beg, c, o_grow(a, s, c)};
+      if (!a.bucket_m) a.grow[s] = 0;
       if (a.counted >= 2) a.cnt[s] = 0;   // ranked: ordered_fill takes no count back
     }
     return;
@@ -556,8 +586,8 @@ __global__ void __launch_bounds__(256) ordered_place_kernel(OrdArgs a, int4 *pli
     if (t) {
       const int32_t beg = a.bucket_m ? (int32_t)(s * a.bucket_m) : ar + pre[1];
       a.off[s] = beg;
-      plist[at + pre[0]] = int4{(int32_t)s, beg, c, a.grow[s]};
-      a.grow[s] = 0;
+      plist[at + pre[0]] = int4{(int32_t)s, beg, c, o_grow(a, s, c)};
+      if (!a.bucket_m) a.grow[s] = 0;
       if (a.counted >= 2) a.cnt[s] = 0;
     }
     at += tot[0];
@@ -1604,12 +1634,12 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       if (slots) {   // slot i itself: its count state is read and cleared here (ordered_offsets')
         t = false;
         if (i < a.max_rows) {
-          const int32_t c = a.cnt[i], g = a.grow[i];
+          const int32_t c = a.cnt[i];
           nen = a.nent[i];
           t = c > 0;
           if (t) {
-            e = int4{(int32_t)i, (int32_t)(i * a.bucket_m), c, g};
-            a.grow[i] = 0;
+            e = int4{(int32_t)i, (int32_t)(i * a.bucket_m), c, o_grow(a, i, c)};
+            if (!a.bucket_m) a.grow[i] = 0;
             if (a.counted >= 2) a.cnt[i] = 0;
           }
         }

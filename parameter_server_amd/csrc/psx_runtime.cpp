@@ -1595,7 +1595,9 @@ psx_status psx_table_create(psx_ctx *c, const psx_table_config *cfg) {
     if (e == hipSuccess) e = hipMalloc(&t.d_plist, 2 * R * 4 * sizeof(int32_t));
     // bucket lists, up to 2M rows (2 x 256 MiB): a slot's records at [slot][place]
     if (e == hipSuccess && R <= (int64_t)kBucketMaxRows)
-      for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipMalloc(&t.d_bucket[k], R * kBucketM * sizeof(uint64_t));
+      // each slot: the list entries, then each entry's pair count (int32, o_grow)
+      for (int k = 0; k < 2 && e == hipSuccess; ++k)
+        e = hipMalloc(&t.d_bucket[k], R * kBucketM * (sizeof(uint64_t) + sizeof(int32_t)));
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {

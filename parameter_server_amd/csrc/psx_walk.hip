@@ -280,7 +280,9 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
     if (w.wfill) w.wfill[idx] = int2{-1, 0};
     return;
   }
-  atomicAdd(&w.grow[d], n);
+  // bucket lists: no growth atomic (the pair count goes beside the list entry below and the
+  // ordered prep sums them, psx_ordered.hip o_grow)
+  if (!w.bucket) atomicAdd(&w.grow[d], n);
 #ifdef PSX_DEBUG_BUILD
   // timing probes (PSX_ORD_PROBE bits 8, 9): one more fire-and-forget count atomic, or one
   // more returning one, that change nothing
@@ -296,8 +298,13 @@ __device__ __forceinline__ void walk_count(const uint8_t *p, const WalkCount &w,
     const int32_t k = atomicAdd(&w.cnt[d], 1);
     w.wfill[idx] = int2{(int32_t)d, k};
     if (w.bucket) {   // bucket lists: the list entry itself, no ordered_fill
-      if (k < w.bucket_m) w.bucket[d * w.bucket_m + k] = ref;
-      else atomicOr(call_status, kStDuplicateRow);   // more records than a bucket holds: replay
+      if (k < w.bucket_m) {
+        w.bucket[d * w.bucket_m + k] = ref;
+        // its pair count beside the entries (psx_ordered.hip bucket_pairs, o_grow)
+        reinterpret_cast<int32_t *>(w.bucket + w.max_rows * w.bucket_m)[d * w.bucket_m + k] = n;
+      } else {
+        atomicOr(call_status, kStDuplicateRow);   // more records than a bucket holds: replay
+      }
     }
   } else {
     atomicAdd(&w.cnt[d], 1);

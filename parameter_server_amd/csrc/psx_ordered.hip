@@ -120,20 +120,28 @@ __device__ __forceinline__ const uint8_t *rec_ptr(const OrdArgs &a, uint64_t e) 
 __device__ __forceinline__ const int32_t *bucket_pairs(uint64_t *bucket, int64_t max_rows, int32_t m) {
   return reinterpret_cast<const int32_t *>(bucket + max_rows * m);
 }
-__device__ __forceinline__ int32_t o_grow(const OrdArgs &a, int64_t s, int32_t c) {
-  if (!a.bucket_m) return a.grow[s];
+__device__ __forceinline__ const int4 *bucket_pairs4(const OrdArgs &a, int64_t s) {
   static_assert(kMaxFused == 16, "four int4 per slot");
+  return reinterpret_cast<const int4 *>(bucket_pairs(a.list, a.max_rows, a.bucket_m) + s * kMaxFused);
+}
+// the sum of the first min(c, 16) pair counts of a slot's line
+__device__ __forceinline__ int32_t pairs_sum(const int4 (&v)[4], int32_t c) {
   const int m = c < kMaxFused ? c : kMaxFused;   // (more records: the call replays, any value)
-  const int4 *q = reinterpret_cast<const int4 *>(bucket_pairs(a.list, a.max_rows, a.bucket_m) + s * kMaxFused);
-  int4 v[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] = 4 * k < m ? q[k] : int4{0, 0, 0, 0};
   int32_t g = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     g += (4 * k < m ? v[k].x : 0) + (4 * k + 1 < m ? v[k].y : 0) + (4 * k + 2 < m ? v[k].z : 0) +
          (4 * k + 3 < m ? v[k].w : 0);
   return g;
+}
+__device__ __forceinline__ int32_t o_grow(const OrdArgs &a, int64_t s, int32_t c) {
+  if (!a.bucket_m) return a.grow[s];
+  const int m = c < kMaxFused ? c : kMaxFused;
+  const int4 *q = bucket_pairs4(a, s);
+  int4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = 4 * k < m ? q[k] : int4{0, 0, 0, 0};
+  return pairs_sum(v, c);
 }
 
 // Does any column of the sparse record at p lie outside [0, lim)?  Eight loads in flight
@@ -1599,6 +1607,20 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
   // the gate's words and the launch's row counts read at once (not one after another)
   const uint32_t st0 = *a.call_status, sk0 = *a.sticky;
   const uint32_t kf0 = DRY && a.keyflag ? *a.keyflag : 0u;
+  // slots mode: the slot's count, image size and bucket pair counts loaded beside the gate's
+  // words (all in bounds; the pairs are used only for a counted slot behind a passing gate)
+  int32_t pc = 0, pnen = 0;
+  int4 pv[kLocal ? 4 : 1];
+  if constexpr (kLocal) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a.classify_slots && i < a.max_rows) {
+      pc = a.cnt[i];
+      pnen = a.nent[i];
+      const int4 *q = bucket_pairs4(a, i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pv[k] = q[k];
+    }
+  }
   // slots: the classification reads the slots themselves (cnt, grow; bucket lists, whose
   // ranges need no prefix) instead of ordered_place's compact list
   const bool slots = kLocal && a.classify_slots;
@@ -1634,11 +1656,11 @@ __global__ void __launch_bounds__(256, (J <= 4 ? 7 : (sizeof(V) == 4 ? 3 : 2))) 
       if (slots) {   // slot i itself: its count state is read and cleared here (ordered_offsets')
         t = false;
         if (i < a.max_rows) {
-          const int32_t c = a.cnt[i];
-          nen = a.nent[i];
+          const int32_t c = pc;
+          nen = pnen;
           t = c > 0;
           if (t) {
-            e = int4{(int32_t)i, (int32_t)(i * a.bucket_m), c, o_grow(a, i, c)};
+            e = int4{(int32_t)i, (int32_t)(i * a.bucket_m), c, pairs_sum(pv, c)};
             if (!a.bucket_m) a.grow[i] = 0;
             if (a.counted >= 2) a.cnt[i] = 0;
           }

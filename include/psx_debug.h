@@ -92,6 +92,11 @@ enum {
                                    walk then takes max(PSX_VARIANT_WALK_CUS_PIPELINED, 1)
                                    blocks per CU of it); -k also the context's own
                                    stream on the other words */
+  PSX_VARIANT_EVENT_SCOPE = 33, /* read at psx_ctx_create: the release scope of the events that order
+                                   one of the context's streams after another (pipelined call slots,
+                                   concurrent apply launches): 0 system (HIP's default), 1 device
+                                   (hipEventReleaseToDevice), 2 no system fence
+                                   (hipEventDisableSystemFence) */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

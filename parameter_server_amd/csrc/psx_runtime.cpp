@@ -59,6 +59,7 @@ int g_stream_priority = 0;      // PSX_VARIANT_STREAM_PRIORITY (read when a cont
 int g_ord_bucket = 1;           // PSX_VARIANT_ORD_BUCKET: split tables' record lists in buckets
 int g_pipe_slots = 0;           // PSX_VARIANT_PIPE_SLOTS: pipelined bucket calls classify slots in the dry run
 int g_side_cu_mask = 0;        // PSX_VARIANT_SIDE_CU_MASK (read when a context is created)
+int g_event_scope = 0;         // PSX_VARIANT_EVENT_SCOPE (read when a context is created)
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -1326,16 +1327,24 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
   hipError_t side_e = km >= 2 && words > 0
                           ? hipExtStreamCreateWithCUMask(&c->side, words, side_mask.data())
                           : hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, sp >= 1 ? prio_lo : 0);
+  // Events that only order one of the context's streams after another on this device (the
+  // pipelined call slots' ev_ready / ev_free, the concurrent apply launches' fork / join):
+  // PSX_VARIANT_EVENT_SCOPE 1 records them with a device-scope release, 2 with no system-scope
+  // fence; 0 the default (system scope).  Events the host waits on, or that order a copy to
+  // the host, keep the default.
+  const unsigned dev_ev = hipEventDisableTiming | (psx::g_event_scope == 1   ? hipEventReleaseToDevice
+                                                   : psx::g_event_scope == 2 ? hipEventDisableSystemFence
+                                                                             : 0u);
   if (side_e != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, dev_ev) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, dev_ev) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_push[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_push[1], hipEventDisableTiming) != hipSuccess)
     return cleanup(PSX_ERR_DEVICE);
   for (int k = 0; k < 2; ++k) {
-    if (hipEventCreateWithFlags(&c->ev_ready[k], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&c->ev_ready[k], dev_ev) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_free[k], dev_ev) != hipSuccess)
       return cleanup(PSX_ERR_DEVICE);
     if (hipMalloc(&c->d_segs[k], sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
         hipMalloc(&c->d_counters[k], sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
@@ -3027,6 +3036,7 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_ORD_BUCKET: return &psx::g_ord_bucket;
     case PSX_VARIANT_PIPE_SLOTS: return &psx::g_pipe_slots;
     case PSX_VARIANT_SIDE_CU_MASK: return &psx::g_side_cu_mask;
+    case PSX_VARIANT_EVENT_SCOPE: return &psx::g_event_scope;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;

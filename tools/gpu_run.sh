@@ -63,6 +63,9 @@ for s in "$@"; do
     walked) run walked 300 python -u bench.py --walked --steps 20 --warmup 5 --cpu-seconds 0 ;;
     stats) run stats 300 rocprofv3 --kernel-trace --stats -d "$R/stats" -o c2 -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 --skip-walked --no-extras
            python3 tools/kernel_stats.py "$(find "$R/stats" -name '*.db' | head -1)" "$O/c2_kernel_stats.csv" && head -4 "$O/c2_kernel_stats.csv" | cut -c1-160 ;;
+    ptrace3) say "ptrace3"   # kernel trace of one pipelined C3 measurement (tools/c3_pipe_only.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$R/ptrace3" -o pt -- python3 tools/c3_pipe_only.py --steps 30 --warmup 3 > "$O/ptrace3.log" 2>&1 || { echo "!! ptrace3"; tail -20 "$O/ptrace3.log"; exit 1; }
+      f=$(find "$R/ptrace3" -name "*kernel_trace.csv" | head -1); cp "$f" "$O/c3_pipe_kernel_trace.csv" && tail -1 "$O/ptrace3.log" ;;
     stats3) run stats3 300 rocprofv3 --kernel-trace --stats -d "$R/stats3" -o c3 -- python3 bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 0
            python3 tools/kernel_stats.py "$(find "$R/stats3" -name '*.db' | head -1)" "$O/c3_kernel_stats.csv" && head -6 "$O/c3_kernel_stats.csv" | cut -c1-160 ;;
     pmc)

@@ -95,7 +95,7 @@ enum {
   PSX_VARIANT_EVENT_SCOPE = 33, /* read at psx_ctx_create: the release scope of the events that order
                                    one of the context's streams after another (pipelined call slots,
                                    concurrent apply launches): 0 system (HIP's default), 1 device
-                                   (hipEventReleaseToDevice), 2 no system fence
+                                   (hipEventReleaseToDevice), 2 (default) no system fence
                                    (hipEventDisableSystemFence) */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */

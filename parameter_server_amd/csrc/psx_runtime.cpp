@@ -59,7 +59,7 @@ int g_stream_priority = 0;      // PSX_VARIANT_STREAM_PRIORITY (read when a cont
 int g_ord_bucket = 1;           // PSX_VARIANT_ORD_BUCKET: split tables' record lists in buckets
 int g_pipe_slots = 0;           // PSX_VARIANT_PIPE_SLOTS: pipelined bucket calls classify slots in the dry run
 int g_side_cu_mask = 0;        // PSX_VARIANT_SIDE_CU_MASK (read when a context is created)
-int g_event_scope = 0;         // PSX_VARIANT_EVENT_SCOPE (read when a context is created)
+int g_event_scope = 2;         // PSX_VARIANT_EVENT_SCOPE (read when a context is created)
 // Granule tags of the window-parallel decode: unique per call across every context of the
 // process, so a granule left in a recycled allocation by another context (or an earlier
 // call of this slot) can never carry the tag a walk waits for.  (Round 2's fault: epochs
@@ -1329,9 +1329,13 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
                           : hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, sp >= 1 ? prio_lo : 0);
   // Events that only order one of the context's streams after another on this device (the
   // pipelined call slots' ev_ready / ev_free, the concurrent apply launches' fork / join):
-  // PSX_VARIANT_EVENT_SCOPE 1 records them with a device-scope release, 2 with no system-scope
-  // fence; 0 the default (system scope).  Events the host waits on, or that order a copy to
-  // the host, keep the default.
+  // PSX_VARIANT_EVENT_SCOPE 2 (the default) records them with no system-scope fence (the
+  // kernels' own device-scope fences order them on this device; hipEventDisableSystemFence
+  // gives up visibility to the host and other devices only), 1 with a device-scope release,
+  // 0 HIP's default (system scope).  The system-scope acquire at each wait cost a pipelined C3
+  // call ~3 us (16,400-16,550 -> 16,880-17,120 M updates/s, indexed 19,190-19,260 ->
+  // 20,090-20,170; a device-scope release alone changes nothing, profiles/r06/s21).  Events
+  // the host waits on, or that order a copy to the host, keep HIP's default.
   const unsigned dev_ev = hipEventDisableTiming | (psx::g_event_scope == 1   ? hipEventReleaseToDevice
                                                    : psx::g_event_scope == 2 ? hipEventDisableSystemFence
                                                                              : 0u);

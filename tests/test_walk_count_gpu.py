@@ -534,3 +534,41 @@ def test_cu_masked_streams_leave_results_unchanged(mask, walk_rank):
             assert orc.apply_stream(s, bg, v) == 0
     assert got == orc.serialize_records(3, list(range(rows)))
     orc.close()
+
+
+EVENT_SCOPE = 33
+
+
+@pytest.mark.parametrize("scope", [2, 0], ids=["no-system-fence", "system-fence"])
+def test_pipelined_many_calls_small_table(scope, walk_rank):
+    """The call slots' cross-stream events (PSX_VARIANT_EVENT_SCOPE, read at context creation;
+    2 the default: no system-scope fence): 24 pipelined calls back to back on a table small
+    enough to stay in the XCDs' L2s, every call's records different, the slots' lists and
+    counts reused every second call — the rows must equal the oracle's byte for byte."""
+    L = _abi.load()
+    old = [L.psx_debug_set_variant(EVENT_SCOPE, scope), L.psx_debug_set_variant(DECODE, 1)]
+    rng = np.random.RandomState(800 + scope)
+    rows, K, bgs = 3_000, 1024, [100, 101, 102, 103]
+    calls = _batches(rng, rows, K, 24, per_batch=1_200)
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(PIPELINE_ALL)
+        srv.CreateTable(3, psa.TableInfo(row_kind=SORTED_MAP, dtype=I32, row_capacity=K,
+                                         oplog_dense_serialized=False, max_rows=rows, max_entries=K))
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, msgs in enumerate(dev):
+            srv.apply_device([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)])
+        srv.sync()
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(EVENT_SCOPE, old[0])
+        L.psx_debug_set_variant(DECODE, old[1])
+    orc = OracleServer(bgs)
+    orc.create_table(3, SORTED_MAP, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    assert got == orc.serialize_records(3, list(range(rows)))
+    orc.close()

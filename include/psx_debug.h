@@ -97,7 +97,6 @@ enum {
                                    concurrent apply launches): 0 system (HIP's default), 1 device
                                    (hipEventReleaseToDevice), 2 (default) no system fence
                                    (hipEventDisableSystemFence) */
-  PSX_VARIANT_SPILL_GRID = 34,  /* the spill (1,024-entry) launch's grid cap (default 768 blocks) */
   PSX_STAT_DENSE_LAST = 24,     /* read: the dense apply kernel the last call launched (2 v2, 3 v3,
                                    4 v4; 0 none since load) */
   PSX_DEBUG_WALK_SKEW = 21      /* tests only: 1 skews every exit state the walk publishes early from

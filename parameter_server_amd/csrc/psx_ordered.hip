@@ -2185,7 +2185,6 @@ static unsigned row_blocks(int64_t n, int wpb) {
 // blocks of 4 waves on 256 CUs) and loop over their rows: an empty 4,096-block launch
 // cost 4.7-4.9 µs per C3 step (profiles/r03/s26/c3_kernel_stats.csv).
 static unsigned few_row_blocks(int64_t n) { return std::min(row_blocks(n, 4), 768u); }
-int g_spill_blocks = 768;      // PSX_VARIANT_SPILL_GRID: the spill (1,024-entry) launch's grid cap
 int g_offsets_blocks = 1024;   // PSX_VARIANT_OFFSETS_GRID: ordered_offsets' grid cap
 int g_dry_blocks = 128;        // PSX_VARIANT_DRY_GRID: the capacity dry run's grid cap
 int g_classify_blocks = 256;   // PSX_VARIANT_CLASSIFY_GRID: ordered_classify's grid cap
@@ -2386,7 +2385,7 @@ hipError_t launch_ordered_apply(int dtype, const OrdArgs &a, hipStream_t st, con
         hipLaunchKernelGGL((ordered_apply_lite_kernel<V, KIND>), dim3(row_blocks((a.max_rows + 3) / 4, 4)), \
                            dim3(256), 0, st, small);                                               \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \
-      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, false, true>), dim3(std::min(few_row_blocks(a.max_rows), (unsigned)std::max(1, g_spill_blocks))), dim3(256), 0, st, big); \
+      hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16, false, true>), dim3(few_row_blocks(a.max_rows)), dim3(256), 0, st, big); \
     } else if (a.grow) {                                                                           \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 16>), dim3(blocks), dim3(256), 0, fk.aux, big); \
       hipLaunchKernelGGL((ordered_apply_reg_kernel<V, KIND, 4>), dim3(blocks), dim3(256), 0, st, small); \

@@ -3023,7 +3023,6 @@ extern int g_classify_dry;
 extern int g_ord_split;
 extern int g_offsets_blocks;
 extern int g_dry_blocks;
-extern int g_spill_blocks;
 }  // namespace psx
 
 static int *variant_slot(int32_t which) {
@@ -3042,7 +3041,6 @@ static int *variant_slot(int32_t which) {
     case PSX_VARIANT_PIPE_SLOTS: return &psx::g_pipe_slots;
     case PSX_VARIANT_SIDE_CU_MASK: return &psx::g_side_cu_mask;
     case PSX_VARIANT_EVENT_SCOPE: return &psx::g_event_scope;
-    case PSX_VARIANT_SPILL_GRID: return &psx::g_spill_blocks;
     case PSX_VARIANT_DENSE_STORE: return &psx::g_dense_store_nt;
     case PSX_DEBUG_WALK_TRACE: return &psx::g_walk_trace;
     case PSX_VARIANT_WALK_CUS: return &psx::g_walk_all_cus;

@@ -45,24 +45,30 @@ constexpr int kJumpLevels = 5;              // 1, 2, 4, 8, 16 records
 constexpr uint16_t kU16 = 0xFFFFu;          // chain leaves the window / bad header
 
 // Indexed messages (ix.p[b] set, psx_apply_indexed): a sparse table's record offsets come
-// from the producer's index; all threads copy them and check the chain in parallel
-// (first offset = the table's first byte, each record ends where the next begins, all
-// inside the message) instead of hopping it.
+// from the producer's index.  This kernel (one workgroup per message) checks only the
+// table's first and last offsets and steps to the table's end; idx_verify (psx_walk.hip,
+// a grid over every record) checks the chain (each record ends where the next begins,
+// inside the message), writes the offsets and, for walk-counted split tables, does
+// ordered_count's work.  What this kernel finds wrong after an indexed table of the
+// message may come from a bad index: those status bits wait in idxw[4 b] and reach the
+// call only if idx_verify finds the message's index sound (a bad index is kStMalformed).
+// idxw: 4 words per message ([0] pending bits, [1] bad index, [2] idx_verify's blocks done).
 __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSet ss, TableDir dir, Seg *segs,
                                                                         uint64_t *recoff, uint32_t *call_status,
                                                                         uint32_t *counters, uint32_t *ntouched,
-                                                                        IdxSet ix) {
+                                                                        IdxSet ix, uint32_t *idxw) {
   __shared__ uint32_t win[kDecodeWindowWords + 1];                 // + 1 halo word
   __shared__ uint16_t jt[kJumpLevels][kDecodeWindowWords];          // jt[l]: 2^l records on
   __shared__ uint16_t a16[kDecodeWindowWords / 32];                 // starts of 16-record hops
   __shared__ uint16_t a4[8], a1s[16];                               // 4-record hops (<= 3), single records (<= 4)
   __shared__ uint32_t sh_n16, sh_n4, sh_ns;
   __shared__ int32_t sh_bad;
-  __shared__ uint64_t sh_off, sh_rk, sh_left, sh_kk, sh_end, sh_t0;
+  __shared__ uint64_t sh_off, sh_rk, sh_left, sh_kk, sh_t0;
   uint32_t pf[kDecodeWindowWords / kDecodeThreads];                 // the prefetched window
   uint64_t pf_w0 = ~0ull;
   __shared__ int32_t sh_state;   // 0 walking headers, 1 sparse walk needs a window, 2 done, 3 indexed sparse table
   __shared__ int32_t sh_t, sh_ntab, sh_k;
+  __shared__ uint32_t *sh_err;   // where header errors go: call_status, or idxw[4 b] after an indexed table
   const int b = blockIdx.x;
   for (int t = threadIdx.x; t < kMaxTables; t += blockDim.x) {
     Seg s;
@@ -77,6 +83,12 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
   const uint8_t *p = ss.data[b];
   const uint64_t size = ss.size[b];
   if (threadIdx.x == 0) {
+    sh_err = call_status;
+    if (ix.p[b]) {
+      idxw[4 * b + 0] = 0;
+      idxw[4 * b + 1] = 0;
+      idxw[4 * b + 2] = 0;
+    }
     sh_state = 2;
     sh_off = 4;
     sh_k = 0;
@@ -99,7 +111,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
         // next table header (SerializedOpLogReader::StartNewTable, :87-121)
         if (sh_k >= sh_ntab) { sh_state = 2; break; }
         uint64_t off = sh_off;
-        if (off + 16 > size) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
+        if (off + 16 > size) { atomicOr(sh_err, kStMalformed); sh_state = 2; break; }
         const int32_t tid = ld32(p + off);
         const uint64_t usz = ld64_a4(p + off + 4);
         const int32_t nrows = ld32(p + off + 12);
@@ -107,14 +119,14 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
         int t = -1;
         for (int i = 0; i < dir.n; ++i)
           if (dir.table_id[i] == tid) t = i;
-        if (t < 0) { atomicOr(call_status, kStUnknownTable); sh_state = 2; break; }
-        if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
+        if (t < 0) { atomicOr(sh_err, kStUnknownTable); sh_state = 2; break; }
+        if (usz != (uint64_t)dir.vsize[t] || nrows < 0) { atomicOr(sh_err, kStMalformed); sh_state = 2; break; }
         Seg *sg = &segs[b * kMaxTables + t];
-        if (sg->rec0 >= 0) { atomicOr(call_status, kStUnsupported); sh_state = 2; break; }
+        if (sg->rec0 >= 0) { atomicOr(sh_err, kStUnsupported); sh_state = 2; break; }
         if (dir.dense_serialized[t]) {
           const uint64_t stride = 4 + (uint64_t)dir.dense_body[t];
           const uint64_t need = (uint64_t)nrows * stride;
-          if (off + need > size) { atomicOr(call_status, kStMalformed); sh_state = 2; break; }
+          if (off + need > size) { atomicOr(sh_err, kStMalformed); sh_state = 2; break; }
           sg->rec0 = (int64_t)off;
           sg->num_rows = nrows;
           sg->sparse = 0;
@@ -125,7 +137,7 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
         } else if (off & 3) {
           // the sparse walk stages 4-byte words: a sparse table behind a version table's
           // odd-sized records (9-byte trailers) is not supported
-          atomicOr(call_status, kStUnsupported); sh_state = 2; break;
+          atomicOr(sh_err, kStUnsupported); sh_state = 2; break;
         } else {
           sg->rec0 = (int64_t)sh_rk;   // index of the first record offset
           sg->num_rows = nrows;
@@ -144,34 +156,34 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
     __syncthreads();
     if (sh_state == 2) break;
     if (sh_state == 3) {
-      // A') indexed sparse table: copy + verify the producer's offsets (all threads)
-      const uint64_t *ofs = ix.p[b] + sh_kk;
-      const uint64_t nrec = sh_left, start = sh_off, rk = sh_rk;
-      const uint64_t pair = 4 + (uint64_t)dir.vsize[sh_t];
-      for (uint64_t i = threadIdx.x; i < nrec; i += blockDim.x) {
-        const uint64_t o = ofs[i];
-        bool ok = (o & 3) == 0 && o >= start && o + 8 <= size && (i > 0 || o == start);
+      // A') indexed sparse table: its first and last offsets here (the first at the
+      // table's first byte, the last record inside the message, every record >= 8 bytes),
+      // the chain in idx_verify; later header errors of this message wait for its verdict
+      if (threadIdx.x == 0) {
+        const uint64_t *ofs = ix.p[b] + sh_kk;
+        const uint64_t nrec = sh_left, start = sh_off;
+        const uint64_t pair = 4 + (uint64_t)dir.vsize[sh_t];
+        bool ok = start < size && nrec <= (size - start) / 8;
         uint64_t end = 0;
         if (ok) {
-          const int32_t n = ld32(p + o + 4);
-          end = o + 8 + (uint64_t)(n < 0 ? 0 : n) * pair;
-          ok = n >= 0 && end <= size;
+          const uint64_t o0 = ofs[0], ol = ofs[nrec - 1];
+          ok = o0 == start && (ol & 3) == 0 && ol >= start && ol + 8 <= size;
+          if (ok) {
+            const int32_t n = ld32(p + ol + 4);
+            end = ol + 8 + (uint64_t)(n < 0 ? 0 : n) * pair;
+            ok = n >= 0 && end <= size;
+          }
         }
-        if (ok && i + 1 < nrec) ok = ofs[i + 1] == end;
-        if (!ok) sh_bad = 1;
-        recoff[rk + i] = o;
-        if (i + 1 == nrec) sh_end = end;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        if (sh_bad) {
+        if (!ok) {
           atomicOr(call_status, kStMalformed);
+          segs[b * kMaxTables + sh_t].num_rows = 0;   // idx_verify skips it (the call fails)
           sh_state = 2;
         } else {
-          sh_off = sh_end;
-          sh_rk = rk + nrec;
+          sh_off = end;
+          sh_rk = sh_rk + nrec;
           sh_kk = sh_kk + nrec;
           sh_k = sh_k + 1;
+          sh_err = idxw + 4 * b;
           sh_state = 0;
         }
       }
@@ -1203,12 +1215,21 @@ __global__ void gather_flags_kernel(const uint8_t *flags, const int64_t *slots, 
 
 // ---------------------------------------------------------------------------
 // Host-side launchers (internal to libpsx).
+hipError_t launch_idx_verify(StreamSet ss, const TableDir &dir, const Seg *segs, const IdxSet &ix, uint64_t *recoff,
+                             uint32_t *call_status, uint32_t *idxw, const WalkCount *wc, hipStream_t st);
+
+// idxw: 4 words per message (indexed messages); wc: null, or the walk-counted split tables'
+// WalkCount (idx_verify counts their records, as the window-parallel walk does)
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
                          uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
-                         hipStream_t st) {
+                         uint32_t *idxw, const WalkCount *wc, hipStream_t st) {
   hipLaunchKernelGGL(decode_streams_kernel, dim3(ss.n), dim3(kDecodeThreads), 0, st, ss, dir, segs, recoff,
-                     call_status, counters, ntouched, ix);
-  return hipGetLastError();
+                     call_status, counters, ntouched, ix, idxw);
+  hipError_t e = hipGetLastError();
+  bool any = false;
+  for (int b = 0; b < ss.n; ++b) any = any || ix.p[b];
+  if (e == hipSuccess && any) e = launch_idx_verify(ss, dir, segs, ix, recoff, call_status, idxw, wc, st);
+  return e;
 }
 
 // Resident-capacity grid for a persistent-style kernel (blocks per CU x CUs).

@@ -23,7 +23,7 @@
 namespace psx {
 hipError_t launch_decode(StreamSet ss, const TableDir &dir, Seg *segs, uint64_t *recoff,
                          uint32_t *call_status, uint32_t *counters, uint32_t *ntouched, const IdxSet &ix,
-                         hipStream_t st);
+                         uint32_t *idxw, const WalkCount *wc, hipStream_t st);
 bool dense_apply_checks_rows(const DenseArgs &a, bool rec_f16);
 hipError_t launch_split_count(const SplitArgs &a, hipStream_t st);
 hipError_t launch_split_scatter(const SplitArgs &a, const int64_t *pos, const uint32_t *val, int32_t nwords,
@@ -692,8 +692,12 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
   // writes the record offsets (WalkCount), into this call slot's count state (a pipelined
   // walk runs beside the previous call's ordered work, which uses the other slot's), and
   // the ordered prep skips that launch.
+  // An indexed call (every message with the producer's record offsets) counts the same way,
+  // in idx_verify (psx_walk.hip), which checks the offsets over a grid.
+  bool idx_all = !walk && n > 0;
+  for (int i = 0; i < n; ++i) idx_all = idx_all && ix.p[i];
   bool wcount = false;
-  if (walk && psx::g_walk_count) {
+  if ((walk || idx_all) && psx::g_walk_count) {
     std::vector<psx::WalkCount> w(c->tables.size());
     for (size_t ti = 0; ti < c->tables.size(); ++ti) {
       TableState &t = c->tables[ti];
@@ -742,7 +746,8 @@ psx_status enqueue_apply(psx_ctx *c, const psx_stream *s, int32_t n, bool force_
                                   c->walk_epoch[slot], psx::g_walk_trace ? c->walk_cap[slot] ? items : 0 : 0,
                                   wcount ? c->d_wcount[slot] : nullptr, items,
                                   walk_levels | (psx::g_walk_skew && walk_levels > 0 ? 0x100 : 0), walk_shape, prep);
-        return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix, prep);
+        return psx::launch_decode(ss, dir, segs, c->d_recoff[slot], call_st, counters, c->d_ntouched[slot], ix,
+                                  c->d_ntouched[slot] + psx::kMaxTables, wcount ? c->d_wcount[slot] : nullptr, prep);
       },
       prep);
   if (st) return st;
@@ -1352,7 +1357,8 @@ psx_status psx_ctx_create(int32_t device, int32_t server_id, psx_ctx **out) {
       return cleanup(PSX_ERR_DEVICE);
     if (hipMalloc(&c->d_segs[k], sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
         hipMalloc(&c->d_counters[k], sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess ||
-        hipMalloc(&c->d_ntouched[k], sizeof(uint32_t) * psx::kMaxTables) != hipSuccess)
+        // (then idx_verify's 4 words per message: psx_kernels.hip decode_streams)
+        hipMalloc(&c->d_ntouched[k], sizeof(uint32_t) * (psx::kMaxTables + 4 * psx::kMaxFused)) != hipSuccess)
       return cleanup(PSX_ERR_OOM);
     if (hipMemset(c->d_counters[k], 0, sizeof(uint32_t) * psx::kMaxFused * psx::kMaxTables) != hipSuccess)
       return cleanup(PSX_ERR_DEVICE);
@@ -2318,7 +2324,7 @@ static psx_status split_impl(psx_ctx *c, const std::vector<TableState> &fmts, co
   };
   // 1) decode the message (tables, sparse record offsets) into the split's own buffers
   psx_status e = grow(c->d_split_fixed, c->split_fixed_cap,
-                      sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables + 4096);
+                      sizeof(psx::Seg) * psx::kMaxFused * psx::kMaxTables + 8192);
   if (e) return e;
   if ((e = grow(c->d_split_recoff, c->split_recoff_cap, nrecoff * sizeof(uint64_t)))) return e;
   psx::Seg *segs = reinterpret_cast<psx::Seg *>(c->d_split_fixed);
@@ -2341,7 +2347,8 @@ static psx_status split_impl(psx_ctx *c, const std::vector<TableState> &fmts, co
   psx::IdxSet ix{};
   ix.p[0] = record_offsets;
   uint64_t *recoff = reinterpret_cast<uint64_t *>(c->d_split_recoff);
-  HIP_TRY(c, psx::launch_decode(ss, dir, segs, recoff, status, counters, ntouched, ix, st));
+  HIP_TRY(c, psx::launch_decode(ss, dir, segs, recoff, status, counters, ntouched, ix, ntouched + psx::kMaxTables,
+                                nullptr, st));
   std::vector<psx::Seg> hs(psx::kMaxTables);
   uint32_t hst = 0;
   HIP_TRY(c, hipMemcpyAsync(hs.data(), segs, sizeof(psx::Seg) * psx::kMaxTables, hipMemcpyDeviceToHost, st));

@@ -831,6 +831,77 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
   }
 }
 
+// idx_verify: the indexed messages' record chains (psx_kernels.hip decode_streams found
+// each indexed table's segment and checked its first and last offsets).  Grid (G, B): the
+// G blocks of message b take its records in a grid stride: each record's offset aligned,
+// its header and pairs inside the message, the next offset where it ends; the offset goes
+// to recoff and, for a walk-counted split table, ordered_count's work is done here
+// (walk_count).  A bad record fails the call (kStMalformed); the last block of message b
+// releases the header errors decode_streams held back (idxw[4 b]) only when the message's
+// index was sound.  No block waits on another.
+__global__ void __launch_bounds__(256) idx_verify_kernel(StreamSet ss, TableDir dir, const Seg *segs, IdxSet ix,
+                                                         uint64_t *recoff, uint32_t *call_status, uint32_t *idxw,
+                                                         const WalkCount *wc) {
+  const int b = blockIdx.y;
+  const uint8_t *p = ss.data[b];
+  const uint64_t size = ss.size[b];
+  const uint64_t *idx = ix.p[b];
+  if (wc && blockIdx.x == 0 && b == 0) {   // ordered_count's reset of ordered_offsets' counters
+    // (walk_head's job on walked calls; nothing in this launch reads them)
+    for (int t = threadIdx.x; t < dir.n; t += blockDim.x)
+      if (wc[t].on) {
+        for (int i = 0; i < 5; ++i) wc[t].nsplit[i * kNsStride] = 0;
+        wc[t].tsum[0] = 0;
+      }
+  }
+  bool bad = false;
+  if (idx) {
+    for (int t = 0; t < dir.n; ++t) {
+      const Seg sg = segs[b * kMaxTables + t];
+      if (sg.rec0 < 0 || !sg.sparse || sg.num_rows <= 0) continue;
+      const uint64_t *ofs = idx + sg.ord0;
+      const uint64_t nrec = (uint64_t)sg.num_rows, rk = (uint64_t)sg.rec0, pair = 4 + (uint64_t)dir.vsize[t];
+      const bool counted = wc && wc[t].on;
+      for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec;
+           i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = ofs[i];
+        bool ok = (o & 3) == 0 && o + 8 <= size;
+        uint64_t end = 0;
+        if (ok) {
+          const int32_t n = *reinterpret_cast<const int32_t *>(p + o + 4);
+          end = o + 8 + (uint64_t)(n < 0 ? 0 : n) * pair;
+          ok = n >= 0 && end <= size;
+        }
+        if (ok && i + 1 < nrec) ok = ofs[i + 1] == end;
+        recoff[rk + i] = o;
+        if (!ok) bad = true;
+        else if (counted) walk_count(p + o, wc[t], call_status, rk + i, ((uint64_t)b << 56) | o);
+      }
+    }
+  }
+  if (bad) {
+    atomicOr(call_status, kStMalformed);
+    atomicOr(&idxw[4 * b + 1], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && idx) {
+    __threadfence();
+    if (atomicAdd(&idxw[4 * b + 2], 1u) == gridDim.x - 1) {   // the message's last block
+      __threadfence();
+      const uint32_t bd = atomicOr(&idxw[4 * b + 1], 0u), pend = atomicOr(&idxw[4 * b + 0], 0u);
+      if (!bd && pend) atomicOr(call_status, pend);
+    }
+  }
+}
+
+hipError_t launch_idx_verify(StreamSet ss, const TableDir &dir, const Seg *segs, const IdxSet &ix, uint64_t *recoff,
+                             uint32_t *call_status, uint32_t *idxw, const WalkCount *wc, hipStream_t st) {
+  const unsigned B = (unsigned)(ss.n < 1 ? 1 : ss.n);
+  const unsigned G = (2048u + B - 1) / B;   // ~2,048 blocks in all
+  hipLaunchKernelGGL(idx_verify_kernel, dim3(G, B), dim3(256), 0, st, ss, dir, segs, ix, recoff, call_status, idxw, wc);
+  return hipGetLastError();
+}
+
 // ws: walk_ws_bytes(items) bytes (items >= B x the largest message's window count at `shape`);
 // epoch: nonzero, different from the previous call's on this workspace (granule tags);
 // trace_items: nonzero = write the per-item timestamps (the workspace's item count);

@@ -114,3 +114,33 @@ def test_bad_index_is_malformed(where):
         srv.sync()
     assert e.value.status == 4
     assert not (srv.row_flags(3, 0, rows) & 1).any() and not (srv.row_flags(1, 0, rows) & 1).any()
+
+
+@pytest.mark.parametrize("index", ["sound", "bad"])
+def test_header_error_after_an_indexed_table(index):
+    """decode_streams checks an indexed table's first and last offsets and steps past it;
+    idx_verify checks the chain over a grid.  A header error found after the indexed table
+    (here an unknown table id) waits for the index's verdict: with a sound index it is the
+    call's error (PSX_ERR_UNKNOWN_TABLE, as the reader's CHECK), with a bad one the call is
+    PSX_ERR_MALFORMED; nothing is applied either way."""
+    rng = np.random.RandomState(11)
+    rows, K = 200, 32
+    srv, _ = _servers(rows, K, [1])
+    m = _message(rng, rows, K)
+    o = wire.stream_record_offsets(m, {1: 4 * K, 3: None}).copy()
+    nsp = int(np.frombuffer(m[16:20].tobytes(), "<i4")[0])   # sparse records come first
+    # the second table's id (its header follows the sparse table's last record) -> 9
+    last = int(o[nsp - 1])
+    n_last = int(np.frombuffer(m[last + 4:last + 8].tobytes(), "<i4")[0])
+    hdr = last + 8 + 8 * n_last
+    m[hdr:hdr + 4] = np.array([9], np.int32).view(np.uint8)
+    if index == "bad":
+        o[nsp // 2] += 4
+    dm = torch.from_numpy(m.copy()).cuda()
+    do = torch.from_numpy(o.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    srv.apply_indexed([(dm.data_ptr(), dm.numel(), 1, 0)], [do.data_ptr()])
+    with pytest.raises(PsxError) as e:
+        srv.sync()
+    assert e.value.status == (3 if index == "sound" else 4)
+    assert not (srv.row_flags(3, 0, rows) & 1).any() and not (srv.row_flags(1, 0, rows) & 1).any()

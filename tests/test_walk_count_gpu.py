@@ -572,3 +572,45 @@ def test_pipelined_many_calls_small_table(scope, walk_rank):
             assert orc.apply_stream(s, bg, v) == 0
     assert got == orc.serialize_records(3, list(range(rows)))
     orc.close()
+
+
+@pytest.mark.parametrize("pipeline", [0, PIPELINE_ALL], ids=["unpipelined", "pipelined"])
+@pytest.mark.parametrize("kind", [SORTED_MAP, MAP], ids=["sorted_map", "map"])
+def test_indexed_calls_counted_by_idx_verify(kind, pipeline, walk_rank):
+    """Indexed calls (every message with the producer's record offsets): idx_verify checks
+    the chains over a grid and does ordered_count's work for the split tables, as the walk
+    does on walked calls (including the reset of the split lists' counters).  Ten calls back
+    to back, no sync between them, against the oracle byte for byte."""
+    L = _abi.load()
+    old = L.psx_debug_set_variant(WALK_COUNT, 1)
+    rng = np.random.RandomState(900 + pipeline + kind)
+    rows, K, bgs = 6_000, 1024, [100, 101, 102, 103]
+    calls = _batches(rng, rows, K, 10, per_batch=2_500)
+    try:
+        srv = psa.Server(0, 1, bgs)
+        srv.set_pipeline(pipeline)
+        srv.CreateTable(3, psa.TableInfo(row_kind=kind, dtype=I32, row_capacity=K, oplog_dense_serialized=False,
+                                         max_rows=rows, max_entries=K))
+        dev = [[torch.from_numpy(np.array(s, copy=True)).cuda() for s in msgs] for msgs in calls]
+        idx = [[torch.from_numpy(wire.stream_record_offsets(np.asarray(s), {3: None}).view(np.int64)).cuda()
+                for s in msgs] for msgs in calls]
+        torch.cuda.synchronize()
+        for v, (msgs, offs) in enumerate(zip(dev, idx)):
+            srv.apply_indexed([(d.data_ptr(), d.numel(), bg, v) for d, bg in zip(msgs, bgs)],
+                              [o.data_ptr() for o in offs])
+        srv.sync()
+        got = srv.serialize_rows(3, list(range(rows)))
+        srv.close()
+    finally:
+        L.psx_debug_set_variant(WALK_COUNT, old)
+    orc = OracleServer(bgs)
+    orc.create_table(3, kind, I32, 0, oplog_dense_serialized=False)
+    for v, msgs in enumerate(calls):
+        for s, bg in zip(msgs, bgs):
+            assert orc.apply_stream(s, bg, v) == 0
+    want = orc.serialize_records(3, list(range(rows)))
+    orc.close()
+    if kind == SORTED_MAP:
+        assert got == want
+    else:
+        assert _map_rows(got) == _map_rows(want)

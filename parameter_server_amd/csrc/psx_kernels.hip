@@ -52,7 +52,7 @@ constexpr uint16_t kU16 = 0xFFFFu;          // chain leaves the window / bad hea
 // ordered_count's work.  What this kernel finds wrong after an indexed table of the
 // message may come from a bad index: those status bits wait in idxw[4 b] and reach the
 // call only if idx_verify finds the message's index sound (a bad index is kStMalformed).
-// idxw: 4 words per message ([0] pending bits, [1] bad index, [2] idx_verify's blocks done).
+// idxw: 4 words per message ([0] pending bits, [1] bad index).
 __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSet ss, TableDir dir, Seg *segs,
                                                                         uint64_t *recoff, uint32_t *call_status,
                                                                         uint32_t *counters, uint32_t *ntouched,
@@ -87,7 +87,6 @@ __global__ void __launch_bounds__(kDecodeThreads) decode_streams_kernel(StreamSe
     if (ix.p[b]) {
       idxw[4 * b + 0] = 0;
       idxw[4 * b + 1] = 0;
-      idxw[4 * b + 2] = 0;
     }
     sh_state = 2;
     sh_off = 4;

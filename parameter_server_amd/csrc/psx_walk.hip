@@ -836,9 +836,9 @@ __global__ void __launch_bounds__(T_) walk_kernel(StreamSet ss, TableDir dir, Se
 // G blocks of message b take its records in a grid stride: each record's offset aligned,
 // its header and pairs inside the message, the next offset where it ends; the offset goes
 // to recoff and, for a walk-counted split table, ordered_count's work is done here
-// (walk_count).  A bad record fails the call (kStMalformed); the last block of message b
-// releases the header errors decode_streams held back (idxw[4 b]) only when the message's
-// index was sound.  No block waits on another.
+// (walk_count).  A bad record fails the call (kStMalformed) and marks the message
+// (idxw[4 b + 1]); idx_settle then releases the header errors decode_streams held back
+// (idxw[4 b]) for the messages whose index was sound.
 __global__ void __launch_bounds__(256) idx_verify_kernel(StreamSet ss, TableDir dir, const Seg *segs, IdxSet ix,
                                                          uint64_t *recoff, uint32_t *call_status, uint32_t *idxw,
                                                          const WalkCount *wc) {
@@ -883,22 +883,21 @@ __global__ void __launch_bounds__(256) idx_verify_kernel(StreamSet ss, TableDir 
     atomicOr(call_status, kStMalformed);
     atomicOr(&idxw[4 * b + 1], 1u);
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && idx) {
-    __threadfence();
-    if (atomicAdd(&idxw[4 * b + 2], 1u) == gridDim.x - 1) {   // the message's last block
-      __threadfence();
-      const uint32_t bd = atomicOr(&idxw[4 * b + 1], 0u), pend = atomicOr(&idxw[4 * b + 0], 0u);
-      if (!bd && pend) atomicOr(call_status, pend);
-    }
-  }
+}
+
+// After idx_verify (a kernel boundary): message b's held-back header errors reach the call
+// only when its index was sound.
+__global__ void __launch_bounds__(64) idx_settle_kernel(IdxSet ix, int B, uint32_t *call_status, const uint32_t *idxw) {
+  const int b = threadIdx.x;
+  if (b < B && ix.p[b] && !idxw[4 * b + 1] && idxw[4 * b + 0]) atomicOr(call_status, idxw[4 * b + 0]);
 }
 
 hipError_t launch_idx_verify(StreamSet ss, const TableDir &dir, const Seg *segs, const IdxSet &ix, uint64_t *recoff,
                              uint32_t *call_status, uint32_t *idxw, const WalkCount *wc, hipStream_t st) {
   const unsigned B = (unsigned)(ss.n < 1 ? 1 : ss.n);
-  const unsigned G = (2048u + B - 1) / B;   // ~2,048 blocks in all
+  const unsigned G = (512u + B - 1) / B;   // ~512 blocks in all (grid stride over larger messages)
   hipLaunchKernelGGL(idx_verify_kernel, dim3(G, B), dim3(256), 0, st, ss, dir, segs, ix, recoff, call_status, idxw, wc);
+  hipLaunchKernelGGL(idx_settle_kernel, dim3(1), dim3(64), 0, st, ix, (int)B, call_status, idxw);
   return hipGetLastError();
 }
 
